@@ -1,0 +1,274 @@
+#!/usr/bin/env python3
+"""bench.py -- gradient GiB/s encode+decode+aggregate (device-resident) on MI355X.
+
+One step = the hot path over one batch of M synthetic client gradient buckets
+already resident in HBM:
+  1. client-side encode  (Base64::encode(vector<float>) of every bucket; k_encode_f32)
+  2. server aggregation  (CppNNUpdater.update's decode/dampen/sum/average/merge
+                          chain, bit-exact; k_update) -> merged Base64 + fp32
+  3. N>1 only: all_gather of the merged element-range shards over RCCL.
+
+Multi-GPU: element-range sharding, weak scaling -- every rank owns
+a fixed slice of G 3-value groups of a model N times larger; no collective in
+the data path, one all_gather of the merged slices (the real exchange step).
+
+Output: ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# workload name -> (layout, clients M, BASELINE.json config index or note)
+WORKLOADS = {
+    "mnist64": ("mnist", 64, "configs[1]: MNIST cppNN gradient buckets, 64 simulated clients"),
+    "cifar10_256": ("cifar10", 256, "configs[2]: CIFAR-10 cppNN gradient buckets, 256 clients"),
+    "cifar100_1024": ("cifar100", 1024, "configs[3]: CIFAR-100 cppNN gradient buckets, 1024 clients"),
+    "synth1m_256": ("synth1m", 256, "north-star target: 1M-float buckets, C=256 (SURVEY.md §8d)"),
+    "synth4m_4096": ("synth4m", 4096, "configs[4]: synthetic 4M-float buckets x 4096 clients"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md:36
+
+
+def dampen_policy(M: int):
+    """policy 1 (inverse, CppNNUpdater.java:307-308) with tau = c mod 3."""
+    return [1.0 / ((c % 3) + 1) for c in range(M)]
+
+
+class Shard:
+    """One rank's device-resident slice of a workload."""
+
+    def __init__(self, codec, torch, layout, M, rank, world, seed=1):
+        import fleet_amd as F
+        self.F = F
+        self.torch = torch
+        self.codec = codec
+        self.M = M
+        n_up_rank = layout.n_up  # weak scaling: every rank owns one full-size bucket slice
+        groups = (n_up_rank + 2) // 3
+        self.groups = groups
+        self.n_local = n_up_rank
+        self.g0 = rank * groups  # global group offset of this slice
+        # global layout = the per-rank layout replicated world times; headers of
+        # this slice in local coordinates (the slice is one copy of the layout)
+        self.hpos = layout.header_positions()
+        self.hval = layout.header_values()
+        self.L = F.b64_len(self.n_local)
+        self.pitch = 16 * groups
+        self.vpitch = 3 * groups
+        dev = torch.device("cuda", torch.cuda.current_device())
+        self.values = torch.empty((M, self.vpitch), dtype=torch.float32, device=dev)
+        self.text = torch.empty((M, self.pitch), dtype=torch.uint8, device=dev)
+        self.merged = torch.empty((self.pitch,), dtype=torch.uint8, device=dev)
+        self.merged_f32 = torch.empty((self.vpitch,), dtype=torch.float32, device=dev)
+        codec.synth_device(seed + rank * 1000003, self.values, self.n_local, self.hpos, self.hval)
+        self.dampen = dampen_policy(M)
+        torch.cuda.synchronize()
+
+    def encode(self):
+        self.codec.encode_device(self.values, self.n_local, self.text)
+
+    def aggregate(self):
+        self.codec.update_device(self.text, self.L, self.dampen, self.hpos, self.merged, self.merged_f32)
+
+    def algorithmic_bytes(self):
+        """Per launch: k_update reads M*L Base64, writes L Base64 + 4*n fp32;
+        k_encode_f32 reads 4*n*M fp32, writes M*L Base64."""
+        upd = self.M * self.L + self.L + 4 * self.n_local
+        enc = self.M * (4 * self.n_local + self.L)
+        return upd, enc
+
+
+def time_workload(torch, dist, codec, name, steps, warmup, rank, world):
+    from fleet_amd.layouts import LAYOUTS
+    lay_name, M, note = WORKLOADS[name]
+    layout = LAYOUTS[lay_name]
+    sh = Shard(codec, torch, layout, M, rank, world)
+    gathered = None
+    if world > 1:
+        gathered = torch.empty((world * sh.pitch,), dtype=torch.uint8, device=sh.merged.device)
+
+    def step(ev=None):
+        if ev:
+            ev[0].record()
+        sh.encode()
+        if ev:
+            ev[1].record()
+        sh.aggregate()
+        if ev:
+            ev[2].record()
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, sh.merged)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    codec.check()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    codec.check()
+    enc_ms = float(np.mean([evs[k][0].elapsed_time(evs[k][1]) for k in range(steps)]))
+    upd_ms = float(np.mean([evs[k][1].elapsed_time(evs[k][2]) for k in range(steps)]))
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=sh.merged.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / steps * 1e3
+    total_bytes_fp32 = world * M * sh.n_local * 4
+    gib_s = total_bytes_fp32 / (elapsed / steps) / 2**30
+    upd_b, enc_b = sh.algorithmic_bytes()
+    res = {
+        "workload": name, "note": note, "layout": lay_name, "clients": M, "n_up_per_rank": sh.n_local,
+        "ms_per_step": ms, "gib_s": gib_s, "update_kernel_ms": upd_ms, "encode_kernel_ms": enc_ms,
+        "update_bytes": upd_b, "encode_bytes": enc_b,
+        "update_gbs": upd_b / (upd_ms * 1e-3) / 1e9, "encode_gbs": enc_b / (enc_ms * 1e-3) / 1e9,
+        "element_clients_per_s": world * M * sh.n_local / (elapsed / steps),
+    }
+    del sh
+    torch.cuda.empty_cache()
+    return res
+
+
+def cpu_baseline(budget_s: float = 20.0):
+    """The reference's own C++ (oracle/_ref, -O0 = Server/Makefile flags) if built,
+    else the C restatement's faithful per-op chain; single thread (update() is
+    synchronized in the reference). Sample: MNIST layout, 64 clients (= configs[1]),
+    client encode + CppNNUpdater.update chain, repeated while under budget."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    from fleet_amd.layouts import MNIST
+    o = pyoracle.Oracle()
+    kind, impl = "port", None
+    if os.path.exists(pyoracle.REF_SO):
+        try:
+            impl = pyoracle.Reference()
+            kind = "reference"
+        except OSError:
+            impl = None
+    M = 64
+    floats = [o.synth_upload(1, c, list(MNIST.w_sizes), list(MNIST.b_sizes)) for c in range(M)]
+    d = dampen_policy(M)
+    reps, t_total = 0, 0.0
+    while t_total < budget_s and reps < 10:
+        t0 = time.perf_counter()
+        if impl is not None:
+            ups = [impl.encode_floats(v) for v in floats]
+            impl.update(ups, d)
+        else:
+            ups = [o.encode_floats(v) for v in floats]
+            o.update_faithful(ups, d)
+        t_total += time.perf_counter() - t0
+        reps += 1
+        if t_total > budget_s / 2:
+            break
+    per = t_total / reps
+    value = M * MNIST.n_up * 4 / per / 2**30
+    import platform
+    cpu = platform.processor() or "x86_64"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"value": value, "unit": "GiB/s", "cores": 1, "kind": kind,
+            "sample": f"MNIST layout (22,961 floats) x 64 clients: client encode + CppNNUpdater.update chain, "
+                      f"{reps} rep(s), {per:.3f} s/rep, {'oracle/_ref -O0 (reference C++)' if kind == 'reference' else 'oracle faithful port -O2'}",
+            "cpu_model": cpu, "host_nproc": os.cpu_count()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="mnist64", choices=sorted(WORKLOADS))
+    ap.add_argument("--extras", default="cifar10_256,synth1m_256",
+                    help="comma list of extra workloads measured in the same run (N=1 only); '' for none")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import fleet_amd as F
+    codec = F.Codec(local)
+
+    main_res = time_workload(torch, dist, codec, args.workload, args.steps, args.warmup, rank, world)
+    extras = {}
+    if world == 1 and args.extras:
+        for w in [x for x in args.extras.split(",") if x and x != args.workload]:
+            extras[w] = time_workload(torch, dist, codec, w, max(3, args.steps // 4), 2, rank, world)
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    cpu = None
+    if not args.no_cpu_baseline and world == 1:
+        cpu = cpu_baseline(args.cpu_budget)
+    r = main_res
+    achieved = r["update_gbs"]
+    line = {
+        "metric": "gradient GiB/s encode+decode+aggregate (device-resident); % HBM roofline",
+        "value": r["gib_s"],
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": r["ms_per_step"],
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (Philox4x32-10 value mix, SURVEY.md §8d), device-resident",
+        "config": {"workload": args.workload, "layout": r["layout"], "clients": r["clients"],
+                   "n_up_per_rank": r["n_up_per_rank"], "parallelism": f"element-shard x{world}",
+                   "dampening": "policy 1 inverse, tau = c mod 3"},
+        "roofline": {"bound": "hbm", "kernel": "k_update", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_launch": r["update_bytes"], "kernel_ms": r["update_kernel_ms"]},
+        "cpu_baseline": cpu,
+        "kernels": {"k_update_ms": r["update_kernel_ms"], "k_encode_f32_ms": r["encode_kernel_ms"],
+                    "k_encode_gbs": r["encode_gbs"], "element_clients_per_s": r["element_clients_per_s"]},
+        "extra": extras,
+    }
+    if cpu:
+        line["vs_cpu_baseline"] = r["gib_s"] / cpu["value"]
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

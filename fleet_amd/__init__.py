@@ -1,0 +1,372 @@
+"""fleet_amd -- MI355X-native FLeet gradient codec + server-side aggregation.
+
+Python host layer over the C-ABI of ``include/fleet_codec.h`` (libfleetcodec.so,
+gfx950 HIP kernels). It mirrors the reference's native surface:
+
+* :class:`Codec` -- one device context; the JNI natives of the reference's
+  server backend (Server/src/main/c++/cppNN_backend.cpp) as methods with the
+  same names and argument meaning (``getFlatGradient``, ``mergeFlatGradient``,
+  ``scalarMulNative``, ``addNative``, ``subtractNative``, ``getNorm``) plus the
+  fused batched ``update`` and the device-resident entry points.
+* :class:`ByteVec` -- mirror of Server/src/main/java/utils/ByteVec.java.
+* :mod:`fleet_amd.updater` -- mirror of CppNNUpdater's aggregation logic.
+
+There is no CPU compute path: if the HIP library is missing or no GPU is
+visible, constructing a :class:`Codec` raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+from .layouts import LAYOUTS, Layout  # noqa: F401
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+LIB_PATH = os.path.join(PKG, "libfleetcodec.so")
+HEADER_PATH = os.path.join(ROOT, "include", "fleet_codec.h")
+
+FLEET_OK = 0
+FLEET_ERR_ARG = -1
+FLEET_ERR_BASE64 = -2
+FLEET_ERR_LAYOUT = -3
+FLEET_ERR_HIP = -4
+FLEET_ERR_NOMEM = -5
+FLEET_ERR_CAPACITY = -6
+FLEET_MAX_HEADERS = 4096
+
+
+class FleetError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class Base64Error(FleetError):
+    pass
+
+
+class LayoutError(FleetError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libfleetcodec.so (build it with ``python -m fleet_amd.build``)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run `python -m fleet_amd.build` (HIP extension not built)")
+    # One HIP runtime per process: when torch (ROCm build) is present, load it first so
+    # libfleetcodec.so binds to the libamdhip64 torch already mapped (two runtimes in
+    # one process cannot share streams/pointers and the second fails to initialise).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = C.CDLL(LIB_PATH)
+    sz, vp, i32, i64 = C.c_size_t, C.c_void_p, C.c_int, C.c_int64
+    szp = C.POINTER(C.c_size_t)
+    sig = {
+        "fleet_version": (C.c_char_p, []),
+        "fleet_create": (i32, [i32, C.POINTER(vp)]),
+        "fleet_destroy": (None, [vp]),
+        "fleet_last_error": (C.c_char_p, [vp]),
+        "fleet_sync": (i32, [vp, vp]),
+        "fleet_check": (i32, [vp, vp]),
+        "fleet_b64_len": (sz, [sz]),
+        "fleet_b64_count": (sz, [sz]),
+        "fleet_layout_from_sizes": (i32, [vp, i32, vp, i32, vp, i32, C.POINTER(i32), szp]),
+        "fleet_layout_parse": (i32, [vp, vp, sz, vp, i32, C.POINTER(i32), szp]),
+        "fleet_encode_f32": (i32, [vp, vp, sz, vp, sz, szp]),
+        "fleet_encode_i32": (i32, [vp, vp, sz, vp, sz, szp]),
+        "fleet_decode_f32": (i32, [vp, vp, sz, vp, sz, szp]),
+        "fleet_decode_i32": (i32, [vp, vp, sz, vp, sz, szp]),
+        "fleet_flat_gradient": (i32, [vp, vp, sz, vp, sz, szp]),
+        "fleet_merge_flat_gradient": (i32, [vp, vp, sz, vp, sz, vp, sz, szp]),
+        "fleet_scalar_mul": (i32, [vp, vp, sz, C.c_double, vp, sz, szp]),
+        "fleet_add": (i32, [vp, vp, sz, vp, sz, vp, sz, szp]),
+        "fleet_subtract": (i32, [vp, vp, sz, vp, sz, vp, sz, szp]),
+        "fleet_norm": (i32, [vp, vp, sz, C.POINTER(C.c_double)]),
+        "fleet_update": (i32, [vp, vp, vp, i32, vp, vp, sz, szp, vp]),
+        "fleet_update_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, sz, sz, vp, vp, vp]),
+        "fleet_encode_device": (i32, [vp, vp, sz, sz, i32, vp, sz, vp]),
+        "fleet_decode_device": (i32, [vp, vp, sz, sz, i32, vp, sz, vp]),
+        "fleet_synth_device": (i32, [vp, C.c_uint64, i32, i32, vp, vp, i32, sz, vp, sz, vp]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _ = i64
+    _lib = L
+    return L
+
+
+def exported_symbols_from_header(path: str = HEADER_PATH):
+    """Function names declared in include/fleet_codec.h."""
+    import re
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(fleet_[a-z0-9_]+)\s*\(", text)))
+
+
+def b64_len(n_values: int) -> int:
+    """Base64 length of n int32 values: 4*ceil(4n/3) (Base64.cpp:166-175)."""
+    return 4 * ((4 * n_values + 2) // 3)
+
+
+def b64_count(length: int) -> int:
+    return 3 * length // 16
+
+
+def layout_from_sizes(w_sizes: Sequence[int], b_sizes: Sequence[int]):
+    """Header slot positions + n_up of the gradients() layout (network.h:1038-1056)."""
+    w = np.ascontiguousarray(w_sizes, dtype=np.int32)
+    b = np.ascontiguousarray(b_sizes, dtype=np.int32)
+    cap = len(w) + len(b) + 2
+    pos = np.empty(cap, np.int32)
+    nh = C.c_int(0)
+    n_up = C.c_size_t(0)
+    rc = lib().fleet_layout_from_sizes(w.ctypes.data, len(w), b.ctypes.data, len(b), pos.ctypes.data, cap,
+                                       C.byref(nh), C.byref(n_up))
+    if rc != FLEET_OK:
+        raise FleetError(rc, "bad layout sizes")
+    return pos[: nh.value].copy(), int(n_up.value)
+
+
+def _stream(stream):
+    """Device calls default to torch's current stream so they order with torch ops
+    (NULL = the null stream, which is torch's default stream)."""
+    if stream is not None:
+        return C.c_void_p(int(stream)) if int(stream) else None
+    try:
+        import torch
+        if torch.cuda.is_available():
+            h = torch.cuda.current_stream().cuda_stream
+            return C.c_void_p(h) if h else None
+    except ImportError:
+        pass
+    return None
+
+
+def _as_bytes(x) -> bytes:
+    if isinstance(x, (bytes, bytearray, memoryview)):
+        return bytes(x)
+    if isinstance(x, np.ndarray):
+        return x.tobytes()
+    if isinstance(x, str):
+        return x.encode("ascii")
+    raise TypeError(f"expected Base64 bytes, got {type(x)}")
+
+
+class Codec:
+    """One HIP device context (``fleet_ctx``). Raises if no GPU / library."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        h = C.c_void_p()
+        rc = L.fleet_create(device, C.byref(h))
+        if rc != FLEET_OK:
+            raise FleetError(rc, f"fleet_create(device={device}) failed: no usable MI355X/HIP device")
+        self._h = h
+        self._L = L
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.fleet_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- error plumbing -------------------------------------------------------
+    def _check(self, rc: int):
+        if rc == FLEET_OK:
+            return
+        msg = self._L.fleet_last_error(self._h).decode(errors="replace")
+        if rc == FLEET_ERR_BASE64:
+            raise Base64Error(rc, msg)
+        if rc == FLEET_ERR_LAYOUT:
+            raise LayoutError(rc, msg)
+        raise FleetError(rc, msg)
+
+    def _text_call(self, fn, args, cap):
+        out = np.empty(max(cap, 1), np.uint8)
+        n = C.c_size_t(0)
+        rc = fn(self._h, *args, out.ctypes.data, cap, C.byref(n))
+        self._check(rc)
+        return out[: n.value].tobytes()
+
+    # -- Base64.cpp -------------------------------------------------------------
+    def encode_floats(self, v) -> bytes:
+        """Base64::encode(std::vector<float>) (Base64.cpp:140-142)."""
+        v = np.ascontiguousarray(v, dtype=np.float32)
+        return self._text_call(self._L.fleet_encode_f32, (v.ctypes.data, len(v)), b64_len(len(v)))
+
+    def encode_ints(self, v) -> bytes:
+        """Base64::encode(std::vector<int>) (Base64.cpp:145-151)."""
+        v = np.ascontiguousarray(v, dtype=np.int32)
+        return self._text_call(self._L.fleet_encode_i32, (v.ctypes.data, len(v)), b64_len(len(v)))
+
+    def decode_floats(self, text) -> np.ndarray:
+        """Base64::decodeFloat (Base64.cpp:207-209)."""
+        s = _as_bytes(text)
+        out = np.empty(b64_count(len(s)) + 1, np.float32)
+        n = C.c_size_t(0)
+        self._check(self._L.fleet_decode_f32(self._h, s, len(s), out.ctypes.data, len(out), C.byref(n)))
+        return out[: n.value].copy()
+
+    def decode_ints(self, text) -> np.ndarray:
+        """Base64::decodeInt (Base64.cpp:211-219)."""
+        s = _as_bytes(text)
+        out = np.empty(b64_count(len(s)) + 1, np.int32)
+        n = C.c_size_t(0)
+        self._check(self._L.fleet_decode_i32(self._h, s, len(s), out.ctypes.data, len(out), C.byref(n)))
+        return out[: n.value].copy()
+
+    # -- cppNN_backend.cpp natives (same names as the Java declarations) -------
+    def getFlatGradient(self, grad) -> bytes:  # noqa: N802  (CppNNUpdater.java:159)
+        s = _as_bytes(grad)
+        return self._text_call(self._L.fleet_flat_gradient, (s, len(s)), len(s) + 16)
+
+    def mergeFlatGradient(self, grad, flat) -> bytes:  # noqa: N802  (CppNNUpdater.java:160)
+        g, f = _as_bytes(grad), _as_bytes(flat)
+        return self._text_call(self._L.fleet_merge_flat_gradient, (g, len(g), f, len(f)), len(g) + 16)
+
+    def scalarMulNative(self, v, a: float) -> bytes:  # noqa: N802  (ByteVec.java:26)
+        s = _as_bytes(v)
+        return self._text_call(self._L.fleet_scalar_mul, (s, len(s), float(a)), len(s) + 16)
+
+    def addNative(self, a, b) -> bytes:  # noqa: N802  (ByteVec.java:25)
+        x, y = _as_bytes(a), _as_bytes(b)
+        return self._text_call(self._L.fleet_add, (x, len(x), y, len(y)), len(x) + 16)
+
+    def subtractNative(self, a, b) -> bytes:  # noqa: N802  (ByteVec.java:24)
+        x, y = _as_bytes(a), _as_bytes(b)
+        return self._text_call(self._L.fleet_subtract, (x, len(x), y, len(y)), len(x) + 16)
+
+    def getNorm(self, v) -> float:  # noqa: N802  (ByteVec.java:23)
+        s = _as_bytes(v)
+        out = C.c_double(0)
+        self._check(self._L.fleet_norm(self._h, s, len(s), C.byref(out)))
+        return out.value
+
+    def layout_parse(self, upload):
+        s = _as_bytes(upload)
+        pos = np.empty(FLEET_MAX_HEADERS, np.int32)
+        nh = C.c_int(0)
+        n_up = C.c_size_t(0)
+        self._check(self._L.fleet_layout_parse(self._h, s, len(s), pos.ctypes.data, FLEET_MAX_HEADERS,
+                                               C.byref(nh), C.byref(n_up)))
+        return pos[: nh.value].copy(), int(n_up.value)
+
+    # -- fused update ------------------------------------------------------------
+    def update(self, uploads: Sequence, dampen: Sequence[float], want_f32: bool = False):
+        """Aggregation of CppNNUpdater.update (CppNNUpdater.java:420-509) in one call.
+
+        Returns the merged Base64 (what mergeFlatGradient returns) and, with
+        ``want_f32``, Base64::decodeFloat of it (what descentNative decodes).
+        """
+        ups = [_as_bytes(u) for u in uploads]
+        M = len(ups)
+        if M == 0:
+            raise ValueError("no uploads")
+        if len(dampen) != M:
+            raise ValueError("one dampening factor per upload")
+        arr = (C.c_char_p * M)(*ups)
+        lens = np.array([len(u) for u in ups], dtype=np.uint64)
+        d = np.ascontiguousarray(dampen, dtype=np.float64)
+        L = len(ups[0])
+        out = np.empty(L + 16, np.uint8)
+        n = C.c_size_t(0)
+        f32 = np.empty(b64_count(L) + 1, np.float32) if want_f32 else None
+        rc = self._L.fleet_update(self._h, C.cast(arr, C.c_void_p), lens.ctypes.data, M, d.ctypes.data,
+                                  out.ctypes.data, len(out), C.byref(n), f32.ctypes.data if want_f32 else None)
+        self._check(rc)
+        merged = out[: n.value].tobytes()
+        if want_f32:
+            return merged, f32[: b64_count(L)].copy()
+        return merged
+
+    # -- device-resident (torch tensors on this device) -----------------------
+    def update_device(self, uploads_u8, length: int, dampen: Sequence[float], header_pos, merged_u8,
+                      merged_f32=None, group_begin: int = 0, group_end: Optional[int] = None, stream=None):
+        """uploads_u8: uint8 CUDA tensor [M, pitch]; merged_u8: uint8 [>= 16*groups]."""
+        M, pitch = uploads_u8.shape
+        groups = (b64_count(length) + 2) // 3
+        ge = groups if group_end is None else group_end
+        hp = np.ascontiguousarray(header_pos, dtype=np.int32)
+        d = np.ascontiguousarray(dampen, dtype=np.float64)
+        rc = self._L.fleet_update_device(self._h, uploads_u8.data_ptr(), pitch, length, M, d.ctypes.data,
+                                         hp.ctypes.data, len(hp), group_begin, ge, merged_u8.data_ptr(),
+                                         merged_f32.data_ptr() if merged_f32 is not None else None,
+                                         _stream(stream))
+        self._check(rc)
+
+    def encode_device(self, values_f32, n: int, out_u8, stream=None):
+        """values_f32: float32 CUDA tensor [M, vpitch]; out_u8: uint8 [M, pitch]."""
+        M, vpitch = values_f32.shape
+        _, pitch = out_u8.shape
+        rc = self._L.fleet_encode_device(self._h, values_f32.data_ptr(), n, vpitch, M, out_u8.data_ptr(), pitch,
+                                         _stream(stream))
+        self._check(rc)
+
+    def decode_device(self, text_u8, length: int, out_f32, stream=None):
+        M, pitch = text_u8.shape
+        _, vpitch = out_f32.shape
+        rc = self._L.fleet_decode_device(self._h, text_u8.data_ptr(), length, pitch, M, out_f32.data_ptr(), vpitch,
+                                         _stream(stream))
+        self._check(rc)
+
+    def synth_device(self, seed: int, values_f32, n_up: int, header_pos, header_val, client0: int = 0,
+                     stream=None):
+        M, vpitch = values_f32.shape
+        hp = np.ascontiguousarray(header_pos, dtype=np.int32)
+        hv = np.ascontiguousarray(header_val, dtype=np.float32)
+        rc = self._L.fleet_synth_device(self._h, seed, M, client0, hp.ctypes.data, hv.ctypes.data, len(hp), n_up,
+                                        values_f32.data_ptr(), vpitch, _stream(stream))
+        self._check(rc)
+
+    def check(self, stream=None):
+        self._check(self._L.fleet_check(self._h, _stream(stream)))
+
+    def sync(self, stream=None):
+        self._check(self._L.fleet_sync(self._h, _stream(stream)))
+
+
+class ByteVec:
+    """Mirror of Server/src/main/java/utils/ByteVec.java: a Base64 vector whose
+    arithmetic runs through the natives (here: the HIP codec)."""
+
+    def __init__(self, v, codec: Codec):
+        self.v = _as_bytes(v)  # ByteVec.java:33-35 clones
+        self.codec = codec
+
+    def add(self, other: "ByteVec") -> "ByteVec":  # :85-88
+        return ByteVec(self.codec.addNative(self.v, other.v), self.codec)
+
+    def subtract(self, other: "ByteVec") -> "ByteVec":  # :96-99
+        return ByteVec(self.codec.subtractNative(self.v, other.v), self.codec)
+
+    def scalarMultiply(self, a: float) -> "ByteVec":  # noqa: N802  :121-123
+        return ByteVec(self.codec.scalarMulNative(self.v, a), self.codec)
+
+    def getNorm(self) -> float:  # noqa: N802  :69-71
+        return self.codec.getNorm(self.v)

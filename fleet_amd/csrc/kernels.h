@@ -1,0 +1,26 @@
+// fleet_amd/csrc/kernels.h -- internal launchers (fleet_codec.cpp <-> kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fleet {
+hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
+                         int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
+                         uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s);
+hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int rows, uint8_t* out, size_t pitch,
+                             hipStream_t s);
+hipError_t launch_encode_i32(const int32_t* codes, int64_t n, uint8_t* out, hipStream_t s);
+hipError_t launch_decode(const uint8_t* text, int64_t n, size_t pitch, int rows, void* out, size_t vpitch,
+                         int as_codes, int* d_err, hipStream_t s);
+hipError_t launch_elementwise(const uint8_t* a, const uint8_t* b, int op, double scale, int64_t n, uint8_t* out,
+                              int* d_err, hipStream_t s);
+hipError_t launch_norm_partials(const uint8_t* a, int64_t n, double* partials, int* nblocks, int* d_err,
+                                hipStream_t s);
+hipError_t launch_flat(const uint8_t* up, const int32_t* d_hdr, int n_hdr, int64_t n_flat, uint8_t* out,
+                       int* d_err, hipStream_t s);
+hipError_t launch_merge(const uint8_t* up, const uint8_t* flat, const int32_t* d_hdr, int n_hdr, int64_t walk_end,
+                        int64_t n_up, uint8_t* out, int* d_err, hipStream_t s);
+hipError_t launch_layout_parse(const uint8_t* up, int64_t n, int cap, int32_t* out, hipStream_t s);
+hipError_t launch_synth(uint64_t seed, int client0, int rows, int64_t n_up, float* out, size_t vpitch,
+                        const int32_t* d_hpos, const float* d_hval, int n_hdr, hipStream_t s);
+}  // namespace fleet

@@ -1,0 +1,454 @@
+// fleet_amd/csrc/kernels.hip -- gfx950 kernels of the FLeet codec / aggregation path.
+//
+// Data layout in HBM: client uploads are rows of `pitch` bytes
+// (pitch % 16 == 0) of Base64 text. One lane owns one 16-char group = 12
+// bytes = 3 int32 codes = 3 gradient values, and walks every client row in
+// order (the per-element chain is serial across clients, CppNNUpdater.java:
+// 420-509); a wave reads 1 KiB contiguous per client row (global_load_dwordx4).
+#include "kernels.h"
+
+#include "codec_device.h"
+
+namespace fleet {
+
+#define FLEET_ERRBIT_BASE64 1
+#define FLEET_ERRBIT_LAYOUT 2
+
+// chars of the group that must be alphabet chars, for r valid int32 values
+__device__ __forceinline__ uint32_t needed_chars_mask(int r) {
+  return r >= 3 ? 0xffffu : r == 2 ? 0x7ffu : r == 1 ? 0x3fu : 0u;
+}
+
+// Base64.cpp:196-198 -- trailing '=' for the missing bytes of a partial group
+__device__ __forceinline__ uint4 pad_group(uint4 v, int r) {
+  if (r == 1) {  // 4 bytes -> 6 chars + "=="
+    v.y = (v.y & 0x0000ffffu) | 0x3d3d0000u;
+    v.z = 0;
+    v.w = 0;
+  } else if (r == 2) {  // 8 bytes -> 11 chars + "="
+    v.z = (v.z & 0x00ffffffu) | 0x3d000000u;
+    v.w = 0;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int headers_in_group(const int32_t* __restrict__ hdr, int n_hdr, int64_t p0,
+                                                bool is_hdr[3]) {
+  // hdr is sorted; n_hdr is small (layers), a binary search keeps it O(log n)
+  int lo = 0, hi = n_hdr;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (hdr[mid] < p0) lo = mid + 1; else hi = mid;
+  }
+  int cnt = 0;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) is_hdr[e] = false;
+  for (int i = lo; i < n_hdr && hdr[i] < p0 + 3; ++i) {
+    is_hdr[hdr[i] - p0] = true;
+    ++cnt;
+  }
+  return cnt;
+}
+
+// ----------------------------------------------------------------------------
+// Fused update: CppNNUpdater.update's aggregation (java:420-509) for the
+// groups [g_begin, g_end). Per value and client c (CppNNUpdater order):
+//   y = Q(dec(code_c))                  getFlatGradient decode+encode, scalarMul decode
+//   p = Q((float)((double)y * d_c))     scalarMultiply(getDampen) encode, add decode
+//   A = (c == 0) ? p : Q(A + p)         ByteVec.add encode/decode
+// then r = Q((float)((double)A * inv)) (scalarMultiply(1/avgSize) + merge decode) and
+// merged code = enc(r); header slots take enc(dec(code_{M-1})) (mergeFlatGradient).
+__global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                const double* __restrict__ dampen, double inv_avg,
+                                                int64_t n_up, int64_t g_begin, int64_t g_end,
+                                                const int32_t* __restrict__ hdr_block,
+                                                uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                int* __restrict__ err) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  // hdr_block = {status, n_headers, walk_end, 0, positions...} (k_layout_parse / host-built);
+  // slots at or after walk_end are outside network::flatGrad's walk and, like
+  // header slots, come from the last upload in mergeFlatGrad.
+  const int n_hdr = hdr_block[1];
+  const int64_t walk_end = hdr_block[2];
+  const int32_t* hdr = hdr_block + 4;
+
+  const int64_t g = g_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= g_end) return;
+  const int64_t p0 = 3 * g;
+  const int r = (int)min<int64_t>(3, n_up - p0);
+  const uint32_t need = needed_chars_mask(r);
+  bool is_hdr[3];
+  headers_in_group(hdr, n_hdr, p0, is_hdr);
+  bool keep_last[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) keep_last[e] = is_hdr[e] || p0 + e >= walk_end;
+
+  const uint8_t* row = uploads + 16 * g;
+  float acc[3] = {0.f, 0.f, 0.f};
+  int32_t codes[3] = {0, 0, 0};
+  int32_t last_hdr[3] = {0, 0, 0};
+  uint32_t bad = 0;
+  int layout_bad = 0;
+
+  uint4 next = *reinterpret_cast<const uint4*>(row);
+  for (int c = 0; c < M; ++c) {
+    const uint4 cur = next;
+    if (c + 1 < M) next = *reinterpret_cast<const uint4*>(row + (size_t)(c + 1) * pitch);
+    bad |= b64_decode_group(cur, &tab, codes);
+    const double d = dampen[c];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      const float y = q(dec(codes[e]));
+      const float p = q((float)((double)y * d));
+      acc[e] = c == 0 ? p : q(acc[e] + p);
+    }
+  }
+  // every upload must carry the same header slots as the last one
+  if (n_hdr) {
+    for (int e = 0; e < 3; ++e) last_hdr[e] = codes[e];
+    bool any = is_hdr[0] | is_hdr[1] | is_hdr[2];
+    if (any) {
+      for (int c = 0; c < M - 1; ++c) {
+        int32_t cc[3];
+        bad |= b64_decode_group(*reinterpret_cast<const uint4*>(row + (size_t)c * pitch), &tab, cc);
+        for (int e = 0; e < 3; ++e)
+          if (is_hdr[e] && e < r && cc[e] != last_hdr[e]) layout_bad = 1;
+      }
+    }
+  }
+  if (bad & need) atomicOr(err, FLEET_ERRBIT_BASE64);
+  if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+
+  int32_t out[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    int32_t o;
+    if (keep_last[e]) {
+      o = enc(dec(codes[e]));
+    } else {
+      o = enc(q((float)((double)acc[e] * inv_avg)));
+    }
+    out[e] = e < r ? o : 0;
+  }
+  uint4 text = pad_group(b64_encode_group(out, &tab), r);
+  *reinterpret_cast<uint4*>(merged + 16 * g) = text;
+  if (merged_f32) {
+    for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec(out[e]);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
+__global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ values, int64_t n, size_t vpitch,
+                                                    uint8_t* __restrict__ out, size_t pitch, int64_t groups) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= groups) return;
+  const int64_t row_id = blockIdx.y;
+  const float* v = values + row_id * vpitch + 3 * g;
+  const int r = (int)min<int64_t>(3, n - 3 * g);
+  int32_t codes[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) codes[e] = e < r ? enc(v[e]) : 0;
+  *reinterpret_cast<uint4*>(out + row_id * pitch + 16 * g) = pad_group(b64_encode_group(codes, &tab), r);
+}
+
+// int32 codes -> Base64 (Base64::encode(vector<int>))
+__global__ void __launch_bounds__(256) k_encode_i32(const int32_t* __restrict__ codes_in, int64_t n,
+                                                    uint8_t* __restrict__ out, int64_t groups) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= groups) return;
+  const int r = (int)min<int64_t>(3, n - 3 * g);
+  int32_t codes[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) codes[e] = e < r ? codes_in[3 * g + e] : 0;
+  *reinterpret_cast<uint4*>(out + 16 * g) = pad_group(b64_encode_group(codes, &tab), r);
+}
+
+// Base64 rows -> fp32 rows (decodeFloat) or int32 (decodeInt, as_codes)
+__global__ void __launch_bounds__(256) k_decode(const uint8_t* __restrict__ text, int64_t n, size_t pitch,
+                                                void* __restrict__ out, size_t vpitch, int64_t groups,
+                                                int as_codes, int* __restrict__ err) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= groups) return;
+  const int64_t row_id = blockIdx.y;
+  const int r = (int)min<int64_t>(3, n - 3 * g);
+  int32_t codes[3];
+  uint32_t bad = b64_decode_group(*reinterpret_cast<const uint4*>(text + row_id * pitch + 16 * g), &tab, codes);
+  if (bad & needed_chars_mask(r)) atomicOr(err, FLEET_ERRBIT_BASE64);
+  if (as_codes) {
+    int32_t* o = (int32_t*)out + row_id * vpitch + 3 * g;
+    for (int e = 0; e < r; ++e) o[e] = codes[e];
+  } else {
+    float* o = (float*)out + row_id * vpitch + 3 * g;
+    for (int e = 0; e < r; ++e) o[e] = dec(codes[e]);
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Per-op JNI replacements on equal-length Base64 vectors.
+// op 0: x*a (scalarMulNative), 1: a+b (addNative), 2: a-b (subtractNative)
+__global__ void __launch_bounds__(256) k_elementwise(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b,
+                                                     int op, double s, int64_t n, uint8_t* __restrict__ out,
+                                                     int64_t groups, int* __restrict__ err) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= groups) return;
+  const int r = (int)min<int64_t>(3, n - 3 * g);
+  int32_t ca[3], cb[3] = {0, 0, 0};
+  uint32_t bad = b64_decode_group(*reinterpret_cast<const uint4*>(a + 16 * g), &tab, ca);
+  if (op != 0) bad |= b64_decode_group(*reinterpret_cast<const uint4*>(b + 16 * g), &tab, cb);
+  if (bad & needed_chars_mask(r)) atomicOr(err, FLEET_ERRBIT_BASE64);
+  int32_t o[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    float x = dec(ca[e]);
+    float res;
+    if (op == 0) res = (float)((double)x * s);
+    else if (op == 1) res = x + dec(cb[e]);
+    else res = x - dec(cb[e]);
+    o[e] = e < r ? enc(res) : 0;
+  }
+  *reinterpret_cast<uint4*>(out + 16 * g) = pad_group(b64_encode_group(o, &tab), r);
+}
+
+// getNorm: per-group (double)(x*x) partial sums; the host finishes the sum.
+__global__ void __launch_bounds__(256) k_norm_partials(const uint8_t* __restrict__ a, int64_t n,
+                                                       double* __restrict__ partials, int64_t groups,
+                                                       int* __restrict__ err) {
+  __shared__ B64Tables tab;
+  __shared__ double red[256];
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double s = 0.0;
+  if (g < groups) {
+    const int r = (int)min<int64_t>(3, n - 3 * g);
+    int32_t ca[3];
+    uint32_t bad = b64_decode_group(*reinterpret_cast<const uint4*>(a + 16 * g), &tab, ca);
+    if (bad & needed_chars_mask(r)) atomicOr(err, FLEET_ERRBIT_BASE64);
+    for (int e = 0; e < r; ++e) {
+      float x = dec(ca[e]);
+      float sq = x * x;
+      s += (double)sq;
+    }
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partials[blockIdx.x] = red[0];
+}
+
+// read the code at value position p of a Base64 vector
+__device__ __forceinline__ int32_t code_at(const uint8_t* text, int64_t p, const B64Tables* tab, uint32_t* bad) {
+  int32_t cc[3];
+  uint32_t b = b64_decode_group(*reinterpret_cast<const uint4*>(text + 16 * (p / 3)), tab, cc);
+  int e = (int)(p % 3);
+  const uint32_t carry[3] = {0x003fu, 0x07e0u, 0xfc00u};  // chars carrying bytes 4e..4e+3
+  *bad |= b & carry[e];
+  return cc[e];
+}
+
+// getFlatGradient: flat[i] = enc(dec(upload[pos(i)])), pos skips header slots
+__global__ void __launch_bounds__(256) k_flat(const uint8_t* __restrict__ up, const int32_t* __restrict__ hdr,
+                                              int n_hdr, int64_t n_flat, uint8_t* __restrict__ out,
+                                              int64_t groups, int* __restrict__ err) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= groups) return;
+  const int r = (int)min<int64_t>(3, n_flat - 3 * g);
+  int32_t o[3] = {0, 0, 0};
+  uint32_t bad = 0;
+  for (int e = 0; e < r; ++e) {
+    int64_t pos = 3 * g + e;
+    for (int h = 0; h < n_hdr; ++h)
+      if (hdr[h] <= pos) ++pos;
+    o[e] = enc(dec(code_at(up, pos, &tab, &bad)));
+  }
+  if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
+  *reinterpret_cast<uint4*>(out + 16 * g) = pad_group(b64_encode_group(o, &tab), r);
+}
+
+// mergeFlatGradient: header slots from g, payload slots from flat, all re-encoded
+__global__ void __launch_bounds__(256) k_merge(const uint8_t* __restrict__ up, const uint8_t* __restrict__ flat,
+                                               const int32_t* __restrict__ hdr, int n_hdr, int64_t walk_end,
+                                               int64_t n_up,
+                                               uint8_t* __restrict__ out, int64_t groups, int* __restrict__ err) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= groups) return;
+  const int r = (int)min<int64_t>(3, n_up - 3 * g);
+  int32_t o[3] = {0, 0, 0};
+  uint32_t bad = 0;
+  for (int e = 0; e < r; ++e) {
+    const int64_t p = 3 * g + e;
+    int before = 0;
+    bool is_h = false;
+    for (int h = 0; h < n_hdr; ++h) {
+      if (hdr[h] < p) ++before;
+      if (hdr[h] == p) is_h = true;
+    }
+    if (p >= walk_end) is_h = true;  // outside the layout walk: kept from g
+    int32_t c = is_h ? code_at(up, p, &tab, &bad) : code_at(flat, p - before, &tab, &bad);
+    o[e] = enc(dec(c));
+  }
+  if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
+  *reinterpret_cast<uint4*>(out + 16 * g) = pad_group(b64_encode_group(o, &tab), r);
+}
+
+// network::flatGrad's header walk (network.h:1206-1223), one thread.
+// out[0] = status (0 ok, 1 malformed), out[1] = n_headers, out[2] = walk end,
+// out[4..] = header positions.
+__global__ void k_layout_parse(const uint8_t* __restrict__ up, int64_t n, int cap, int32_t* __restrict__ out) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  int64_t idx = 0;
+  int nh = 0;
+  uint32_t bad = 0;
+  int status = 0;
+  for (int part = 0; part < 2 && !status; ++part) {
+    if (idx >= n || nh >= cap) { status = 1; break; }
+    out[4 + nh++] = (int32_t)idx;
+    int cnt = cvtt(dec(code_at(up, idx++, &tab, &bad)));
+    for (int i = 0; i < cnt; ++i) {
+      if (idx >= n || nh >= cap) { status = 1; break; }
+      out[4 + nh++] = (int32_t)idx;
+      int size = cvtt(dec(code_at(up, idx++, &tab, &bad)));
+      if (size < 0 || idx + size > n) { status = 1; break; }
+      idx += size;
+    }
+  }
+  if (bad) status = 1;
+  out[0] = status;
+  out[1] = nh;
+  out[2] = (int32_t)idx;
+  out[3] = 0;
+}
+
+// synthetic buckets + layout header values
+__global__ void __launch_bounds__(256) k_synth(uint64_t seed, int client0, int64_t n_up, float* __restrict__ out,
+                                               size_t vpitch, const int32_t* __restrict__ hpos,
+                                               const float* __restrict__ hval, int n_hdr) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  if (i < n_up) out[(size_t)c * vpitch + i] = synth_value(seed, (uint32_t)(client0 + c), (uint32_t)i);
+}
+
+__global__ void k_synth_headers(float* __restrict__ out, size_t vpitch, const int32_t* __restrict__ hpos,
+                                const float* __restrict__ hval, int n_hdr) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_hdr) out[(size_t)blockIdx.y * vpitch + hpos[i]] = hval[i];
+}
+
+// ---------------------------------------------------------------- launchers
+
+static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
+                         int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
+                         uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
+  if (g_end <= g_begin) return hipSuccess;
+  hipLaunchKernelGGL(k_update, dim3(blocks_for(g_end - g_begin, 256)), dim3(256), 0, s, uploads, pitch, M,
+                     d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int rows, uint8_t* out, size_t pitch,
+                             hipStream_t s) {
+  int64_t groups = (n + 2) / 3;
+  if (groups == 0 || rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_encode_f32, dim3(blocks_for(groups, 256), rows), dim3(256), 0, s, values, n, vpitch, out,
+                     pitch, groups);
+  return hipGetLastError();
+}
+
+hipError_t launch_encode_i32(const int32_t* codes, int64_t n, uint8_t* out, hipStream_t s) {
+  int64_t groups = (n + 2) / 3;
+  if (groups == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_encode_i32, dim3(blocks_for(groups, 256)), dim3(256), 0, s, codes, n, out, groups);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode(const uint8_t* text, int64_t n, size_t pitch, int rows, void* out, size_t vpitch,
+                         int as_codes, int* d_err, hipStream_t s) {
+  int64_t groups = (n + 2) / 3;
+  if (groups == 0 || rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_decode, dim3(blocks_for(groups, 256), rows), dim3(256), 0, s, text, n, pitch, out, vpitch,
+                     groups, as_codes, d_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_elementwise(const uint8_t* a, const uint8_t* b, int op, double scale, int64_t n, uint8_t* out,
+                              int* d_err, hipStream_t s) {
+  int64_t groups = (n + 2) / 3;
+  if (groups == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_elementwise, dim3(blocks_for(groups, 256)), dim3(256), 0, s, a, b, op, scale, n, out,
+                     groups, d_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_norm_partials(const uint8_t* a, int64_t n, double* partials, int* nblocks, int* d_err,
+                                hipStream_t s) {
+  int64_t groups = (n + 2) / 3;
+  *nblocks = (int)blocks_for(groups, 256);
+  if (groups == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_norm_partials, dim3(*nblocks), dim3(256), 0, s, a, n, partials, groups, d_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_flat(const uint8_t* up, const int32_t* d_hdr, int n_hdr, int64_t n_flat, uint8_t* out,
+                       int* d_err, hipStream_t s) {
+  int64_t groups = (n_flat + 2) / 3;
+  if (groups == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_flat, dim3(blocks_for(groups, 256)), dim3(256), 0, s, up, d_hdr, n_hdr, n_flat, out, groups,
+                     d_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge(const uint8_t* up, const uint8_t* flat, const int32_t* d_hdr, int n_hdr, int64_t walk_end,
+                        int64_t n_up, uint8_t* out, int* d_err, hipStream_t s) {
+  int64_t groups = (n_up + 2) / 3;
+  if (groups == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_merge, dim3(blocks_for(groups, 256)), dim3(256), 0, s, up, flat, d_hdr, n_hdr, walk_end,
+                     n_up, out, groups, d_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_layout_parse(const uint8_t* up, int64_t n, int cap, int32_t* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_layout_parse, dim3(1), dim3(64), 0, s, up, n, cap, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_synth(uint64_t seed, int client0, int rows, int64_t n_up, float* out, size_t vpitch,
+                        const int32_t* d_hpos, const float* d_hval, int n_hdr, hipStream_t s) {
+  if (rows == 0 || n_up == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_synth, dim3(blocks_for(n_up, 256), rows), dim3(256), 0, s, seed, client0, n_up, out, vpitch,
+                     d_hpos, d_hval, n_hdr);
+  if (n_hdr > 0)
+    hipLaunchKernelGGL(k_synth_headers, dim3(blocks_for(n_hdr, 256), rows), dim3(256), 0, s, out, vpitch, d_hpos,
+                       d_hval, n_hdr);
+  return hipGetLastError();
+}
+
+}  // namespace fleet

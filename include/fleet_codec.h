@@ -1,0 +1,147 @@
+/*
+ * include/fleet_codec.h -- C-ABI of the MI355X-native FLeet gradient codec and
+ * server-side aggregation path (libfleetcodec.so).
+ *
+ * This is the drop-in boundary under the reference's JNI layer. Every entry
+ * point below replaces a native function of the reference's server backend
+ * (libnative.so built from Server/src/main/c++/cppNN_backend.cpp), or the
+ * call sequence CppNNUpdater.update drives through them, and produces the
+ * same bytes. The JNI shim (fleet_amd/csrc/jni_shim.cpp, libfleet_native.so)
+ * re-exports the reference's Java_* symbols on top of this ABI; see
+ * INTEGRATION.md for the Java-side binding.
+ *
+ * Conventions
+ *   - Plain pointers and sizes; no torch/HIP types. `stream` arguments are a
+ *     hipStream_t passed as void* (NULL = the null/default stream). Host-buffer
+ *     entry points run on the context's own stream and return synchronously.
+ *   - "Base64" buffers are the reference's wire format: Base64 (RFC 4648
+ *     alphabet; '-' and '_' accepted as 62/63 on input, Base64.cpp:56-68) of
+ *     little-endian int32 decimal fixed-point codes (Base64::float2int,
+ *     Base64.cpp:84-114). Host buffers are NOT NUL-terminated.
+ *   - Every function returns FLEET_OK (0) or a negative FLEET_ERR_* code;
+ *     fleet_last_error() gives a message. The reference has no error
+ *     reporting (malformed input is UB there); here it is rejected.
+ *   - Thread safety: a context serialises its own calls with an internal
+ *     mutex (the reference serialises all updater natives under
+ *     `synchronized(acc)`, CppNNUpdater.java:259,333). Use one context per
+ *     thread/GPU for concurrency.
+ *   - Input contract: Base64 text produced by Base64::encode -- length a
+ *     multiple of 4, '=' only as trailing padding. Anything else returns
+ *     FLEET_ERR_BASE64 (the reference would silently drop bytes).
+ */
+#ifndef FLEET_CODEC_H
+#define FLEET_CODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FLEET_OK 0
+#define FLEET_ERR_ARG (-1)      /* bad argument / size mismatch */
+#define FLEET_ERR_BASE64 (-2)   /* text outside the Base64::encode output contract */
+#define FLEET_ERR_LAYOUT (-3)   /* gradient layout header inconsistent (network.h:1038-1056) */
+#define FLEET_ERR_HIP (-4)      /* HIP runtime failure (or no GPU) */
+#define FLEET_ERR_NOMEM (-5)
+#define FLEET_ERR_CAPACITY (-6) /* output buffer too small; *out_len holds the size needed */
+
+#define FLEET_MAX_HEADERS 4096
+
+typedef struct fleet_ctx fleet_ctx;
+
+/* Library / context ------------------------------------------------------ */
+const char* fleet_version(void);
+int fleet_create(int device, fleet_ctx** out);
+void fleet_destroy(fleet_ctx* ctx);
+const char* fleet_last_error(const fleet_ctx* ctx);
+int fleet_sync(fleet_ctx* ctx, void* stream);
+
+/* Base64 length of n int32/fp32 values: 4*ceil(4n/3) (Base64.cpp:166-175). */
+size_t fleet_b64_len(size_t n_values);
+/* Number of int32 values carried by a Base64::encode output of length len. */
+size_t fleet_b64_count(size_t len);
+
+/* Gradient layout (network.h:1038-1056): [nW,(size_i,dW_i..)*,nB,(size_j,db_j..)*].
+ * Writes the sorted header slot positions; returns FLEET_OK and *n_headers,
+ * *n_up (total floats). */
+int fleet_layout_from_sizes(const int32_t* w_sizes, int n_w, const int32_t* b_sizes, int n_b,
+                            int32_t* header_pos, int cap, int* n_headers, size_t* n_up);
+/* Same, parsed from an upload (Base64 host buffer) by decoding its header
+ * slots on the device, exactly as network::flatGrad walks them (:1206-1223). */
+int fleet_layout_parse(fleet_ctx* ctx, const char* upload, size_t len, int32_t* header_pos, int cap,
+                       int* n_headers, size_t* n_up);
+
+/* Codec (Base64.cpp) -- host buffers ------------------------------------- */
+/* Base64::encode(std::vector<float>) (:140-142) */
+int fleet_encode_f32(fleet_ctx* ctx, const float* values, size_t n, char* out, size_t cap, size_t* out_len);
+/* Base64::encode(std::vector<int>) (:145-151) */
+int fleet_encode_i32(fleet_ctx* ctx, const int32_t* codes, size_t n, char* out, size_t cap, size_t* out_len);
+/* Base64::decodeFloat (:207-209) */
+int fleet_decode_f32(fleet_ctx* ctx, const char* text, size_t len, float* out, size_t cap, size_t* n_out);
+/* Base64::decodeInt (:211-219) */
+int fleet_decode_i32(fleet_ctx* ctx, const char* text, size_t len, int32_t* out, size_t cap, size_t* n_out);
+
+/* Per-op JNI replacements (cppNN_backend.cpp) -- host Base64 buffers ------ */
+/* Java_apps_cppNN_CppNNUpdater_getFlatGradient (:701-720) */
+int fleet_flat_gradient(fleet_ctx* ctx, const char* g, size_t len, char* out, size_t cap, size_t* out_len);
+/* Java_apps_cppNN_CppNNUpdater_mergeFlatGradient (:722-750) */
+int fleet_merge_flat_gradient(fleet_ctx* ctx, const char* g, size_t glen, const char* flat, size_t flen,
+                              char* out, size_t cap, size_t* out_len);
+/* Java_utils_ByteVec_scalarMulNative (:753-777) */
+int fleet_scalar_mul(fleet_ctx* ctx, const char* v, size_t len, double a, char* out, size_t cap,
+                     size_t* out_len);
+/* Java_utils_ByteVec_addNative (:797-846) */
+int fleet_add(fleet_ctx* ctx, const char* a, size_t alen, const char* b, size_t blen, char* out, size_t cap,
+              size_t* out_len);
+/* Java_utils_ByteVec_subtractNative (:848-892) */
+int fleet_subtract(fleet_ctx* ctx, const char* a, size_t alen, const char* b, size_t blen, char* out,
+                   size_t cap, size_t* out_len);
+/* Java_utils_ByteVec_getNorm (:779-795): sqrt(sum_i (double)(x_i*x_i)) in index order */
+int fleet_norm(fleet_ctx* ctx, const char* v, size_t len, double* out);
+
+/* The fused update -- host buffers ---------------------------------------
+ * One call = the aggregation part of CppNNUpdater.update (CppNNUpdater.java:
+ * 420-509): for the M picked uploads in order,
+ *   pickedGrad = getFlatGradient(g_i).scalarMultiply(dampen[i]); avg += pickedGrad
+ *   merged = mergeFlatGradient(g_{M-1}, avg.scalarMultiply(1.0/M))
+ * with every intermediate re-quantised exactly as the per-op JNI chain does.
+ * All uploads must share one layout and length. `merged` receives the
+ * Base64 the reference returns; `merged_f32` (nullable, n_up floats) receives
+ * Base64::decodeFloat(merged), i.e. what descentNative decodes (:336). */
+int fleet_update(fleet_ctx* ctx, const char* const* uploads, const size_t* lens, int M, const double* dampen,
+                 char* merged, size_t cap, size_t* out_len, float* merged_f32);
+
+/* Device-resident entry points (all buffers are device pointers) ----------
+ * Uploads are stored as M rows of `pitch` bytes (pitch >= 16*ceil(len/16),
+ * multiple of 16); each row holds `len` Base64 chars. group_begin/group_end
+ * select the 16-char / 3-value groups this call processes (element-range
+ * sharding; [0, ceil(len/16)) = everything). `dampen` is a host array of M
+ * doubles. Outputs are written for the selected groups only: merged Base64
+ * at byte 16*g, merged_f32 (nullable) at value 3*g. */
+int fleet_update_device(fleet_ctx* ctx, const void* d_uploads, size_t pitch, size_t len, int M,
+                        const double* dampen, const int32_t* header_pos, int n_headers, size_t group_begin,
+                        size_t group_end, void* d_merged, void* d_merged_f32, void* stream);
+/* Client-side encode of M fp32 buckets (rows of `n` floats, `vpitch` floats
+ * apart) into Base64 rows of `pitch` bytes: Base64::encode(vector<float>) per row. */
+int fleet_encode_device(fleet_ctx* ctx, const void* d_values, size_t n, size_t vpitch, int M, void* d_out,
+                        size_t pitch, void* stream);
+/* Base64 rows -> fp32 (decodeFloat) per row. */
+int fleet_decode_device(fleet_ctx* ctx, const void* d_text, size_t len, size_t pitch, int M, void* d_values,
+                        size_t vpitch, void* stream);
+/* Deterministic synthetic gradient buckets on the device (SURVEY.md §8d value
+ * mix; Philox4x32-10 keyed by seed, counter = (element, client)), with the
+ * given layout's header values written in place. Rows of `vpitch` floats. */
+int fleet_synth_device(fleet_ctx* ctx, uint64_t seed, int M, int client0, const int32_t* header_pos,
+                       const float* header_val, int n_headers, size_t n_up, void* d_values, size_t vpitch,
+                       void* stream);
+/* Returns FLEET_ERR_BASE64 / FLEET_ERR_LAYOUT if a device call since the last
+ * check saw malformed text or a header that differs from the last upload's
+ * (synchronises the stream), and clears the flag. */
+int fleet_check(fleet_ctx* ctx, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,83 @@
+/*
+ * oracle/fleet_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference (gdamaskinos/fleet) compressed-SGD
+ * gradient codec and server-side aggregation path, used as the parity
+ * checker for the HIP path (tests/, __graft_entry__.smoke) and as the
+ * `cpu_baseline` "port" leg of bench.py. The product (fleet_amd/) never links
+ * or calls this. Parity of this restatement with the reference itself is
+ * pinned by tests/golden/ fixtures generated from oracle/_ref (the reference's
+ * own C++ compiled by oracle/Makefile) -- see tests/test_oracle_golden.py.
+ *
+ * Every function cites the reference file:line it restates.
+ */
+#ifndef FLEET_ORACLE_H
+#define FLEET_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* commonLib/cpp_utils/Base64.cpp:73-82 */
+int fo_num_digits(int32_t number);
+/* x86-64 `(int) float` (cvttss2si): INT32_MIN when |x| >= 2^31 or NaN. */
+int32_t fo_cvtt(float x);
+/* Base64.cpp:84-114, intNum == 1, precision == 9 */
+int32_t fo_float2int(float x);
+/* Base64.cpp:116-139, intNum == 1, precision == 9 */
+float fo_int2float(int32_t c);
+/* Q = int2float o float2int: what the next JNI op sees after an encode. */
+float fo_q(float x);
+
+/* Base64.cpp:160-205: bytes -> text; returns text length (4*ceil(len/3)). */
+size_t fo_b64_encode(const uint8_t* buf, size_t len, char* out);
+/* Base64.cpp:211-253: text -> bytes (pad/invalid sextets drop bytes). */
+size_t fo_b64_decode(const char* s, size_t len, uint8_t* out);
+size_t fo_b64_len(size_t n_values);
+
+/* Base64::encode(vector<float>) (:140-142) / decodeFloat (:207-209) / decodeInt (:211-219) */
+size_t fo_encode_floats(const float* v, size_t n, char* out);
+size_t fo_encode_ints(const int32_t* v, size_t n, char* out);
+size_t fo_decode_floats(const char* s, size_t len, float* out);
+size_t fo_decode_ints(const char* s, size_t len, int32_t* out);
+
+/* Per-op restatements of Server/src/main/c++/cppNN_backend.cpp (all Base64 in/out).
+ * Return the output length, or (size_t)-1 on malformed input. `out` must hold
+ * fo_b64_len(decoded values) bytes. */
+size_t fo_flat_gradient(const char* g, size_t len, char* out);                                      /* :701-720 */
+size_t fo_merge_flat_gradient(const char* g, size_t glen, const char* flat, size_t flen, char* out); /* :722-750 */
+size_t fo_scalar_mul(const char* v, size_t len, double a, char* out);                               /* :753-777 */
+double fo_norm(const char* v, size_t len);                                                          /* :779-795 */
+size_t fo_add(const char* a, size_t alen, const char* b, size_t blen, char* out);                   /* :797-846 */
+size_t fo_subtract(const char* a, size_t alen, const char* b, size_t blen, char* out);              /* :848-892 */
+
+/* CppNNUpdater.update (CppNNUpdater.java:420-509) as the per-op string chain
+ * (faithful: same op sequence and string round trips as the reference). */
+size_t fo_update_faithful(const char* const* uploads, const size_t* lens, int M, const double* dampen,
+                          char* merged);
+
+/* The same update computed element-wise (identical results), OpenMP over
+ * element groups with `threads` threads (<=0: all cores). `header_mask[i]`
+ * (N_up bytes) marks the layout slots of the upload (network.h:1038-1056).
+ * Optional merged_f32 receives decodeFloat(merged). */
+size_t fo_update_fused(const char* const* uploads, size_t len, int M, const double* dampen,
+                       const uint8_t* header_mask, char* merged, float* merged_f32, int threads);
+
+/* Layout of gradients() (network.h:1038-1056): header mask for given sizes. */
+size_t fo_layout_n_up(const int32_t* w_sizes, int n_w, const int32_t* b_sizes, int n_b);
+void fo_layout_header_mask(const int32_t* w_sizes, int n_w, const int32_t* b_sizes, int n_b, uint8_t* mask);
+
+/* Synthetic inputs: Philox4x32-10 keyed by seed, counter (element, client). */
+void fo_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+float fo_synth_value(uint64_t seed, uint32_t client, uint32_t element);
+/* Full client upload as floats: layout headers + synthetic payload. */
+void fo_synth_upload(uint64_t seed, uint32_t client, const int32_t* w_sizes, int n_w, const int32_t* b_sizes,
+                     int n_b, float* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,324 @@
+"""oracle/pyoracle.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes bindings for
+  * ``liboracle.so``         -- the clean-room C restatement (fleet_oracle.c), and
+  * ``_ref/libfleetref.so``  -- the reference's own C++ compiled by oracle/Makefile
+                                (present only where /root/reference was available at
+                                build time; absent on a box that never built it).
+
+Only tests/, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of bench.py
+import this module. The product package (fleet_amd/) never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libfleetref.so")
+REF_O2_SO = os.path.join(HERE, "_ref", "libfleetref_O2.so")
+
+_c_char_pp = C.POINTER(C.c_char_p)
+
+
+def build(force: bool = False) -> None:
+    """Compile liboracle.so (and the reference build when /root/reference exists)."""
+    if force or not os.path.exists(ORACLE_SO):
+        subprocess.check_call(["make", "-s", "liboracle.so"], cwd=HERE)
+    if os.path.isdir("/root/reference/Server") and (force or not os.path.exists(REF_SO)):
+        subprocess.check_call(["make", "-s", "ref"], cwd=HERE)
+
+
+def _u8(a):
+    return a.ctypes.data_as(C.POINTER(C.c_uint8))
+
+
+def _f32(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _i32(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+def _f64(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def b64_len(n_values: int) -> int:
+    return 4 * ((4 * n_values + 2) // 3)
+
+
+class Oracle:
+    """The C restatement (fleet_oracle.c)."""
+
+    def __init__(self, path: str = ORACLE_SO):
+        if not os.path.exists(path):
+            build()
+        L = C.CDLL(path)
+        self.lib = L
+        sz = C.c_size_t
+        L.fo_float2int.restype = C.c_int32
+        L.fo_float2int.argtypes = [C.c_float]
+        L.fo_int2float.restype = C.c_float
+        L.fo_int2float.argtypes = [C.c_int32]
+        L.fo_encode_floats.restype = sz
+        L.fo_encode_floats.argtypes = [C.c_void_p, sz, C.c_void_p]
+        L.fo_encode_ints.restype = sz
+        L.fo_encode_ints.argtypes = [C.c_void_p, sz, C.c_void_p]
+        L.fo_decode_floats.restype = sz
+        L.fo_decode_floats.argtypes = [C.c_void_p, sz, C.c_void_p]
+        L.fo_decode_ints.restype = sz
+        L.fo_decode_ints.argtypes = [C.c_void_p, sz, C.c_void_p]
+        for name in ("fo_flat_gradient",):
+            getattr(L, name).restype = sz
+            getattr(L, name).argtypes = [C.c_void_p, sz, C.c_void_p]
+        L.fo_merge_flat_gradient.restype = sz
+        L.fo_merge_flat_gradient.argtypes = [C.c_void_p, sz, C.c_void_p, sz, C.c_void_p]
+        L.fo_scalar_mul.restype = sz
+        L.fo_scalar_mul.argtypes = [C.c_void_p, sz, C.c_double, C.c_void_p]
+        L.fo_norm.restype = C.c_double
+        L.fo_norm.argtypes = [C.c_void_p, sz]
+        for name in ("fo_add", "fo_subtract"):
+            getattr(L, name).restype = sz
+            getattr(L, name).argtypes = [C.c_void_p, sz, C.c_void_p, sz, C.c_void_p]
+        L.fo_update_faithful.restype = sz
+        L.fo_update_faithful.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.fo_update_fused.restype = sz
+        L.fo_update_fused.argtypes = [C.c_void_p, sz, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_int]
+        L.fo_layout_n_up.restype = sz
+        L.fo_layout_n_up.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int]
+        L.fo_layout_header_mask.restype = None
+        L.fo_layout_header_mask.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p]
+        L.fo_synth_value.restype = C.c_float
+        L.fo_synth_value.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32]
+        L.fo_synth_upload.restype = None
+        L.fo_synth_upload.argtypes = [C.c_uint64, C.c_uint32, C.c_void_p, C.c_int, C.c_void_p, C.c_int,
+                                      C.c_void_p]
+        L.fo_philox4x32_10.restype = None
+        L.fo_philox4x32_10.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+
+    # -- scalars / vectors ------------------------------------------------
+    def float2int(self, x: np.ndarray) -> np.ndarray:
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        return np.array([self.lib.fo_float2int(float(v)) for v in x], dtype=np.int32)
+
+    def int2float(self, c: np.ndarray) -> np.ndarray:
+        c = np.ascontiguousarray(c, dtype=np.int32)
+        return np.array([self.lib.fo_int2float(int(v)) for v in c], dtype=np.float32)
+
+    def encode_floats(self, v: np.ndarray) -> bytes:
+        v = np.ascontiguousarray(v, dtype=np.float32)
+        out = np.empty(b64_len(len(v)) + 4, np.uint8)
+        n = self.lib.fo_encode_floats(v.ctypes.data, len(v), out.ctypes.data)
+        return out[:n].tobytes()
+
+    def encode_ints(self, v: np.ndarray) -> bytes:
+        v = np.ascontiguousarray(v, dtype=np.int32)
+        out = np.empty(b64_len(len(v)) + 4, np.uint8)
+        n = self.lib.fo_encode_ints(v.ctypes.data, len(v), out.ctypes.data)
+        return out[:n].tobytes()
+
+    def decode_floats(self, s: bytes) -> np.ndarray:
+        out = np.empty(len(s) // 4 * 3 + 4, np.float32)
+        n = self.lib.fo_decode_floats(s, len(s), out.ctypes.data)
+        return out[:n].copy()
+
+    def decode_ints(self, s: bytes) -> np.ndarray:
+        out = np.empty(len(s) // 4 * 3 + 4, np.int32)
+        n = self.lib.fo_decode_ints(s, len(s), out.ctypes.data)
+        return out[:n].copy()
+
+    # -- JNI ops ------------------------------------------------------------
+    def _buf(self, nbytes):
+        return np.empty(nbytes + 64, np.uint8)
+
+    def flat_gradient(self, g: bytes) -> bytes:
+        out = self._buf(len(g))
+        n = self.lib.fo_flat_gradient(g, len(g), out.ctypes.data)
+        if n == C.c_size_t(-1).value:
+            raise ValueError("malformed upload")
+        return out[:n].tobytes()
+
+    def merge_flat_gradient(self, g: bytes, flat: bytes) -> bytes:
+        out = self._buf(len(g))
+        n = self.lib.fo_merge_flat_gradient(g, len(g), flat, len(flat), out.ctypes.data)
+        if n == C.c_size_t(-1).value:
+            raise ValueError("malformed upload")
+        return out[:n].tobytes()
+
+    def scalar_mul(self, v: bytes, a: float) -> bytes:
+        out = self._buf(len(v))
+        n = self.lib.fo_scalar_mul(v, len(v), a, out.ctypes.data)
+        return out[:n].tobytes()
+
+    def add(self, a: bytes, b: bytes) -> bytes:
+        out = self._buf(len(a))
+        n = self.lib.fo_add(a, len(a), b, len(b), out.ctypes.data)
+        return out[:n].tobytes()
+
+    def subtract(self, a: bytes, b: bytes) -> bytes:
+        out = self._buf(len(a))
+        n = self.lib.fo_subtract(a, len(a), b, len(b), out.ctypes.data)
+        return out[:n].tobytes()
+
+    def norm(self, v: bytes) -> float:
+        return self.lib.fo_norm(v, len(v))
+
+    def update_faithful(self, uploads, dampen) -> bytes:
+        M = len(uploads)
+        arr = (C.c_char_p * M)(*uploads)
+        lens = np.array([len(u) for u in uploads], dtype=np.uint64)
+        d = np.ascontiguousarray(dampen, dtype=np.float64)
+        out = self._buf(max(len(u) for u in uploads))
+        n = self.lib.fo_update_faithful(C.cast(arr, C.c_void_p), lens.ctypes.data, M, d.ctypes.data,
+                                        out.ctypes.data)
+        if n == C.c_size_t(-1).value:
+            raise ValueError("malformed upload")
+        return out[:n].tobytes()
+
+    def update_fused(self, uploads, dampen, header_mask, threads: int = 0, want_f32: bool = False):
+        M = len(uploads)
+        arr = (C.c_char_p * M)(*uploads)
+        d = np.ascontiguousarray(dampen, dtype=np.float64)
+        L = len(uploads[0])
+        out = self._buf(L)
+        hm = np.ascontiguousarray(header_mask, dtype=np.uint8)
+        f32 = np.empty(len(hm), np.float32) if want_f32 else None
+        n = self.lib.fo_update_fused(C.cast(arr, C.c_void_p), L, M, d.ctypes.data, hm.ctypes.data,
+                                     out.ctypes.data, f32.ctypes.data if want_f32 else None, threads)
+        if n == C.c_size_t(-1).value:
+            raise ValueError("malformed upload")
+        return (out[:n].tobytes(), f32) if want_f32 else out[:n].tobytes()
+
+    # -- layout / synthetic ---------------------------------------------------
+    def header_mask(self, w_sizes, b_sizes) -> np.ndarray:
+        w = np.ascontiguousarray(w_sizes, dtype=np.int32)
+        b = np.ascontiguousarray(b_sizes, dtype=np.int32)
+        n = self.lib.fo_layout_n_up(w.ctypes.data, len(w), b.ctypes.data, len(b))
+        m = np.empty(n, np.uint8)
+        self.lib.fo_layout_header_mask(w.ctypes.data, len(w), b.ctypes.data, len(b), m.ctypes.data)
+        return m
+
+    def synth_upload(self, seed: int, client: int, w_sizes, b_sizes) -> np.ndarray:
+        w = np.ascontiguousarray(w_sizes, dtype=np.int32)
+        b = np.ascontiguousarray(b_sizes, dtype=np.int32)
+        n = self.lib.fo_layout_n_up(w.ctypes.data, len(w), b.ctypes.data, len(b))
+        out = np.empty(n, np.float32)
+        self.lib.fo_synth_upload(seed, client, w.ctypes.data, len(w), b.ctypes.data, len(b), out.ctypes.data)
+        return out
+
+    def philox(self, ctr, key):
+        c = np.ascontiguousarray(ctr, dtype=np.uint32)
+        k = np.ascontiguousarray(key, dtype=np.uint32)
+        o = np.empty(4, np.uint32)
+        self.lib.fo_philox4x32_10(c.ctypes.data, k.ctypes.data, o.ctypes.data)
+        return o
+
+
+class Reference:
+    """The reference's own C++ (oracle/_ref), driven through its Java_* entry points."""
+
+    def __init__(self, path: str = REF_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        L = C.CDLL(path)
+        self.lib = L
+        lng = C.c_long
+        L.ref_float2int.restype = C.c_int
+        L.ref_float2int.argtypes = [C.c_void_p, lng, C.c_void_p]
+        L.ref_int2float.restype = C.c_int
+        L.ref_int2float.argtypes = [C.c_void_p, lng, C.c_void_p]
+        for name in ("ref_encode_floats", "ref_encode_ints", "ref_decode_floats", "ref_decode_ints",
+                     "ref_flat_gradient"):
+            getattr(L, name).restype = lng
+            getattr(L, name).argtypes = [C.c_void_p, lng, C.c_void_p, lng]
+        L.ref_scalar_mul.restype = lng
+        L.ref_scalar_mul.argtypes = [C.c_void_p, lng, C.c_double, C.c_void_p, lng]
+        for name in ("ref_add", "ref_subtract", "ref_merge_flat_gradient"):
+            getattr(L, name).restype = lng
+            getattr(L, name).argtypes = [C.c_void_p, lng, C.c_void_p, lng, C.c_void_p, lng]
+        L.ref_norm.restype = C.c_double
+        L.ref_norm.argtypes = [C.c_void_p, lng]
+        L.ref_update.restype = lng
+        L.ref_update.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, lng,
+                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, lng]
+
+    def float2int(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        o = np.empty(len(x), np.int32)
+        assert self.lib.ref_float2int(x.ctypes.data, len(x), o.ctypes.data) == 0
+        return o
+
+    def int2float(self, c):
+        c = np.ascontiguousarray(c, dtype=np.int32)
+        o = np.empty(len(c), np.float32)
+        assert self.lib.ref_int2float(c.ctypes.data, len(c), o.ctypes.data) == 0
+        return o
+
+    def _call_bytes(self, fn, *args, cap):
+        out = np.empty(cap, np.uint8)
+        n = fn(*args, out.ctypes.data, cap)
+        assert 0 <= n <= cap
+        return out[:n].tobytes()
+
+    def encode_floats(self, v):
+        v = np.ascontiguousarray(v, dtype=np.float32)
+        return self._call_bytes(self.lib.ref_encode_floats, v.ctypes.data, len(v), cap=b64_len(len(v)) + 8)
+
+    def encode_ints(self, v):
+        v = np.ascontiguousarray(v, dtype=np.int32)
+        return self._call_bytes(self.lib.ref_encode_ints, v.ctypes.data, len(v), cap=b64_len(len(v)) + 8)
+
+    def decode_floats(self, s: bytes):
+        out = np.empty(len(s) // 4 * 3 + 4, np.float32)
+        n = self.lib.ref_decode_floats(s, len(s), out.ctypes.data, len(out))
+        return out[:n].copy()
+
+    def decode_ints(self, s: bytes):
+        out = np.empty(len(s) // 4 * 3 + 4, np.int32)
+        n = self.lib.ref_decode_ints(s, len(s), out.ctypes.data, len(out))
+        return out[:n].copy()
+
+    def flat_gradient(self, g: bytes) -> bytes:
+        return self._call_bytes(self.lib.ref_flat_gradient, g, len(g), cap=len(g) + 64)
+
+    def scalar_mul(self, v: bytes, a: float) -> bytes:
+        return self._call_bytes(self.lib.ref_scalar_mul, v, len(v), a, cap=len(v) + 64)
+
+    def add(self, a: bytes, b: bytes) -> bytes:
+        return self._call_bytes(self.lib.ref_add, a, len(a), b, len(b), cap=len(a) + 64)
+
+    def subtract(self, a: bytes, b: bytes) -> bytes:
+        return self._call_bytes(self.lib.ref_subtract, a, len(a), b, len(b), cap=len(a) + 64)
+
+    def merge_flat_gradient(self, g: bytes, flat: bytes) -> bytes:
+        return self._call_bytes(self.lib.ref_merge_flat_gradient, g, len(g), flat, len(flat), cap=len(g) + 64)
+
+    def norm(self, v: bytes) -> float:
+        return self.lib.ref_norm(v, len(v))
+
+    def update(self, uploads, dampen, intermediates: bool = False):
+        M = len(uploads)
+        arr = (C.c_char_p * M)(*uploads)
+        lens = np.array([len(u) for u in uploads], dtype=np.int64)
+        d = np.ascontiguousarray(dampen, dtype=np.float64)
+        cap = max(len(u) for u in uploads) + 64
+        out = np.empty(cap, np.uint8)
+        inter = None
+        ptrs = [None, None, None, None]
+        if intermediates:
+            inter = [np.zeros((M, cap), np.uint8), np.zeros((M, cap), np.uint8), np.zeros((M, cap), np.uint8),
+                     np.zeros((1, cap), np.uint8)]
+            ptrs = [a.ctypes.data for a in inter]
+        n = self.lib.ref_update(C.cast(arr, C.c_void_p), lens.ctypes.data, M, d.ctypes.data, out.ctypes.data,
+                                cap, ptrs[0], ptrs[1], ptrs[2], ptrs[3], cap)
+        assert 0 <= n <= cap
+        if not intermediates:
+            return out[:n].tobytes()
+        return out[:n].tobytes(), inter

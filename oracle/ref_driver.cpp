@@ -1,0 +1,202 @@
+/*
+ * oracle/ref_driver.cpp -- TEST INFRASTRUCTURE ONLY (oracle harness).
+ *
+ * Drives the reference's OWN native code, compiled by path from
+ * /root/reference (see oracle/Makefile), through its real JNI entry points,
+ * and exposes a flat C API for ctypes (tests/golden/make_golden.py) and for the
+ * `cpu_baseline` leg of bench.py.  Nothing in fleet_amd/ links or loads this.
+ *
+ * What is restated here (Java is not available in this image):
+ *   ref_update() replays the call sequence of CppNNUpdater.update
+ *   (Server/src/main/java/apps/cppNN/CppNNUpdater.java:420-509) with the
+ *   pruning thresholds at 0 and the Kardam decision bypassed (`if (true || ...)`
+ *   at :488), i.e.
+ *       pickedGrad = ByteVec(getFlatGradient(g_i)).scalarMultiply(d_i)   (:463-464)
+ *       avg = avg == null ? pickedGrad : avg.add(pickedGrad)              (:490-493)
+ *       avg = avg.scalarMultiply((double) 1/avgSize)                       (:507)
+ *       merged = mergeFlatGradient(pickedG_last, avg.v)                    (:508)
+ *   The dampening factors d_i (CppNNUpdater.getDampen :300-327) are inputs.
+ * Everything else is the reference's compiled C++ (Base64.cpp, cppNN_backend.cpp,
+ * network.h).
+ */
+#include <jni.h>
+
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstring>
+#include <iostream>
+#include <string>
+#include <vector>
+
+#include "Base64.h"
+
+extern "C" {
+jbyteArray Java_apps_cppNN_CppNNUpdater_getFlatGradient(JNIEnv*, jobject, jbyteArray);
+jbyteArray Java_apps_cppNN_CppNNUpdater_mergeFlatGradient(JNIEnv*, jobject, jbyteArray, jbyteArray);
+jbyteArray Java_utils_ByteVec_scalarMulNative(JNIEnv*, jobject, jbyteArray, jdouble);
+jbyteArray Java_utils_ByteVec_addNative(JNIEnv*, jobject, jbyteArray, jbyteArray);
+jbyteArray Java_utils_ByteVec_subtractNative(JNIEnv*, jobject, jbyteArray, jbyteArray);
+double Java_utils_ByteVec_getNorm(JNIEnv*, jobject, jbyteArray);
+}
+
+namespace {
+JNIEnv g_env;
+_jobject g_this;
+
+struct Quiet {  // the reference printf()s debug lines on every op; silence fd 1
+  int saved = -1;
+  Quiet() {
+    fflush(stdout);
+    std::cout.flush();
+    saved = dup(1);
+    int devnull = open("/dev/null", O_WRONLY);
+    dup2(devnull, 1);
+    close(devnull);
+  }
+  ~Quiet() {
+    fflush(stdout);
+    std::cout.flush();
+    dup2(saved, 1);
+    close(saved);
+  }
+};
+
+jbyteArray mk(const char* p, long n) {
+  jbyteArray a = g_env.NewByteArray((jsize)n);
+  g_env.SetByteArrayRegion(a, 0, (jsize)n, (const jbyte*)p);
+  return a;
+}
+long take(jbyteArray a, char* out, long cap) {
+  long n = g_env.GetArrayLength(a);
+  if (out && n <= cap) std::memcpy(out, fakejni::payload(a), (size_t)n);
+  std::free(a);
+  return n;
+}
+long put_string(const std::string& s, char* out, long cap) {
+  long n = (long)s.size();
+  if (out && n <= cap) std::memcpy(out, s.data(), (size_t)n);
+  return n;
+}
+}  // namespace
+
+extern "C" {
+
+/* Base64::float2int via the public surface: decodeInt(encode(vector<float>)). */
+int ref_float2int(const float* v, long n, int32_t* out) {
+  std::vector<float> in(v, v + n);
+  std::vector<int> codes = Base64::decodeInt(Base64::encode(in));
+  if ((long)codes.size() != n) return -1;
+  std::memcpy(out, codes.data(), sizeof(int32_t) * n);
+  return 0;
+}
+
+/* Base64::int2float via decodeFloat(encode(vector<int>)). */
+int ref_int2float(const int32_t* c, long n, float* out) {
+  std::vector<int> in(c, c + n);
+  std::vector<float> vals = Base64::decodeFloat(Base64::encode(in));
+  if ((long)vals.size() != n) return -1;
+  std::memcpy(out, vals.data(), sizeof(float) * n);
+  return 0;
+}
+
+long ref_encode_floats(const float* v, long n, char* out, long cap) {
+  return put_string(Base64::encode(std::vector<float>(v, v + n)), out, cap);
+}
+long ref_encode_ints(const int32_t* v, long n, char* out, long cap) {
+  return put_string(Base64::encode(std::vector<int>(v, v + n)), out, cap);
+}
+long ref_decode_floats(const char* s, long len, float* out, long cap) {
+  std::vector<float> r = Base64::decodeFloat(std::string(s, (size_t)len));
+  if (out && (long)r.size() <= cap) std::memcpy(out, r.data(), sizeof(float) * r.size());
+  return (long)r.size();
+}
+long ref_decode_ints(const char* s, long len, int32_t* out, long cap) {
+  std::vector<int> r = Base64::decodeInt(std::string(s, (size_t)len));
+  if (out && (long)r.size() <= cap) std::memcpy(out, r.data(), sizeof(int32_t) * r.size());
+  return (long)r.size();
+}
+
+/* cppNN_backend.cpp:701-720 */
+long ref_flat_gradient(const char* g, long len, char* out, long cap) {
+  Quiet q;
+  return take(Java_apps_cppNN_CppNNUpdater_getFlatGradient(&g_env, &g_this, mk(g, len)), out, cap);
+}
+/* cppNN_backend.cpp:753-777 */
+long ref_scalar_mul(const char* v, long len, double a, char* out, long cap) {
+  Quiet q;
+  return take(Java_utils_ByteVec_scalarMulNative(&g_env, &g_this, mk(v, len), a), out, cap);
+}
+/* cppNN_backend.cpp:797-846 */
+long ref_add(const char* a, long alen, const char* b, long blen, char* out, long cap) {
+  Quiet q;
+  return take(Java_utils_ByteVec_addNative(&g_env, &g_this, mk(a, alen), mk(b, blen)), out, cap);
+}
+/* cppNN_backend.cpp:848-892 */
+long ref_subtract(const char* a, long alen, const char* b, long blen, char* out, long cap) {
+  Quiet q;
+  return take(Java_utils_ByteVec_subtractNative(&g_env, &g_this, mk(a, alen), mk(b, blen)), out, cap);
+}
+/* cppNN_backend.cpp:779-795 */
+double ref_norm(const char* v, long len) {
+  Quiet q;
+  return Java_utils_ByteVec_getNorm(&g_env, &g_this, mk(v, len));
+}
+/* cppNN_backend.cpp:722-750 */
+long ref_merge_flat_gradient(const char* g, long glen, const char* flat, long flen, char* out, long cap) {
+  Quiet q;
+  return take(Java_apps_cppNN_CppNNUpdater_mergeFlatGradient(&g_env, &g_this, mk(g, glen), mk(flat, flen)),
+              out, cap);
+}
+
+/*
+ * Replay of CppNNUpdater.update (:420-509), see header comment.
+ * Optional intermediates (each may be NULL): for client i, flat_i (after
+ * getFlatGradient), damp_i (after scalarMultiply), acc_i (avg after client i);
+ * avg_scaled; every one written at stride `istride` bytes.
+ */
+long ref_update(const char* const* uploads, const long* lens, int M, const double* dampen, char* merged,
+                long cap, char* flat_out, char* damp_out, char* acc_out, char* avg_out, long istride) {
+  if (M <= 0) return -1;
+  Quiet q;
+  jbyteArray avg = nullptr;
+  int avgSize = 0;
+  for (int i = 0; i < M; ++i) {
+    jbyteArray g = mk(uploads[i], lens[i]);
+    jbyteArray flat = Java_apps_cppNN_CppNNUpdater_getFlatGradient(&g_env, &g_this, g);
+    std::free(g);
+    jbyteArray damp = Java_utils_ByteVec_scalarMulNative(&g_env, &g_this, flat, dampen[i]);
+    if (flat_out) take(flat, flat_out + (long)i * istride, istride); else std::free(flat);
+    if (damp_out) {
+      long n = g_env.GetArrayLength(damp);
+      if (n <= istride) std::memcpy(damp_out + (long)i * istride, fakejni::payload(damp), n);
+    }
+    if (avg == nullptr) {
+      avg = damp;
+    } else {
+      jbyteArray s = Java_utils_ByteVec_addNative(&g_env, &g_this, avg, damp);
+      std::free(avg);
+      std::free(damp);
+      avg = s;
+    }
+    avgSize++;
+    if (acc_out) {
+      long n = g_env.GetArrayLength(avg);
+      if (n <= istride) std::memcpy(acc_out + (long)i * istride, fakejni::payload(avg), n);
+    }
+  }
+  jbyteArray scaled = Java_utils_ByteVec_scalarMulNative(&g_env, &g_this, avg, (double)1 / avgSize);
+  std::free(avg);
+  if (avg_out) {
+    long n = g_env.GetArrayLength(scaled);
+    if (n <= istride) std::memcpy(avg_out, fakejni::payload(scaled), n);
+  }
+  jbyteArray last = mk(uploads[M - 1], lens[M - 1]);
+  jbyteArray out = Java_apps_cppNN_CppNNUpdater_mergeFlatGradient(&g_env, &g_this, last, scaled);
+  std::free(last);
+  std::free(scaled);
+  return take(out, merged, cap);
+}
+
+}  // extern "C"

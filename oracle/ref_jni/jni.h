@@ -1,0 +1,89 @@
+/*
+ * oracle/ref_jni/jni.h -- TEST INFRASTRUCTURE ONLY (oracle harness).
+ *
+ * A minimal stand-in for the JNI surface that the reference's native server
+ * backend touches (/root/reference/Server/src/main/c++/cppNN_backend.cpp), so
+ * that file can be compiled unmodified, by path, into oracle/_ref/ and driven
+ * through its real Java_* entry points from oracle/ref_driver.cpp.
+ *
+ * Used surface (grep env-> in cppNN_backend.cpp): GetArrayLength,
+ * Get/ReleaseByteArrayElements, NewByteArray, SetByteArrayRegion,
+ * GetDoubleArrayElements, Get/ReleaseStringUTFChars, DeleteLocalRef.
+ *
+ * Arrays are heap blocks {len, payload}. GetByteArrayElements hands out a
+ * NUL-terminated copy: the reference reads JVM arrays as C strings
+ * (`std::string encoded = (char*)buffer`), which over-reads a real JVM
+ * array; the terminator makes that read well defined here.
+ */
+#ifndef FLEET_ORACLE_FAKE_JNI_H
+#define FLEET_ORACLE_FAKE_JNI_H
+
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+
+#define JNIEXPORT __attribute__((visibility("default")))
+#define JNICALL
+
+typedef int8_t jbyte;
+typedef int32_t jint;
+typedef int32_t jsize;
+typedef int64_t jlong;
+typedef double jdouble;
+typedef float jfloat;
+typedef uint8_t jboolean;
+
+struct _jobject {};
+typedef _jobject* jobject;
+
+struct fake_jarray_hdr {
+  jsize len;
+  jsize elem;
+};
+
+struct _jbyteArray : _jobject {};
+struct _jdoubleArray : _jobject {};
+struct _jstring : _jobject {};
+typedef _jbyteArray* jbyteArray;
+typedef _jdoubleArray* jdoubleArray;
+typedef _jstring* jstring;
+typedef _jobject* jarray;
+
+namespace fakejni {
+inline fake_jarray_hdr* hdr(const void* a) { return (fake_jarray_hdr*)a; }
+inline char* payload(const void* a) { return (char*)a + sizeof(fake_jarray_hdr); }
+inline void* alloc(jsize len, jsize elem) {
+  char* p = (char*)std::calloc(1, sizeof(fake_jarray_hdr) + (size_t)len * elem + 1);
+  hdr(p)->len = len;
+  hdr(p)->elem = elem;
+  return p;
+}
+}  // namespace fakejni
+
+struct JNIEnv {
+  jsize GetArrayLength(const void* a) { return fakejni::hdr(a)->len; }
+
+  jbyte* GetByteArrayElements(jbyteArray a, jboolean*) {
+    jsize n = fakejni::hdr(a)->len;
+    jbyte* c = (jbyte*)std::malloc((size_t)n + 1);
+    std::memcpy(c, fakejni::payload(a), (size_t)n);
+    c[n] = 0;
+    return c;
+  }
+  void ReleaseByteArrayElements(jbyteArray a, jbyte* c, jint mode) {
+    if (mode == 0) std::memcpy(fakejni::payload(a), c, (size_t)fakejni::hdr(a)->len);
+    std::free(c);
+  }
+  jbyteArray NewByteArray(jsize n) { return (jbyteArray)fakejni::alloc(n, 1); }
+  void SetByteArrayRegion(jbyteArray a, jsize start, jsize n, const jbyte* src) {
+    std::memcpy(fakejni::payload(a) + start, src, (size_t)n);
+  }
+  jdouble* GetDoubleArrayElements(jdoubleArray a, jboolean*) {
+    return (jdouble*)fakejni::payload(a);
+  }
+  const char* GetStringUTFChars(jstring s, jboolean*) { return fakejni::payload(s); }
+  void ReleaseStringUTFChars(jstring, const char*) {}
+  void DeleteLocalRef(void*) {}
+};
+
+#endif

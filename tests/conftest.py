@@ -1,0 +1,43 @@
+"""Shared test setup.
+
+Markers: ``gpu`` -- needs an MI355X (runs the HIP path through the C-ABI).
+Tests without the marker run on CPU: oracle vs golden vectors, host logic,
+library/symbol checks and gloo multi-process tests.
+"""
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: requires an AMD Instinct MI355X (gfx950) GPU")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import pyoracle
+    pyoracle.build()
+    return pyoracle.Oracle()
+
+
+@pytest.fixture(scope="session")
+def reference():
+    import pyoracle
+    if not os.path.exists(pyoracle.REF_SO):
+        if os.path.isdir("/root/reference/Server"):
+            pyoracle.build()
+        else:
+            pytest.skip("reference build (oracle/_ref) not available on this machine")
+    return pyoracle.Reference()
+
+
+@pytest.fixture(scope="session")
+def codec():
+    import fleet_amd
+    fleet_amd.build_if_needed = None
+    return fleet_amd.Codec(0)

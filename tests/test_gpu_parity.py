@@ -1,0 +1,182 @@
+"""HIP path vs the oracle (bit-exact), through the C-ABI (libfleetcodec.so).
+
+The oracle is the C restatement in oracle/ (itself pinned to the reference's
+own compiled C++ by tests/test_oracle_golden.py). Every comparison of Base64
+output is byte-for-byte; decoded floats are compared bitwise. getNorm is the
+one floating-point reduction: the reference sums in index order in fp64, the
+GPU in a tree, so it is checked to 1e-12 relative (documented in DESIGN.md).
+"""
+import math
+
+import numpy as np
+import pytest
+
+import fleet_amd as F
+from fleet_amd.layouts import CIFAR10, MNIST, Layout, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def edge_floats():
+    v = [0.0, -0.0, 1.0, -1.0, 9.99, -9.99, 10.0, -10.0, 1e-9, -1e-9, 9.99999e8, -9.99999e8, 1e-45, -1e-45,
+         0.5, 0.05, 123456.789, -123456.789, 0.0168, 99999999.0, 1e8, -1e8, 999999999.0, 1e9, 2.1e9, -2.1e9,
+         3e9, -3e9, float("inf"), float("-inf"), float("nan"), 1.17549435e-38, 3.4e38]
+    return np.array(v, dtype=np.float32)
+
+
+def random_floats(rng, n):
+    parts = [rng.normal(0, 1e-3, n), rng.normal(0, 1, n), rng.uniform(-1e8, 1e8, n // 4),
+             np.exp(rng.uniform(-40, 20, n)) * rng.choice([-1, 1], n)]
+    return np.concatenate(parts).astype(np.float32)
+
+
+def uploads_for(oracle, layout: Layout, M: int, seed: int):
+    return [oracle.encode_floats(oracle.synth_upload(seed, c, list(layout.w_sizes), list(layout.b_sizes)))
+            for c in range(M)]
+
+
+def test_encode_floats_bitexact(codec, oracle):
+    rng = np.random.default_rng(1)
+    for v in (edge_floats(), random_floats(rng, 20000), random_floats(rng, 7)[:7], np.zeros(0, np.float32)):
+        assert codec.encode_floats(v) == oracle.encode_floats(v)
+
+
+def test_decode_bitexact(codec, oracle):
+    rng = np.random.default_rng(2)
+    codes = np.concatenate([rng.integers(-2**31, 2**31, 30001), np.arange(-30, 30),
+                            [2**31 - 1, -2**31, 10, -10, 1000000000, -1000000000]]).astype(np.int32)
+    for n in (len(codes), 1, 2, 3, 4, 5):
+        text = oracle.encode_ints(codes[:n])
+        assert codec.decode_ints(text).tolist() == oracle.decode_ints(text).tolist()
+        got = codec.decode_floats(text)
+        exp = oracle.decode_floats(text)
+        assert np.array_equal(got.view(np.uint32), exp.view(np.uint32))
+    assert codec.encode_ints(codes) == oracle.encode_ints(codes)
+
+
+def test_url_safe_alphabet_accepted(codec, oracle):
+    v = np.arange(-3000, 3000, dtype=np.int32) * 7919
+    t = oracle.encode_ints(v)
+    u = t.replace(b"+", b"-").replace(b"/", b"_")
+    assert codec.decode_ints(u).tolist() == oracle.decode_ints(u).tolist() == v.tolist()
+
+
+def test_invalid_base64_rejected(codec):
+    good = codec.encode_floats(np.ones(30, np.float32))
+    for bad in (good[:-1], good[:8] + b"*" + good[9:], good[:20] + b"=" + good[21:]):
+        with pytest.raises(F.Base64Error):
+            codec.decode_floats(bad)
+
+
+def test_elementwise_ops_bitexact(codec, oracle):
+    rng = np.random.default_rng(3)
+    for n in (3000, 3001, 3002, 159):
+        a = oracle.encode_floats(random_floats(rng, n)[:n])
+        b = oracle.encode_floats(random_floats(rng, n)[:n])
+        for s in (0.5, 1 / 3, 1.0, math.exp(-0.7), 7.25):
+            assert codec.scalarMulNative(a, s) == oracle.scalar_mul(a, s)
+        assert codec.addNative(a, b) == oracle.add(a, b)
+        assert codec.subtractNative(a, b) == oracle.subtract(a, b)
+        ref = oracle.norm(a)
+        assert abs(codec.getNorm(a) - ref) <= 1e-12 * abs(ref)
+
+
+@pytest.mark.parametrize("layout", [MNIST, synthetic(1000), synthetic(1001), synthetic(1002)])
+def test_flat_and_merge_bitexact(codec, oracle, layout):
+    ups = uploads_for(oracle, layout, 2, seed=11)
+    flat = oracle.flat_gradient(ups[0])
+    assert codec.getFlatGradient(ups[0]) == flat
+    other = oracle.flat_gradient(ups[1])
+    assert codec.mergeFlatGradient(ups[0], other) == oracle.merge_flat_gradient(ups[0], other)
+    pos, n_up = codec.layout_parse(ups[0])
+    assert n_up == layout.n_up and pos.tolist() == layout.header_positions()
+
+
+def policy(name, M):
+    if name == "avg":
+        return [1.0] * M
+    if name == "inverse":
+        return [1 / ((c % 3) + 1) for c in range(M)]
+    if name == "exp":
+        return [math.exp(-0.5 * min(c, 4)) for c in range(M)]
+    raise KeyError(name)
+
+
+@pytest.mark.parametrize("M", [1, 2, 8])
+@pytest.mark.parametrize("pol", ["avg", "inverse", "exp"])
+def test_update_mnist_vs_faithful_chain(codec, oracle, M, pol):
+    ups = uploads_for(oracle, MNIST, M, seed=100 + M)
+    d = policy(pol, M)
+    merged, f32 = codec.update(ups, d, want_f32=True)
+    exp = oracle.update_faithful(ups, d)
+    assert merged == exp
+    assert np.array_equal(f32.view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
+
+
+@pytest.mark.parametrize("layout,M", [(MNIST, 64), (CIFAR10, 16), (synthetic(100000), 9), (synthetic(99998), 5)])
+def test_update_vs_elementwise_oracle(codec, oracle, layout, M):
+    ups = uploads_for(oracle, layout, M, seed=7)
+    d = policy("inverse", M)
+    hm = oracle.header_mask(list(layout.w_sizes), list(layout.b_sizes))
+    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
+
+
+def test_update_layout_mismatch_rejected(codec, oracle):
+    a = uploads_for(oracle, synthetic(3000), 2, seed=3)
+    b = uploads_for(oracle, Layout("x", (1000, 1996), ()), 1, seed=3)
+    assert len(a[0]) == len(b[0])
+    with pytest.raises(F.LayoutError):
+        codec.update([a[0], b[0], a[1]], [1.0, 1.0, 1.0])
+
+
+def test_device_resident_update_sharded(codec, oracle):
+    torch = pytest.importorskip("torch")
+    lay = synthetic(30001)
+    M = 6
+    ups = uploads_for(oracle, lay, M, seed=5)
+    L = len(ups[0])
+    pitch = (L + 15) // 16 * 16
+    host = np.zeros((M, pitch), np.uint8)
+    for i, u in enumerate(ups):
+        host[i, :L] = np.frombuffer(u, np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    groups = (F.b64_count(L) + 2) // 3
+    out = torch.zeros(16 * groups, dtype=torch.uint8, device="cuda")
+    f32 = torch.zeros(3 * groups, dtype=torch.float32, device="cuda")
+    d = policy("inverse", M)
+    hp = lay.header_positions()
+    half = groups // 2
+    codec.update_device(dev, L, d, hp, out, f32, 0, half)
+    codec.update_device(dev, L, d, hp, out, f32, half, groups)
+    codec.check()
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()[:L].tobytes()
+    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+    exp = oracle.update_fused(ups, d, hm)
+    assert got == exp
+    assert np.array_equal(f32.cpu().numpy()[: lay.n_up].view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
+
+
+def test_device_synth_and_encode(codec, oracle):
+    torch = pytest.importorskip("torch")
+    lay = synthetic(20002)
+    M = 3
+    vals = torch.zeros((M, lay.n_up + 5), dtype=torch.float32, device="cuda")
+    codec.synth_device(1234, vals, lay.n_up, lay.header_positions(), lay.header_values())
+    host = vals.cpu().numpy()
+    for c in range(M):
+        exp = oracle.synth_upload(1234, c, list(lay.w_sizes), list(lay.b_sizes))
+        assert np.array_equal(host[c, : lay.n_up].view(np.uint32), exp.view(np.uint32))
+    L = F.b64_len(lay.n_up)
+    pitch = (L + 15) // 16 * 16
+    text = torch.zeros((M, pitch), dtype=torch.uint8, device="cuda")
+    codec.encode_device(vals, lay.n_up, text)
+    back = torch.zeros((M, lay.n_up + 5), dtype=torch.float32, device="cuda")
+    codec.decode_device(text, L, back)
+    codec.check()
+    t = text.cpu().numpy()
+    b = back.cpu().numpy()
+    for c in range(M):
+        exp = oracle.encode_floats(host[c, : lay.n_up])
+        assert t[c, :L].tobytes() == exp
+        assert np.array_equal(b[c, : lay.n_up].view(np.uint32), oracle.decode_floats(exp).view(np.uint32))

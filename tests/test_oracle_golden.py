@@ -1,0 +1,105 @@
+"""Pin the oracle (oracle/fleet_oracle.c, the C restatement) to the reference.
+
+1. Against the committed golden fixtures in tests/golden/ -- outputs of the
+   reference's own C++ (Base64.cpp + Server cppNN_backend.cpp compiled
+   unmodified, driven through its Java_* natives; tests/golden/make_golden.py).
+2. Live against that reference build (oracle/_ref) on fresh random inputs,
+   when it is present on this machine.
+CPU only.
+"""
+import glob
+import hashlib
+import math
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _text(a, n=None):
+    a = np.asarray(a, np.uint8)
+    return (a if n is None else a[:n]).tobytes().rstrip(b"\0")
+
+
+def test_codec_scalars_match_golden(oracle):
+    g = np.load(os.path.join(GOLDEN, "codec.npz"))
+    assert np.array_equal(oracle.float2int(g["f_in"]), g["f_codes"])
+    got = oracle.int2float(g["c_in"])
+    assert np.array_equal(got.view(np.uint32), g["c_vals"].view(np.uint32))
+    # Q(Q(x)) != Q(x) is part of the reference's behaviour
+    q1 = oracle.int2float(g["f_codes"])
+    assert np.array_equal(oracle.float2int(q1), g["f_codes2"])
+    assert (g["f_codes2"] != g["f_codes"]).mean() > 0.01
+
+
+def test_codec_text_matches_golden(oracle):
+    g = np.load(os.path.join(GOLDEN, "codec.npz"))
+    assert oracle.encode_ints(g["c_in"][:1001]) == g["text_ints"].tobytes()
+    assert oracle.encode_floats(g["f_in"][:1000]) == g["text_floats"].tobytes()
+    assert np.array_equal(oracle.decode_ints(g["text_ints"].tobytes()), g["c_in"][:1001])
+
+
+def test_known_answers():
+    """Values quoted in SURVEY.md §8c, measured on the reference."""
+    import pyoracle
+    o = pyoracle.Oracle()
+    assert o.lib.fo_float2int(1.0) == 100000001
+    assert o.lib.fo_float2int(-1.0) == -10000002
+    assert o.lib.fo_float2int(10.0) == 100000002
+    assert np.float32(o.lib.fo_int2float(-10000002)) == np.float32(-1.00000024)
+    q = o.int2float(o.float2int(np.array([1e-6], np.float32)))
+    assert q[0] == np.float32(9.9e-7)
+
+
+def test_ops_match_golden(oracle):
+    g = np.load(os.path.join(GOLDEN, "ops.npz"))
+    for n in (300, 301, 302):
+        a, b = g[f"a{n}"].tobytes(), g[f"b{n}"].tobytes()
+        for i, s in enumerate(g["scales"]):
+            assert oracle.scalar_mul(a, float(s)) == g[f"mul{n}_{i}"].tobytes()
+        assert oracle.add(a, b) == g[f"add{n}"].tobytes()
+        assert oracle.subtract(a, b) == g[f"sub{n}"].tobytes()
+        assert oracle.norm(a) == float(g[f"norm{n}"][0])
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "chain_*.npz"))), ids=os.path.basename)
+def test_update_chain_matches_golden(oracle, path):
+    g = np.load(path)
+    w, b, M, seed = list(g["w_sizes"]), list(g["b_sizes"]), int(g["M"]), int(g["seed"])
+    ups = [oracle.encode_floats(oracle.synth_upload(seed, c, w, b)) for c in range(M)]
+    # the generator is pinned too
+    assert [hashlib.sha256(u).hexdigest() for u in ups] == [str(h) for h in g["uploads_sha256"]]
+    d = list(g["dampen"])
+    merged = g["merged"].tobytes()
+    assert oracle.update_faithful(ups, d) == merged
+    hm = oracle.header_mask(w, b)
+    assert oracle.update_fused(ups, d, hm, threads=2) == merged
+    if "flat" in g.files:  # per-op intermediates of the reference chain
+        for i in range(M):
+            flat = oracle.flat_gradient(ups[i])
+            assert flat == _text(g["flat"][i], len(flat))
+            damp = oracle.scalar_mul(flat, d[i])
+            assert damp == _text(g["damp"][i], len(flat))
+        acc = oracle.scalar_mul(oracle.flat_gradient(ups[0]), d[0])
+        assert acc == _text(g["acc"][0], len(acc))
+        for i in range(1, M):
+            acc = oracle.add(acc, oracle.scalar_mul(oracle.flat_gradient(ups[i]), d[i]))
+            assert acc == _text(g["acc"][i], len(acc))
+        avg = oracle.scalar_mul(acc, 1.0 / M)
+        assert avg == _text(g["avg"][0], len(avg))
+
+
+def test_oracle_vs_live_reference(oracle, reference):
+    rng = np.random.default_rng(12345)
+    x = np.concatenate([rng.normal(0, 1e-3, 5000), rng.normal(0, 3, 5000),
+                        np.exp(rng.uniform(-45, 21, 5000)) * rng.choice([-1, 1], 5000)]).astype(np.float32)
+    assert np.array_equal(oracle.float2int(x), reference.float2int(x))
+    c = rng.integers(-2**31, 2**31, 20000).astype(np.int32)
+    assert np.array_equal(oracle.int2float(c).view(np.uint32), reference.int2float(c).view(np.uint32))
+    w, b = [300, 0, 50], [200, 7]
+    ups = [oracle.encode_floats(oracle.synth_upload(99, k, w, b)) for k in range(5)]
+    d = [math.exp(-0.3 * k) for k in range(5)]
+    assert oracle.update_faithful(ups, d) == reference.update(ups, d)
+    assert oracle.norm(ups[0]) == reference.norm(ups[0])
