@@ -99,6 +99,7 @@ def lib() -> C.CDLL:
         "fleet_encode_device": (i32, [vp, vp, sz, sz, i32, vp, sz, vp]),
         "fleet_decode_device": (i32, [vp, vp, sz, sz, i32, vp, sz, vp]),
         "fleet_synth_device": (i32, [vp, C.c_uint64, i32, i32, vp, vp, i32, sz, vp, sz, vp]),
+        "fleet_selftest_digest": (i32, [vp, i32, C.POINTER(C.c_uint64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -343,6 +344,12 @@ class Codec:
         rc = self._L.fleet_synth_device(self._h, seed, M, client0, hp.ctypes.data, hv.ctypes.data, len(hp), n_up,
                                         values_f32.data_ptr(), vpitch, _stream(stream))
         self._check(rc)
+
+    def selftest_digest(self, fn: int) -> int:
+        """Digest of the device codec arithmetic over a whole input domain (fleet_codec.h)."""
+        out = C.c_uint64(0)
+        self._check(self._L.fleet_selftest_digest(self._h, fn, C.byref(out)))
+        return out.value
 
     def check(self, stream=None):
         self._check(self._L.fleet_check(self._h, _stream(stream)))

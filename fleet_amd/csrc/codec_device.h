@@ -1,85 +1,15 @@
-// fleet_amd/csrc/codec_device.h -- device-side FLeet codec arithmetic for gfx950.
-//
-// Bit-exact restatement, for CDNA4 VALU, of
-//   Base64::numDigits / float2int / int2float  (commonLib/cpp_utils/Base64.cpp:73-139)
-//   Base64 text <-> bytes                     (Base64.cpp:56-68,160-205,221-253)
-// as the reference's x86-64 SSE build computes them (one IEEE binary32 RNE
-// rounding per operation, cvttss2si truncation). Built with
-// -ffp-contract=off: every fused multiply-add below is written explicitly.
+// fleet_amd/csrc/codec_device.h -- device-side FLeet codec pieces for gfx950:
+//   decimal fixed-point arithmetic (codec_math.h, Base64.cpp:73-139)
+//   Base64 text <-> bytes           (Base64.cpp:56-68,160-205,221-253)
+//   Philox synthetic gradient source
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "codec_math.h"
+
 namespace fleet {
-
-// RN(0.1) and RN(0.1 - RN(0.1)): t*0.1 as an unevaluated pair.
-constexpr float kTenthHi = 0x1.99999ap-4f;
-constexpr float kTenthLo = -0x1.99999ap-30f;
-
-// Correctly rounded t/10 in two VALU ops (v_mul_f32 + v_fma_f32): the exact
-// t*hi plus RN(t*lo) lies within 2^-49 (relative) of t/10, while t/10 is
-// never closer than 2^-27.3 to a binary32 rounding midpoint (t has a 24-bit
-// significand, so 10*midpoint - t is an odd multiple of the finer ulp).
-// Exhaustively checked against IEEE division for every binary32 t with
-// |t| >= 1e-30 (tests/test_div10.py); int2float never divides anything
-// smaller than 1e-9 in magnitude.
-__device__ __forceinline__ float div10(float t) { return __builtin_fmaf(t, kTenthHi, t * kTenthLo); }
-
-// x86-64 `(int)x` (cvttss2si): INT_MIN when |x| >= 2^31 or x is NaN
-// (v_cvt_i32_f32 would saturate instead).
-__device__ __forceinline__ int32_t cvtt(float x) {
-  return __builtin_fabsf(x) < 2147483648.0f ? (int32_t)x : INT32_MIN;
-}
-
-// Base64::numDigits (Base64.cpp:73-82): decimal digits of n, '-' counted.
-__device__ __forceinline__ int num_digits(int32_t n) {
-  uint32_t a = n < 0 ? 0u - (uint32_t)n : (uint32_t)n;
-  int d = n < 0;
-  d += a >= 1u;
-  d += a >= 10u;
-  d += a >= 100u;
-  d += a >= 1000u;
-  d += a >= 10000u;
-  d += a >= 100000u;
-  d += a >= 1000000u;
-  d += a >= 10000000u;
-  d += a >= 100000000u;
-  d += a >= 1000000000u;
-  return d;
-}
-
-// Base64::int2float, intNum = 1, precision = 9 (Base64.cpp:127-134):
-// k = 9 - |c % 10| fp32 divisions by 10 of (float)c.
-__device__ __forceinline__ float dec(int32_t c) {
-  int dd = c % 10;
-  dd = dd < 0 ? -dd : dd;
-  float t = (float)c;
-#pragma unroll
-  for (int j = 0; j < 9; ++j) {
-    float q = div10(t);
-    t = (j + dd < 9) ? q : t;
-  }
-  return t;
-}
-
-// Base64::float2int, intNum = 1, precision = 9 (Base64.cpp:96-109).
-__device__ __forceinline__ int32_t enc(float x) {
-  int d = num_digits(cvtt(x));
-#pragma unroll
-  for (int j = 0; j < 9; ++j) {
-    float w = x * 10.0f;
-    x = (j + d < 9) ? w : x;
-  }
-  int32_t t = cvtt(x);
-  int32_t lsb = t % 10;
-  uint32_t u = (uint32_t)t - (uint32_t)lsb;
-  u = t >= 0 ? u + (uint32_t)d : u - (uint32_t)d;
-  return (int32_t)u;
-}
-
-// Q = int2float o float2int: the value the next JNI op decodes after an encode.
-__device__ __forceinline__ float q(float x) { return dec(enc(x)); }
 
 // ------------------------------------------------------------------ Base64
 

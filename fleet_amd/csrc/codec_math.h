@@ -1,0 +1,150 @@
+// fleet_amd/csrc/codec_math.h -- the FLeet decimal fixed-point codec arithmetic,
+// host+device (the host build exists only so tests/native can check the fast
+// paths exhaustively against the oracle on CPU).
+//
+// Bit-exact restatement of commonLib/cpp_utils/Base64.cpp:73-139 as the
+// reference's x86-64 SSE build computes it: one IEEE binary32 RNE rounding per
+// multiply/divide, `(int)` = cvttss2si. Compile with -ffp-contract=off; every
+// fused multiply-add below is explicit.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define FLEET_HD __host__ __device__ __forceinline__
+#else
+#define FLEET_HD static inline __attribute__((always_inline))
+#endif
+
+namespace fleet {
+
+typedef float f2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+
+// RN(0.1) and RN(0.1 - RN(0.1)).
+constexpr float kTenthHi = 0x1.99999ap-4f;
+constexpr float kTenthLo = -0x1.99999ap-30f;
+
+FLEET_HD uint32_t f2u(float x) { return __builtin_bit_cast(uint32_t, x); }
+FLEET_HD float u2f(uint32_t x) { return __builtin_bit_cast(float, x); }
+
+// Correctly rounded t/10 in two ops (mul + fma): t*hi exact inside the fma plus
+// RN(t*lo) is within 2^-49 (relative) of t/10, while t/10 is never closer than
+// 2^-27.3 to a binary32 rounding midpoint (10*midpoint - t is a nonzero odd
+// multiple of the finer ulp). Exhaustively checked for every binary32 t with
+// |t| >= 1e-30 (tests/test_native_math.py); int2float never divides values
+// below 1e-9 in magnitude. div10(-0.0) = +0.0, as -0.0/10 is not needed:
+// int2float starts from (float)code, never -0.0.
+FLEET_HD float div10(float t) { return __builtin_fmaf(t, kTenthHi, t * kTenthLo); }
+FLEET_HD f2 div10x2(f2 t) {
+  return __builtin_elementwise_fma(t, f2{kTenthHi, kTenthHi}, t * f2{kTenthLo, kTenthLo});
+}
+
+// x86-64 `(int)x` (cvttss2si): INT_MIN when |x| >= 2^31 or x is NaN.
+FLEET_HD int32_t cvtt(float x) { return __builtin_fabsf(x) < 2147483648.0f ? (int32_t)x : INT32_MIN; }
+
+// Base64::numDigits (Base64.cpp:73-82): decimal digits of n, '-' counted.
+FLEET_HD int num_digits(int32_t n) {
+  uint32_t a = n < 0 ? 0u - (uint32_t)n : (uint32_t)n;
+  int d = n < 0;
+  d += a >= 1u;
+  d += a >= 10u;
+  d += a >= 100u;
+  d += a >= 1000u;
+  d += a >= 10000u;
+  d += a >= 100000u;
+  d += a >= 1000000u;
+  d += a >= 10000000u;
+  d += a >= 100000000u;
+  d += a >= 1000000000u;
+  return d;
+}
+
+// ------------------------------------------------------------ general, exact
+
+// Base64::int2float (Base64.cpp:127-134): k = 9 - |c % 10| divisions of (float)c.
+FLEET_HD float dec(int32_t c) {
+  int dd = c % 10;
+  dd = dd < 0 ? -dd : dd;
+  float t = (float)c;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    float q = div10(t);
+    t = (j + dd < 9) ? q : t;
+  }
+  return t;
+}
+
+// Base64::float2int (Base64.cpp:96-109): 9 - d multiplications by 10,
+// truncation, last decimal digit replaced by d.
+FLEET_HD int32_t enc(float x) {
+  int d = num_digits(cvtt(x));
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    float w = x * 10.0f;
+    x = (j + d < 9) ? w : x;
+  }
+  int32_t t = cvtt(x);
+  int32_t lsb = t % 10;
+  uint32_t u = (uint32_t)t - (uint32_t)lsb;
+  u = t >= 0 ? u + (uint32_t)d : u - (uint32_t)d;
+  return (int32_t)u;
+}
+
+// Q = int2float o float2int: what the next JNI op decodes after an encode.
+FLEET_HD float q(float x) { return dec(enc(x)); }
+
+// ------------------------------------------------------------- fast paths
+// Exact only under their stated preconditions; callers test the precondition
+// per value and send the rest through dec()/q() (kernels.hip, compaction).
+
+// |c| % 10 == 0 (int2float then divides exactly 9 times): modular-inverse
+// divisibility test, n % 10 == 0 <=> ror(n * 5^-1 mod 2^32, 1) <= (2^32-1)/10.
+FLEET_HD bool dec9_ok(int32_t c) {
+  uint32_t a = c < 0 ? 0u - (uint32_t)c : (uint32_t)c;
+  uint32_t m = a * 0xCCCCCCCDu;
+  uint32_t r = (m >> 1) | (m << 31);
+  return r <= 0x19999999u;
+}
+
+FLEET_HD float d9(float t) {
+#pragma unroll
+  for (int j = 0; j < 9; ++j) t = div10(t);
+  return t;
+}
+FLEET_HD f2 d9x2(f2 t) {
+#pragma unroll
+  for (int j = 0; j < 9; ++j) t = div10x2(t);
+  return t;
+}
+
+// int2float(c) when dec9_ok(c)
+FLEET_HD float dec_fast(int32_t c) { return d9((float)c); }
+FLEET_HD f2 dec_fast2(int32_t c0, int32_t c1) { return d9x2(f2{(float)c0, (float)c1}); }
+
+// Q(x) when |x| < 1 (numDigits((int)x) == 0): 9 multiplications, truncation to
+// a multiple of 10 (the last digit becomes 0), then 9 divisions. The sign is
+// put on (float)code before dividing: code 0 gives -0.0 there, which div10
+// turns into +0.0 exactly like int2float(0).
+FLEET_HD float q_fast(float x) {
+  float X = __builtin_fabsf(x);
+#pragma unroll
+  for (int j = 0; j < 9; ++j) X = X * 10.0f;
+  uint32_t n = (uint32_t)X;  // X < 1e9
+  uint32_t c = (n / 10u) * 10u;
+  float t = u2f(f2u((float)c) | (f2u(x) & 0x80000000u));
+  return d9(t);
+}
+FLEET_HD f2 q_fast2(f2 x) {
+  f2 X = __builtin_elementwise_abs(x);
+#pragma unroll
+  for (int j = 0; j < 9; ++j) X = X * f2{10.0f, 10.0f};
+  uint32_t n0 = (uint32_t)X.x, n1 = (uint32_t)X.y;
+  uint32_t c0 = (n0 / 10u) * 10u, c1 = (n1 / 10u) * 10u;
+  f2 t = f2{u2f(f2u((float)c0) | (f2u(x.x) & 0x80000000u)), u2f(f2u((float)c1) | (f2u(x.y) & 0x80000000u))};
+  return d9x2(t);
+}
+
+// precondition of q_fast (also false for NaN)
+FLEET_HD bool q_ok(float x) { return __builtin_fabsf(x) < 1.0f; }
+
+}  // namespace fleet

@@ -546,4 +546,20 @@ int fleet_synth_device(fleet_ctx* c, uint64_t seed, int M, int client0, const in
   return FLEET_OK;
 }
 
+int fleet_selftest_digest(fleet_ctx* c, int fn, uint64_t* out) {
+  if (!c || !out || fn < 0 || fn > 5) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  unsigned long long* d = nullptr;
+  HIP_TRY(c, hipMalloc((void**)&d, sizeof(unsigned long long)));
+  HIP_TRY(c, hipMemsetAsync(d, 0, sizeof(unsigned long long), c->stream));
+  HIP_TRY(c, fleet::launch_digest(fn, d, c->stream));
+  unsigned long long h = 0;
+  HIP_TRY(c, hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  (void)hipFree(d);
+  *out = h;
+  return FLEET_OK;
+}
+
 }  // extern "C"

@@ -7,6 +7,8 @@
 // 420-509); a wave reads 1 KiB contiguous per client row (global_load_dwordx4).
 #include "kernels.h"
 
+#include <cstdlib>
+
 #include "codec_device.h"
 
 namespace fleet {
@@ -51,22 +53,79 @@ __device__ __forceinline__ int headers_in_group(const int32_t* __restrict__ hdr,
 }
 
 // ----------------------------------------------------------------------------
+// Rare-value compaction. The fast paths (codec_math.h) cover |value| < 1 and
+// upload codes whose last digit is 0 -- gradients, in practice. The other
+// values of a stage are gathered, across the whole wave, into a per-wave LDS
+// list, run through the general exact codec by consecutive lanes, and
+// scattered back: one general pass per wave and stage instead of one per
+// value slot, while the fast path stays branch-free for every lane.
+// KIND 0: in = upload code, out = Q(int2float(code)); KIND 1: in = x, out = Q(x).
+template <int S, int KIND>
+__device__ __forceinline__ void resolve_slow(float (&out)[S], const uint32_t (&in)[S], uint32_t slow,
+                                             uint32_t* __restrict__ wscratch, int lane) {
+  if (__ballot(slow != 0) == 0) return;  // wave-uniform
+  uint32_t count = 0;
+  int pos[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const bool f = (slow >> i) & 1u;
+    const unsigned long long b = __ballot(f);
+    if (b) {
+      if (f) {
+        const int p = (int)count + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+        wscratch[p] = in[i];
+        pos[i] = p;
+      }
+      count += (uint32_t)__popcll(b);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (uint32_t base = 0; base < count; base += 64) {
+    const uint32_t idx = base + (uint32_t)lane;
+    if (idx < count) {
+      const uint32_t v = wscratch[idx];
+      const float r = KIND == 0 ? q(dec((int32_t)v)) : q(u2f(v));
+      wscratch[idx] = f2u(r);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+    if ((slow >> i) & 1u) out[i] = u2f(wscratch[pos[i]]);
+}
+
+// ----------------------------------------------------------------------------
 // Fused update: CppNNUpdater.update's aggregation (java:420-509) for the
-// groups [g_begin, g_end). Per value and client c (CppNNUpdater order):
+// groups [g_begin, g_end). Per value and client c, in CppNNUpdater order:
 //   y = Q(dec(code_c))                  getFlatGradient decode+encode, scalarMul decode
 //   p = Q((float)((double)y * d_c))     scalarMultiply(getDampen) encode, add decode
 //   A = (c == 0) ? p : Q(A + p)         ByteVec.add encode/decode
 // then r = Q((float)((double)A * inv)) (scalarMultiply(1/avgSize) + merge decode) and
 // merged code = enc(r); header slots take enc(dec(code_{M-1})) (mergeFlatGradient).
+//
+// Layout: lane owns K groups (3K values) g = g_begin + (blockIdx*K + k)*256 + tid,
+// so every wave-wide load of a client row is 1 KiB contiguous; the next
+// client's K loads are in flight while the current one computes.
+template <int K>
 __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                 const double* __restrict__ dampen, double inv_avg,
                                                 int64_t n_up, int64_t g_begin, int64_t g_end,
                                                 const int32_t* __restrict__ hdr_block,
                                                 uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
                                                 int* __restrict__ err) {
+  constexpr int S = 3 * K;
   __shared__ B64Tables tab;
+  __shared__ uint32_t scratch[4][64 * S];
   b64_tables_init(&tab);
   __syncthreads();
+  const int lane = threadIdx.x & 63;
+  uint32_t* ws = scratch[threadIdx.x >> 6];
+
   // hdr_block = {status, n_headers, walk_end, 0, positions...} (k_layout_parse / host-built);
   // slots at or after walk_end are outside network::flatGrad's walk and, like
   // header slots, come from the last upload in mergeFlatGrad.
@@ -74,68 +133,133 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
   const int64_t walk_end = hdr_block[2];
   const int32_t* hdr = hdr_block + 4;
 
-  const int64_t g = g_begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= g_end) return;
-  const int64_t p0 = 3 * g;
-  const int r = (int)min<int64_t>(3, n_up - p0);
-  const uint32_t need = needed_chars_mask(r);
-  bool is_hdr[3];
-  headers_in_group(hdr, n_hdr, p0, is_hdr);
-  bool keep_last[3];
+  int64_t g[K];
+  bool live[K];
+  const uint8_t* rowp[K];
 #pragma unroll
-  for (int e = 0; e < 3; ++e) keep_last[e] = is_hdr[e] || p0 + e >= walk_end;
+  for (int k = 0; k < K; ++k) {
+    g[k] = g_begin + ((int64_t)blockIdx.x * K + k) * 256 + threadIdx.x;
+    live[k] = g[k] < g_end;
+    rowp[k] = uploads + 16 * (live[k] ? g[k] : g_begin);
+  }
 
-  const uint8_t* row = uploads + 16 * g;
-  float acc[3] = {0.f, 0.f, 0.f};
-  int32_t codes[3] = {0, 0, 0};
-  int32_t last_hdr[3] = {0, 0, 0};
-  uint32_t bad = 0;
-  int layout_bad = 0;
+  float acc[S];
+  int32_t codes[S];
+  uint32_t bad[K];
+#pragma unroll
+  for (int i = 0; i < S; ++i) acc[i] = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) bad[k] = 0;
 
-  uint4 next = *reinterpret_cast<const uint4*>(row);
+  uint4 nxt[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) nxt[k] = *reinterpret_cast<const uint4*>(rowp[k]);
   for (int c = 0; c < M; ++c) {
-    const uint4 cur = next;
-    if (c + 1 < M) next = *reinterpret_cast<const uint4*>(row + (size_t)(c + 1) * pitch);
-    bad |= b64_decode_group(cur, &tab, codes);
-    const double d = dampen[c];
+    uint4 cur[K];
 #pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      const float y = q(dec(codes[e]));
-      const float p = q((float)((double)y * d));
-      acc[e] = c == 0 ? p : q(acc[e] + p);
+    for (int k = 0; k < K; ++k) cur[k] = nxt[k];
+    if (c + 1 < M) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) nxt[k] = *reinterpret_cast<const uint4*>(rowp[k] + (size_t)(c + 1) * pitch);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) bad[k] |= b64_decode_group(cur[k], &tab, codes + 3 * k);
+
+    // stage A: y = Q(int2float(code))
+    float y[S];
+    uint32_t in[S];
+    uint32_t slow = 0;
+#pragma unroll
+    for (int i = 0; i + 1 < S; i += 2) {
+      f2 y0 = dec_fast2(codes[i], codes[i + 1]);
+      f2 yy = q_fast2(y0);
+      y[i] = yy.x;
+      y[i + 1] = yy.y;
+      slow |= (uint32_t)!(dec9_ok(codes[i]) && q_ok(y0.x)) << i;
+      slow |= (uint32_t)!(dec9_ok(codes[i + 1]) && q_ok(y0.y)) << (i + 1);
+    }
+    if (S & 1) {
+      float y0 = dec_fast(codes[S - 1]);
+      y[S - 1] = q_fast(y0);
+      slow |= (uint32_t)!(dec9_ok(codes[S - 1]) && q_ok(y0)) << (S - 1);
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) in[i] = (uint32_t)codes[i];
+    resolve_slow<S, 0>(y, in, slow, ws, lane);
+
+    // stage B: p = Q((float)((double)y * d))
+    const double d = dampen[c];
+    float r[S], p[S];
+    slow = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      r[i] = (float)((double)y[i] * d);
+      slow |= (uint32_t)!q_ok(r[i]) << i;
+      in[i] = f2u(r[i]);
+    }
+#pragma unroll
+    for (int i = 0; i + 1 < S; i += 2) {
+      f2 pp = q_fast2(f2{r[i], r[i + 1]});
+      p[i] = pp.x;
+      p[i + 1] = pp.y;
+    }
+    if (S & 1) p[S - 1] = q_fast(r[S - 1]);
+    resolve_slow<S, 1>(p, in, slow, ws, lane);
+
+    // stage C: A = Q(A + p)
+    if (c == 0) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) acc[i] = p[i];
+    } else {
+      float sm[S];
+      slow = 0;
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        sm[i] = acc[i] + p[i];
+        slow |= (uint32_t)!q_ok(sm[i]) << i;
+        in[i] = f2u(sm[i]);
+      }
+#pragma unroll
+      for (int i = 0; i + 1 < S; i += 2) {
+        f2 aa = q_fast2(f2{sm[i], sm[i + 1]});
+        acc[i] = aa.x;
+        acc[i + 1] = aa.y;
+      }
+      if (S & 1) acc[S - 1] = q_fast(sm[S - 1]);
+      resolve_slow<S, 1>(acc, in, slow, ws, lane);
     }
   }
-  // every upload must carry the same header slots as the last one
-  if (n_hdr) {
-    for (int e = 0; e < 3; ++e) last_hdr[e] = codes[e];
-    bool any = is_hdr[0] | is_hdr[1] | is_hdr[2];
-    if (any) {
+
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    if (!live[k]) continue;
+    const int64_t p0 = 3 * g[k];
+    const int r = (int)min<int64_t>(3, n_up - p0);
+    bool is_hdr[3];
+    headers_in_group(hdr, n_hdr, p0, is_hdr);
+    // every upload must carry the same header slots as the last one
+    int layout_bad = 0;
+    if (is_hdr[0] | is_hdr[1] | is_hdr[2]) {
       for (int c = 0; c < M - 1; ++c) {
         int32_t cc[3];
-        bad |= b64_decode_group(*reinterpret_cast<const uint4*>(row + (size_t)c * pitch), &tab, cc);
+        bad[k] |= b64_decode_group(*reinterpret_cast<const uint4*>(rowp[k] + (size_t)c * pitch), &tab, cc);
         for (int e = 0; e < 3; ++e)
-          if (is_hdr[e] && e < r && cc[e] != last_hdr[e]) layout_bad = 1;
+          if (is_hdr[e] && e < r && cc[e] != codes[3 * k + e]) layout_bad = 1;
       }
     }
-  }
-  if (bad & need) atomicOr(err, FLEET_ERRBIT_BASE64);
-  if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
-
-  int32_t out[3];
+    if (bad[k] & needed_chars_mask(r)) atomicOr(err, FLEET_ERRBIT_BASE64);
+    if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+    int32_t out[3];
 #pragma unroll
-  for (int e = 0; e < 3; ++e) {
-    int32_t o;
-    if (keep_last[e]) {
-      o = enc(dec(codes[e]));
-    } else {
-      o = enc(q((float)((double)acc[e] * inv_avg)));
+    for (int e = 0; e < 3; ++e) {
+      const bool keep_last = is_hdr[e] || p0 + e >= walk_end;
+      int32_t o = keep_last ? enc(dec(codes[3 * k + e])) : enc(q((float)((double)acc[3 * k + e] * inv_avg)));
+      out[e] = e < r ? o : 0;
     }
-    out[e] = e < r ? o : 0;
-  }
-  uint4 text = pad_group(b64_encode_group(out, &tab), r);
-  *reinterpret_cast<uint4*>(merged + 16 * g) = text;
-  if (merged_f32) {
-    for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec(out[e]);
+    *reinterpret_cast<uint4*>(merged + 16 * g[k]) = pad_group(b64_encode_group(out, &tab), r);
+    if (merged_f32) {
+      for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec(out[e]);
+    }
   }
 }
 
@@ -365,12 +489,31 @@ __global__ void k_synth_headers(float* __restrict__ out, size_t vpitch, const in
 
 static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
+// groups per lane: as many as keep >= ~4 waves per SIMD busy (256 CUs x 4 SIMDs)
+int update_groups_per_lane(int64_t groups) {
+  if (const char* e = getenv("FLEET_UPDATE_K")) return atoi(e);
+  const int64_t lanes_for_4_waves = 256LL * 4 * 4 * 64;
+  if (groups >= 4 * lanes_for_4_waves) return 4;
+  if (groups >= 2 * lanes_for_4_waves) return 2;
+  return 1;
+}
+
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
   if (g_end <= g_begin) return hipSuccess;
-  hipLaunchKernelGGL(k_update, dim3(blocks_for(g_end - g_begin, 256)), dim3(256), 0, s, uploads, pitch, M,
-                     d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
+  const int64_t groups = g_end - g_begin;
+  const int K = update_groups_per_lane(groups);
+  const unsigned blocks = (unsigned)((groups + 256 * K - 1) / (256 * K));
+  if (K >= 4)
+    hipLaunchKernelGGL(k_update<4>, dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
+                       g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
+  else if (K == 2)
+    hipLaunchKernelGGL(k_update<2>, dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
+                       g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
+  else
+    hipLaunchKernelGGL(k_update<1>, dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
+                       g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
   return hipGetLastError();
 }
 
@@ -448,6 +591,49 @@ hipError_t launch_synth(uint64_t seed, int client0, int rows, int64_t n_up, floa
   if (n_hdr > 0)
     hipLaunchKernelGGL(k_synth_headers, dim3(blocks_for(n_hdr, 256), rows), dim3(256), 0, s, out, vpitch, d_hpos,
                        d_hval, n_hdr);
+  return hipGetLastError();
+}
+
+// ----------------------------------------------------------------------------
+// Self-test: order-independent digests of the device codec arithmetic over
+// whole input domains (all 2^32 codes / float bit patterns), compared with
+// the oracle's digests (tests/golden/digests.json, tests/native/digest_ref.cpp).
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __restrict__ out) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t sum = 0;
+  for (uint64_t i = tid; i < (1ull << 32); i += nthreads) {
+    const uint32_t u = (uint32_t)i;
+    uint32_t o;
+    bool use = true;
+    switch (fn) {
+      case 0: o = f2u(dec((int32_t)u)); break;                       // int2float, all codes
+      case 1: o = (uint32_t)enc(u2f(u)); break;                      // float2int, all bit patterns
+      case 2: use = (u & 0x7fffffffu) < 0x3f800000u;                 // Q fast path, |x| < 1
+              o = use ? f2u(q_fast(u2f(u))) : 0u; break;
+      case 3: use = ((int32_t)u % 10) == 0;                          // int2float fast path
+              o = use ? f2u(dec_fast((int32_t)u)) : 0u; break;
+      case 4: use = u >= 0x0DA24260u && u < 0x7F800000u;             // div10, t >= 1e-30
+              o = use ? f2u(div10(u2f(u))) : 0u; break;
+      case 5: { f2 v = q_fast2(f2{u2f(u), -u2f(u)});                   // packed Q fast path on (x, -x)
+              use = (u & 0x7fffffffu) < 0x3f800000u; o = use ? f2u(v.x) + 3u * f2u(v.y) : 0u; break; }
+      default: o = 0; use = false;
+    }
+    if (use) sum += splitmix64(((uint64_t)u << 32) | o);
+  }
+  for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)sum);
+}
+
+hipError_t launch_digest(int fn, unsigned long long* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_digest, dim3(256 * 16), dim3(256), 0, s, fn, out);
   return hipGetLastError();
 }
 

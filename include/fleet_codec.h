@@ -141,6 +141,14 @@ int fleet_synth_device(fleet_ctx* ctx, uint64_t seed, int M, int client0, const 
  * (synchronises the stream), and clears the flag. */
 int fleet_check(fleet_ctx* ctx, void* stream);
 
+/* Self-test of the device codec arithmetic over whole input domains: an
+ * order-independent 64-bit digest sum_i splitmix64(i<<32 | f(i)) of
+ *   fn 0: int2float over all 2^32 codes      fn 1: float2int over all 2^32 bit patterns
+ *   fn 2: Q fast path over |x| < 1           fn 3: int2float fast path (codes % 10 == 0)
+ *   fn 4: t/10 (div10) for 1e-30 <= t < inf  fn 5: packed Q fast path
+ * computed on the GPU; compare with the oracle's digests. */
+int fleet_selftest_digest(fleet_ctx* ctx, int fn, uint64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,94 @@
+// tests/native/check_math.cpp -- CPU check of fleet_amd/csrc/codec_math.h (the
+// arithmetic the gfx950 kernels run) against the oracle (oracle/fleet_oracle.c).
+//
+//   check_math sample      ~1e8 sampled inputs per function (CPU test suite)
+//   check_math exhaustive  every input in each fast path's domain (dev check; ~1 min on 8 cores)
+//
+// Exit status 0 = all bit-identical.
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../fleet_amd/csrc/codec_math.h"
+extern "C" {
+#include "../../oracle/fleet_oracle.h"
+}
+
+using namespace fleet;
+static std::atomic<long> g_bad{0};
+
+template <typename F>
+void par_for(uint64_t begin, uint64_t end, uint64_t stride, F f) {
+  unsigned nt = std::max(1u, std::thread::hardware_concurrency());
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([=] {
+      for (uint64_t i = begin + t * stride; i < end; i += (uint64_t)nt * stride) f(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+static void report(const char* name, long bad_before) {
+  long b = g_bad.load() - bad_before;
+  printf("%-28s %s (%ld mismatches)\n", name, b ? "FAIL" : "ok", b);
+}
+
+static inline bool same(float a, float b) { return f2u(a) == f2u(b); }
+
+int main(int argc, char** argv) {
+  bool exhaustive = argc > 1 && std::string(argv[1]) == "exhaustive";
+  const uint64_t s = exhaustive ? 1 : 97;  // sampling stride (odd, walks every residue class)
+  long b0;
+
+  b0 = g_bad;  // div10 vs IEEE division, all positive finite floats >= 1e-30 (0x0DA24260)
+  par_for(0x0DA24260ull, 0x7F800000ull, s, [](uint64_t i) {
+    float t = u2f((uint32_t)i);
+    if (!same(div10(t), t / 10.0f) || !same(div10(-t), -t / 10.0f)) g_bad++;
+  });
+  report("div10", b0);
+
+  b0 = g_bad;  // dec9_ok vs c % 10 == 0, all int32
+  par_for(0, 1ull << 32, s, [](uint64_t i) {
+    int32_t c = (int32_t)(uint32_t)i;
+    if (dec9_ok(c) != (c % 10 == 0)) g_bad++;
+  });
+  report("dec9_ok", b0);
+
+  b0 = g_bad;  // dec_fast vs int2float on its domain (multiples of 10)
+  par_for(0, 1ull << 32, 10 * s, [](uint64_t i) {
+    int32_t c = (int32_t)(uint32_t)i;
+    if (c % 10 != 0) return;
+    if (!same(dec_fast(c), fo_int2float(c))) g_bad++;
+  });
+  report("dec_fast", b0);
+
+  b0 = g_bad;  // q_fast (+ packed) vs Q on its domain |x| < 1, both signs
+  par_for(0, 0x3F800000ull, s, [](uint64_t i) {
+    float x = u2f((uint32_t)i);
+    float r = fo_int2float(fo_float2int(x)), rn = fo_int2float(fo_float2int(-x));
+    f2 p = q_fast2(f2{x, -x});
+    if (!same(q_fast(x), r) || !same(q_fast(-x), rn) || !same(p.x, r) || !same(p.y, rn)) g_bad++;
+  });
+  report("q_fast/q_fast2 (|x|<1)", b0);
+
+  b0 = g_bad;  // general dec vs int2float, all int32 (sampled more coarsely in sample mode)
+  par_for(0, 1ull << 32, exhaustive ? 1 : 1009, [](uint64_t i) {
+    int32_t c = (int32_t)(uint32_t)i;
+    if (!same(dec(c), fo_int2float(c))) g_bad++;
+  });
+  report("dec (general)", b0);
+
+  b0 = g_bad;  // general enc vs float2int, all float bit patterns (incl. inf/NaN)
+  par_for(0, 1ull << 32, exhaustive ? 1 : 1009, [](uint64_t i) {
+    float x = u2f((uint32_t)i);
+    if (enc(x) != fo_float2int(x)) g_bad++;
+  });
+  report("enc (general)", b0);
+
+  printf("%s\n", g_bad ? "FAILED" : "ALL OK");
+  return g_bad ? 1 : 0;
+}

@@ -1,0 +1,60 @@
+"""The C-ABI library without a GPU: it loads, exports every symbol declared in
+include/fleet_codec.h, its host-only helpers work, and compute entry points
+fail loudly (no CPU fallback exists)."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import fleet_amd as F
+from fleet_amd.layouts import CIFAR10, CIFAR100, LAYOUTS, MNIST
+
+
+def test_library_exports_every_declared_symbol():
+    L = F.lib()
+    declared = F.exported_symbols_from_header()
+    assert len(declared) >= 25
+    missing = [s for s in declared if not hasattr(L, s)]
+    assert not missing, missing
+    assert F.lib().fleet_version().startswith(b"fleet-mi355x")
+
+
+def test_b64_lengths():
+    for n in list(range(0, 50)) + [22961, 313867, 1 << 20]:
+        L = F.lib().fleet_b64_len(n)
+        assert L == 4 * ((4 * n + 2) // 3) == F.b64_len(n)
+        assert F.lib().fleet_b64_count(L) == n
+
+
+@pytest.mark.parametrize("lay", [MNIST, CIFAR10, CIFAR100, LAYOUTS["synth1m"]])
+def test_layout_from_sizes(lay):
+    pos, n_up = F.layout_from_sizes(lay.w_sizes, lay.b_sizes)
+    assert n_up == lay.n_up
+    assert pos.tolist() == lay.header_positions()
+
+
+def test_layout_matches_oracle_mask(oracle):
+    for lay in (MNIST, CIFAR10):
+        mask = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+        assert np.nonzero(mask)[0].tolist() == lay.header_positions()
+
+
+def test_no_cpu_fallback_without_gpu():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("a GPU is present")
+    except ImportError:
+        pass
+    with pytest.raises(F.FleetError) as e:
+        F.Codec(0)
+    assert e.value.code == F.FLEET_ERR_HIP
+    h = C.c_void_p()
+    assert F.lib().fleet_create(0, C.byref(h)) == F.FLEET_ERR_HIP
+
+
+def test_null_context_rejected():
+    L = F.lib()
+    n = C.c_size_t(0)
+    assert L.fleet_encode_f32(None, None, 0, None, 0, C.byref(n)) == F.FLEET_ERR_ARG
+    assert L.fleet_update(None, None, None, 0, None, None, 0, None, None) == F.FLEET_ERR_ARG

@@ -180,3 +180,43 @@ def test_device_synth_and_encode(codec, oracle):
         exp = oracle.encode_floats(host[c, : lay.n_up])
         assert t[c, :L].tobytes() == exp
         assert np.array_equal(b[c, : lay.n_up].view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
+
+
+@pytest.mark.parametrize("fn", range(6))
+def test_device_codec_exhaustive_digest(codec, fn):
+    """Every input of each device codec function's domain (2^32 codes / bit
+    patterns), digested on the GPU, equals the oracle's digest."""
+    import json
+    import os
+    ref = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "digests.json")))
+    assert f"{codec.selftest_digest(fn):016x}" == ref[f"fn{fn}"]
+
+
+@pytest.mark.parametrize("K", [1, 2, 4])
+def test_update_groups_per_lane_variants(codec, oracle, monkeypatch, K):
+    """k_update<K> (K groups per lane, chosen by problem size) on ragged sizes."""
+    monkeypatch.setenv("FLEET_UPDATE_K", str(K))
+    for lay, M in ((synthetic(300001), 3), (synthetic(20000), 7), (MNIST, 5)):
+        ups = uploads_for(oracle, lay, M, seed=21 + K)
+        d = policy("exp", M)
+        hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+        assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
+
+
+def test_update_large_magnitudes_slow_path(codec, oracle):
+    """Values far outside the fast path (|x| >= 1, digits != 0, >= 2^31) force
+    every compaction pass; dampening > 1 (class-aware policy) too."""
+    rng = np.random.default_rng(8)
+    lay = synthetic(4000)
+    M = 6
+    ups = []
+    for c in range(M):
+        v = oracle.synth_upload(3, c, list(lay.w_sizes), list(lay.b_sizes))
+        big = rng.random(len(v)) < 0.3
+        v[big] = (np.exp(rng.uniform(0, 21, big.sum())) * rng.choice([-1, 1], big.sum())).astype(np.float32)
+        v[0], v[1], v[-1] = 1.0, float(lay.w_sizes[0]), 0.0
+        v[5:9] = [9.99e8, -9.99e8, 2.1e9, 0.999999]
+        ups.append(oracle.encode_floats(v))
+    d = [1.0, 7.5, 0.25, 10.0, 1 / 3, 1.0]
+    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm) == oracle.update_faithful(ups, d)

@@ -49,8 +49,10 @@ def test_known_answers():
     assert o.lib.fo_float2int(-1.0) == -10000002
     assert o.lib.fo_float2int(10.0) == 100000002
     assert np.float32(o.lib.fo_int2float(-10000002)) == np.float32(-1.00000024)
+    # 1e-6 * 10^9 in fp32 steps lands just below 1000 -> truncated to 990: Q(1e-6) ~ 9.9e-7
+    assert o.float2int(np.array([1e-6], np.float32))[0] == 990
     q = o.int2float(o.float2int(np.array([1e-6], np.float32)))
-    assert q[0] == np.float32(9.9e-7)
+    assert abs(float(q[0]) - 9.9e-7) < 1e-12
 
 
 def test_ops_match_golden(oracle):
