@@ -16,6 +16,7 @@ namespace fleet {
 // Base64.cpp:56-68 `from_base64`, extended with 0xff for bytes >= 0x80
 // (the reference indexes out of bounds there; such text is rejected here).
 struct B64Tables {
+  DigitEntry digits[32];  // numDigits by frexp exponent (codec_math.h)
   uint8_t from[256];
   uint8_t to[64];
 };
@@ -35,8 +36,10 @@ __device__ __forceinline__ uint8_t b64_to_value(int s) {
 
 // Fill the block's LDS tables (call from every thread, then __syncthreads()).
 __device__ __forceinline__ void b64_tables_init(B64Tables* t) {
+  constexpr DigitEntry dig[32] = FLEET_DIGIT_TABLE;
   for (int i = threadIdx.x; i < 256; i += blockDim.x) t->from[i] = b64_from_value(i);
   for (int i = threadIdx.x; i < 64; i += blockDim.x) t->to[i] = b64_to_value(i);
+  for (int i = threadIdx.x; i < 32; i += blockDim.x) t->digits[i] = dig[i];
 }
 
 // One 16-char group -> 12 bytes -> 3 little-endian int32 codes.

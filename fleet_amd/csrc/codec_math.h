@@ -147,4 +147,135 @@ FLEET_HD f2 q_fast2(f2 x) {
 // precondition of q_fast (also false for NaN)
 FLEET_HD bool q_ok(float x) { return __builtin_fabsf(x) < 1.0f; }
 
+// ------------------------------------------------- variable-length fast paths
+// For 0 <= d <= 7 the reference runs k = 9 - d in [2, 9] multiplications and
+// as many divisions. All chain steps are the same operation, so with
+// r = k - 2 = 4*b2 + 2*b1 + b0 each chain is: 2 unconditional steps, then
+// groups of 1, 2 and 4 steps, each kept or dropped by one select on b0/b1/b2
+// -- 9 steps and 3 selects instead of 9 per-step selects.
+
+// Digit-count table indexed by e = frexp exponent (|x| in [2^(e-1), 2^e)):
+// numDigits(trunc|x|) = base[e] + (|x| >= 10^base[e]).
+struct DigitEntry {
+  uint32_t base;
+  float thr;
+};
+#define FLEET_DIGIT_TABLE                                                                                  \
+  {{0, __builtin_inff()}, {1, 10.f}, {1, 10.f}, {1, 10.f}, {1, 10.f}, {2, 100.f}, {2, 100.f}, {2, 100.f}, \
+   {3, 1e3f}, {3, 1e3f}, {3, 1e3f}, {4, 1e4f}, {4, 1e4f}, {4, 1e4f}, {4, 1e4f}, {5, 1e5f}, {5, 1e5f},     \
+   {5, 1e5f}, {6, 1e6f}, {6, 1e6f}, {6, 1e6f}, {7, 1e7f}, {7, 1e7f}, {7, 1e7f}, {7, 1e7f}, {8, 1e8f},      \
+   {8, 1e8f}, {8, 1e8f}, {9, 1e9f}, {9, 1e9f}, {9, 1e9f}, {10, 1e10f}}
+
+FLEET_HD int frexp_exp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_frexp_expf(x);
+#else
+  int e = 0;
+  (void)__builtin_frexpf(x, &e);
+  return e;
+#endif
+}
+
+// numDigits((int)x) for |x| < 2^31 (table: DigitEntry[32])
+FLEET_HD int digits_of(float x, const DigitEntry* tab) {
+  float ax = __builtin_fabsf(x);
+  int e = frexp_exp(ax);
+  e = e < 0 ? 0 : e > 31 ? 31 : e;
+  const DigitEntry t = tab[e];
+  return (int)t.base + (ax >= t.thr) + (x <= -1.0f);
+}
+
+// Q(x) for -1e6 < x < 1e7 (numDigits((int)x) <= 7).
+FLEET_HD bool q_gen_ok(float x) { return x < 1e7f && x > -1e6f; }
+
+FLEET_HD float steps_mul10(float X, bool b0, bool b1, bool b2) {
+  X = X * 10.0f;
+  X = X * 10.0f;
+  float Y = X * 10.0f;
+  X = b0 ? Y : X;
+  Y = X * 10.0f;
+  Y = Y * 10.0f;
+  X = b1 ? Y : X;
+  Y = X * 10.0f;
+  Y = Y * 10.0f;
+  Y = Y * 10.0f;
+  Y = Y * 10.0f;
+  return b2 ? Y : X;
+}
+FLEET_HD float steps_div10(float t, bool b0, bool b1, bool b2) {
+  t = div10(div10(t));
+  float u = div10(t);
+  t = b0 ? u : t;
+  u = div10(div10(t));
+  t = b1 ? u : t;
+  u = div10(div10(div10(div10(t))));
+  return b2 ? u : t;
+}
+FLEET_HD f2 steps_mul10x2(f2 X, const bool (&b0)[2], const bool (&b1)[2], const bool (&b2)[2]) {
+  const f2 ten = f2{10.0f, 10.0f};
+  X = X * ten;
+  X = X * ten;
+  f2 Y = X * ten;
+  X = f2{b0[0] ? Y.x : X.x, b0[1] ? Y.y : X.y};
+  Y = X * ten;
+  Y = Y * ten;
+  X = f2{b1[0] ? Y.x : X.x, b1[1] ? Y.y : X.y};
+  Y = X * ten;
+  Y = Y * ten;
+  Y = Y * ten;
+  Y = Y * ten;
+  return f2{b2[0] ? Y.x : X.x, b2[1] ? Y.y : X.y};
+}
+FLEET_HD f2 steps_div10x2(f2 t, const bool (&b0)[2], const bool (&b1)[2], const bool (&b2)[2]) {
+  t = div10x2(div10x2(t));
+  f2 u = div10x2(t);
+  t = f2{b0[0] ? u.x : t.x, b0[1] ? u.y : t.y};
+  u = div10x2(div10x2(t));
+  t = f2{b1[0] ? u.x : t.x, b1[1] ? u.y : t.y};
+  u = div10x2(div10x2(div10x2(div10x2(t))));
+  return f2{b2[0] ? u.x : t.x, b2[1] ? u.y : t.y};
+}
+
+// |code| = 10*(n/10) + d with n = trunc(|x| * 10^(9-d)) (Base64.cpp:104-108)
+FLEET_HD float signed_code_float(uint32_t n, int d, float x) {
+  uint32_t c = (n / 10u) * 10u + (uint32_t)d;
+  return u2f(f2u((float)c) | (f2u(x) & 0x80000000u));
+}
+
+FLEET_HD float q_gen(float x, const DigitEntry* tab) {
+  const int d = digits_of(x, tab);
+  const uint32_t r = (uint32_t)(7 - d);
+  const bool b0 = r & 1u, b1 = r & 2u, b2 = r & 4u;
+  const float X = steps_mul10(__builtin_fabsf(x), b0, b1, b2);
+  return steps_div10(signed_code_float((uint32_t)X, d, x), b0, b1, b2);
+}
+FLEET_HD f2 q_gen2(f2 x, const DigitEntry* tab) {
+  const int d0 = digits_of(x.x, tab), d1 = digits_of(x.y, tab);
+  const uint32_t r0 = (uint32_t)(7 - d0), r1 = (uint32_t)(7 - d1);
+  const bool b0[2] = {(r0 & 1u) != 0, (r1 & 1u) != 0};
+  const bool b1[2] = {(r0 & 2u) != 0, (r1 & 2u) != 0};
+  const bool b2[2] = {(r0 & 4u) != 0, (r1 & 4u) != 0};
+  const f2 X = steps_mul10x2(__builtin_elementwise_abs(x), b0, b1, b2);
+  const f2 t = f2{signed_code_float((uint32_t)X.x, d0, x.x), signed_code_float((uint32_t)X.y, d1, x.y)};
+  return steps_div10x2(t, b0, b1, b2);
+}
+
+// int2float(c) for |c % 10| <= 7 (k = 9 - |c % 10| >= 2 divisions)
+FLEET_HD uint32_t last_digit(int32_t c) {
+  uint32_t a = c < 0 ? 0u - (uint32_t)c : (uint32_t)c;
+  return a - (a / 10u) * 10u;
+}
+FLEET_HD bool dec_gen_ok(int32_t c) { return last_digit(c) <= 7u; }
+FLEET_HD float dec_gen(int32_t c) {
+  const uint32_t r = 7u - last_digit(c);
+  return steps_div10((float)c, r & 1u, r & 2u, r & 4u);
+}
+FLEET_HD f2 dec_gen2(int32_t c0, int32_t c1) {
+  const uint32_t r0 = 7u - last_digit(c0), r1 = 7u - last_digit(c1);
+  const bool b0[2] = {(r0 & 1u) != 0, (r1 & 1u) != 0};
+  const bool b1[2] = {(r0 & 2u) != 0, (r1 & 2u) != 0};
+  const bool b2[2] = {(r0 & 4u) != 0, (r1 & 4u) != 0};
+  return steps_div10x2(f2{(float)c0, (float)c1}, b0, b1, b2);
+}
+
 }  // namespace fleet

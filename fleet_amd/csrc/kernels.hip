@@ -59,7 +59,8 @@ __device__ __forceinline__ int headers_in_group(const int32_t* __restrict__ hdr,
 // list, run through the general exact codec by consecutive lanes, and
 // scattered back: one general pass per wave and stage instead of one per
 // value slot, while the fast path stays branch-free for every lane.
-// KIND 0: in = upload code, out = Q(int2float(code)); KIND 1: in = x, out = Q(x).
+// KIND 0: in = upload code, out = Q(int2float(code)); KIND 1: in = x, out = Q(x);
+// KIND 2: in = code, out = int2float(code).
 template <int S, int KIND>
 __device__ __forceinline__ void resolve_slow(float (&out)[S], const uint32_t (&in)[S], uint32_t slow,
                                              uint32_t* __restrict__ wscratch, int lane) {
@@ -87,7 +88,7 @@ __device__ __forceinline__ void resolve_slow(float (&out)[S], const uint32_t (&i
     const uint32_t idx = base + (uint32_t)lane;
     if (idx < count) {
       const uint32_t v = wscratch[idx];
-      const float r = KIND == 0 ? q(dec((int32_t)v)) : q(u2f(v));
+      const float r = KIND == 0 ? q(dec((int32_t)v)) : KIND == 1 ? q(u2f(v)) : dec((int32_t)v);
       wscratch[idx] = f2u(r);
     }
   }
@@ -97,6 +98,41 @@ __device__ __forceinline__ void resolve_slow(float (&out)[S], const uint32_t (&i
 #pragma unroll
   for (int i = 0; i < S; ++i)
     if ((slow >> i) & 1u) out[i] = u2f(wscratch[pos[i]]);
+}
+
+// out[i] = Q(x[i]) for a stage of S values: fixed 9-step chains when the
+// whole wave is in |x| < 1, else the variable chains; resolve_slow for the rest.
+template <int S>
+__device__ __forceinline__ void q_stage(float (&out)[S], const float (&x)[S], const DigitEntry* dig,
+                                        uint32_t* __restrict__ ws, int lane) {
+  bool all_fast = true;
+#pragma unroll
+  for (int i = 0; i < S; ++i) all_fast &= q_ok(x[i]);
+  uint32_t slow = 0;
+  if (__ballot(!all_fast) == 0) {
+#pragma unroll
+    for (int i = 0; i + 1 < S; i += 2) {
+      const f2 v = q_fast2(f2{x[i], x[i + 1]});
+      out[i] = v.x;
+      out[i + 1] = v.y;
+    }
+    if (S & 1) out[S - 1] = q_fast(x[S - 1]);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i + 1 < S; i += 2) {
+    const f2 v = q_gen2(f2{x[i], x[i + 1]}, dig);
+    out[i] = v.x;
+    out[i + 1] = v.y;
+  }
+  if (S & 1) out[S - 1] = q_gen(x[S - 1], dig);
+  uint32_t in[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    slow |= (uint32_t)!q_gen_ok(x[i]) << i;
+    in[i] = f2u(x[i]);
+  }
+  resolve_slow<S, 1>(out, in, slow, ws, lane);
 }
 
 // ----------------------------------------------------------------------------
@@ -165,46 +201,50 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
 #pragma unroll
     for (int k = 0; k < K; ++k) bad[k] |= b64_decode_group(cur[k], &tab, codes + 3 * k);
 
+    // Per stage and wave: if every value of the wave is inside the |x| < 1
+    // fast domain, run the fixed 9-step chains; otherwise the 2+1+2+4-step
+    // variable chains (numDigits <= 7). Values outside both go through the
+    // general codec via resolve_slow (|x| >= 1e7: never for gradients).
     // stage A: y = Q(int2float(code))
-    float y[S];
-    uint32_t in[S];
-    uint32_t slow = 0;
+    float y0[S], y[S];
+    {
+      uint32_t in[S];
+      uint32_t slow = 0;
+      bool all9 = true;
 #pragma unroll
-    for (int i = 0; i + 1 < S; i += 2) {
-      f2 y0 = dec_fast2(codes[i], codes[i + 1]);
-      f2 yy = q_fast2(y0);
-      y[i] = yy.x;
-      y[i + 1] = yy.y;
-      slow |= (uint32_t)!(dec9_ok(codes[i]) && q_ok(y0.x)) << i;
-      slow |= (uint32_t)!(dec9_ok(codes[i + 1]) && q_ok(y0.y)) << (i + 1);
-    }
-    if (S & 1) {
-      float y0 = dec_fast(codes[S - 1]);
-      y[S - 1] = q_fast(y0);
-      slow |= (uint32_t)!(dec9_ok(codes[S - 1]) && q_ok(y0)) << (S - 1);
-    }
+      for (int i = 0; i < S; ++i) all9 &= dec9_ok(codes[i]);
+      if (__ballot(!all9) == 0) {
 #pragma unroll
-    for (int i = 0; i < S; ++i) in[i] = (uint32_t)codes[i];
-    resolve_slow<S, 0>(y, in, slow, ws, lane);
+        for (int i = 0; i + 1 < S; i += 2) {
+          const f2 v = dec_fast2(codes[i], codes[i + 1]);
+          y0[i] = v.x;
+          y0[i + 1] = v.y;
+        }
+        if (S & 1) y0[S - 1] = dec_fast(codes[S - 1]);
+      } else {
+#pragma unroll
+        for (int i = 0; i + 1 < S; i += 2) {
+          const f2 v = dec_gen2(codes[i], codes[i + 1]);
+          y0[i] = v.x;
+          y0[i + 1] = v.y;
+        }
+        if (S & 1) y0[S - 1] = dec_gen(codes[S - 1]);
+#pragma unroll
+        for (int i = 0; i < S; ++i) {
+          slow |= (uint32_t)!dec_gen_ok(codes[i]) << i;
+          in[i] = (uint32_t)codes[i];
+        }
+        resolve_slow<S, 2>(y0, in, slow, ws, lane);
+      }
+    }
+    q_stage<S>(y, y0, tab.digits, ws, lane);
 
     // stage B: p = Q((float)((double)y * d))
     const double d = dampen[c];
     float r[S], p[S];
-    slow = 0;
 #pragma unroll
-    for (int i = 0; i < S; ++i) {
-      r[i] = (float)((double)y[i] * d);
-      slow |= (uint32_t)!q_ok(r[i]) << i;
-      in[i] = f2u(r[i]);
-    }
-#pragma unroll
-    for (int i = 0; i + 1 < S; i += 2) {
-      f2 pp = q_fast2(f2{r[i], r[i + 1]});
-      p[i] = pp.x;
-      p[i + 1] = pp.y;
-    }
-    if (S & 1) p[S - 1] = q_fast(r[S - 1]);
-    resolve_slow<S, 1>(p, in, slow, ws, lane);
+    for (int i = 0; i < S; ++i) r[i] = (float)((double)y[i] * d);
+    q_stage<S>(p, r, tab.digits, ws, lane);
 
     // stage C: A = Q(A + p)
     if (c == 0) {
@@ -212,21 +252,9 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
       for (int i = 0; i < S; ++i) acc[i] = p[i];
     } else {
       float sm[S];
-      slow = 0;
 #pragma unroll
-      for (int i = 0; i < S; ++i) {
-        sm[i] = acc[i] + p[i];
-        slow |= (uint32_t)!q_ok(sm[i]) << i;
-        in[i] = f2u(sm[i]);
-      }
-#pragma unroll
-      for (int i = 0; i + 1 < S; i += 2) {
-        f2 aa = q_fast2(f2{sm[i], sm[i + 1]});
-        acc[i] = aa.x;
-        acc[i + 1] = aa.y;
-      }
-      if (S & 1) acc[S - 1] = q_fast(sm[S - 1]);
-      resolve_slow<S, 1>(acc, in, slow, ws, lane);
+      for (int i = 0; i < S; ++i) sm[i] = acc[i] + p[i];
+      q_stage<S>(acc, sm, tab.digits, ws, lane);
     }
   }
 
@@ -606,6 +634,12 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 }
 
 __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __restrict__ out) {
+  __shared__ DigitEntry dig[32];
+  {
+    constexpr DigitEntry init[32] = FLEET_DIGIT_TABLE;
+    if (threadIdx.x < 32) dig[threadIdx.x] = init[threadIdx.x];
+    __syncthreads();
+  }
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
   uint64_t sum = 0;
@@ -624,6 +658,18 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
               o = use ? f2u(div10(u2f(u))) : 0u; break;
       case 5: { f2 v = q_fast2(f2{u2f(u), -u2f(u)});                   // packed Q fast path on (x, -x)
               use = (u & 0x7fffffffu) < 0x3f800000u; o = use ? f2u(v.x) + 3u * f2u(v.y) : 0u; break; }
+      case 6: use = q_gen_ok(u2f(u));                                 // variable-length Q, numDigits <= 7
+              o = use ? f2u(q_gen(u2f(u), dig)) : 0u; break;
+      case 7: use = dec_gen_ok((int32_t)u);                           // variable-length int2float
+              o = use ? f2u(dec_gen((int32_t)u)) : 0u; break;
+      case 8: { const float x = u2f(u);                               // packed variable-length Q on (x, -x/4)
+              use = q_gen_ok(x) && q_gen_ok(-0.25f * x);
+              const f2 v = q_gen2(f2{x, -0.25f * x}, dig);
+              o = use ? f2u(v.x) + 3u * f2u(v.y) : 0u; break; }
+      case 9: { const int32_t c = (int32_t)u, c2 = (int32_t)(u * 2654435761u);  // packed int2float
+              use = dec_gen_ok(c) && dec_gen_ok(c2);
+              const f2 v = dec_gen2(c, c2);
+              o = use ? f2u(v.x) + 3u * f2u(v.y) : 0u; break; }
       default: o = 0; use = false;
     }
     if (use) sum += splitmix64(((uint64_t)u << 32) | o);

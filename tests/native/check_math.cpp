@@ -75,6 +75,37 @@ int main(int argc, char** argv) {
   });
   report("q_fast/q_fast2 (|x|<1)", b0);
 
+  static const DigitEntry tab[32] = FLEET_DIGIT_TABLE;
+  b0 = g_bad;  // digits_of vs numDigits((int)x), |x| < 2^31
+  par_for(0, 1ull << 32, s, [](uint64_t i) {
+    float x = u2f((uint32_t)i);
+    if (!(__builtin_fabsf(x) < 2147483648.0f)) return;
+    if (digits_of(x, tab) != fo_num_digits(fo_cvtt(x))) g_bad++;
+  });
+  report("digits_of", b0);
+
+  b0 = g_bad;  // q_gen (+ packed) vs Q on its domain -1e6 < x < 1e7
+  par_for(0, 1ull << 32, s, [](uint64_t i) {
+    float x = u2f((uint32_t)i);
+    if (!q_gen_ok(x)) return;
+    float r = fo_int2float(fo_float2int(x));
+    f2 p = q_gen2(f2{x, x * 0.5f}, tab);
+    float r2 = fo_int2float(fo_float2int(x * 0.5f));
+    if (!same(q_gen(x, tab), r) || !same(p.x, r) || !same(p.y, r2)) g_bad++;
+  });
+  report("q_gen/q_gen2", b0);
+
+  b0 = g_bad;  // dec_gen (+ packed) vs int2float on |c % 10| <= 7
+  par_for(0, 1ull << 32, s, [](uint64_t i) {
+    int32_t c = (int32_t)(uint32_t)i;
+    if (!dec_gen_ok(c)) return;
+    float r = fo_int2float(c);
+    int32_t c2 = c / 7 * 3;
+    f2 p = dec_gen2(c, c2);
+    if (!same(dec_gen(c), r) || !same(p.x, r) || (dec_gen_ok(c2) && !same(p.y, fo_int2float(c2)))) g_bad++;
+  });
+  report("dec_gen/dec_gen2", b0);
+
   b0 = g_bad;  // general dec vs int2float, all int32 (sampled more coarsely in sample mode)
   par_for(0, 1ull << 32, exhaustive ? 1 : 1009, [](uint64_t i) {
     int32_t c = (int32_t)(uint32_t)i;
