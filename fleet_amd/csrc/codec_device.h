@@ -17,7 +17,8 @@ namespace fleet {
 // (the reference indexes out of bounds there; such text is rejected here).
 struct B64Tables {
   DigitEntry digits[32];  // numDigits by frexp exponent (codec_math.h)
-  uint8_t from[256];
+  uint8_t from[256];      // Base64.cpp:56-68, 0xff = not in the alphabet
+  uint8_t fromf[256];     // same, 0x40 = not in the alphabet
   uint8_t to[64];
 };
 
@@ -30,6 +31,13 @@ __device__ __forceinline__ uint8_t b64_from_value(int ch) {
   return 0xff;
 }
 
+// 0..63, or 0x40 for a byte outside the alphabet (one flag bit, so a group's
+// validity is the OR of its sextets)
+__device__ __forceinline__ uint8_t b64_from_value_flag(int ch) {
+  const uint8_t v = b64_from_value(ch);
+  return v == 0xff ? 0x40 : v;
+}
+
 __device__ __forceinline__ uint8_t b64_to_value(int s) {
   return (uint8_t)(s < 26 ? 'A' + s : s < 52 ? 'a' + s - 26 : s < 62 ? '0' + s - 52 : s == 62 ? '+' : '/');
 }
@@ -37,7 +45,10 @@ __device__ __forceinline__ uint8_t b64_to_value(int s) {
 // Fill the block's LDS tables (call from every thread, then __syncthreads()).
 __device__ __forceinline__ void b64_tables_init(B64Tables* t) {
   constexpr DigitEntry dig[32] = FLEET_DIGIT_TABLE;
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) t->from[i] = b64_from_value(i);
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    t->from[i] = b64_from_value(i);
+    t->fromf[i] = b64_from_value_flag(i);
+  }
   for (int i = threadIdx.x; i < 64; i += blockDim.x) t->to[i] = b64_to_value(i);
   for (int i = threadIdx.x; i < 32; i += blockDim.x) t->digits[i] = dig[i];
 }
@@ -62,6 +73,27 @@ __device__ __forceinline__ uint32_t b64_decode_group(uint4 w, const B64Tables* t
   codes[1] = (int32_t)__builtin_amdgcn_perm(V[2], V[1], 0x05060001u);
   codes[2] = (int32_t)__builtin_amdgcn_perm(V[3], V[2], 0x04050600u);
   return bad;
+}
+
+// Same decode for a full group (all 16 chars carry data): returns nonzero if any
+// char is outside the alphabet. Sextets compose by shift-or; no per-char mask.
+__device__ __forceinline__ uint32_t b64_decode_group_full(uint4 w, const B64Tables* t, int32_t codes[3]) {
+  const uint32_t words[4] = {w.x, w.y, w.z, w.w};
+  uint32_t V[4];
+  uint32_t anyf = 0;
+#pragma unroll
+  for (int qd = 0; qd < 4; ++qd) {
+    const uint32_t s0 = t->fromf[words[qd] & 0xff];
+    const uint32_t s1 = t->fromf[(words[qd] >> 8) & 0xff];
+    const uint32_t s2 = t->fromf[(words[qd] >> 16) & 0xff];
+    const uint32_t s3 = t->fromf[words[qd] >> 24];
+    anyf |= s0 | s1 | s2 | s3;
+    V[qd] = (((((s0 << 6) | s1) << 6) | s2) << 6) | s3;  // flag bits only land above bit 23
+  }
+  codes[0] = (int32_t)__builtin_amdgcn_perm(V[1], V[0], 0x06000102u);
+  codes[1] = (int32_t)__builtin_amdgcn_perm(V[2], V[1], 0x05060001u);
+  codes[2] = (int32_t)__builtin_amdgcn_perm(V[3], V[2], 0x04050600u);
+  return anyf & 0x40u;
 }
 
 // 3 codes -> 12 bytes -> 16 chars (Base64.cpp:176-195).

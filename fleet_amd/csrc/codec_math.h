@@ -148,11 +148,19 @@ FLEET_HD f2 q_fast2(f2 x) {
 FLEET_HD bool q_ok(float x) { return __builtin_fabsf(x) < 1.0f; }
 
 // ------------------------------------------------- variable-length fast paths
-// For 0 <= d <= 7 the reference runs k = 9 - d in [2, 9] multiplications and
-// as many divisions. All chain steps are the same operation, so with
-// r = k - 2 = 4*b2 + 2*b1 + b0 each chain is: 2 unconditional steps, then
-// groups of 1, 2 and 4 steps, each kept or dropped by one select on b0/b1/b2
-// -- 9 steps and 3 selects instead of 9 per-step selects.
+// For numDigits d <= 9 the reference runs k = 9 - d in [0, 9] multiplications
+// and as many divisions. Every chain step is the same operation, so each chain
+// is computed as groups of 2, 1, 2 and 4 steps, each kept or dropped by one
+// select: with e = (k >= 8) and k' = k - 2e = 4*b2 + 2*b1 + b0, k = 2e + k'.
+// 9 steps and 4 selects instead of 9 per-step selects.
+struct Steps {
+  bool e, b0, b1, b2;
+};
+FLEET_HD Steps steps_of(uint32_t k) {
+  const bool e = k >= 8u;
+  const uint32_t r = k - (e ? 2u : 0u);
+  return Steps{e, (r & 1u) != 0, (r & 2u) != 0, (r & 4u) != 0};
+}
 
 // Digit-count table indexed by e = frexp exponent (|x| in [2^(e-1), 2^e)):
 // numDigits(trunc|x|) = base[e] + (|x| >= 10^base[e]).
@@ -185,55 +193,68 @@ FLEET_HD int digits_of(float x, const DigitEntry* tab) {
   return (int)t.base + (ax >= t.thr) + (x <= -1.0f);
 }
 
-// Q(x) for -1e6 < x < 1e7 (numDigits((int)x) <= 7).
-FLEET_HD bool q_gen_ok(float x) { return x < 1e7f && x > -1e6f; }
+// numDigits((int)x) on the q_gen domain by compares only (no table load:
+// for latency-bound callers).
+FLEET_HD int digits_cmp(float x) {
+  const float ax = __builtin_fabsf(x);
+  return (ax >= 1.0f) + (ax >= 10.0f) + (ax >= 100.0f) + (ax >= 1e3f) + (ax >= 1e4f) + (ax >= 1e5f) +
+         (ax >= 1e6f) + (ax >= 1e7f) + (ax >= 1e8f) + (x <= -1.0f);
+}
 
-FLEET_HD float steps_mul10(float X, bool b0, bool b1, bool b2) {
-  X = X * 10.0f;
-  X = X * 10.0f;
+// Q(x) for -1e8 < x < 1e9 (numDigits((int)x) <= 9).
+FLEET_HD bool q_gen_ok(float x) { return x < 1e9f && x > -1e8f; }
+
+FLEET_HD float steps_mul10(float X, Steps s) {
   float Y = X * 10.0f;
-  X = b0 ? Y : X;
+  Y = Y * 10.0f;
+  X = s.e ? Y : X;
+  Y = X * 10.0f;
+  X = s.b0 ? Y : X;
   Y = X * 10.0f;
   Y = Y * 10.0f;
-  X = b1 ? Y : X;
+  X = s.b1 ? Y : X;
   Y = X * 10.0f;
   Y = Y * 10.0f;
   Y = Y * 10.0f;
   Y = Y * 10.0f;
-  return b2 ? Y : X;
+  return s.b2 ? Y : X;
 }
-FLEET_HD float steps_div10(float t, bool b0, bool b1, bool b2) {
-  t = div10(div10(t));
-  float u = div10(t);
-  t = b0 ? u : t;
+FLEET_HD float steps_div10(float t, Steps s) {
+  float u = div10(div10(t));
+  t = s.e ? u : t;
+  u = div10(t);
+  t = s.b0 ? u : t;
   u = div10(div10(t));
-  t = b1 ? u : t;
+  t = s.b1 ? u : t;
   u = div10(div10(div10(div10(t))));
-  return b2 ? u : t;
+  return s.b2 ? u : t;
 }
-FLEET_HD f2 steps_mul10x2(f2 X, const bool (&b0)[2], const bool (&b1)[2], const bool (&b2)[2]) {
+FLEET_HD f2 sel2(bool a, bool b, f2 y, f2 x) { return f2{a ? y.x : x.x, b ? y.y : x.y}; }
+FLEET_HD f2 steps_mul10x2(f2 X, Steps s0, Steps s1) {
   const f2 ten = f2{10.0f, 10.0f};
-  X = X * ten;
-  X = X * ten;
   f2 Y = X * ten;
-  X = f2{b0[0] ? Y.x : X.x, b0[1] ? Y.y : X.y};
+  Y = Y * ten;
+  X = sel2(s0.e, s1.e, Y, X);
+  Y = X * ten;
+  X = sel2(s0.b0, s1.b0, Y, X);
   Y = X * ten;
   Y = Y * ten;
-  X = f2{b1[0] ? Y.x : X.x, b1[1] ? Y.y : X.y};
+  X = sel2(s0.b1, s1.b1, Y, X);
   Y = X * ten;
   Y = Y * ten;
   Y = Y * ten;
   Y = Y * ten;
-  return f2{b2[0] ? Y.x : X.x, b2[1] ? Y.y : X.y};
+  return sel2(s0.b2, s1.b2, Y, X);
 }
-FLEET_HD f2 steps_div10x2(f2 t, const bool (&b0)[2], const bool (&b1)[2], const bool (&b2)[2]) {
-  t = div10x2(div10x2(t));
-  f2 u = div10x2(t);
-  t = f2{b0[0] ? u.x : t.x, b0[1] ? u.y : t.y};
+FLEET_HD f2 steps_div10x2(f2 t, Steps s0, Steps s1) {
+  f2 u = div10x2(div10x2(t));
+  t = sel2(s0.e, s1.e, u, t);
+  u = div10x2(t);
+  t = sel2(s0.b0, s1.b0, u, t);
   u = div10x2(div10x2(t));
-  t = f2{b1[0] ? u.x : t.x, b1[1] ? u.y : t.y};
+  t = sel2(s0.b1, s1.b1, u, t);
   u = div10x2(div10x2(div10x2(div10x2(t))));
-  return f2{b2[0] ? u.x : t.x, b2[1] ? u.y : t.y};
+  return sel2(s0.b2, s1.b2, u, t);
 }
 
 // |code| = 10*(n/10) + d with n = trunc(|x| * 10^(9-d)) (Base64.cpp:104-108)
@@ -243,39 +264,27 @@ FLEET_HD float signed_code_float(uint32_t n, int d, float x) {
 }
 
 FLEET_HD float q_gen(float x, const DigitEntry* tab) {
-  const int d = digits_of(x, tab);
-  const uint32_t r = (uint32_t)(7 - d);
-  const bool b0 = r & 1u, b1 = r & 2u, b2 = r & 4u;
-  const float X = steps_mul10(__builtin_fabsf(x), b0, b1, b2);
-  return steps_div10(signed_code_float((uint32_t)X, d, x), b0, b1, b2);
+  const int d = tab ? digits_of(x, tab) : digits_cmp(x);
+  const Steps st = steps_of((uint32_t)(9 - d));
+  const float X = steps_mul10(__builtin_fabsf(x), st);
+  return steps_div10(signed_code_float((uint32_t)X, d, x), st);
 }
 FLEET_HD f2 q_gen2(f2 x, const DigitEntry* tab) {
   const int d0 = digits_of(x.x, tab), d1 = digits_of(x.y, tab);
-  const uint32_t r0 = (uint32_t)(7 - d0), r1 = (uint32_t)(7 - d1);
-  const bool b0[2] = {(r0 & 1u) != 0, (r1 & 1u) != 0};
-  const bool b1[2] = {(r0 & 2u) != 0, (r1 & 2u) != 0};
-  const bool b2[2] = {(r0 & 4u) != 0, (r1 & 4u) != 0};
-  const f2 X = steps_mul10x2(__builtin_elementwise_abs(x), b0, b1, b2);
+  const Steps s0 = steps_of((uint32_t)(9 - d0)), s1 = steps_of((uint32_t)(9 - d1));
+  const f2 X = steps_mul10x2(__builtin_elementwise_abs(x), s0, s1);
   const f2 t = f2{signed_code_float((uint32_t)X.x, d0, x.x), signed_code_float((uint32_t)X.y, d1, x.y)};
-  return steps_div10x2(t, b0, b1, b2);
+  return steps_div10x2(t, s0, s1);
 }
 
-// int2float(c) for |c % 10| <= 7 (k = 9 - |c % 10| >= 2 divisions)
+// int2float(c) for every code (k = 9 - |c % 10| in [0, 9]) -- total.
 FLEET_HD uint32_t last_digit(int32_t c) {
   uint32_t a = c < 0 ? 0u - (uint32_t)c : (uint32_t)c;
   return a - (a / 10u) * 10u;
 }
-FLEET_HD bool dec_gen_ok(int32_t c) { return last_digit(c) <= 7u; }
-FLEET_HD float dec_gen(int32_t c) {
-  const uint32_t r = 7u - last_digit(c);
-  return steps_div10((float)c, r & 1u, r & 2u, r & 4u);
-}
+FLEET_HD float dec_gen(int32_t c) { return steps_div10((float)c, steps_of(9u - last_digit(c))); }
 FLEET_HD f2 dec_gen2(int32_t c0, int32_t c1) {
-  const uint32_t r0 = 7u - last_digit(c0), r1 = 7u - last_digit(c1);
-  const bool b0[2] = {(r0 & 1u) != 0, (r1 & 1u) != 0};
-  const bool b1[2] = {(r0 & 2u) != 0, (r1 & 2u) != 0};
-  const bool b2[2] = {(r0 & 4u) != 0, (r1 & 4u) != 0};
-  return steps_div10x2(f2{(float)c0, (float)c1}, b0, b1, b2);
+  return steps_div10x2(f2{(float)c0, (float)c1}, steps_of(9u - last_digit(c0)), steps_of(9u - last_digit(c1)));
 }
 
 }  // namespace fleet

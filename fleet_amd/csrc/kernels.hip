@@ -8,6 +8,7 @@
 #include "kernels.h"
 
 #include <cstdlib>
+#include <cstring>
 
 #include "codec_device.h"
 
@@ -135,6 +136,19 @@ __device__ __forceinline__ void q_stage(float (&out)[S], const float (&x)[S], co
   resolve_slow<S, 1>(out, in, slow, ws, lane);
 }
 
+// Single value per thread on a latency-bound serial chain: same as q_stage<1>
+// but the digit count comes from compares (no LDS load inside the chain).
+__device__ __forceinline__ void q_stage_lat(float (&out)[1], const float (&x)[1], uint32_t* __restrict__ ws,
+                                            int lane) {
+  if (__ballot(!q_ok(x[0])) == 0) {
+    out[0] = q_fast(x[0]);
+    return;
+  }
+  out[0] = q_gen(x[0], nullptr);
+  uint32_t in[1] = {f2u(x[0])};
+  resolve_slow<1, 1>(out, in, (uint32_t)!q_gen_ok(x[0]), ws, lane);
+}
+
 // ----------------------------------------------------------------------------
 // Fused update: CppNNUpdater.update's aggregation (java:420-509) for the
 // groups [g_begin, g_end). Per value and client c, in CppNNUpdater order:
@@ -181,7 +195,9 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
 
   float acc[S];
   int32_t codes[S];
-  uint32_t bad[K];
+  uint32_t bad[K], need[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) need[k] = needed_chars_mask((int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g[k])));
 #pragma unroll
   for (int i = 0; i < S; ++i) acc[i] = 0.f;
 #pragma unroll
@@ -199,7 +215,12 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
       for (int k = 0; k < K; ++k) nxt[k] = *reinterpret_cast<const uint4*>(rowp[k] + (size_t)(c + 1) * pitch);
     }
 #pragma unroll
-    for (int k = 0; k < K; ++k) bad[k] |= b64_decode_group(cur[k], &tab, codes + 3 * k);
+    for (int k = 0; k < K; ++k) {
+      if (need[k] == 0xffffu)
+        bad[k] |= b64_decode_group_full(cur[k], &tab, codes + 3 * k);
+      else  // the partial last group: only the chars carrying its values must be valid
+        bad[k] |= b64_decode_group(cur[k], &tab, codes + 3 * k) & need[k];
+    }
 
     // Per stage and wave: if every value of the wave is inside the |x| < 1
     // fast domain, run the fixed 9-step chains; otherwise the 2+1+2+4-step
@@ -208,8 +229,6 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
     // stage A: y = Q(int2float(code))
     float y0[S], y[S];
     {
-      uint32_t in[S];
-      uint32_t slow = 0;
       bool all9 = true;
 #pragma unroll
       for (int i = 0; i < S; ++i) all9 &= dec9_ok(codes[i]);
@@ -229,12 +248,6 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
           y0[i + 1] = v.y;
         }
         if (S & 1) y0[S - 1] = dec_gen(codes[S - 1]);
-#pragma unroll
-        for (int i = 0; i < S; ++i) {
-          slow |= (uint32_t)!dec_gen_ok(codes[i]) << i;
-          in[i] = (uint32_t)codes[i];
-        }
-        resolve_slow<S, 2>(y0, in, slow, ws, lane);
       }
     }
     q_stage<S>(y, y0, tab.digits, ws, lane);
@@ -270,12 +283,12 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
     if (is_hdr[0] | is_hdr[1] | is_hdr[2]) {
       for (int c = 0; c < M - 1; ++c) {
         int32_t cc[3];
-        bad[k] |= b64_decode_group(*reinterpret_cast<const uint4*>(rowp[k] + (size_t)c * pitch), &tab, cc);
+        bad[k] |= b64_decode_group(*reinterpret_cast<const uint4*>(rowp[k] + (size_t)c * pitch), &tab, cc) & need[k];
         for (int e = 0; e < 3; ++e)
           if (is_hdr[e] && e < r && cc[e] != codes[3 * k + e]) layout_bad = 1;
       }
     }
-    if (bad[k] & needed_chars_mask(r)) atomicOr(err, FLEET_ERRBIT_BASE64);
+    if (bad[k]) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
     int32_t out[3];
 #pragma unroll
@@ -288,6 +301,157 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
     if (merged_f32) {
       for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec(out[e]);
     }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Two-phase tile variant for small buckets (MNIST: 7,654 groups -- too few
+// lanes to fill 1,024 SIMDs when every lane walks all clients serially).
+// A block owns TG groups (E = 3*TG values) and walks the clients in chunks
+// of CM:
+//   phase 1 -- all 256 threads: p[c][e] = Q(f32(f64(Q(dec(code))) * d_c)) for
+//              every (client, group) item of the chunk, into LDS. These are
+//              independent across clients (CppNNUpdater.java:463-464).
+//   phase 2 -- one thread per value: the serial A = Q(A + p_c) (:490-493),
+//              the only part that must follow client order.
+template <int TG>
+__global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                      const double* __restrict__ dampen, double inv_avg,
+                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
+                                                      const int32_t* __restrict__ hdr_block,
+                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                      int* __restrict__ err) {
+  constexpr int E = 3 * TG;
+  constexpr int CM = 6144 / E;  // 24 KiB of p per chunk
+  constexpr int S = 6;          // two items per thread per pass
+  __shared__ B64Tables tab;
+  __shared__ float ptile[CM * E];
+  __shared__ uint32_t scratch[4][64 * S];
+  __shared__ int32_t last_codes[E];
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int tid = threadIdx.x, lane = tid & 63;
+  uint32_t* ws = scratch[tid >> 6];
+  const int64_t g0 = g_begin + (int64_t)blockIdx.x * TG;
+  const int ng = (int)min<int64_t>(TG, g_end - g0);
+
+  float A = 0.f;  // phase-2 value: element tid of the tile (tid < E)
+  uint32_t badacc = 0;
+  for (int c0 = 0; c0 < M; c0 += CM) {
+    const int cm = min(CM, M - c0);
+    const int nitems = cm * TG;
+    for (int base = 0; base < nitems; base += 512) {
+      int32_t codes[S];
+      int cc[2], gl[2];
+      bool live[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int item = base + h * 256 + tid;
+        live[h] = item < nitems && (item % TG) < ng;
+        cc[h] = live[h] ? item / TG : 0;
+        gl[h] = live[h] ? item % TG : 0;
+        const uint4 w = *reinterpret_cast<const uint4*>(uploads + (size_t)(c0 + cc[h]) * pitch + 16 * (g0 + gl[h]));
+        const int r = (int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * (g0 + gl[h])));
+        uint32_t b;
+        if (r == 3)
+          b = b64_decode_group_full(w, &tab, codes + 3 * h);
+        else
+          b = b64_decode_group(w, &tab, codes + 3 * h) & needed_chars_mask(r);
+        if (live[h]) {
+          badacc |= b;
+          if (c0 + cc[h] == M - 1)
+            for (int e = 0; e < 3; ++e) last_codes[3 * gl[h] + e] = codes[3 * h + e];
+        }
+      }
+      // stage A
+      float y0[S], y[S];
+      {
+        bool all9 = true;
+#pragma unroll
+        for (int i = 0; i < S; ++i) all9 &= dec9_ok(codes[i]);
+        if (__ballot(!all9) == 0) {
+#pragma unroll
+          for (int i = 0; i < S; i += 2) {
+            const f2 v = dec_fast2(codes[i], codes[i + 1]);
+            y0[i] = v.x;
+            y0[i + 1] = v.y;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < S; i += 2) {
+            const f2 v = dec_gen2(codes[i], codes[i + 1]);
+            y0[i] = v.x;
+            y0[i + 1] = v.y;
+          }
+        }
+      }
+      q_stage<S>(y, y0, tab.digits, ws, lane);
+      // stage B (per-item client: dampening factor is a per-lane load)
+      float r[S], p[S];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const double d = dampen[c0 + cc[h]];
+#pragma unroll
+        for (int e = 0; e < 3; ++e) r[3 * h + e] = (float)((double)y[3 * h + e] * d);
+      }
+      q_stage<S>(p, r, tab.digits, ws, lane);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (live[h])
+#pragma unroll
+          for (int e = 0; e < 3; ++e) ptile[cc[h] * E + 3 * gl[h] + e] = p[3 * h + e];
+    }
+    __syncthreads();
+    // phase 2: serial accumulation, one value per thread
+    if (tid < E) {
+      for (int k = 0; k < cm; ++k) {
+        const float pk = ptile[k * E + tid];
+        if (c0 + k == 0) {
+          A = pk;
+        } else {
+          float sm[1] = {A + pk}, o[1];
+          q_stage_lat(o, sm, ws, lane);
+          A = o[0];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (badacc) atomicOr(err, FLEET_ERRBIT_BASE64);
+  // gather the tile's final values per group
+  if (tid < E) ptile[tid] = A;
+  __syncthreads();
+  if (tid >= ng) return;
+  const int n_hdr = hdr_block[1];
+  const int64_t walk_end = hdr_block[2];
+  const int32_t* hdr = hdr_block + 4;
+  const int64_t g = g0 + tid;
+  const int64_t p0 = 3 * g;
+  const int r = (int)min<int64_t>(3, n_up - p0);
+  bool is_hdr[3];
+  headers_in_group(hdr, n_hdr, p0, is_hdr);
+  int layout_bad = 0;
+  uint32_t bad = 0;
+  if (is_hdr[0] | is_hdr[1] | is_hdr[2]) {
+    for (int c = 0; c < M - 1; ++c) {
+      int32_t cc3[3];
+      bad |= b64_decode_group(*reinterpret_cast<const uint4*>(uploads + (size_t)c * pitch + 16 * g), &tab, cc3);
+      for (int e = 0; e < 3; ++e)
+        if (is_hdr[e] && e < r && cc3[e] != last_codes[3 * tid + e]) layout_bad = 1;
+    }
+  }
+  if (bad & needed_chars_mask(r)) atomicOr(err, FLEET_ERRBIT_BASE64);
+  if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+  int32_t out[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    const bool keep_last = is_hdr[e] || p0 + e >= walk_end;
+    const int32_t o = keep_last ? enc(dec(last_codes[3 * tid + e])) : enc(q((float)((double)ptile[3 * tid + e] * inv_avg)));
+    out[e] = e < r ? o : 0;
+  }
+  *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &tab), r);
+  if (merged_f32) {
+    for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec(out[e]);
   }
 }
 
@@ -526,11 +690,26 @@ int update_groups_per_lane(int64_t groups) {
   return 1;
 }
 
+// FLEET_UPDATE_MODE = stream | tiled | auto (default: tiled below ~2 waves per SIMD of stream lanes)
+static bool use_tiled(int64_t groups) {
+  if (const char* e = getenv("FLEET_UPDATE_MODE")) {
+    if (!strcmp(e, "tiled")) return true;
+    if (!strcmp(e, "stream")) return false;
+  }
+  return groups < 256LL * 4 * 2 * 64;
+}
+
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
   if (g_end <= g_begin) return hipSuccess;
   const int64_t groups = g_end - g_begin;
+  if (use_tiled(groups)) {
+    constexpr int TG = 32;
+    hipLaunchKernelGGL(k_update_tiled<TG>, dim3((unsigned)((groups + TG - 1) / TG)), dim3(256), 0, s, uploads, pitch,
+                       M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
+    return hipGetLastError();
+  }
   const int K = update_groups_per_lane(groups);
   const unsigned blocks = (unsigned)((groups + 256 * K - 1) / (256 * K));
   if (K >= 4)
@@ -660,16 +839,14 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
               use = (u & 0x7fffffffu) < 0x3f800000u; o = use ? f2u(v.x) + 3u * f2u(v.y) : 0u; break; }
       case 6: use = q_gen_ok(u2f(u));                                 // variable-length Q, numDigits <= 7
               o = use ? f2u(q_gen(u2f(u), dig)) : 0u; break;
-      case 7: use = dec_gen_ok((int32_t)u);                           // variable-length int2float
-              o = use ? f2u(dec_gen((int32_t)u)) : 0u; break;
+      case 7: o = f2u(dec_gen((int32_t)u)); break;                    // variable-length int2float (total)
       case 8: { const float x = u2f(u);                               // packed variable-length Q on (x, -x/4)
               use = q_gen_ok(x) && q_gen_ok(-0.25f * x);
               const f2 v = q_gen2(f2{x, -0.25f * x}, dig);
               o = use ? f2u(v.x) + 3u * f2u(v.y) : 0u; break; }
       case 9: { const int32_t c = (int32_t)u, c2 = (int32_t)(u * 2654435761u);  // packed int2float
-              use = dec_gen_ok(c) && dec_gen_ok(c2);
               const f2 v = dec_gen2(c, c2);
-              o = use ? f2u(v.x) + 3u * f2u(v.y) : 0u; break; }
+              o = f2u(v.x) + 3u * f2u(v.y); break; }
       default: o = 0; use = false;
     }
     if (use) sum += splitmix64(((uint64_t)u << 32) | o);

@@ -38,14 +38,12 @@ static uint64_t digest(int fn) {
           case 3: use = ((int32_t)u % 10) == 0; if (use) o = f2u(fo_int2float((int32_t)u)); break;
           case 4: use = u >= 0x0DA24260u && u < 0x7F800000u; if (use) o = f2u(u2f(u) / 10.0f); break;
           case 5: use = (u & 0x7fffffffu) < 0x3f800000u; if (use) o = f2u(Q(u2f(u))) + 3u * f2u(Q(-u2f(u))); break;
-          case 6: { float x = u2f(u); use = x < 1e7f && x > -1e6f; if (use) o = f2u(Q(x)); break; }
-          case 7: { int32_t c = (int32_t)u; int dd = c % 10; dd = dd < 0 ? -dd : dd; use = dd <= 7;
-                    if (use) o = f2u(fo_int2float(c)); break; }
+          case 6: { float x = u2f(u); use = x < 1e9f && x > -1e8f; if (use) o = f2u(Q(x)); break; }
+          case 7: o = f2u(fo_int2float((int32_t)u)); break;
           case 8: { float x = u2f(u), x2 = -0.25f * x;
-                    use = x < 1e7f && x > -1e6f && x2 < 1e7f && x2 > -1e6f; if (use) o = f2u(Q(x)) + 3u * f2u(Q(x2)); break; }
+                    use = x < 1e9f && x > -1e8f && x2 < 1e9f && x2 > -1e8f; if (use) o = f2u(Q(x)) + 3u * f2u(Q(x2)); break; }
           case 9: { int32_t c = (int32_t)u, c2 = (int32_t)(u * 2654435761u);
-                    int a = c % 10, b = c2 % 10; a = a < 0 ? -a : a; b = b < 0 ? -b : b; use = a <= 7 && b <= 7;
-                    if (use) o = f2u(fo_int2float(c)) + 3u * f2u(fo_int2float(c2)); break; }
+                    o = f2u(fo_int2float(c)) + 3u * f2u(fo_int2float(c2)); break; }
         }
         if (use) sum += splitmix64(((uint64_t)u << 32) | o);
       }

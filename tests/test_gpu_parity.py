@@ -220,3 +220,16 @@ def test_update_large_magnitudes_slow_path(codec, oracle):
     d = [1.0, 7.5, 0.25, 10.0, 1 / 3, 1.0]
     hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm) == oracle.update_faithful(ups, d)
+
+
+@pytest.mark.parametrize("mode", ["tiled", "stream"])
+def test_update_modes(codec, oracle, monkeypatch, mode):
+    """Both aggregation kernels (two-phase tiled for small buckets, streaming
+    for large ones) on ragged tiles, chunked client loops and every layout."""
+    monkeypatch.setenv("FLEET_UPDATE_MODE", mode)
+    for lay, M in ((MNIST, 70), (synthetic(1000), 1), (synthetic(3001), 129), (synthetic(5002), 2),
+                   (CIFAR10, 3)):
+        ups = uploads_for(oracle, lay, M, seed=M)
+        d = policy("inverse", M)
+        hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+        assert codec.update(ups, d) == oracle.update_fused(ups, d, hm), (lay.name, M)
