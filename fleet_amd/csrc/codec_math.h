@@ -263,11 +263,31 @@ FLEET_HD float signed_code_float(uint32_t n, int d, float x) {
   return u2f(f2u((float)c) | (f2u(x) & 0x80000000u));
 }
 
-FLEET_HD float q_gen(float x, const DigitEntry* tab) {
-  const int d = tab ? digits_of(x, tab) : digits_cmp(x);
+FLEET_HD float q_gen_d(float x, int d) {
   const Steps st = steps_of((uint32_t)(9 - d));
   const float X = steps_mul10(__builtin_fabsf(x), st);
   return steps_div10(signed_code_float((uint32_t)X, d, x), st);
+}
+// table lookup for the digit count (throughput paths) / compares (latency paths)
+FLEET_HD float q_gen(float x, const DigitEntry* tab) { return q_gen_d(x, digits_of(x, tab)); }
+FLEET_HD float q_gen_lat(float x) { return q_gen_d(x, digits_cmp(x)); }
+
+// float2int(x) on the q_gen domain: the code itself (client-side encode)
+FLEET_HD int32_t enc_gen(float x, const DigitEntry* tab) {
+  const int d = digits_of(x, tab);
+  const float X = steps_mul10(__builtin_fabsf(x), steps_of((uint32_t)(9 - d)));
+  const uint32_t n = (uint32_t)X;
+  const uint32_t c = (n / 10u) * 10u + (uint32_t)d;
+  return x < 0.0f ? -(int32_t)c : (int32_t)c;
+}
+// float2int(x) for |x| < 1: 9 multiplications, last digit 0
+FLEET_HD int32_t enc_fast(float x) {
+  float X = __builtin_fabsf(x);
+#pragma unroll
+  for (int j = 0; j < 9; ++j) X = X * 10.0f;
+  const uint32_t n = (uint32_t)X;
+  const uint32_t c = (n / 10u) * 10u;
+  return x < 0.0f ? -(int32_t)c : (int32_t)c;
 }
 FLEET_HD f2 q_gen2(f2 x, const DigitEntry* tab) {
   const int d0 = digits_of(x.x, tab), d1 = digits_of(x.y, tab);

@@ -144,7 +144,7 @@ __device__ __forceinline__ void q_stage_lat(float (&out)[1], const float (&x)[1]
     out[0] = q_fast(x[0]);
     return;
   }
-  out[0] = q_gen(x[0], nullptr);
+  out[0] = q_gen_lat(x[0]);
   uint32_t in[1] = {f2u(x[0])};
   resolve_slow<1, 1>(out, in, (uint32_t)!q_gen_ok(x[0]), ws, lane);
 }
@@ -467,9 +467,22 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
   const int64_t row_id = blockIdx.y;
   const float* v = values + row_id * vpitch + 3 * g;
   const int r = (int)min<int64_t>(3, n - 3 * g);
-  int32_t codes[3];
+  float x[3];
 #pragma unroll
-  for (int e = 0; e < 3; ++e) codes[e] = e < r ? enc(v[e]) : 0;
+  for (int e = 0; e < 3; ++e) x[e] = e < r ? v[e] : 0.0f;
+  int32_t codes[3];
+  const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
+  if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_gen(x[e], tab.digits);
+    if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
+#pragma unroll
+      for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
+    }
+  }
   *reinterpret_cast<uint4*>(out + row_id * pitch + 16 * g) = pad_group(b64_encode_group(codes, &tab), r);
 }
 
@@ -705,9 +718,15 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
   if (g_end <= g_begin) return hipSuccess;
   const int64_t groups = g_end - g_begin;
   if (use_tiled(groups)) {
-    constexpr int TG = 32;
-    hipLaunchKernelGGL(k_update_tiled<TG>, dim3((unsigned)((groups + TG - 1) / TG)), dim3(256), 0, s, uploads, pitch,
-                       M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
+    int tg = 32;
+    if (const char* e = getenv("FLEET_TILE_G")) tg = atoi(e);
+#define FLEET_LAUNCH_TILED(TG)                                                                                     \
+  hipLaunchKernelGGL(k_update_tiled<TG>, dim3((unsigned)((groups + TG - 1) / TG)), dim3(256), 0, s, uploads, pitch, \
+                     M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
+    if (tg == 16) FLEET_LAUNCH_TILED(16);
+    else if (tg == 64) FLEET_LAUNCH_TILED(64);
+    else FLEET_LAUNCH_TILED(32);
+#undef FLEET_LAUNCH_TILED
     return hipGetLastError();
   }
   const int K = update_groups_per_lane(groups);
@@ -847,6 +866,10 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
       case 9: { const int32_t c = (int32_t)u, c2 = (int32_t)(u * 2654435761u);  // packed int2float
               const f2 v = dec_gen2(c, c2);
               o = f2u(v.x) + 3u * f2u(v.y); break; }
+      case 10: use = q_gen_ok(u2f(u));                                // variable-length float2int
+               o = use ? (uint32_t)enc_gen(u2f(u), dig) : 0u; break;
+      case 11: use = (u & 0x7fffffffu) < 0x3f800000u;                 // float2int fast path, |x| < 1
+               o = use ? (uint32_t)enc_fast(u2f(u)) : 0u; break;
       default: o = 0; use = false;
     }
     if (use) sum += splitmix64(((uint64_t)u << 32) | o);

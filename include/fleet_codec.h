@@ -148,6 +148,7 @@ int fleet_check(fleet_ctx* ctx, void* stream);
  *   fn 4: t/10 (div10) for 1e-30 <= t < inf  fn 5: packed Q fast path
  *   fn 6: variable-length Q (-1e8 < x < 1e9)  fn 7: variable-length int2float (all codes)
  *   fn 8: packed fn 6 on (x, -x/4)            fn 9: packed fn 7 on (c, c*2654435761)
+ *   fn 10: variable-length float2int (-1e8 < x < 1e9)   fn 11: float2int fast path (|x| < 1)
  * computed on the GPU; compare with the oracle's digests. */
 int fleet_selftest_digest(fleet_ctx* ctx, int fn, uint64_t* out);
 

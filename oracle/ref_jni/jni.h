@@ -8,7 +8,9 @@
  *
  * Used surface (grep env-> in cppNN_backend.cpp): GetArrayLength,
  * Get/ReleaseByteArrayElements, NewByteArray, SetByteArrayRegion,
- * GetDoubleArrayElements, Get/ReleaseStringUTFChars, DeleteLocalRef.
+ * GetDoubleArrayElements, Get/ReleaseStringUTFChars, DeleteLocalRef; plus
+ * GetObjectArrayElement / ReleaseDoubleArrayElements for the test build of
+ * fleet_amd's JNI shim (jni_shim.cpp).
  *
  * Arrays are heap blocks {len, payload}. GetByteArrayElements hands out a
  * NUL-terminated copy: the reference reads JVM arrays as C strings
@@ -43,9 +45,11 @@ struct fake_jarray_hdr {
 
 struct _jbyteArray : _jobject {};
 struct _jdoubleArray : _jobject {};
+struct _jobjectArray : _jobject {};
 struct _jstring : _jobject {};
 typedef _jbyteArray* jbyteArray;
 typedef _jdoubleArray* jdoubleArray;
+typedef _jobjectArray* jobjectArray;
 typedef _jstring* jstring;
 typedef _jobject* jarray;
 
@@ -81,6 +85,8 @@ struct JNIEnv {
   jdouble* GetDoubleArrayElements(jdoubleArray a, jboolean*) {
     return (jdouble*)fakejni::payload(a);
   }
+  void ReleaseDoubleArrayElements(jdoubleArray, jdouble*, jint) {}
+  jobject GetObjectArrayElement(jobjectArray a, jsize i) { return ((jobject*)fakejni::payload(a))[i]; }
   const char* GetStringUTFChars(jstring s, jboolean*) { return fakejni::payload(s); }
   void ReleaseStringUTFChars(jstring, const char*) {}
   void DeleteLocalRef(void*) {}

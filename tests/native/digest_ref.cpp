@@ -44,6 +44,8 @@ static uint64_t digest(int fn) {
                     use = x < 1e9f && x > -1e8f && x2 < 1e9f && x2 > -1e8f; if (use) o = f2u(Q(x)) + 3u * f2u(Q(x2)); break; }
           case 9: { int32_t c = (int32_t)u, c2 = (int32_t)(u * 2654435761u);
                     o = f2u(fo_int2float(c)) + 3u * f2u(fo_int2float(c2)); break; }
+          case 10: { float x = u2f(u); use = x < 1e9f && x > -1e8f; if (use) o = (uint32_t)fo_float2int(x); break; }
+          case 11: use = (u & 0x7fffffffu) < 0x3f800000u; if (use) o = (uint32_t)fo_float2int(u2f(u)); break;
         }
         if (use) sum += splitmix64(((uint64_t)u << 32) | o);
       }
@@ -59,9 +61,9 @@ int main(int argc, char** argv) {
   const char* path = argc > 1 ? argv[1] : "tests/golden/digests.json";
   FILE* f = fopen(path, "w");
   fprintf(f, "{\n  \"generator\": \"tests/native/digest_ref.cpp over oracle/fleet_oracle.c\",\n");
-  for (int fn = 0; fn <= 9; ++fn) {
+  for (int fn = 0; fn <= 11; ++fn) {
     uint64_t d = digest(fn);
-    fprintf(f, "  \"fn%d\": \"%016llx\"%s\n", fn, (unsigned long long)d, fn < 9 ? "," : "");
+    fprintf(f, "  \"fn%d\": \"%016llx\"%s\n", fn, (unsigned long long)d, fn < 11 ? "," : "");
     printf("fn%d %016llx\n", fn, (unsigned long long)d);
     fflush(stdout);
   }

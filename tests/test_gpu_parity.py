@@ -182,7 +182,7 @@ def test_device_synth_and_encode(codec, oracle):
         assert np.array_equal(b[c, : lay.n_up].view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
 
 
-@pytest.mark.parametrize("fn", range(10))
+@pytest.mark.parametrize("fn", range(12))
 def test_device_codec_exhaustive_digest(codec, fn):
     """Every input of each device codec function's domain (2^32 codes / bit
     patterns), digested on the GPU, equals the oracle's digest."""
