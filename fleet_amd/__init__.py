@@ -308,16 +308,28 @@ class Codec:
 
     # -- device-resident (torch tensors on this device) -----------------------
     def update_device(self, uploads_u8, length: int, dampen: Sequence[float], header_pos, merged_u8,
-                      merged_f32=None, group_begin: int = 0, group_end: Optional[int] = None, stream=None):
-        """uploads_u8: uint8 CUDA tensor [M, pitch]; merged_u8: uint8 [>= 16*groups]."""
+                      merged_f32=None, group_begin: int = 0, group_end: Optional[int] = None, stream=None,
+                      window: bool = False):
+        """uploads_u8: uint8 CUDA tensor [M, pitch]; merged_u8: uint8 [>= 16*groups].
+
+        window=False: the tensors hold whole rows (group 0 at column 0).
+        window=True: they hold only the groups [group_begin, group_end) of every
+        row (uploads [M, >= 16*(ge-gb)], merged [16*(ge-gb)], merged_f32
+        [3*(ge-gb)]); header_pos stay in whole-upload coordinates."""
         M, pitch = uploads_u8.shape
         groups = (b64_count(length) + 2) // 3
-        ge = groups if group_end is None else group_end
+        ge = groups if group_end is None else min(group_end, groups)
         hp = np.ascontiguousarray(header_pos, dtype=np.int32)
         d = np.ascontiguousarray(dampen, dtype=np.float64)
-        rc = self._L.fleet_update_device(self._h, uploads_u8.data_ptr(), pitch, length, M, d.ctypes.data,
-                                         hp.ctypes.data, len(hp), group_begin, ge, merged_u8.data_ptr(),
-                                         merged_f32.data_ptr() if merged_f32 is not None else None,
+        shift_b = 16 * group_begin if window else 0
+        shift_f = 3 * 4 * group_begin if window else 0
+        if window:
+            w = ge - group_begin
+            if pitch < 16 * w or merged_u8.numel() < 16 * w or (merged_f32 is not None and merged_f32.numel() < 3 * w):
+                raise ValueError("window tensors smaller than the selected groups")
+        rc = self._L.fleet_update_device(self._h, uploads_u8.data_ptr() - shift_b, pitch, length, M, d.ctypes.data,
+                                         hp.ctypes.data, len(hp), group_begin, ge, merged_u8.data_ptr() - shift_b,
+                                         merged_f32.data_ptr() - shift_f if merged_f32 is not None else None,
                                          _stream(stream))
         self._check(rc)
 

@@ -253,9 +253,10 @@ int fleet_layout_parse(fleet_ctx* c, const char* upload, size_t len, int32_t* he
   size_t n = fleet_b64_count(len);
   if ((rc = stage_text(c, upload, len, &c->d_a, &c->d_a_cap))) return rc;
   int nh = 0;
-  if ((rc = parse_layout(c, c->d_a, n, &nh))) return rc;
+  size_t walk_end = n;
+  if ((rc = parse_layout(c, c->d_a, n, &nh, &walk_end))) return rc;
   if (n_headers) *n_headers = nh;
-  if (n_up) *n_up = n;
+  if (n_up) *n_up = walk_end;
   if (header_pos) std::memcpy(header_pos, c->h_hdr + 4, sizeof(int32_t) * std::min(nh, cap));
   return nh <= cap ? FLEET_OK : FLEET_ERR_CAPACITY;
 }
@@ -464,7 +465,6 @@ int fleet_update_device(fleet_ctx* c, const void* d_uploads, size_t pitch, size_
   if (!c || !d_uploads || !dampen || M <= 0 || !d_merged || n_headers < 0 || n_headers > FLEET_MAX_HEADERS ||
       (n_headers && !header_pos))
     return FLEET_ERR_ARG;
-  if (pitch % 16 != 0 || pitch < round16(len)) return fail(c, FLEET_ERR_ARG, "pitch must be a multiple of 16 >= len");
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   int rc = check_text_len(c, len);
@@ -473,6 +473,10 @@ int fleet_update_device(fleet_ctx* c, const void* d_uploads, size_t pitch, size_
   const size_t groups = groups_of(n);
   if (group_end > groups) group_end = groups;
   if (group_begin > group_end) return FLEET_ERR_ARG;
+  // only columns [16*group_begin, 16*group_end) of each row are touched: rows
+  // must not overlap there (a full row, or a window of just those columns)
+  if (pitch % 16 != 0 || pitch < 16 * (group_end - group_begin))
+    return fail(c, FLEET_ERR_ARG, "pitch must be a multiple of 16 covering the selected groups");
   hipStream_t s = pick(c, stream);
   // {status, count, walk_end, 0, positions}: the caller's layout covers the whole upload
   std::vector<int32_t> hdr_words((size_t)n_headers + 4);

@@ -718,7 +718,9 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
   if (g_end <= g_begin) return hipSuccess;
   const int64_t groups = g_end - g_begin;
   if (use_tiled(groups)) {
-    int tg = 32;
+    // widest tile that still gives >= 4 blocks per CU (phase 2 is one wave per
+    // block walking the clients serially: more, narrower tiles hide its latency)
+    int tg = groups >= 64LL * 1024 ? 64 : groups >= 32LL * 1024 ? 32 : 16;
     if (const char* e = getenv("FLEET_TILE_G")) tg = atoi(e);
 #define FLEET_LAUNCH_TILED(TG)                                                                                     \
   hipLaunchKernelGGL(k_update_tiled<TG>, dim3((unsigned)((groups + TG - 1) / TG)), dim3(256), 0, s, uploads, pitch, \

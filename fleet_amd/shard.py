@@ -1,0 +1,124 @@
+"""Element-range sharding of the aggregation over the GPUs of a node.
+
+The per-element chain of CppNNUpdater.update (CppNNUpdater.java:420-509) is
+serial across clients but independent across elements, so rank r of N owns a
+contiguous range of 16-char / 3-value Base64 groups of EVERY upload, runs the
+exact chain there (fleet_update_device on just that window), and the merged
+slices are all-gathered -- RCCL over xGMI with the "nccl" backend, gloo on CPU.
+No reduction crosses ranks, so the result is byte-identical to one GPU's; a
+client-sharded sum would reorder the re-quantised adds and is not offered.
+
+One process per GPU (torch.distributed); every rank receives the full merged
+Base64 (the reference returns it to the Java updater on the server host).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import b64_count
+
+
+def group_range(groups: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous, balanced split of `groups` 3-value groups: [begin, end) of `rank`."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"rank {rank} outside world {world}")
+    base, rem = divmod(groups, world)
+    begin = rank * base + min(rank, rem)
+    return begin, begin + base + (1 if rank < rem else 0)
+
+
+def byte_range(length: int, begin: int, end: int) -> Tuple[int, int]:
+    """Base64 bytes of groups [begin, end) in a text of `length` bytes."""
+    return min(length, 16 * begin), min(length, 16 * end)
+
+
+def gather_slices(local, sizes: Sequence[int], group=None):
+    """All-gather variable-sized uint8 slices in rank order into one tensor.
+
+    Slices are padded to the largest one so a single all_gather_into_tensor
+    (one RCCL call over xGMI) moves them; sizes are known to every rank."""
+    import torch
+    import torch.distributed as dist
+    world = len(sizes)
+    mx = max(sizes) if sizes else 0
+    buf = torch.zeros(max(mx, 1), dtype=torch.uint8, device=local.device)
+    buf[: local.numel()] = local
+    out = torch.empty(world * buf.numel(), dtype=torch.uint8, device=local.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    return torch.cat([out[r * buf.numel(): r * buf.numel() + sizes[r]] for r in range(world)])
+
+
+class ShardedUpdater:
+    """One rank's part of an N-GPU fused update (host uploads in, merged Base64 out).
+
+    update(uploads, dampen) has CppNNUpdater.update's aggregation semantics
+    (fleet_update): the same bytes on every rank, whatever N."""
+
+    def __init__(self, codec, group=None, device=None):
+        import torch
+        import torch.distributed as dist
+        self.codec = codec
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+
+    # -- per-rank compute (HIP); the CPU tests substitute these two ---------
+    def layout(self, last_upload: bytes) -> List[int]:
+        """Header slots of the last picked upload (network::flatGrad walk, on device)."""
+        pos, walk_end = self.codec.layout_parse(last_upload)
+        n = b64_count(len(last_upload))
+        # slots past the walk come from the last upload, exactly like header slots
+        return [int(p) for p in pos] + list(range(walk_end, n))
+
+    def local_update(self, window: np.ndarray, length: int, dampen, header_pos, begin: int, end: int):
+        """Merged Base64 of groups [begin, end) from a host window [M, 16*(end-begin)]."""
+        import torch
+        dev = torch.from_numpy(window).pin_memory().to(self.device, non_blocking=True)
+        merged = torch.empty(16 * (end - begin), dtype=torch.uint8, device=self.device)
+        self.codec.update_device(dev, length, dampen, header_pos, merged, None, begin, end, window=True)
+        self.codec.check()
+        return merged
+
+    # -----------------------------------------------------------------------
+    def update(self, uploads: Sequence[bytes], dampen: Sequence[float]) -> bytes:
+        import torch
+        import torch.distributed as dist
+        M = len(uploads)
+        if M == 0 or len(dampen) != M:
+            raise ValueError("need one dampening factor per upload")
+        L = len(uploads[0])
+        if any(len(u) != L for u in uploads):
+            raise ValueError("uploads differ in length (one layout per update)")
+        groups = (b64_count(L) + 2) // 3
+        begin, end = group_range(groups, self.world, self.rank)
+        b0, b1 = byte_range(L, begin, end)
+        status = 0
+        local = torch.zeros(b1 - b0, dtype=torch.uint8, device=self.device)
+        err: Optional[BaseException] = None
+        try:
+            hpos = self.layout(uploads[-1])
+            window = np.zeros((M, 16 * (end - begin)), np.uint8)
+            for c, u in enumerate(uploads):
+                window[c, : b1 - b0] = np.frombuffer(u, np.uint8, count=b1 - b0, offset=b0)
+            if end > begin:
+                local = self.local_update(window, L, dampen, hpos, begin, end)[: b1 - b0]
+        except Exception as e:  # keep the ranks in step: every rank raises together below
+            err, status = e, 1
+        if self.world > 1:
+            flag = torch.tensor([status], dtype=torch.int32, device=self.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+            status = int(flag.item())
+        if status:
+            if err is not None:
+                raise err
+            raise RuntimeError("fleet update failed on another rank")
+        if self.world == 1:
+            return local.cpu().numpy().tobytes()
+        sizes = [byte_range(L, *group_range(groups, self.world, r)) for r in range(self.world)]
+        full = gather_slices(local, [s1 - s0 for s0, s1 in sizes], self.group)
+        return full.cpu().numpy().tobytes()

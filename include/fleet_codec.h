@@ -69,7 +69,9 @@ size_t fleet_b64_count(size_t len);
 int fleet_layout_from_sizes(const int32_t* w_sizes, int n_w, const int32_t* b_sizes, int n_b,
                             int32_t* header_pos, int cap, int* n_headers, size_t* n_up);
 /* Same, parsed from an upload (Base64 host buffer) by decoding its header
- * slots on the device, exactly as network::flatGrad walks them (:1206-1223). */
+ * slots on the device, exactly as network::flatGrad walks them (:1206-1223).
+ * *n_up = the floats the walk covers (= the upload's count for gradients()
+ * output); slots past it are carried from the last upload, like headers. */
 int fleet_layout_parse(fleet_ctx* ctx, const char* upload, size_t len, int32_t* header_pos, int cap,
                        int* n_headers, size_t* n_up);
 
@@ -119,7 +121,12 @@ int fleet_update(fleet_ctx* ctx, const char* const* uploads, const size_t* lens,
  * select the 16-char / 3-value groups this call processes (element-range
  * sharding; [0, ceil(len/16)) = everything). `dampen` is a host array of M
  * doubles. Outputs are written for the selected groups only: merged Base64
- * at byte 16*g, merged_f32 (nullable) at value 3*g. */
+ * at byte 16*g, merged_f32 (nullable) at value 3*g.
+ * Only bytes [16*group_begin, 16*group_end) of each row (and of d_merged,
+ * values [3*group_begin, 3*group_end) of d_merged_f32) are dereferenced, so a
+ * rank holding just its window of every upload passes the window's address
+ * minus 16*group_begin (3*group_begin floats for merged_f32) and pitch >=
+ * 16*(group_end - group_begin): fleet_amd/shard.py does exactly that. */
 int fleet_update_device(fleet_ctx* ctx, const void* d_uploads, size_t pitch, size_t len, int M,
                         const double* dampen, const int32_t* header_pos, int n_headers, size_t group_begin,
                         size_t group_end, void* d_merged, void* d_merged_f32, void* stream);

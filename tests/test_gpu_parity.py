@@ -233,3 +233,37 @@ def test_update_modes(codec, oracle, monkeypatch, mode):
         d = policy("inverse", M)
         hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
         assert codec.update(ups, d) == oracle.update_fused(ups, d, hm), (lay.name, M)
+
+
+def test_device_window_update(codec, oracle):
+    """A rank holding only its column window of every upload (fleet_amd.shard)."""
+    torch = pytest.importorskip("torch")
+    from fleet_amd.shard import ShardedUpdater, byte_range, group_range
+    lay = MNIST
+    M = 5
+    ups = uploads_for(oracle, lay, M, seed=21)
+    L = len(ups[0])
+    d = policy("exp", M)
+    hp = lay.header_positions()
+    groups = (F.b64_count(L) + 2) // 3
+    exp = oracle.update_faithful(ups, d)
+    parts = []
+    for r in range(3):
+        gb, ge = group_range(groups, 3, r)
+        b0, b1 = byte_range(L, gb, ge)
+        win = np.zeros((M, 16 * (ge - gb)), np.uint8)
+        for c, u in enumerate(ups):
+            win[c, : b1 - b0] = np.frombuffer(u, np.uint8)[b0:b1]
+        dev = torch.from_numpy(win).cuda()
+        out = torch.zeros(16 * (ge - gb), dtype=torch.uint8, device="cuda")
+        f32 = torch.zeros(3 * (ge - gb), dtype=torch.float32, device="cuda")
+        codec.update_device(dev, L, d, hp, out, f32, gb, ge, window=True)
+        codec.check()
+        torch.cuda.synchronize()
+        parts.append(out.cpu().numpy()[: b1 - b0].tobytes())
+        n_loc = min(lay.n_up, 3 * ge) - 3 * gb
+        assert np.array_equal(f32.cpu().numpy()[:n_loc].view(np.uint32),
+                              oracle.decode_floats(exp)[3 * gb: 3 * gb + n_loc].view(np.uint32))
+    assert b"".join(parts) == exp
+    # the single-rank driver (no process group): same bytes
+    assert ShardedUpdater(codec).update(ups, d) == exp
