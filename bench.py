@@ -147,6 +147,48 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world):
     return res
 
 
+def pmc_traffic(workload: str):
+    """HBM bytes per k_update launch for `workload` from the newest committed
+    rocprofv3 PMC summary (profiles/rNN/traffic.json, written by
+    scripts/pmc_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE passes,
+    FETCH_SIZE doubled per the gfx950 correction). None when absent."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+        try:
+            with open(path) as f:
+                kern = json.load(f)["workloads"].get(workload, {})
+        except (OSError, ValueError, KeyError):
+            continue
+        for k, v in kern.items():
+            if k.startswith("k_update") and "hbm_bytes" in v:
+                return v["hbm_bytes"], k, os.path.relpath(path, ROOT)
+    return None
+
+
+def end_to_end(torch, codec, name, reps=5):
+    """Host-buffer path (fleet_update: pinned staging, H2D of the M uploads, layout
+    parse, update, D2H of the merged Base64 + error check) on the same synthetic
+    uploads: the PCIe-inclusive rate the JNI shim sees. Not `value`."""
+    import fleet_amd as F
+    from fleet_amd.layouts import LAYOUTS
+    lay_name, M, _ = WORKLOADS[name]
+    layout = LAYOUTS[lay_name]
+    sh = Shard(codec, torch, layout, M, 0, 1)
+    sh.encode()
+    torch.cuda.synchronize()
+    host = sh.text.cpu().numpy()
+    ups = [host[c, : sh.L].tobytes() for c in range(M)]
+    del sh
+    d = dampen_policy(M)
+    codec.update(ups, d)  # warm (allocations, staging)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        merged = codec.update(ups, d)
+    dt = (time.perf_counter() - t0) / reps
+    return {"workload": name, "ms": dt * 1e3, "gib_s": M * layout.n_up * 4 / dt / 2**30,
+            "h2d_bytes": M * F.b64_len(layout.n_up), "d2h_bytes": len(merged)}
+
+
 def cpu_baseline(budget_s: float = 20.0):
     """The reference's own C++ (oracle/_ref, -O0 = Server/Makefile flags) if built,
     else the C restatement's faithful per-op chain; single thread (update() is
@@ -206,6 +248,7 @@ def main():
     ap.add_argument("--extras", default="cifar10_256,synth1m_256",
                     help="comma list of extra workloads measured in the same run (N=1 only); '' for none")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
 
@@ -228,6 +271,10 @@ def main():
         for w in [x for x in args.extras.split(",") if x and x != args.workload]:
             extras[w] = time_workload(torch, dist, codec, w, max(3, args.steps // 4), 2, rank, world)
 
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        e2e = end_to_end(torch, codec, args.workload)
+
     if rank != 0:
         if world > 1:
             dist.barrier()
@@ -238,6 +285,7 @@ def main():
         cpu = cpu_baseline(args.cpu_budget)
     r = main_res
     achieved = r["update_gbs"]
+    traffic = pmc_traffic(args.workload) if world == 1 else None
     line = {
         "metric": "gradient GiB/s encode+decode+aggregate (device-resident); % HBM roofline",
         "value": r["gib_s"],
@@ -255,12 +303,15 @@ def main():
                    "n_up_per_rank": r["n_up_per_rank"], "parallelism": f"element-shard x{world}",
                    "dampening": "policy 1 inverse, tau = c mod 3"},
         "roofline": {"bound": "hbm", "kernel": "k_update", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic[0] if traffic else None,
+                     "traffic_source": f"{traffic[2]} ({traffic[1]})" if traffic else None,
                      "bytes_per_launch": r["update_bytes"], "kernel_ms": r["update_kernel_ms"]},
         "cpu_baseline": cpu,
         "kernels": {"k_update_ms": r["update_kernel_ms"], "k_encode_f32_ms": r["encode_kernel_ms"],
                     "k_encode_gbs": r["encode_gbs"], "element_clients_per_s": r["element_clients_per_s"]},
         "extra": extras,
+        "end_to_end_host_buffers": e2e,
     }
     if cpu:
         line["vs_cpu_baseline"] = r["gib_s"] / cpu["value"]

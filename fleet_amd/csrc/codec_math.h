@@ -174,6 +174,10 @@ struct DigitEntry {
    {5, 1e5f}, {6, 1e6f}, {6, 1e6f}, {6, 1e6f}, {7, 1e7f}, {7, 1e7f}, {7, 1e7f}, {7, 1e7f}, {8, 1e8f},      \
    {8, 1e8f}, {8, 1e8f}, {9, 1e9f}, {9, 1e9f}, {9, 1e9f}, {10, 1e10f}}
 
+// 10^i for i = -1..10 (exact in binary32 for i >= 0), indexed i + 1
+constexpr float kPow10Tab[12] = {0.1f, 1.f, 10.f, 100.f, 1e3f, 1e4f, 1e5f, 1e6f, 1e7f, 1e8f, 1e9f, 1e10f};
+#define kPow10 (kPow10Tab + 1)
+
 FLEET_HD int frexp_exp(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_frexp_expf(x);
@@ -295,6 +299,41 @@ FLEET_HD f2 q_gen2(f2 x, const DigitEntry* tab) {
   const f2 X = steps_mul10x2(__builtin_elementwise_abs(x), s0, s1);
   const f2 t = f2{signed_code_float((uint32_t)X.x, d0, x.x), signed_code_float((uint32_t)X.y, d1, x.y)};
   return steps_div10x2(t, s0, s1);
+}
+
+// Q(x) on the q_gen domain with the shortest dependent chain, for the serial
+// accumulation (one value per lane, latency-bound). The 9-step mul chain runs
+// from |x| unconditionally and a select chain that tracks it keeps step j iff
+// j <= k = 9 - d; the k-step division chain is picked the same way. The keep
+// conditions come from compares on x (d <= 9 - j <=> |x| < 10^(9-j), or
+// 10^(8-j) when x <= -1: the '-' counts as a digit), so they are ready before
+// the chains need them.
+FLEET_HD float q_lat(float x) {
+  const float ax = __builtin_fabsf(x);
+  const bool neg1 = x <= -1.0f;
+  bool keep[10];
+#pragma unroll
+  for (int j = 1; j <= 9; ++j) {
+    const float tp = kPow10[9 - j], tn = kPow10[8 - j];
+    keep[j] = ax < (neg1 ? tn : tp);
+  }
+  int d = 0;  // for x <= -1 the j = 9 term (|x| >= 0.1) is the '-' digit
+#pragma unroll
+  for (int j = 1; j <= 9; ++j) d += !keep[j];
+  float X = ax, t = ax;
+#pragma unroll
+  for (int j = 1; j <= 9; ++j) {
+    X = X * 10.0f;
+    t = keep[j] ? X : t;
+  }
+  const float cf = signed_code_float((uint32_t)t, d, x);
+  float U = cf, r = cf;
+#pragma unroll
+  for (int j = 1; j <= 9; ++j) {
+    U = div10(U);
+    r = keep[j] ? U : r;
+  }
+  return r;
 }
 
 // int2float(c) for every code (k = 9 - |c % 10| in [0, 9]) -- total.

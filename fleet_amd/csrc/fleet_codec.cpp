@@ -551,7 +551,7 @@ int fleet_synth_device(fleet_ctx* c, uint64_t seed, int M, int client0, const in
 }
 
 int fleet_selftest_digest(fleet_ctx* c, int fn, uint64_t* out) {
-  if (!c || !out || fn < 0 || fn > 11) return FLEET_ERR_ARG;
+  if (!c || !out || fn < 0 || fn > 12) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   unsigned long long* d = nullptr;

@@ -17,6 +17,20 @@ namespace fleet {
 #define FLEET_ERRBIT_BASE64 1
 #define FLEET_ERRBIT_LAYOUT 2
 
+// Dev-only phase timestamps (scripts/ubench_tiled.hip builds with FLEET_TIMING);
+// compiled out of the library.
+#ifdef FLEET_TIMING
+__device__ unsigned long long g_fleet_timing[16384 * 8];
+#define FLEET_TSTAMP(slot)                                                                  \
+  do {                                                                                      \
+    if (threadIdx.x == 0) g_fleet_timing[blockIdx.x * 8 + (slot)] = wall_clock64();        \
+  } while (0)
+#else
+#define FLEET_TSTAMP(slot) \
+  do {                     \
+  } while (0)
+#endif
+
 // chars of the group that must be alphabet chars, for r valid int32 values
 __device__ __forceinline__ uint32_t needed_chars_mask(int r) {
   return r >= 3 ? 0xffffu : r == 2 ? 0x7ffu : r == 1 ? 0x3fu : 0u;
@@ -51,6 +65,13 @@ __device__ __forceinline__ int headers_in_group(const int32_t* __restrict__ hdr,
     ++cnt;
   }
   return cnt;
+}
+
+// bit e set = value slot p0+e is a layout header slot
+__device__ __forceinline__ uint32_t header_bits(const int32_t* __restrict__ hdr, int n_hdr, int64_t p0) {
+  bool ih[3];
+  headers_in_group(hdr, n_hdr, p0, ih);
+  return (uint32_t)ih[0] | ((uint32_t)ih[1] << 1) | ((uint32_t)ih[2] << 2);
 }
 
 // ----------------------------------------------------------------------------
@@ -150,6 +171,23 @@ __device__ __forceinline__ void q_stage_lat(float (&out)[1], const float (&x)[1]
 }
 
 // ----------------------------------------------------------------------------
+// One merged slot (mergeFlatGradient, cppNN_backend.cpp:722-750, after
+// scalarMultiply(1.0/avgSize), CppNNUpdater.java:507-508): header and unwalked
+// slots re-encode the last upload's decoded value, payload slots encode
+// Q(f32(f64(A) * inv)). Variable-length chains on their domain, the general
+// codec for the rest (divergent, rare).
+__device__ __forceinline__ int32_t merged_code(float A, double inv, int32_t last_code, bool keep_last,
+                                               const DigitEntry* dig) {
+  if (keep_last) return enc(dec(last_code));
+  const float r = (float)((double)A * inv);
+  if (q_gen_ok(r)) {
+    const float y = q_gen(r, dig);
+    if (q_gen_ok(y)) return enc_gen(y, dig);
+  }
+  return enc(q(r));
+}
+
+// ----------------------------------------------------------------------------
 // Fused update: CppNNUpdater.update's aggregation (java:420-509) for the
 // groups [g_begin, g_end). Per value and client c, in CppNNUpdater order:
 //   y = Q(dec(code_c))                  getFlatGradient decode+encode, scalarMul decode
@@ -198,6 +236,16 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
   uint32_t bad[K], need[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) need[k] = needed_chars_mask((int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g[k])));
+  // layout consistency (every upload carries the last one's header codes) is
+  // checked while walking the clients, only in the few waves holding header
+  // slots: hbits bit i = value slot i of this lane is a header slot
+  uint32_t hbits = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (live[k]) hbits |= header_bits(hdr, n_hdr, 3 * g[k]) << (3 * k);
+  const bool wave_hdr = __ballot(hbits != 0) != 0;
+  int32_t hfirst[S];
+  uint32_t layout_bad = 0;
 #pragma unroll
   for (int i = 0; i < S; ++i) acc[i] = 0.f;
 #pragma unroll
@@ -220,6 +268,13 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
         bad[k] |= b64_decode_group_full(cur[k], &tab, codes + 3 * k);
       else  // the partial last group: only the chars carrying its values must be valid
         bad[k] |= b64_decode_group(cur[k], &tab, codes + 3 * k) & need[k];
+    }
+    if (wave_hdr) {  // wave-uniform
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        if (c == 0) hfirst[i] = codes[i];
+        layout_bad |= (((hbits >> i) & 1u) & (uint32_t)(codes[i] != hfirst[i])) << i;
+      }
     }
 
     // Per stage and wave: if every value of the wave is inside the |x| < 1
@@ -276,44 +331,52 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
     if (!live[k]) continue;
     const int64_t p0 = 3 * g[k];
     const int r = (int)min<int64_t>(3, n_up - p0);
-    bool is_hdr[3];
-    headers_in_group(hdr, n_hdr, p0, is_hdr);
-    // every upload must carry the same header slots as the last one
-    int layout_bad = 0;
-    if (is_hdr[0] | is_hdr[1] | is_hdr[2]) {
-      for (int c = 0; c < M - 1; ++c) {
-        int32_t cc[3];
-        bad[k] |= b64_decode_group(*reinterpret_cast<const uint4*>(rowp[k] + (size_t)c * pitch), &tab, cc) & need[k];
-        for (int e = 0; e < 3; ++e)
-          if (is_hdr[e] && e < r && cc[e] != codes[3 * k + e]) layout_bad = 1;
-      }
-    }
     if (bad[k]) atomicOr(err, FLEET_ERRBIT_BASE64);
-    if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+    if ((layout_bad >> (3 * k)) & 7u) atomicOr(err, FLEET_ERRBIT_LAYOUT);
     int32_t out[3];
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
-      const bool keep_last = is_hdr[e] || p0 + e >= walk_end;
-      int32_t o = keep_last ? enc(dec(codes[3 * k + e])) : enc(q((float)((double)acc[3 * k + e] * inv_avg)));
+      const bool keep_last = ((hbits >> (3 * k + e)) & 1u) || p0 + e >= walk_end;
+      const int32_t o = merged_code(acc[3 * k + e], inv_avg, codes[3 * k + e], keep_last, tab.digits);
       out[e] = e < r ? o : 0;
     }
     *reinterpret_cast<uint4*>(merged + 16 * g[k]) = pad_group(b64_encode_group(out, &tab), r);
     if (merged_f32) {
-      for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec(out[e]);
+      for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec_gen(out[e]);
     }
   }
 }
 
-// ----------------------------------------------------------------------------
+// The exact chain of one value recomputed from global memory with the general
+// codec: the fallback when the serial accumulation leaves the q_lat domain
+// (|A| >= 1e8; never for gradients). Per lane, divergent, slow, exact.
+__device__ __noinline__ float chain_general(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                            const double* __restrict__ dampen, int64_t g, int e,
+                                            const B64Tables* tab) {
+  float A = 0.f;
+  for (int c = 0; c < M; ++c) {
+    int32_t cc[3];
+    b64_decode_group(*reinterpret_cast<const uint4*>(uploads + (size_t)c * pitch + 16 * g), tab, cc);
+    const float y = q(dec(cc[e]));
+    const float p = q((float)((double)y * dampen[c]));
+    A = c == 0 ? p : q(A + p);
+  }
+  return A;
+}
+
 // Two-phase tile variant for small buckets (MNIST: 7,654 groups -- too few
 // lanes to fill 1,024 SIMDs when every lane walks all clients serially).
-// A block owns TG groups (E = 3*TG values) and walks the clients in chunks
-// of CM:
+// A block owns TG groups (E = 3*TG values) and walks the clients in
+// chunks of CM:
 //   phase 1 -- all 256 threads: p[c][e] = Q(f32(f64(Q(dec(code))) * d_c)) for
 //              every (client, group) item of the chunk, into LDS. These are
 //              independent across clients (CppNNUpdater.java:463-464).
-//   phase 2 -- one thread per value: the serial A = Q(A + p_c) (:490-493),
-//              the only part that must follow client order.
+//   phase 2 -- one thread per value: the serial A = Q(A + p_c)
+//              (:490-493), the only part that must follow client order, as
+//              straight-line q_lat steps (no per-step branch); a lane that
+//              ever leaves the q_lat domain is recomputed by chain_general.
+// Layout consistency (all uploads carry the last one's header codes) is
+// checked in phase 1 with per-slot LDS min/max of the header codes.
 template <int TG>
 __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                       const double* __restrict__ dampen, double inv_avg,
@@ -322,20 +385,34 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
                                                       uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
                                                       int* __restrict__ err) {
   constexpr int E = 3 * TG;
+  static_assert(E <= 256, "phase 2 is one thread per value");
   constexpr int CM = 6144 / E;  // 24 KiB of p per chunk
   constexpr int S = 6;          // two items per thread per pass
+  FLEET_TSTAMP(0);
   __shared__ B64Tables tab;
   __shared__ float ptile[CM * E];
   __shared__ uint32_t scratch[4][64 * S];
   __shared__ int32_t last_codes[E];
-  b64_tables_init(&tab);
-  __syncthreads();
+  __shared__ int32_t hmin[E], hmax[E];
+  __shared__ uint32_t hmask[TG];
   const int tid = threadIdx.x, lane = tid & 63;
-  uint32_t* ws = scratch[tid >> 6];
   const int64_t g0 = g_begin + (int64_t)blockIdx.x * TG;
   const int ng = (int)min<int64_t>(TG, g_end - g0);
+  const int n_hdr = hdr_block[1];
+  const int64_t walk_end = hdr_block[2];
+  const int32_t* hdr = hdr_block + 4;
+  b64_tables_init(&tab);
+  if (tid < TG) hmask[tid] = tid < ng ? header_bits(hdr, n_hdr, 3 * (g0 + tid)) : 0u;
+  if (tid < E) {
+    hmin[tid] = INT32_MAX;
+    hmax[tid] = INT32_MIN;
+  }
+  __syncthreads();
+  FLEET_TSTAMP(1);
+  uint32_t* ws = scratch[tid >> 6];
 
   float A = 0.f;  // phase-2 value: element tid of the tile (tid < E)
+  uint32_t off_domain = 0;
   uint32_t badacc = 0;
   for (int c0 = 0; c0 < M; c0 += CM) {
     const int cm = min(CM, M - c0);
@@ -361,6 +438,14 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
           badacc |= b;
           if (c0 + cc[h] == M - 1)
             for (int e = 0; e < 3; ++e) last_codes[3 * gl[h] + e] = codes[3 * h + e];
+          const uint32_t hm = hmask[gl[h]];
+          if (hm) {
+            for (int e = 0; e < 3; ++e)
+              if ((hm >> e) & 1u) {
+                atomicMin(&hmin[3 * gl[h] + e], codes[3 * h + e]);
+                atomicMax(&hmax[3 * gl[h] + e], codes[3 * h + e]);
+              }
+          }
         }
       }
       // stage A
@@ -400,59 +485,56 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
         if (live[h])
 #pragma unroll
           for (int e = 0; e < 3; ++e) ptile[cc[h] * E + 3 * gl[h] + e] = p[3 * h + e];
+      if (base == 0) FLEET_TSTAMP(2);
     }
     __syncthreads();
+    FLEET_TSTAMP(3);
     // phase 2: serial accumulation, one value per thread
     if (tid < E) {
-      for (int k = 0; k < cm; ++k) {
-        const float pk = ptile[k * E + tid];
-        if (c0 + k == 0) {
-          A = pk;
-        } else {
-          float sm[1] = {A + pk}, o[1];
-          q_stage_lat(o, sm, ws, lane);
-          A = o[0];
-        }
+      const int col = tid;
+      int k = 0;
+      if (c0 == 0) {
+        A = ptile[col];
+        k = 1;
+      }
+#pragma unroll 4
+      for (; k < cm; ++k) {
+        const float s = A + ptile[k * E + col];
+        off_domain |= (uint32_t)!q_gen_ok(s);
+        A = q_lat(s);
       }
     }
     __syncthreads();
   }
+  FLEET_TSTAMP(4);
   if (badacc) atomicOr(err, FLEET_ERRBIT_BASE64);
-  // gather the tile's final values per group
+  if (tid >= 3 * ng) off_domain = 0;  // columns past the last group hold no values
+  if (__ballot(off_domain != 0)) {  // wave-uniform, never for gradients
+    if (off_domain) A = chain_general(uploads, pitch, M, dampen, g0 + tid / 3, tid % 3, &tab);
+  }
   if (tid < E) ptile[tid] = A;
   __syncthreads();
   if (tid >= ng) return;
-  const int n_hdr = hdr_block[1];
-  const int64_t walk_end = hdr_block[2];
-  const int32_t* hdr = hdr_block + 4;
   const int64_t g = g0 + tid;
   const int64_t p0 = 3 * g;
   const int r = (int)min<int64_t>(3, n_up - p0);
-  bool is_hdr[3];
-  headers_in_group(hdr, n_hdr, p0, is_hdr);
+  const uint32_t hm = hmask[tid];
   int layout_bad = 0;
-  uint32_t bad = 0;
-  if (is_hdr[0] | is_hdr[1] | is_hdr[2]) {
-    for (int c = 0; c < M - 1; ++c) {
-      int32_t cc3[3];
-      bad |= b64_decode_group(*reinterpret_cast<const uint4*>(uploads + (size_t)c * pitch + 16 * g), &tab, cc3);
-      for (int e = 0; e < 3; ++e)
-        if (is_hdr[e] && e < r && cc3[e] != last_codes[3 * tid + e]) layout_bad = 1;
-    }
-  }
-  if (bad & needed_chars_mask(r)) atomicOr(err, FLEET_ERRBIT_BASE64);
+  for (int e = 0; e < 3; ++e)
+    if ((hm >> e) & 1u) layout_bad |= hmin[3 * tid + e] != hmax[3 * tid + e];
   if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
   int32_t out[3];
 #pragma unroll
   for (int e = 0; e < 3; ++e) {
-    const bool keep_last = is_hdr[e] || p0 + e >= walk_end;
-    const int32_t o = keep_last ? enc(dec(last_codes[3 * tid + e])) : enc(q((float)((double)ptile[3 * tid + e] * inv_avg)));
+    const bool keep_last = ((hm >> e) & 1u) || p0 + e >= walk_end;
+    const int32_t o = merged_code(ptile[3 * tid + e], inv_avg, last_codes[3 * tid + e], keep_last, tab.digits);
     out[e] = e < r ? o : 0;
   }
   *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &tab), r);
   if (merged_f32) {
-    for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec(out[e]);
+    for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec_gen(out[e]);
   }
+  FLEET_TSTAMP(5);
 }
 
 // ----------------------------------------------------------------------------
@@ -726,6 +808,7 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
   hipLaunchKernelGGL(k_update_tiled<TG>, dim3((unsigned)((groups + TG - 1) / TG)), dim3(256), 0, s, uploads, pitch, \
                      M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
     if (tg == 16) FLEET_LAUNCH_TILED(16);
+    else if (tg == 8) FLEET_LAUNCH_TILED(8);
     else if (tg == 64) FLEET_LAUNCH_TILED(64);
     else FLEET_LAUNCH_TILED(32);
 #undef FLEET_LAUNCH_TILED
@@ -872,6 +955,8 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
                o = use ? (uint32_t)enc_gen(u2f(u), dig) : 0u; break;
       case 11: use = (u & 0x7fffffffu) < 0x3f800000u;                 // float2int fast path, |x| < 1
                o = use ? (uint32_t)enc_fast(u2f(u)) : 0u; break;
+      case 12: use = q_gen_ok(u2f(u));                                // select-chain Q (serial accumulation)
+               o = use ? f2u(q_lat(u2f(u))) : 0u; break;
       default: o = 0; use = false;
     }
     if (use) sum += splitmix64(((uint64_t)u << 32) | o);

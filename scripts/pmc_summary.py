@@ -16,7 +16,8 @@ import sys
 
 
 def short(name: str) -> str:
-    return name.split("(")[0].replace("fleet::", "")
+    n = name.split("(")[0].replace("fleet::", "")
+    return n[5:] if n.startswith("void ") else n
 
 
 def kernel_stats(d):

@@ -90,10 +90,11 @@ int main(int argc, char** argv) {
     if (!q_gen_ok(x)) return;
     if (digits_cmp(x) != fo_num_digits(fo_cvtt(x))) g_bad++;
     if (!same(q_gen_lat(x), fo_int2float(fo_float2int(x)))) g_bad++;
+    if (!same(q_lat(x), fo_int2float(fo_float2int(x)))) g_bad++;
     if (enc_gen(x, tab) != fo_float2int(x)) g_bad++;
     if (q_ok(x) && enc_fast(x) != fo_float2int(x)) g_bad++;
   });
-  report("digits_cmp/q_gen_lat/enc_gen/enc_fast", b0);
+  report("digits_cmp/q_gen_lat/q_lat/enc_gen/enc_fast", b0);
 
   b0 = g_bad;  // q_gen (+ packed) vs Q on its domain -1e6 < x < 1e7
   par_for(0, 1ull << 32, s, [](uint64_t i) {

@@ -46,6 +46,7 @@ static uint64_t digest(int fn) {
                     o = f2u(fo_int2float(c)) + 3u * f2u(fo_int2float(c2)); break; }
           case 10: { float x = u2f(u); use = x < 1e9f && x > -1e8f; if (use) o = (uint32_t)fo_float2int(x); break; }
           case 11: use = (u & 0x7fffffffu) < 0x3f800000u; if (use) o = (uint32_t)fo_float2int(u2f(u)); break;
+          case 12: { float x = u2f(u); use = x < 1e9f && x > -1e8f; if (use) o = f2u(Q(x)); break; }
         }
         if (use) sum += splitmix64(((uint64_t)u << 32) | o);
       }
@@ -61,9 +62,9 @@ int main(int argc, char** argv) {
   const char* path = argc > 1 ? argv[1] : "tests/golden/digests.json";
   FILE* f = fopen(path, "w");
   fprintf(f, "{\n  \"generator\": \"tests/native/digest_ref.cpp over oracle/fleet_oracle.c\",\n");
-  for (int fn = 0; fn <= 11; ++fn) {
+  for (int fn = 0; fn <= 12; ++fn) {
     uint64_t d = digest(fn);
-    fprintf(f, "  \"fn%d\": \"%016llx\"%s\n", fn, (unsigned long long)d, fn < 11 ? "," : "");
+    fprintf(f, "  \"fn%d\": \"%016llx\"%s\n", fn, (unsigned long long)d, fn < 12 ? "," : "");
     printf("fn%d %016llx\n", fn, (unsigned long long)d);
     fflush(stdout);
   }

@@ -182,7 +182,7 @@ def test_device_synth_and_encode(codec, oracle):
         assert np.array_equal(b[c, : lay.n_up].view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
 
 
-@pytest.mark.parametrize("fn", range(12))
+@pytest.mark.parametrize("fn", range(13))
 def test_device_codec_exhaustive_digest(codec, fn):
     """Every input of each device codec function's domain (2^32 codes / bit
     patterns), digested on the GPU, equals the oracle's digest."""
@@ -203,9 +203,19 @@ def test_update_groups_per_lane_variants(codec, oracle, monkeypatch, K):
         assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
-def test_update_large_magnitudes_slow_path(codec, oracle):
+@pytest.mark.parametrize("env", [{"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "8"},
+                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16"},
+                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "32"},
+                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "64"},
+                                 {"FLEET_UPDATE_MODE": "stream", "FLEET_UPDATE_K": "1"},
+                                 {"FLEET_UPDATE_MODE": "stream", "FLEET_UPDATE_K": "4"}])
+def test_update_large_magnitudes_slow_path(codec, oracle, monkeypatch, env):
     """Values far outside the fast path (|x| >= 1, digits != 0, >= 2^31) force
-    every compaction pass; dampening > 1 (class-aware policy) too."""
+    every compaction pass and the tiled kernel's general-chain fallback (the
+    accumulator leaves the q_lat domain); dampening > 1 (class-aware policy) too.
+    Ragged tiles (4000 values = 1334 groups) for every tile width."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     rng = np.random.default_rng(8)
     lay = synthetic(4000)
     M = 6
