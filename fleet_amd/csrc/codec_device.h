@@ -42,15 +42,21 @@ __device__ __forceinline__ uint8_t b64_to_value(int s) {
   return (uint8_t)(s < 26 ? 'A' + s : s < 52 ? 'a' + s - 26 : s < 62 ? '0' + s - 52 : s == 62 ? '+' : '/');
 }
 
-// Fill the block's LDS tables (call from every thread, then __syncthreads()).
+// Fill the block's LDS tables (call from every thread of an NT-thread block,
+// then __syncthreads()). NT is a compile-time constant so the fill is a
+// straight-line pass, not a loop the compiler vectorises over unknown strides.
+template <int NT = 256>
 __device__ __forceinline__ void b64_tables_init(B64Tables* t) {
   constexpr DigitEntry dig[32] = FLEET_DIGIT_TABLE;
-  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int i0 = 0; i0 < 256; i0 += NT) {
+    const int i = i0 + tid;
     t->from[i] = b64_from_value(i);
     t->fromf[i] = b64_from_value_flag(i);
   }
-  for (int i = threadIdx.x; i < 64; i += blockDim.x) t->to[i] = b64_to_value(i);
-  for (int i = threadIdx.x; i < 32; i += blockDim.x) t->digits[i] = dig[i];
+  if (tid < 64) t->to[tid] = b64_to_value(tid);
+  if (tid < 32) t->digits[tid] = dig[tid];
 }
 
 // One 16-char group -> 12 bytes -> 3 little-endian int32 codes.

@@ -35,6 +35,14 @@ FLEET_HD float u2f(uint32_t x) { return __builtin_bit_cast(float, x); }
 // below 1e-9 in magnitude. div10(-0.0) = +0.0, as -0.0/10 is not needed:
 // int2float starts from (float)code, never -0.0.
 FLEET_HD float div10(float t) { return __builtin_fmaf(t, kTenthHi, t * kTenthLo); }
+
+// RN((0.1 - RN(0.1)) / 10): a chain U_j = U_{j-1}/10 may take step j's small
+// term U_{j-1}*lo as U_{j-2}*kTenthLo2. U_{j-1} = U_{j-2}/10 * (1 + 2^-24 at
+// most), so the addend is within 2^-46 of t*(0.1 - RN(0.1)) relative to t/10 --
+// still far inside the 2^-27.3 midpoint margin -- and each step after the
+// first is ONE dependent fma (the mul runs a step ahead). Used by q_lat;
+// verified with it over its whole domain (tests/native, digest fn 12).
+constexpr float kTenthLo2 = -0x1.47ae14p-33f;
 FLEET_HD f2 div10x2(f2 t) {
   return __builtin_elementwise_fma(t, f2{kTenthHi, kTenthHi}, t * f2{kTenthLo, kTenthLo});
 }
@@ -301,37 +309,42 @@ FLEET_HD f2 q_gen2(f2 x, const DigitEntry* tab) {
   return steps_div10x2(t, s0, s1);
 }
 
-// Q(x) on the q_gen domain with the shortest dependent chain, for the serial
-// accumulation (one value per lane, latency-bound). The 9-step mul chain runs
-// from |x| unconditionally and a select chain that tracks it keeps step j iff
-// j <= k = 9 - d; the k-step division chain is picked the same way. The keep
-// conditions come from compares on x (d <= 9 - j <=> |x| < 10^(9-j), or
-// 10^(8-j) when x <= -1: the '-' counts as a digit), so they are ready before
-// the chains need them.
+// Q(x) on the q_gen domain for the serial accumulation (one value per lane, a
+// single wave: bound by issue slots AND the dependent chain, so both are cut).
+//   * sign folding: w = 10|x| when x <= -1 ('-' counts as a digit), else |x|;
+//     then numDigits((int)x) = #{m in 0..8 : w >= 10^m}. RN(10|x|) < 10^m iff
+//     |x| < 10^(m-1) for these powers (10*ulp(f) is 0.625 or 1.25 ulp(10^m)),
+//     so nine compares give both d (as carries) and the keep conditions
+//     (step j <= k = 9 - d kept iff w < 10^(9-j)).
+//   * the 9-step x10 chain runs from |x| unconditionally; a select chain
+//     tracking it keeps X_k.
+//   * the k-step /10 chain is one dependent fma per step, U_j = fma(U_{j-1},
+//     RN(0.1), a_j), with a_{j+1} = U_{j-1} * kTenthLo2 computed alongside (see
+//     kTenthLo2); a select chain keeps U_k.
 FLEET_HD float q_lat(float x) {
   const float ax = __builtin_fabsf(x);
-  const bool neg1 = x <= -1.0f;
-  bool keep[10];
+  const float w = x <= -1.0f ? ax * 10.0f : ax;
+  bool big[9];
+  int d = 0;
 #pragma unroll
-  for (int j = 1; j <= 9; ++j) {
-    const float tp = kPow10[9 - j], tn = kPow10[8 - j];
-    keep[j] = ax < (neg1 ? tn : tp);
+  for (int m = 0; m <= 8; ++m) {
+    big[m] = w >= kPow10[m];
+    d += big[m];
   }
-  int d = 0;  // for x <= -1 the j = 9 term (|x| >= 0.1) is the '-' digit
-#pragma unroll
-  for (int j = 1; j <= 9; ++j) d += !keep[j];
   float X = ax, t = ax;
 #pragma unroll
   for (int j = 1; j <= 9; ++j) {
     X = X * 10.0f;
-    t = keep[j] ? X : t;
+    t = big[9 - j] ? t : X;
   }
   const float cf = signed_code_float((uint32_t)t, d, x);
-  float U = cf, r = cf;
+  float U = cf, a = cf * kTenthLo, r = cf;
 #pragma unroll
   for (int j = 1; j <= 9; ++j) {
-    U = div10(U);
-    r = keep[j] ? U : r;
+    const float Un = __builtin_fmaf(U, kTenthHi, a);  // the only dependent op per step
+    a = U * kTenthLo2;                                 // next step's small term, off the chain
+    U = Un;
+    r = big[9 - j] ? r : U;
   }
   return r;
 }

@@ -364,17 +364,164 @@ __device__ __noinline__ float chain_general(const uint8_t* __restrict__ uploads,
   return A;
 }
 
-// Two-phase tile variant for small buckets (MNIST: 7,654 groups -- too few
-// lanes to fill 1,024 SIMDs when every lane walks all clients serially).
-// A block owns TG groups (E = 3*TG values) and walks the clients in
-// chunks of CM:
-//   phase 1 -- all 256 threads: p[c][e] = Q(f32(f64(Q(dec(code))) * d_c)) for
-//              every (client, group) item of the chunk, into LDS. These are
-//              independent across clients (CppNNUpdater.java:463-464).
+// Shared state of one tile of TG groups (E = 3*TG values) in LDS.
+template <int TG>
+struct TileShared {
+  static constexpr int E = 3 * TG;
+  B64Tables tab;
+  uint32_t scratch[4][64 * 6];  // resolve_slow compaction, one list per wave
+  int32_t last_codes[E];        // codes of the last upload (mergeFlatGradient's g)
+  int32_t hmin[E], hmax[E];     // header-slot codes over all uploads (layout check)
+  uint32_t hmask[TG];           // bit e = slot 3*g+e is a header slot
+};
+
+// Tables, header slots of the tile (every thread checks one header position:
+// one independent load each, not a per-group binary search), min/max init.
+template <int TG>
+__device__ __forceinline__ void tile_init(TileShared<TG>& sh, const int32_t* __restrict__ hdr, int n_hdr,
+                                          int64_t g0, int ng) {
+  constexpr int E = 3 * TG;
+  const int tid = threadIdx.x;
+  const int64_t v0 = 3 * g0, v1 = 3 * (g0 + ng);
+  int32_t hp = -1;
+  if (tid < n_hdr) hp = hdr[tid];
+  b64_tables_init(&sh.tab);
+  if (tid < TG) sh.hmask[tid] = 0u;
+  if (tid < E) {
+    sh.hmin[tid] = INT32_MAX;
+    sh.hmax[tid] = INT32_MIN;
+  }
+  __syncthreads();
+  for (int i = tid; i < n_hdr; i += 256) {
+    if (i != tid) hp = hdr[i];
+    if (hp >= v0 && hp < v1) atomicOr(&sh.hmask[(hp - v0) / 3], 1u << ((hp - v0) % 3));
+  }
+  __syncthreads();
+}
+
+// Client-independent part of the chain for up to two (client, group) items per
+// thread: items it0 and it0 + stride of the nitems items (client-major:
+// item = cc*TG + gl) of clients c_base.. ; p of client c_base+cc, slot 3*gl+e
+// goes to pdst[cc*E + 3*gl + e]:
+//   p = Q(f32(f64(Q(int2float(code))) * d_c))   (CppNNUpdater.java:463-464)
+// Also: Base64 validity, the last upload's codes, header-slot min/max.
+template <int TG>
+__device__ __forceinline__ void tile_produce(TileShared<TG>& sh, const uint8_t* __restrict__ uploads, size_t pitch,
+                                             int M, const double* __restrict__ dampen, int64_t n_up, int64_t g0,
+                                             int ng, int c_base, int nitems, int it0, int stride,
+                                             float* __restrict__ pdst, uint32_t& badacc) {
+  constexpr int E = 3 * TG, S = 6;
+  const int lane = threadIdx.x & 63;
+  uint32_t* ws = sh.scratch[threadIdx.x >> 6];
+  int32_t codes[S];
+  int cc[2], gl[2];
+  bool live[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int item = it0 + h * stride;
+    live[h] = item < nitems && (item % TG) < ng;
+    cc[h] = live[h] ? item / TG : 0;
+    gl[h] = live[h] ? item % TG : 0;
+    const uint4 w = *reinterpret_cast<const uint4*>(uploads + (size_t)(c_base + cc[h]) * pitch + 16 * (g0 + gl[h]));
+    const int r = (int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * (g0 + gl[h])));
+    uint32_t b;
+    if (r == 3)
+      b = b64_decode_group_full(w, &sh.tab, codes + 3 * h);
+    else
+      b = b64_decode_group(w, &sh.tab, codes + 3 * h) & needed_chars_mask(r);
+    if (live[h]) {
+      badacc |= b;
+      if (c_base + cc[h] == M - 1)
+        for (int e = 0; e < 3; ++e) sh.last_codes[3 * gl[h] + e] = codes[3 * h + e];
+      const uint32_t hm = sh.hmask[gl[h]];
+      if (hm) {
+        for (int e = 0; e < 3; ++e)
+          if ((hm >> e) & 1u) {
+            atomicMin(&sh.hmin[3 * gl[h] + e], codes[3 * h + e]);
+            atomicMax(&sh.hmax[3 * gl[h] + e], codes[3 * h + e]);
+          }
+      }
+    }
+  }
+  // stage A: y = Q(int2float(code))
+  float y0[S], y[S];
+  {
+    bool all9 = true;
+#pragma unroll
+    for (int i = 0; i < S; ++i) all9 &= dec9_ok(codes[i]);
+    if (__ballot(!all9) == 0) {
+#pragma unroll
+      for (int i = 0; i < S; i += 2) {
+        const f2 v = dec_fast2(codes[i], codes[i + 1]);
+        y0[i] = v.x;
+        y0[i + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < S; i += 2) {
+        const f2 v = dec_gen2(codes[i], codes[i + 1]);
+        y0[i] = v.x;
+        y0[i + 1] = v.y;
+      }
+    }
+  }
+  q_stage<S>(y, y0, sh.tab.digits, ws, lane);
+  // stage B: p = Q(f32(f64(y) * d)), per-item client
+  float r[S], p[S];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const double d = dampen[c_base + cc[h]];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) r[3 * h + e] = (float)((double)y[3 * h + e] * d);
+  }
+  q_stage<S>(p, r, sh.tab.digits, ws, lane);
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (live[h])
+#pragma unroll
+      for (int e = 0; e < 3; ++e) pdst[cc[h] * E + 3 * gl[h] + e] = p[3 * h + e];
+}
+
+// Final values of the tile (vals[0..E)) -> merged Base64 (+ fp32), layout check.
+template <int TG>
+__device__ __forceinline__ void tile_epilogue(TileShared<TG>& sh, const float* __restrict__ vals, double inv_avg,
+                                              int64_t n_up, int64_t walk_end, int64_t g0, int ng,
+                                              uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                              int* __restrict__ err) {
+  const int tid = threadIdx.x;
+  if (tid >= ng) return;
+  const int64_t g = g0 + tid;
+  const int64_t p0 = 3 * g;
+  const int r = (int)min<int64_t>(3, n_up - p0);
+  const uint32_t hm = sh.hmask[tid];
+  int layout_bad = 0;
+  for (int e = 0; e < 3; ++e)
+    if ((hm >> e) & 1u) layout_bad |= sh.hmin[3 * tid + e] != sh.hmax[3 * tid + e];
+  if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+  int32_t out[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    const bool keep_last = ((hm >> e) & 1u) || p0 + e >= walk_end;
+    const int32_t o = merged_code(vals[3 * tid + e], inv_avg, sh.last_codes[3 * tid + e], keep_last, sh.tab.digits);
+    out[e] = e < r ? o : 0;
+  }
+  *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &sh.tab), r);
+  if (merged_f32) {
+    for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec_gen(out[e]);
+  }
+}
+
+// Two-phase tile variant for small/medium buckets (MNIST: 7,654 groups -- too
+// few lanes to fill 1,024 SIMDs when every lane walks all clients serially).
+// A block owns TG groups (E = 3*TG values) and walks the clients in chunks
+// of CM:
+//   phase 1 -- all 256 threads: p[c][e] for every (client, group) item of the
+//              chunk into LDS (tile_produce; independent across clients).
 //   phase 2 -- one thread per value: the serial A = Q(A + p_c)
-//              (:490-493), the only part that must follow client order, as
-//              straight-line q_lat steps (no per-step branch); a lane that
-//              ever leaves the q_lat domain is recomputed by chain_general.
+//              (CppNNUpdater.java:490-493), the only part that must follow
+//              client order, as straight-line q_lat steps (no per-step
+//              branch); a lane that ever leaves the q_lat domain is recomputed
+//              by chain_general.
 // Layout consistency (all uploads carry the last one's header codes) is
 // checked in phase 1 with per-slot LDS min/max of the header codes.
 template <int TG>
@@ -387,29 +534,14 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
   constexpr int E = 3 * TG;
   static_assert(E <= 256, "phase 2 is one thread per value");
   constexpr int CM = 6144 / E;  // 24 KiB of p per chunk
-  constexpr int S = 6;          // two items per thread per pass
   FLEET_TSTAMP(0);
-  __shared__ B64Tables tab;
+  __shared__ TileShared<TG> sh;
   __shared__ float ptile[CM * E];
-  __shared__ uint32_t scratch[4][64 * S];
-  __shared__ int32_t last_codes[E];
-  __shared__ int32_t hmin[E], hmax[E];
-  __shared__ uint32_t hmask[TG];
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x;
   const int64_t g0 = g_begin + (int64_t)blockIdx.x * TG;
   const int ng = (int)min<int64_t>(TG, g_end - g0);
-  const int n_hdr = hdr_block[1];
-  const int64_t walk_end = hdr_block[2];
-  const int32_t* hdr = hdr_block + 4;
-  b64_tables_init(&tab);
-  if (tid < TG) hmask[tid] = tid < ng ? header_bits(hdr, n_hdr, 3 * (g0 + tid)) : 0u;
-  if (tid < E) {
-    hmin[tid] = INT32_MAX;
-    hmax[tid] = INT32_MIN;
-  }
-  __syncthreads();
+  tile_init<TG>(sh, hdr_block + 4, hdr_block[1], g0, ng);
   FLEET_TSTAMP(1);
-  uint32_t* ws = scratch[tid >> 6];
 
   float A = 0.f;  // phase-2 value: element tid of the tile (tid < E)
   uint32_t off_domain = 0;
@@ -418,88 +550,21 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
     const int cm = min(CM, M - c0);
     const int nitems = cm * TG;
     for (int base = 0; base < nitems; base += 512) {
-      int32_t codes[S];
-      int cc[2], gl[2];
-      bool live[2];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int item = base + h * 256 + tid;
-        live[h] = item < nitems && (item % TG) < ng;
-        cc[h] = live[h] ? item / TG : 0;
-        gl[h] = live[h] ? item % TG : 0;
-        const uint4 w = *reinterpret_cast<const uint4*>(uploads + (size_t)(c0 + cc[h]) * pitch + 16 * (g0 + gl[h]));
-        const int r = (int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * (g0 + gl[h])));
-        uint32_t b;
-        if (r == 3)
-          b = b64_decode_group_full(w, &tab, codes + 3 * h);
-        else
-          b = b64_decode_group(w, &tab, codes + 3 * h) & needed_chars_mask(r);
-        if (live[h]) {
-          badacc |= b;
-          if (c0 + cc[h] == M - 1)
-            for (int e = 0; e < 3; ++e) last_codes[3 * gl[h] + e] = codes[3 * h + e];
-          const uint32_t hm = hmask[gl[h]];
-          if (hm) {
-            for (int e = 0; e < 3; ++e)
-              if ((hm >> e) & 1u) {
-                atomicMin(&hmin[3 * gl[h] + e], codes[3 * h + e]);
-                atomicMax(&hmax[3 * gl[h] + e], codes[3 * h + e]);
-              }
-          }
-        }
-      }
-      // stage A
-      float y0[S], y[S];
-      {
-        bool all9 = true;
-#pragma unroll
-        for (int i = 0; i < S; ++i) all9 &= dec9_ok(codes[i]);
-        if (__ballot(!all9) == 0) {
-#pragma unroll
-          for (int i = 0; i < S; i += 2) {
-            const f2 v = dec_fast2(codes[i], codes[i + 1]);
-            y0[i] = v.x;
-            y0[i + 1] = v.y;
-          }
-        } else {
-#pragma unroll
-          for (int i = 0; i < S; i += 2) {
-            const f2 v = dec_gen2(codes[i], codes[i + 1]);
-            y0[i] = v.x;
-            y0[i + 1] = v.y;
-          }
-        }
-      }
-      q_stage<S>(y, y0, tab.digits, ws, lane);
-      // stage B (per-item client: dampening factor is a per-lane load)
-      float r[S], p[S];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const double d = dampen[c0 + cc[h]];
-#pragma unroll
-        for (int e = 0; e < 3; ++e) r[3 * h + e] = (float)((double)y[3 * h + e] * d);
-      }
-      q_stage<S>(p, r, tab.digits, ws, lane);
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-        if (live[h])
-#pragma unroll
-          for (int e = 0; e < 3; ++e) ptile[cc[h] * E + 3 * gl[h] + e] = p[3 * h + e];
+      tile_produce<TG>(sh, uploads, pitch, M, dampen, n_up, g0, ng, c0, nitems, base + tid, 256, ptile, badacc);
       if (base == 0) FLEET_TSTAMP(2);
     }
     __syncthreads();
     FLEET_TSTAMP(3);
     // phase 2: serial accumulation, one value per thread
     if (tid < E) {
-      const int col = tid;
       int k = 0;
       if (c0 == 0) {
-        A = ptile[col];
+        A = ptile[tid];
         k = 1;
       }
 #pragma unroll 4
       for (; k < cm; ++k) {
-        const float s = A + ptile[k * E + col];
+        const float s = A + ptile[k * E + tid];
         off_domain |= (uint32_t)!q_gen_ok(s);
         A = q_lat(s);
       }
@@ -509,31 +574,111 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
   FLEET_TSTAMP(4);
   if (badacc) atomicOr(err, FLEET_ERRBIT_BASE64);
   if (tid >= 3 * ng) off_domain = 0;  // columns past the last group hold no values
-  if (__ballot(off_domain != 0)) {  // wave-uniform, never for gradients
-    if (off_domain) A = chain_general(uploads, pitch, M, dampen, g0 + tid / 3, tid % 3, &tab);
+  if (__ballot(off_domain != 0)) {    // wave-uniform, never for gradients
+    if (off_domain) A = chain_general(uploads, pitch, M, dampen, g0 + tid / 3, tid % 3, &sh.tab);
   }
   if (tid < E) ptile[tid] = A;
   __syncthreads();
-  if (tid >= ng) return;
-  const int64_t g = g0 + tid;
-  const int64_t p0 = 3 * g;
-  const int r = (int)min<int64_t>(3, n_up - p0);
-  const uint32_t hm = hmask[tid];
-  int layout_bad = 0;
-  for (int e = 0; e < 3; ++e)
-    if ((hm >> e) & 1u) layout_bad |= hmin[3 * tid + e] != hmax[3 * tid + e];
-  if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
-  int32_t out[3];
+  tile_epilogue<TG>(sh, ptile, inv_avg, n_up, hdr_block[2], g0, ng, merged, merged_f32, err);
+  FLEET_TSTAMP(5);
+}
+
+// Pipelined tile variant (E = 3*TG <= 64): waves 1-3 produce p for passes of
+// CPP clients into an LDS ring of RING passes while wave 0 consumes them in
+// client order (the serial A = Q(A + p_c)), so the client-independent work
+// and the serial accumulation overlap instead of running back to back.
+// Hand-off through LDS: a producer wave publishes "passes done" with a
+// workgroup release after its p writes; the consumer acquires the minimum
+// over the three producer waves before reading a pass, and publishes "passes
+// consumed" so producers never overwrite a ring slot still being read. Every
+// wait has a partner that always makes progress, so the grid drains.
+template <int TG>
+__global__ void __launch_bounds__(256) k_update_pipe(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                     const double* __restrict__ dampen, double inv_avg,
+                                                     int64_t n_up, int64_t g_begin, int64_t g_end,
+                                                     const int32_t* __restrict__ hdr_block,
+                                                     uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                     int* __restrict__ err) {
+  constexpr int E = 3 * TG;
+  static_assert(E <= 64, "one consumer wave");
+  constexpr int NPW = 3;                       // producer waves
+  constexpr int CPP = (NPW * 64 * 2) / TG;     // clients per pass: 2 items per producer thread
+  constexpr int RING = (6144 / E) / CPP > 0 ? (6144 / E) / CPP : 1;  // passes in LDS (~24 KiB)
+  FLEET_TSTAMP(0);
+  __shared__ TileShared<TG> sh;
+  __shared__ float ptile[RING * CPP * E];
+  __shared__ float finals[E];
+  __shared__ int prog[NPW];  // passes completed by each producer wave
+  __shared__ int consumed;   // passes completed by the consumer
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int64_t g0 = g_begin + (int64_t)blockIdx.x * TG;
+  const int ng = (int)min<int64_t>(TG, g_end - g0);
+  if (tid < NPW) prog[tid] = 0;
+  if (tid == 0) consumed = 0;
+  tile_init<TG>(sh, hdr_block + 4, hdr_block[1], g0, ng);
+  FLEET_TSTAMP(1);
+  const int npass = (M + CPP - 1) / CPP;
+  uint32_t badacc = 0;
+
+  if (wave > 0) {  // ---------------------------------------------- producers
+    const int pt = tid - 64;
+    for (int pass = 0; pass < npass; ++pass) {
+      if (pass >= RING) {  // ring slot free once the consumer finished pass - RING
+        while (__hip_atomic_load(&consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < pass - RING + 1)
+          __builtin_amdgcn_s_sleep(1);
+      }
+      const int c_base = pass * CPP;
+      const int cm = min(CPP, M - c_base);
+      tile_produce<TG>(sh, uploads, pitch, M, dampen, n_up, g0, ng, c_base, cm * TG, pt, NPW * 64,
+                       ptile + (pass % RING) * CPP * E, badacc);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&prog[wave - 1], pass + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (pass == 0) FLEET_TSTAMP(2);
+    }
+  } else {  // ---------------------------------------------------- consumer
+    float A = 0.f;
+    uint32_t off_domain = 0;
+    const int col = tid < E ? tid : 0;
+    for (int pass = 0; pass < npass; ++pass) {
+      for (;;) {
+        int m = __hip_atomic_load(&prog[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
-  for (int e = 0; e < 3; ++e) {
-    const bool keep_last = ((hm >> e) & 1u) || p0 + e >= walk_end;
-    const int32_t o = merged_code(ptile[3 * tid + e], inv_avg, last_codes[3 * tid + e], keep_last, tab.digits);
-    out[e] = e < r ? o : 0;
+        for (int w = 1; w < NPW; ++w)
+          m = min(m, __hip_atomic_load(&prog[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (m > pass) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      if (pass == 0) {
+        FLEET_TSTAMP(2);
+        FLEET_TSTAMP(3);
+      }
+      const float* pt = ptile + (pass % RING) * CPP * E;
+      const int cm = min(CPP, M - pass * CPP);
+      int k = 0;
+      if (pass == 0) {
+        A = pt[col];
+        k = 1;
+      }
+#pragma unroll 4
+      for (; k < cm; ++k) {
+        const float s = A + pt[k * E + col];
+        off_domain |= (uint32_t)!q_gen_ok(s);
+        A = q_lat(s);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&consumed, pass + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (tid >= 3 * ng) off_domain = 0;  // columns past the last group hold no values
+    if (__ballot(off_domain != 0)) {    // wave-uniform, never for gradients
+      if (off_domain) A = chain_general(uploads, pitch, M, dampen, g0 + tid / 3, tid % 3, &sh.tab);
+    }
+    if (tid < E) finals[tid] = A;
   }
-  *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &tab), r);
-  if (merged_f32) {
-    for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec_gen(out[e]);
-  }
+  FLEET_TSTAMP(4);
+  if (badacc) atomicOr(err, FLEET_ERRBIT_BASE64);
+  __syncthreads();
+  tile_epilogue<TG>(sh, finals, inv_avg, n_up, hdr_block[2], g0, ng, merged, merged_f32, err);
   FLEET_TSTAMP(5);
 }
 
@@ -731,7 +876,7 @@ __global__ void __launch_bounds__(256) k_merge(const uint8_t* __restrict__ up, c
 // out[4..] = header positions.
 __global__ void k_layout_parse(const uint8_t* __restrict__ up, int64_t n, int cap, int32_t* __restrict__ out) {
   __shared__ B64Tables tab;
-  b64_tables_init(&tab);
+  b64_tables_init<64>(&tab);
   __syncthreads();
   if (threadIdx.x != 0) return;
   int64_t idx = 0;
@@ -807,11 +952,20 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
 #define FLEET_LAUNCH_TILED(TG)                                                                                     \
   hipLaunchKernelGGL(k_update_tiled<TG>, dim3((unsigned)((groups + TG - 1) / TG)), dim3(256), 0, s, uploads, pitch, \
                      M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
-    if (tg == 16) FLEET_LAUNCH_TILED(16);
-    else if (tg == 8) FLEET_LAUNCH_TILED(8);
-    else if (tg == 64) FLEET_LAUNCH_TILED(64);
+#define FLEET_LAUNCH_PIPE(TG)                                                                                      \
+  hipLaunchKernelGGL(k_update_pipe<TG>, dim3((unsigned)((groups + TG - 1) / TG)), dim3(256), 0, s, uploads, pitch,  \
+                     M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
+    // FLEET_UPDATE_PIPE=0 selects the two-phase (non-pipelined) tile kernel for tg <= 16
+    const char* pe = getenv("FLEET_UPDATE_PIPE");
+    const bool pipe = !(pe && !strcmp(pe, "0"));
+    if (tg == 16) {
+      if (pipe) FLEET_LAUNCH_PIPE(16); else FLEET_LAUNCH_TILED(16);
+    } else if (tg == 8) {
+      if (pipe) FLEET_LAUNCH_PIPE(8); else FLEET_LAUNCH_TILED(8);
+    } else if (tg == 64) FLEET_LAUNCH_TILED(64);
     else FLEET_LAUNCH_TILED(32);
 #undef FLEET_LAUNCH_TILED
+#undef FLEET_LAUNCH_PIPE
     return hipGetLastError();
   }
   const int K = update_groups_per_lane(groups);

@@ -41,6 +41,16 @@ static inline bool same(float a, float b) { return f2u(a) == f2u(b); }
 
 int main(int argc, char** argv) {
   bool exhaustive = argc > 1 && std::string(argv[1]) == "exhaustive";
+  if (argc > 1 && std::string(argv[1]) == "qlat") {  // q_lat alone, every input of its domain
+    long b = g_bad;
+    par_for(0, 1ull << 32, 1, [](uint64_t i) {
+      float x = u2f((uint32_t)i);
+      if (!q_gen_ok(x)) return;
+      if (!same(q_lat(x), fo_int2float(fo_float2int(x)))) g_bad++;
+    });
+    report("q_lat (exhaustive)", b);
+    return g_bad ? 1 : 0;
+  }
   const uint64_t s = exhaustive ? 1 : 97;  // sampling stride (odd, walks every residue class)
   long b0;
 

@@ -205,6 +205,8 @@ def test_update_groups_per_lane_variants(codec, oracle, monkeypatch, K):
 
 @pytest.mark.parametrize("env", [{"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "8"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16"},
+                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "8", "FLEET_UPDATE_PIPE": "0"},
+                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_UPDATE_PIPE": "0"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "32"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "64"},
                                  {"FLEET_UPDATE_MODE": "stream", "FLEET_UPDATE_K": "1"},
@@ -232,13 +234,18 @@ def test_update_large_magnitudes_slow_path(codec, oracle, monkeypatch, env):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm) == oracle.update_faithful(ups, d)
 
 
-@pytest.mark.parametrize("mode", ["tiled", "stream"])
+@pytest.mark.parametrize("mode", ["tiled", "tiled-nopipe", "tiled-wide", "stream"])
 def test_update_modes(codec, oracle, monkeypatch, mode):
-    """Both aggregation kernels (two-phase tiled for small buckets, streaming
-    for large ones) on ragged tiles, chunked client loops and every layout."""
-    monkeypatch.setenv("FLEET_UPDATE_MODE", mode)
+    """Every aggregation kernel (pipelined and two-phase tiles for small
+    buckets, streaming for large ones) on ragged tiles, client counts that wrap
+    the LDS ring / chunk several times, and every layout."""
+    monkeypatch.setenv("FLEET_UPDATE_MODE", mode.split("-")[0])
+    if mode == "tiled-nopipe":
+        monkeypatch.setenv("FLEET_UPDATE_PIPE", "0")
+    if mode == "tiled-wide":
+        monkeypatch.setenv("FLEET_TILE_G", "64")
     for lay, M in ((MNIST, 70), (synthetic(1000), 1), (synthetic(3001), 129), (synthetic(5002), 2),
-                   (CIFAR10, 3)):
+                   (synthetic(700), 300), (CIFAR10, 3)):
         ups = uploads_for(oracle, lay, M, seed=M)
         d = policy("inverse", M)
         hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
