@@ -59,8 +59,8 @@ class Shard:
         self.g0 = rank * groups  # global group offset of this slice
         # global layout = the per-rank layout replicated world times; headers of
         # this slice in local coordinates (the slice is one copy of the layout)
-        self.hpos = layout.header_positions()
-        self.hval = layout.header_values()
+        self.hpos = np.asarray(layout.header_positions(), dtype=np.int32)
+        self.hval = np.asarray(layout.header_values(), dtype=np.float32)
         self.L = F.b64_len(self.n_local)
         self.pitch = 16 * groups
         self.vpitch = 3 * groups
@@ -70,7 +70,7 @@ class Shard:
         self.merged = torch.empty((self.pitch,), dtype=torch.uint8, device=dev)
         self.merged_f32 = torch.empty((self.vpitch,), dtype=torch.float32, device=dev)
         codec.synth_device(seed + rank * 1000003, self.values, self.n_local, self.hpos, self.hval)
-        self.dampen = dampen_policy(M)
+        self.dampen = np.asarray(dampen_policy(M), dtype=np.float64)
         torch.cuda.synchronize()
 
     def encode(self):
@@ -87,7 +87,45 @@ class Shard:
         return upd, enc
 
 
-def time_workload(torch, dist, codec, name, steps, warmup, rank, world):
+def graph_of(torch, fn, reps: int):
+    """HIP graph (torch.cuda.CUDAGraph) of `reps` back-to-back calls of fn."""
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    return g
+
+
+def kernel_ms(torch, fn, reps: int = 10, rounds: int = 3) -> float:
+    """Average device time of one launch of fn: HIP events around the replay
+    of a graph of `reps` back-to-back launches (on the launch stream), so host
+    launch gaps are not counted. Agrees with rocprofv3's kernel trace."""
+    g = graph_of(torch, fn, reps)
+    g.replay()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    best = []
+    for _ in range(rounds):
+        a.record()
+        g.replay()
+        b.record()
+        b.synchronize()
+        best.append(a.elapsed_time(b) / reps)
+    del g
+    return float(np.mean(best))
+
+
+def steps_per_graph(steps: int, cap: int = 10) -> int:
+    return max(d for d in range(1, min(cap, steps) + 1) if steps % d == 0)
+
+
+def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=True):
+    """Times `steps` steps. graph=True: the local part of a step (encode +
+    aggregation) is captured once into a HIP graph of G steps and replayed
+    steps/G times (the all_gather, N>1, stays eager after each replay);
+    graph=False: eager launches (host launch gaps between the small kernels
+    included). Both variants are reported."""
+    import fleet_amd as F
     from fleet_amd.layouts import LAYOUTS
     lay_name, M, note = WORKLOADS[name]
     layout = LAYOUTS[lay_name]
@@ -96,37 +134,61 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world):
     if world > 1:
         gathered = torch.empty((world * sh.pitch,), dtype=torch.uint8, device=sh.merged.device)
 
-    def step(ev=None):
-        if ev:
-            ev[0].record()
+    def local():
         sh.encode()
-        if ev:
-            ev[1].record()
         sh.aggregate()
-        if ev:
-            ev[2].record()
+
+    def exchange():
         if world > 1:
             dist.all_gather_into_tensor(gathered, sh.merged)
 
+    def run_timed(body, count):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(count):
+            body()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        return time.perf_counter() - t0
+
     for _ in range(warmup):
-        step()
+        local()
+        exchange()
     torch.cuda.synchronize()
     codec.check()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
-    t0 = time.perf_counter()
-    for k in range(steps):
-        step(evs[k])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
+
+    def eager_step():
+        local()
+        exchange()
+    eager_elapsed = run_timed(eager_step, steps)
     codec.check()
-    enc_ms = float(np.mean([evs[k][0].elapsed_time(evs[k][1]) for k in range(steps)]))
-    upd_ms = float(np.mean([evs[k][1].elapsed_time(evs[k][2]) for k in range(steps)]))
+    eager_ms = eager_elapsed / steps * 1e3
+
+    # per-kernel device time (roofline): graph of 10 back-to-back launches each
+    enc_ms = kernel_ms(torch, sh.encode)
+    upd_ms = kernel_ms(torch, sh.aggregate)
+    codec.check()
+
+    elapsed = eager_elapsed
+    G = 1
+    if graph:
+        G = steps_per_graph(steps)
+        g = graph_of(torch, local, G)
+        for _ in range(max(1, warmup // G)):
+            g.replay()
+
+        def graph_block():
+            g.replay()
+            for _ in range(G if world > 1 else 0):  # N>1: every step's all_gather, eager
+                exchange()
+        elapsed = run_timed(graph_block, steps // G)
+        codec.check()
+        del g
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=sh.merged.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -138,6 +200,8 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world):
     res = {
         "workload": name, "note": note, "layout": lay_name, "clients": M, "n_up_per_rank": sh.n_local,
         "ms_per_step": ms, "gib_s": gib_s, "update_kernel_ms": upd_ms, "encode_kernel_ms": enc_ms,
+        "graph": graph, "steps_per_graph": G, "eager_ms_per_step": eager_ms,
+        "update_kernel": F.update_kernel(sh.L),
         "update_bytes": upd_b, "encode_bytes": enc_b,
         "update_gbs": upd_b / (upd_ms * 1e-3) / 1e9, "encode_gbs": enc_b / (enc_ms * 1e-3) / 1e9,
         "element_clients_per_s": world * M * sh.n_local / (elapsed / steps),
@@ -248,6 +312,8 @@ def main():
     ap.add_argument("--extras", default="cifar10_256,synth1m_256",
                     help="comma list of extra workloads measured in the same run (N=1 only); '' for none")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1 (default): replay steps from a captured HIP graph; 0: eager launches")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
@@ -265,11 +331,11 @@ def main():
     import fleet_amd as F
     codec = F.Codec(local)
 
-    main_res = time_workload(torch, dist, codec, args.workload, args.steps, args.warmup, rank, world)
+    main_res = time_workload(torch, dist, codec, args.workload, args.steps, args.warmup, rank, world, args.graph)
     extras = {}
     if world == 1 and args.extras:
         for w in [x for x in args.extras.split(",") if x and x != args.workload]:
-            extras[w] = time_workload(torch, dist, codec, w, max(3, args.steps // 4), 2, rank, world)
+            extras[w] = time_workload(torch, dist, codec, w, max(3, args.steps // 4), 2, rank, world, args.graph)
 
     e2e = None
     if world == 1 and not args.no_e2e:
@@ -302,12 +368,15 @@ def main():
         "config": {"workload": args.workload, "layout": r["layout"], "clients": r["clients"],
                    "n_up_per_rank": r["n_up_per_rank"], "parallelism": f"element-shard x{world}",
                    "dampening": "policy 1 inverse, tau = c mod 3"},
-        "roofline": {"bound": "hbm", "kernel": "k_update", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": r["update_kernel"], "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic[0] if traffic else None,
                      "traffic_source": f"{traffic[2]} ({traffic[1]})" if traffic else None,
                      "bytes_per_launch": r["update_bytes"], "kernel_ms": r["update_kernel_ms"]},
         "cpu_baseline": cpu,
+        "timing": {"graph": bool(r["graph"]), "steps_per_graph": r["steps_per_graph"],
+                   "eager_ms_per_step": r["eager_ms_per_step"],
+                   "kernel_ms": "HIP events around graph replays of 10 back-to-back launches"},
         "kernels": {"k_update_ms": r["update_kernel_ms"], "k_encode_f32_ms": r["encode_kernel_ms"],
                     "k_encode_gbs": r["encode_gbs"], "element_clients_per_s": r["element_clients_per_s"]},
         "extra": extras,

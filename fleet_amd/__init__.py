@@ -96,6 +96,7 @@ def lib() -> C.CDLL:
         "fleet_norm": (i32, [vp, vp, sz, C.POINTER(C.c_double)]),
         "fleet_update": (i32, [vp, vp, vp, i32, vp, vp, sz, szp, vp]),
         "fleet_update_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, sz, sz, vp, vp, vp]),
+        "fleet_update_kernel": (C.c_char_p, [sz]),
         "fleet_encode_device": (i32, [vp, vp, sz, sz, i32, vp, sz, vp]),
         "fleet_decode_device": (i32, [vp, vp, sz, sz, i32, vp, sz, vp]),
         "fleet_synth_device": (i32, [vp, C.c_uint64, i32, i32, vp, vp, i32, sz, vp, sz, vp]),
@@ -125,6 +126,11 @@ def b64_len(n_values: int) -> int:
 
 def b64_count(length: int) -> int:
     return 3 * length // 16
+
+
+def update_kernel(length: int) -> str:
+    """Aggregation kernel the library launches for uploads of `length` bytes."""
+    return lib().fleet_update_kernel(length).decode()
 
 
 def layout_from_sizes(w_sizes: Sequence[int], b_sizes: Sequence[int]):

@@ -550,6 +550,10 @@ int fleet_synth_device(fleet_ctx* c, uint64_t seed, int M, int client0, const in
   return FLEET_OK;
 }
 
+const char* fleet_update_kernel(size_t len) {
+  return fleet::update_kernel_name((int64_t)groups_of(fleet_b64_count(len)));
+}
+
 int fleet_selftest_digest(fleet_ctx* c, int fn, uint64_t* out) {
   if (!c || !out || fn < 0 || fn > 12) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);

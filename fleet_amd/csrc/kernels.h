@@ -7,6 +7,8 @@ namespace fleet {
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s);
+// name of the aggregation kernel launch_update picks for `groups` groups
+const char* update_kernel_name(int64_t groups);
 hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int rows, uint8_t* out, size_t pitch,
                              hipStream_t s);
 hipError_t launch_encode_i32(const int32_t* codes, int64_t n, uint8_t* out, hipStream_t s);

@@ -7,6 +7,7 @@
 // 420-509); a wave reads 1 KiB contiguous per client row (global_load_dwordx4).
 #include "kernels.h"
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -939,46 +940,63 @@ static bool use_tiled(int64_t groups) {
   return groups < 256LL * 4 * 2 * 64;
 }
 
+// Kernel choice for a bucket of `groups` 3-value groups (environment
+// overrides for experiments: FLEET_UPDATE_MODE=stream|tiled, FLEET_TILE_G,
+// FLEET_UPDATE_PIPE=0, FLEET_UPDATE_K).
+struct UpdatePlan {
+  int kind;  // 0 stream k_update<k>, 1 k_update_tiled<tg>, 2 k_update_pipe<tg>
+  int tg, k;
+};
+static UpdatePlan plan_update(int64_t groups) {
+  UpdatePlan p{0, 0, 1};
+  if (use_tiled(groups)) {
+    // widest tile that still gives >= 4 blocks per CU; the narrow tiles are
+    // pipelined (producer waves + one consumer wave)
+    p.tg = groups >= 64LL * 1024 ? 64 : groups >= 32LL * 1024 ? 32 : 16;
+    if (const char* e = getenv("FLEET_TILE_G")) p.tg = atoi(e);
+    if (p.tg != 8 && p.tg != 16 && p.tg != 32 && p.tg != 64) p.tg = 16;
+    const char* pe = getenv("FLEET_UPDATE_PIPE");
+    p.kind = (p.tg <= 16 && !(pe && !strcmp(pe, "0"))) ? 2 : 1;
+    return p;
+  }
+  p.k = update_groups_per_lane(groups);
+  p.k = p.k >= 4 ? 4 : p.k == 2 ? 2 : 1;
+  return p;
+}
+
+const char* update_kernel_name(int64_t groups) {
+  static thread_local char buf[48];
+  const UpdatePlan p = plan_update(groups);
+  if (p.kind == 0)
+    snprintf(buf, sizeof buf, "k_update<%d>", p.k);
+  else
+    snprintf(buf, sizeof buf, "%s<%d>", p.kind == 2 ? "k_update_pipe" : "k_update_tiled", p.tg);
+  return buf;
+}
+
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
   if (g_end <= g_begin) return hipSuccess;
   const int64_t groups = g_end - g_begin;
-  if (use_tiled(groups)) {
-    // widest tile that still gives >= 4 blocks per CU (phase 2 is one wave per
-    // block walking the clients serially: more, narrower tiles hide its latency)
-    int tg = groups >= 64LL * 1024 ? 64 : groups >= 32LL * 1024 ? 32 : 16;
-    if (const char* e = getenv("FLEET_TILE_G")) tg = atoi(e);
-#define FLEET_LAUNCH_TILED(TG)                                                                                     \
-  hipLaunchKernelGGL(k_update_tiled<TG>, dim3((unsigned)((groups + TG - 1) / TG)), dim3(256), 0, s, uploads, pitch, \
-                     M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
-#define FLEET_LAUNCH_PIPE(TG)                                                                                      \
-  hipLaunchKernelGGL(k_update_pipe<TG>, dim3((unsigned)((groups + TG - 1) / TG)), dim3(256), 0, s, uploads, pitch,  \
-                     M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
-    // FLEET_UPDATE_PIPE=0 selects the two-phase (non-pipelined) tile kernel for tg <= 16
-    const char* pe = getenv("FLEET_UPDATE_PIPE");
-    const bool pipe = !(pe && !strcmp(pe, "0"));
-    if (tg == 16) {
-      if (pipe) FLEET_LAUNCH_PIPE(16); else FLEET_LAUNCH_TILED(16);
-    } else if (tg == 8) {
-      if (pipe) FLEET_LAUNCH_PIPE(8); else FLEET_LAUNCH_TILED(8);
-    } else if (tg == 64) FLEET_LAUNCH_TILED(64);
-    else FLEET_LAUNCH_TILED(32);
-#undef FLEET_LAUNCH_TILED
-#undef FLEET_LAUNCH_PIPE
-    return hipGetLastError();
+  const UpdatePlan p = plan_update(groups);
+#define FLEET_LAUNCH(KERNEL, PER_BLOCK)                                                                         \
+  hipLaunchKernelGGL(KERNEL, dim3((unsigned)((groups + (PER_BLOCK)-1) / (PER_BLOCK))), dim3(256), 0, s, uploads, \
+                     pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
+  if (p.kind == 2) {
+    if (p.tg == 8) FLEET_LAUNCH(k_update_pipe<8>, 8);
+    else FLEET_LAUNCH(k_update_pipe<16>, 16);
+  } else if (p.kind == 1) {
+    if (p.tg == 8) FLEET_LAUNCH(k_update_tiled<8>, 8);
+    else if (p.tg == 16) FLEET_LAUNCH(k_update_tiled<16>, 16);
+    else if (p.tg == 32) FLEET_LAUNCH(k_update_tiled<32>, 32);
+    else FLEET_LAUNCH(k_update_tiled<64>, 64);
+  } else {
+    if (p.k == 4) FLEET_LAUNCH(k_update<4>, 256 * 4);
+    else if (p.k == 2) FLEET_LAUNCH(k_update<2>, 256 * 2);
+    else FLEET_LAUNCH(k_update<1>, 256);
   }
-  const int K = update_groups_per_lane(groups);
-  const unsigned blocks = (unsigned)((groups + 256 * K - 1) / (256 * K));
-  if (K >= 4)
-    hipLaunchKernelGGL(k_update<4>, dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
-                       g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
-  else if (K == 2)
-    hipLaunchKernelGGL(k_update<2>, dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
-                       g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
-  else
-    hipLaunchKernelGGL(k_update<1>, dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
-                       g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
+#undef FLEET_LAUNCH
   return hipGetLastError();
 }
 

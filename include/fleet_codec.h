@@ -160,6 +160,11 @@ int fleet_check(fleet_ctx* ctx, void* stream);
  * computed on the GPU; compare with the oracle's digests. */
 int fleet_selftest_digest(fleet_ctx* ctx, int fn, uint64_t* out);
 
+/* Name of the aggregation kernel fleet_update / fleet_update_device launch for
+ * an upload of `len` Base64 bytes (or a group window of that many bytes):
+ * "k_update<K>", "k_update_tiled<TG>" or "k_update_pipe<TG>" (profiling aid). */
+const char* fleet_update_kernel(size_t len);
+
 #ifdef __cplusplus
 }
 #endif

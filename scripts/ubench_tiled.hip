@@ -128,7 +128,34 @@ void run(int64_t n_up, int M, int reps = 1) {
   hipFree(err);
 }
 
+// back-to-back client encodes of M rows of n floats (k_encode_f32)
+static void time_encode(int64_t n_up, int M, int reps) {
+  const int64_t groups = (n_up + 2) / 3;
+  const size_t pitch = 16 * groups, vpitch = 3 * groups;
+  float* vals;
+  uint8_t* text;
+  hipMalloc(&vals, sizeof(float) * vpitch * M);
+  hipMalloc(&text, pitch * M);
+  launch_synth(1, 0, M, n_up, vals, vpitch, nullptr, nullptr, 0, 0);
+  for (int r = 0; r < 3; ++r) launch_encode_f32(vals, n_up, vpitch, M, text, pitch, 0);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a);
+  for (int r = 0; r < reps; ++r) launch_encode_f32(vals, n_up, vpitch, M, text, pitch, 0);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms;
+  hipEventElapsedTime(&ms, a, b);
+  printf("encode n=%ld M=%d: %.2f us per launch (%d back-to-back)\n", (long)n_up, M, ms * 1e3 / reps, reps);
+  hipFree(vals);
+  hipFree(text);
+}
+
 int main() {
+  time_encode(22961, 64, 50);
+  time_encode(22961, 1, 50);
+  time_encode(313867, 256, 5);
   g_hpos.clear();
   g_hval.clear();
   for (int M : {4, 16, 64}) run<16>(22961, M);
