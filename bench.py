@@ -211,7 +211,7 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
     return res
 
 
-def pmc_traffic(workload: str):
+def pmc_traffic(workload: str, kernel: str = ""):
     """HBM bytes per k_update launch for `workload` from the newest committed
     rocprofv3 PMC summary (profiles/rNN/traffic.json, written by
     scripts/pmc_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE passes,
@@ -223,9 +223,9 @@ def pmc_traffic(workload: str):
                 kern = json.load(f)["workloads"].get(workload, {})
         except (OSError, ValueError, KeyError):
             continue
-        for k, v in kern.items():
-            if k.startswith("k_update") and "hbm_bytes" in v:
-                return v["hbm_bytes"], k, os.path.relpath(path, ROOT)
+        # only a profile of the same kernel variant counts
+        if kernel in kern and "hbm_bytes" in kern[kernel]:
+            return kern[kernel]["hbm_bytes"], kernel, os.path.relpath(path, ROOT)
     return None
 
 
@@ -351,7 +351,7 @@ def main():
         cpu = cpu_baseline(args.cpu_budget)
     r = main_res
     achieved = r["update_gbs"]
-    traffic = pmc_traffic(args.workload) if world == 1 else None
+    traffic = pmc_traffic(args.workload, r["update_kernel"]) if world == 1 else None
     line = {
         "metric": "gradient GiB/s encode+decode+aggregate (device-resident); % HBM roofline",
         "value": r["gib_s"],

@@ -374,6 +374,7 @@ struct TileShared {
   int32_t last_codes[E];        // codes of the last upload (mergeFlatGradient's g)
   int32_t hmin[E], hmax[E];     // header-slot codes over all uploads (layout check)
   uint32_t hmask[TG];           // bit e = slot 3*g+e is a header slot
+  int32_t outcodes[E];          // merged codes (epilogue)
 };
 
 // Tables, header slots of the tile (every thread checks one header position:
@@ -400,25 +401,25 @@ __device__ __forceinline__ void tile_init(TileShared<TG>& sh, const int32_t* __r
   __syncthreads();
 }
 
-// Client-independent part of the chain for up to two (client, group) items per
-// thread: items it0 and it0 + stride of the nitems items (client-major:
+// Client-independent part of the chain for IPT (client, group) items per
+// thread: items it0 + h*stride (h < IPT) of the nitems items (client-major:
 // item = cc*TG + gl) of clients c_base.. ; p of client c_base+cc, slot 3*gl+e
 // goes to pdst[cc*E + 3*gl + e]:
 //   p = Q(f32(f64(Q(int2float(code))) * d_c))   (CppNNUpdater.java:463-464)
 // Also: Base64 validity, the last upload's codes, header-slot min/max.
-template <int TG>
+template <int TG, int IPT>
 __device__ __forceinline__ void tile_produce(TileShared<TG>& sh, const uint8_t* __restrict__ uploads, size_t pitch,
                                              int M, const double* __restrict__ dampen, int64_t n_up, int64_t g0,
                                              int ng, int c_base, int nitems, int it0, int stride,
                                              float* __restrict__ pdst, uint32_t& badacc) {
-  constexpr int E = 3 * TG, S = 6;
+  constexpr int E = 3 * TG, S = 3 * IPT;
   const int lane = threadIdx.x & 63;
   uint32_t* ws = sh.scratch[threadIdx.x >> 6];
   int32_t codes[S];
-  int cc[2], gl[2];
-  bool live[2];
+  int cc[IPT], gl[IPT];
+  bool live[IPT];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < IPT; ++h) {
     const int item = it0 + h * stride;
     live[h] = item < nitems && (item % TG) < ng;
     cc[h] = live[h] ? item / TG : 0;
@@ -452,63 +453,67 @@ __device__ __forceinline__ void tile_produce(TileShared<TG>& sh, const uint8_t* 
     for (int i = 0; i < S; ++i) all9 &= dec9_ok(codes[i]);
     if (__ballot(!all9) == 0) {
 #pragma unroll
-      for (int i = 0; i < S; i += 2) {
+      for (int i = 0; i + 1 < S; i += 2) {
         const f2 v = dec_fast2(codes[i], codes[i + 1]);
         y0[i] = v.x;
         y0[i + 1] = v.y;
       }
+      if (S & 1) y0[S - 1] = dec_fast(codes[S - 1]);
     } else {
 #pragma unroll
-      for (int i = 0; i < S; i += 2) {
+      for (int i = 0; i + 1 < S; i += 2) {
         const f2 v = dec_gen2(codes[i], codes[i + 1]);
         y0[i] = v.x;
         y0[i + 1] = v.y;
       }
+      if (S & 1) y0[S - 1] = dec_gen(codes[S - 1]);
     }
   }
   q_stage<S>(y, y0, sh.tab.digits, ws, lane);
   // stage B: p = Q(f32(f64(y) * d)), per-item client
   float r[S], p[S];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < IPT; ++h) {
     const double d = dampen[c_base + cc[h]];
 #pragma unroll
     for (int e = 0; e < 3; ++e) r[3 * h + e] = (float)((double)y[3 * h + e] * d);
   }
   q_stage<S>(p, r, sh.tab.digits, ws, lane);
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < IPT; ++h)
     if (live[h])
 #pragma unroll
       for (int e = 0; e < 3; ++e) pdst[cc[h] * E + 3 * gl[h] + e] = p[3 * h + e];
 }
 
-// Final values of the tile (vals[0..E)) -> merged Base64 (+ fp32), layout check.
+// Final values of the tile (vals[0..E)) -> merged Base64 (+ fp32), layout
+// check. One thread per value computes its merged code (the longest part),
+// then one thread per group assembles the 16 Base64 chars. Call from every
+// thread of the block (contains a barrier).
 template <int TG>
 __device__ __forceinline__ void tile_epilogue(TileShared<TG>& sh, const float* __restrict__ vals, double inv_avg,
                                               int64_t n_up, int64_t walk_end, int64_t g0, int ng,
                                               uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
                                               int* __restrict__ err) {
   const int tid = threadIdx.x;
-  if (tid >= ng) return;
-  const int64_t g = g0 + tid;
-  const int64_t p0 = 3 * g;
-  const int r = (int)min<int64_t>(3, n_up - p0);
-  const uint32_t hm = sh.hmask[tid];
-  int layout_bad = 0;
-  for (int e = 0; e < 3; ++e)
-    if ((hm >> e) & 1u) layout_bad |= sh.hmin[3 * tid + e] != sh.hmax[3 * tid + e];
-  if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
-  int32_t out[3];
-#pragma unroll
-  for (int e = 0; e < 3; ++e) {
-    const bool keep_last = ((hm >> e) & 1u) || p0 + e >= walk_end;
-    const int32_t o = merged_code(vals[3 * tid + e], inv_avg, sh.last_codes[3 * tid + e], keep_last, sh.tab.digits);
-    out[e] = e < r ? o : 0;
+  if (tid < 3 * ng) {
+    const int gl = tid / 3, e = tid % 3;
+    const int64_t p = 3 * g0 + tid;
+    int32_t o = 0;
+    if (p < n_up) {
+      const bool hdr = (sh.hmask[gl] >> e) & 1u;
+      if (hdr && sh.hmin[tid] != sh.hmax[tid]) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+      o = merged_code(vals[tid], inv_avg, sh.last_codes[tid], hdr || p >= walk_end, sh.tab.digits);
+      if (merged_f32) merged_f32[p] = dec_gen(o);
+    }
+    sh.outcodes[tid] = o;
   }
-  *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &sh.tab), r);
-  if (merged_f32) {
-    for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec_gen(out[e]);
+  __syncthreads();
+  if (tid < ng) {
+    const int64_t g = g0 + tid;
+    const int r = (int)min<int64_t>(3, n_up - 3 * g);
+    const int32_t out[3] = {sh.outcodes[3 * tid], sh.outcodes[3 * tid + 1], sh.outcodes[3 * tid + 2]};
+    *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &sh.tab), r);
   }
 }
 
@@ -551,7 +556,7 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
     const int cm = min(CM, M - c0);
     const int nitems = cm * TG;
     for (int base = 0; base < nitems; base += 512) {
-      tile_produce<TG>(sh, uploads, pitch, M, dampen, n_up, g0, ng, c0, nitems, base + tid, 256, ptile, badacc);
+      tile_produce<TG, 2>(sh, uploads, pitch, M, dampen, n_up, g0, ng, c0, nitems, base + tid, 256, ptile, badacc);
       if (base == 0) FLEET_TSTAMP(2);
     }
     __syncthreads();
@@ -593,7 +598,7 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
 // over the three producer waves before reading a pass, and publishes "passes
 // consumed" so producers never overwrite a ring slot still being read. Every
 // wait has a partner that always makes progress, so the grid drains.
-template <int TG>
+template <int TG, int IPT>
 __global__ void __launch_bounds__(256) k_update_pipe(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                      const double* __restrict__ dampen, double inv_avg,
                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
@@ -603,7 +608,7 @@ __global__ void __launch_bounds__(256) k_update_pipe(const uint8_t* __restrict__
   constexpr int E = 3 * TG;
   static_assert(E <= 64, "one consumer wave");
   constexpr int NPW = 3;                       // producer waves
-  constexpr int CPP = (NPW * 64 * 2) / TG;     // clients per pass: 2 items per producer thread
+  constexpr int CPP = (NPW * 64 * IPT) / TG;   // clients per pass: IPT items per producer thread
   constexpr int RING = (6144 / E) / CPP > 0 ? (6144 / E) / CPP : 1;  // passes in LDS (~24 KiB)
   FLEET_TSTAMP(0);
   __shared__ TileShared<TG> sh;
@@ -630,8 +635,8 @@ __global__ void __launch_bounds__(256) k_update_pipe(const uint8_t* __restrict__
       }
       const int c_base = pass * CPP;
       const int cm = min(CPP, M - c_base);
-      tile_produce<TG>(sh, uploads, pitch, M, dampen, n_up, g0, ng, c_base, cm * TG, pt, NPW * 64,
-                       ptile + (pass % RING) * CPP * E, badacc);
+      tile_produce<TG, IPT>(sh, uploads, pitch, M, dampen, n_up, g0, ng, c_base, cm * TG, pt, NPW * 64,
+                            ptile + (pass % RING) * CPP * E, badacc);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&prog[wave - 1], pass + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (pass == 0) FLEET_TSTAMP(2);
@@ -944,11 +949,12 @@ static bool use_tiled(int64_t groups) {
 // overrides for experiments: FLEET_UPDATE_MODE=stream|tiled, FLEET_TILE_G,
 // FLEET_UPDATE_PIPE=0, FLEET_UPDATE_K).
 struct UpdatePlan {
-  int kind;  // 0 stream k_update<k>, 1 k_update_tiled<tg>, 2 k_update_pipe<tg>
-  int tg, k;
+  int kind;  // 0 stream k_update<k>, 1 k_update_tiled<tg>, 2 k_update_pipe<tg, ipt>
+  int tg, k, ipt;
 };
 static UpdatePlan plan_update(int64_t groups) {
-  UpdatePlan p{0, 0, 1};
+  UpdatePlan p{0, 0, 1, 1};
+  if (const char* e = getenv("FLEET_PIPE_IPT")) p.ipt = atoi(e) == 2 ? 2 : 1;
   if (use_tiled(groups)) {
     // widest tile that still gives >= 4 blocks per CU; the narrow tiles are
     // pipelined (producer waves + one consumer wave)
@@ -969,8 +975,10 @@ const char* update_kernel_name(int64_t groups) {
   const UpdatePlan p = plan_update(groups);
   if (p.kind == 0)
     snprintf(buf, sizeof buf, "k_update<%d>", p.k);
+  else if (p.kind == 2)
+    snprintf(buf, sizeof buf, "k_update_pipe<%d, %d>", p.tg, p.ipt);
   else
-    snprintf(buf, sizeof buf, "%s<%d>", p.kind == 2 ? "k_update_pipe" : "k_update_tiled", p.tg);
+    snprintf(buf, sizeof buf, "k_update_tiled<%d>", p.tg);
   return buf;
 }
 
@@ -984,8 +992,13 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
   hipLaunchKernelGGL(KERNEL, dim3((unsigned)((groups + (PER_BLOCK)-1) / (PER_BLOCK))), dim3(256), 0, s, uploads, \
                      pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
   if (p.kind == 2) {
-    if (p.tg == 8) FLEET_LAUNCH(k_update_pipe<8>, 8);
-    else FLEET_LAUNCH(k_update_pipe<16>, 16);
+    if (p.ipt == 2) {
+      if (p.tg == 8) FLEET_LAUNCH((k_update_pipe<8, 2>), 8);
+      else FLEET_LAUNCH((k_update_pipe<16, 2>), 16);
+    } else {
+      if (p.tg == 8) FLEET_LAUNCH((k_update_pipe<8, 1>), 8);
+      else FLEET_LAUNCH((k_update_pipe<16, 1>), 16);
+    }
   } else if (p.kind == 1) {
     if (p.tg == 8) FLEET_LAUNCH(k_update_tiled<8>, 8);
     else if (p.tg == 16) FLEET_LAUNCH(k_update_tiled<16>, 16);

@@ -10,6 +10,7 @@
 #include "fleet_oracle.h"
 
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #ifdef _OPENMP
@@ -444,4 +445,169 @@ void fo_synth_upload(uint64_t seed, uint32_t client, const int32_t* w_sizes, int
     idx += (size_t)b_sizes[i];
   }
   free(mask);
+}
+
+/* ======================================================================
+ * DISTILLATION_MODE=1 model codec.
+ * ==================================================================== */
+
+/* network.h:1683-1774 (non-bucketing path) with matrix::min_max
+ * (core_math.h:881-899), operator+(float)/operator*(float) (:1045-1056) and
+ * round_matrix (:901-912), for one weight matrix of cols*rows*chans floats
+ * (W matrices are built with chan_aligned = 0: chan_stride = cols*rows, no
+ * padding; layer.h:158,787,1297). In place. */
+void fo_quantize_matrix(float* x, int cols, int rows, int chans) {
+  const int s = rows * cols;
+  const size_t n = (size_t)s * (size_t)chans;
+  if (n == 0) return;
+  size_t mini = 0, maxi = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (x[i] < x[mini]) mini = i;
+    if (x[i] > x[maxi]) maxi = i;
+  }
+  const float mn = x[mini], mx = x[maxi];
+  const float alpha = mx - mn, beta = mn;
+  const float nbeta = (float)(-1.0 * (double)beta); /* `+ (-1.0) * beta` -> operator+(float) */
+  const float ialpha = (float)(1.0 / (double)alpha); /* `* (1.0 / alpha)` -> operator*(float) */
+  for (size_t i = 0; i < n; ++i) x[i] = x[i] + nbeta;
+  for (size_t i = 0; i < n; ++i) x[i] = x[i] * ialpha;
+  const float fs = (float)s;
+  const float one_over_s = (float)(1 / s); /* integer division: 1 if s == 1 else 0 */
+  for (size_t i = 0; i < n; ++i) {
+    if (x[i] - floorf(x[i]) > 0.5f)
+      x[i] = floorf(x[i] * fs) / fs + one_over_s;
+    else
+      x[i] = floorf(x[i] * fs) / fs;
+  }
+  for (size_t i = 0; i < n; ++i) x[i] = x[i] * alpha;
+  for (size_t i = 0; i < n; ++i) x[i] = x[i] + beta;
+}
+
+/* network.h:594-608 float_vector_find + the two passes of getParams
+ * (:641-692): pass 1 builds the first-occurrence dictionary (an element joins
+ * the first entry with fabsf(x - e) < 1e-8f, else is appended); pass 2 prints
+ * the first matching entry, -1 when none (NaN/inf never match, not even
+ * themselves). Returns U; dict (capacity n) gets the entries in creation
+ * order, index[i] the printed index of w[i]. */
+int fo_dictionary(const float* w, size_t n, float* dict, int32_t* index) {
+  int U = 0;
+  for (size_t i = 0; i < n; ++i) {
+    int found = 0;
+    for (int k = 0; k < U; ++k)
+      if (fabsf(w[i] - dict[k]) < 0.00000001f) {
+        found = 1;
+        break;
+      }
+    if (!found) dict[U++] = w[i];
+  }
+  for (size_t i = 0; i < n; ++i) {
+    int32_t idx = -1;
+    for (int k = 0; k < U; ++k)
+      if (fabsf(w[i] - dict[k]) < 0.00000001f) {
+        idx = k;
+        break;
+      }
+    index[i] = idx;
+  }
+  return U;
+}
+
+static size_t put(char* out, size_t cap, size_t pos, const char* s) {
+  size_t l = strlen(s);
+  if (out && pos + l <= cap) memcpy(out + pos, s, l);
+  return pos + l;
+}
+
+/* The weights section of getParams in DISTILLATION_MODE=1 (network.h:641-692):
+ * "loop_counter\nU\n" + U x "k\nvalue\n" (ostream default precision 6 == %g)
+ * + per matrix the indices each followed by ' ' and a final '\n'.
+ * w = the already quantized weights, dims = n_mats x {cols, rows, chans}.
+ * Returns the text length (writes only what fits in cap). */
+size_t fo_weights_section(const float* w, const int32_t* dims, int n_mats, char* out, size_t cap) {
+  size_t n = 0;
+  for (int j = 0; j < n_mats; ++j) n += (size_t)dims[3 * j] * dims[3 * j + 1] * dims[3 * j + 2];
+  float* dict = (float*)malloc(sizeof(float) * (n ? n : 1));
+  int32_t* index = (int32_t*)malloc(sizeof(int32_t) * (n ? n : 1));
+  const int U = fo_dictionary(w, n, dict, index);
+  char buf[64];
+  size_t pos = 0;
+  snprintf(buf, sizeof buf, "%zu\n%d\n", n, U);
+  pos = put(out, cap, pos, buf);
+  for (int k = 0; k < U; ++k) {
+    snprintf(buf, sizeof buf, "%d\n%g\n", k, (double)dict[k]);
+    pos = put(out, cap, pos, buf);
+  }
+  size_t i = 0;
+  for (int j = 0; j < n_mats; ++j) {
+    const size_t m = (size_t)dims[3 * j] * dims[3 * j + 1] * dims[3 * j + 2];
+    for (size_t t = 0; t < m; ++t, ++i) {
+      snprintf(buf, sizeof buf, "%d ", index[i]);
+      pos = put(out, cap, pos, buf);
+    }
+    pos = put(out, cap, pos, "\n");
+  }
+  free(dict);
+  free(index);
+  return pos;
+}
+
+/* network::read's DISTILLATION_MODE=1 branch (network.h:958-997) on a weights
+ * section: U pairs (index, value read by `>>` = strtof), then W[i] =
+ * unique_mapping[index] (std::map operator[]: 0.0f for an index it lacks).
+ * Returns 0, or -1 on malformed text. */
+int fo_read_weights_section(const char* text, size_t len, const int32_t* dims, int n_mats, float* w_out) {
+  char* s = (char*)malloc(len + 1);
+  memcpy(s, text, len);
+  s[len] = 0;
+  char* p = s;
+  char* e;
+  long loop_counter = strtol(p, &e, 10);
+  if (e == p) goto bad;
+  p = e;
+  long U = strtol(p, &e, 10);
+  if (e == p || U < 0) goto bad;
+  p = e;
+  (void)loop_counter;
+  {
+    /* std::map semantics: insert keeps the first value for a repeated key */
+    long* keys = (long*)malloc(sizeof(long) * (U ? U : 1));
+    float* vals = (float*)malloc(sizeof(float) * (U ? U : 1));
+    long nk = 0;
+    for (long k = 0; k < U; ++k) {
+      long idx = strtol(p, &e, 10);
+      if (e == p) { free(keys); free(vals); goto bad; }
+      p = e;
+      float v = strtof(p, &e);
+      if (e == p) { free(keys); free(vals); goto bad; }
+      p = e;
+      int dup = 0;
+      for (long q = 0; q < nk; ++q)
+        if (keys[q] == idx) { dup = 1; break; }
+      if (!dup) { keys[nk] = idx; vals[nk] = v; ++nk; }
+    }
+    size_t i = 0;
+    for (int j = 0; j < n_mats; ++j) {
+      const size_t m = (size_t)dims[3 * j] * dims[3 * j + 1] * dims[3 * j + 2];
+      for (size_t t = 0; t < m; ++t, ++i) {
+        long idx = strtol(p, &e, 10);
+        if (e == p) { free(keys); free(vals); goto bad; }
+        p = e;
+        float v = 0.0f;
+        /* dictionary indices are 0..U-1 in order: direct lookup, else search */
+        if (idx >= 0 && idx < nk && keys[idx] == idx)
+          v = vals[idx];
+        else
+          for (long q = 0; q < nk; ++q)
+            if (keys[q] == idx) { v = vals[q]; break; }
+        w_out[i] = v;
+      }
+    }
+    free(keys);
+    free(vals);
+  }
+  free(s);
+  return 0;
+bad:
+  free(s);
+  return -1;
 }

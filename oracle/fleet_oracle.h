@@ -77,6 +77,16 @@ float fo_synth_value(uint64_t seed, uint32_t client, uint32_t element);
 void fo_synth_upload(uint64_t seed, uint32_t client, const int32_t* w_sizes, int n_w, const int32_t* b_sizes,
                      int n_b, float* out);
 
+/* ---- DISTILLATION_MODE=1 model codec ---- */
+/* network.h:1683-1774 + core_math.h:881-912: quantise one W matrix in place. */
+void fo_quantize_matrix(float* x, int cols, int rows, int chans);
+/* network.h:594-608,641-692: first-occurrence dictionary + printed indices. */
+int fo_dictionary(const float* w, size_t n, float* dict, int32_t* index);
+/* getParams' DISTILLATION_MODE=1 weights section for quantised weights. */
+size_t fo_weights_section(const float* w, const int32_t* dims, int n_mats, char* out, size_t cap);
+/* network::read's DISTILLATION_MODE=1 weights branch (network.h:958-997). */
+int fo_read_weights_section(const char* text, size_t len, const int32_t* dims, int n_mats, float* w_out);
+
 #ifdef __cplusplus
 }
 #endif

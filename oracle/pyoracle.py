@@ -21,6 +21,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libfleetref.so")
 REF_O2_SO = os.path.join(HERE, "_ref", "libfleetref_O2.so")
+REF_MODEL_SO = os.path.join(HERE, "_ref", "libfleetref_model.so")
 
 _c_char_pp = C.POINTER(C.c_char_p)
 
@@ -102,6 +103,14 @@ class Oracle:
                                       C.c_void_p]
         L.fo_philox4x32_10.restype = None
         L.fo_philox4x32_10.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.fo_quantize_matrix.restype = None
+        L.fo_quantize_matrix.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+        L.fo_dictionary.restype = C.c_int
+        L.fo_dictionary.argtypes = [C.c_void_p, sz, C.c_void_p, C.c_void_p]
+        L.fo_weights_section.restype = sz
+        L.fo_weights_section.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, sz]
+        L.fo_read_weights_section.restype = C.c_int
+        L.fo_read_weights_section.argtypes = [C.c_void_p, sz, C.c_void_p, C.c_int, C.c_void_p]
 
     # -- scalars / vectors ------------------------------------------------
     def float2int(self, x: np.ndarray) -> np.ndarray:
@@ -213,6 +222,42 @@ class Oracle:
         self.lib.fo_synth_upload(seed, client, w.ctypes.data, len(w), b.ctypes.data, len(b), out.ctypes.data)
         return out
 
+    # -- DISTILLATION_MODE=1 model codec -----------
+    def quantize(self, w, dims) -> np.ndarray:
+        """quantization_weight_model over the concatenated matrices (dims: [(cols, rows, chans)])."""
+        w = np.array(w, dtype=np.float32, copy=True)
+        off = 0
+        for c, r, ch in dims:
+            n = c * r * ch
+            seg = np.ascontiguousarray(w[off:off + n])
+            self.lib.fo_quantize_matrix(seg.ctypes.data, c, r, ch)
+            w[off:off + n] = seg
+            off += n
+        return w
+
+    def dictionary(self, w):
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        d = np.empty(max(1, len(w)), np.float32)
+        idx = np.empty(max(1, len(w)), np.int32)
+        U = self.lib.fo_dictionary(w.ctypes.data, len(w), d.ctypes.data, idx.ctypes.data)
+        return d[:U].copy(), idx[: len(w)].copy()
+
+    def weights_section(self, wq, dims) -> bytes:
+        wq = np.ascontiguousarray(wq, dtype=np.float32)
+        dm = np.ascontiguousarray(dims, dtype=np.int32).reshape(-1)
+        n = self.lib.fo_weights_section(wq.ctypes.data, dm.ctypes.data, len(dm) // 3, None, 0)
+        buf = np.empty(n, np.uint8)
+        self.lib.fo_weights_section(wq.ctypes.data, dm.ctypes.data, len(dm) // 3, buf.ctypes.data, n)
+        return buf.tobytes()
+
+    def read_weights_section(self, text: bytes, dims) -> np.ndarray:
+        dm = np.ascontiguousarray(dims, dtype=np.int32).reshape(-1)
+        n = int(sum(c * r * ch for c, r, ch in np.asarray(dims).reshape(-1, 3)))
+        out = np.empty(n, np.float32)
+        if self.lib.fo_read_weights_section(text, len(text), dm.ctypes.data, len(dm) // 3, out.ctypes.data):
+            raise ValueError("malformed weights section")
+        return out
+
     def philox(self, ctr, key):
         c = np.ascontiguousarray(ctr, dtype=np.uint32)
         k = np.ascontiguousarray(key, dtype=np.uint32)
@@ -322,3 +367,49 @@ class Reference:
         if not intermediates:
             return out[:n].tobytes()
         return out[:n].tobytes(), inter
+
+
+class ReferenceModel:
+    """The reference's own DISTILLATION_MODE=1 model codec (oracle/_ref/libfleetref_model.so:
+    the header-only mojo network of commonLib/cppNN, compiled by oracle/Makefile)."""
+
+    def __init__(self, path: str = REF_MODEL_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        L = C.CDLL(path)
+        self.lib = L
+        sz = C.c_size_t
+        L.ref_quantize_params.restype = sz
+        L.ref_quantize_params.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, sz]
+        L.ref_mnist_roundtrip.restype = sz
+        L.ref_mnist_roundtrip.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_void_p, sz]
+
+    def quantize_params(self, w, dims):
+        """(quantised weights, getParams text) of a network whose W are the given matrices."""
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        dm = np.ascontiguousarray(dims, dtype=np.int32).reshape(-1)
+        wq = np.empty_like(w)
+        n = self.lib.ref_quantize_params(w.ctypes.data, dm.ctypes.data, len(dm) // 3, None, None, 0)
+        buf = np.empty(n, np.uint8)
+        self.lib.ref_quantize_params(w.ctypes.data, dm.ctypes.data, len(dm) // 3, wq.ctypes.data,
+                                     buf.ctypes.data, n)
+        return wq, buf.tobytes()
+
+    def mnist_roundtrip(self, w_in=None):
+        """The Driver's MNIST network: dims, initial W, quantised W, getParams text, W read back."""
+        nm = C.c_int(0)
+        dims = np.zeros(48, np.int32)
+        n_text = self.lib.ref_mnist_roundtrip(None, C.byref(nm), dims.ctypes.data, None, None, None, None, 0)
+        dims = dims[: 3 * nm.value].reshape(-1, 3)
+        n = int(sum(int(c) * int(r) * int(ch) for c, r, ch in dims))
+        win = None if w_in is None else np.ascontiguousarray(w_in, dtype=np.float32)
+        w0 = np.empty(n, np.float32)
+        wq = np.empty(n, np.float32)
+        wr = np.empty(n, np.float32)
+        if win is not None:
+            n_text = self.lib.ref_mnist_roundtrip(win.ctypes.data, C.byref(nm), None, None, None, None, None, 0)
+        buf = np.empty(n_text, np.uint8)
+        self.lib.ref_mnist_roundtrip(None if win is None else win.ctypes.data, C.byref(nm), None, w0.ctypes.data,
+                                     wq.ctypes.data, wr.ctypes.data, buf.ctypes.data, n_text)
+        return [tuple(int(v) for v in d) for d in dims], w0, wq, buf.tobytes(), wr

@@ -1,0 +1,127 @@
+/*
+ * oracle/ref_model_driver.cpp -- TEST INFRASTRUCTURE ONLY (oracle harness).
+ *
+ * Drives the reference's OWN DISTILLATION_MODE=1 model codec -- the header-only
+ * mojo network of commonLib/cppNN compiled by path from /root/reference (see
+ * oracle/Makefile) -- and exposes a flat C API for ctypes (tests, fixtures).
+ * Nothing in fleet_amd/ links or loads this.
+ *
+ *   ref_quantize_params: an empty mojo::network whose W holds the given
+ *     matrices; getParametersNative's mode-1 sequence on it
+ *     (Server/src/main/c++/cppNN_backend.cpp:244-280: save_model_weights,
+ *     quantization_weight_model, getParams, load_model_weights).
+ *   ref_mnist_roundtrip: the Driver's MNIST network (Driver/src/main/c++/
+ *     cppNN_backend.cpp:109-117) with its own weight init, optionally
+ *     overwritten; the same mode-1 getParams, then network::read of that text
+ *     into a fresh network (the client/Driver side, network.h:840-997).
+ */
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "mojo.h"
+
+namespace {
+
+size_t copy_out(const std::string& s, char* out, size_t cap) {
+  if (out && cap) std::memcpy(out, s.data(), s.size() < cap ? s.size() : cap);
+  return s.size();
+}
+
+std::string quantized_params(mojo::network& net) {
+  std::vector<mojo::matrix*> unquantized;
+  net.save_model_weights(&unquantized);
+  net.quantization_weight_model();
+  return net.getParams();
+}
+
+}  // namespace
+
+extern "C" {
+
+// dims: n_mats x {cols, rows, chans}; w: the concatenated matrices.
+// wq_out (nullable): the quantised weights; returns the getParams text length.
+size_t ref_quantize_params(const float* w, const int* dims, int n_mats, float* wq_out, char* text, size_t cap) {
+  mojo::network net("sgd");
+  size_t off = 0;
+  for (int j = 0; j < n_mats; ++j) {
+    mojo::matrix* m = new mojo::matrix(dims[3 * j], dims[3 * j + 1], dims[3 * j + 2]);
+    std::memcpy(m->x, w + off, sizeof(float) * m->size());
+    off += m->size();
+    net.W.push_back(m);
+  }
+  std::vector<mojo::matrix*> unquantized;
+  net.save_model_weights(&unquantized);
+  net.quantization_weight_model();
+  const std::string params = net.getParams();
+  if (wq_out) {
+    size_t o = 0;
+    for (auto* m : net.W) {
+      std::memcpy(wq_out + o, m->x, sizeof(float) * m->size());
+      o += m->size();
+    }
+  }
+  net.load_model_weights(unquantized);
+  return copy_out(params, text, cap);
+}
+
+// The MNIST network. n_mats/dims_out (<= 16 matrices) describe its non-null W
+// in order; w_in (nullable) overwrites the initial weights; w_init_out,
+// wq_out, w_read_out (nullable) receive the initial, quantised and read-back
+// weights. Returns the text length (call with text == NULL to size it).
+size_t ref_mnist_roundtrip(const float* w_in, int* n_mats, int* dims_out, float* w_init_out, float* wq_out,
+                           float* w_read_out, char* text, size_t cap) {
+  mojo::network cnn("sgd");
+  cnn.push_back("I1", "input 28 28 1");
+  cnn.push_back("C1", "convolution 5 8 1 elu");
+  cnn.push_back("P1", "semi_stochastic_pool 3 3");
+  cnn.push_back("C2i", "convolution 1 16 1 elu");
+  cnn.push_back("C2", "convolution 5 48 1 elu");
+  cnn.push_back("P2", "semi_stochastic_pool 2 2");
+  cnn.push_back("FC2", "softmax 10");
+  cnn.connect_all();
+  int nm = 0;
+  size_t off = 0;
+  for (auto* m : cnn.W) {
+    if (!m) continue;
+    if (dims_out) {
+      dims_out[3 * nm] = m->cols;
+      dims_out[3 * nm + 1] = m->rows;
+      dims_out[3 * nm + 2] = m->chans;
+    }
+    if (w_in) std::memcpy(m->x, w_in + off, sizeof(float) * m->size());
+    if (w_init_out) std::memcpy(w_init_out + off, m->x, sizeof(float) * m->size());
+    off += m->size();
+    ++nm;
+  }
+  if (n_mats) *n_mats = nm;
+  std::vector<mojo::matrix*> unquantized;
+  cnn.save_model_weights(&unquantized);
+  cnn.quantization_weight_model();
+  const std::string params = cnn.getParams();
+  if (wq_out) {
+    size_t o = 0;
+    for (auto* m : cnn.W)
+      if (m) {
+        std::memcpy(wq_out + o, m->x, sizeof(float) * m->size());
+        o += m->size();
+      }
+  }
+  cnn.load_model_weights(unquantized);
+  if (w_read_out) {
+    mojo::network rd("sgd");
+    std::istringstream ss(params);
+    rd.read(ss);
+    size_t o = 0;
+    for (auto* m : rd.W)
+      if (m) {
+        std::memcpy(w_read_out + o, m->x, sizeof(float) * m->size());
+        o += m->size();
+      }
+  }
+  return copy_out(params, text, cap);
+}
+
+}  // extern "C"

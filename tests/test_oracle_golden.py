@@ -105,3 +105,70 @@ def test_oracle_vs_live_reference(oracle, reference):
     d = [math.exp(-0.3 * k) for k in range(5)]
     assert oracle.update_faithful(ups, d) == reference.update(ups, d)
     assert oracle.norm(ups[0]) == reference.norm(ups[0])
+
+
+# ---- DISTILLATION_MODE=1 model codec ---------------------------------
+
+def _model_fixture(name):
+    return np.load(os.path.join(GOLDEN, f"model_{name}.npz"))
+
+
+@pytest.mark.parametrize("name", ["mnist_init", "mnist_seeded"])
+def test_oracle_model_codec_matches_reference_mnist(oracle, name):
+    """quantization_weight_model, the getParams dictionary/index section and
+    network::read, restated in C, against the reference's own mojo network
+    (Driver MNIST architecture, oracle/_ref/libfleetref_model.so)."""
+    f = _model_fixture(name)
+    dims = [tuple(int(v) for v in d) for d in f["dims"]]
+    wq = oracle.quantize(f["w"], dims)
+    assert np.array_equal(wq.view(np.uint32), f["wq"].view(np.uint32))
+    sec = oracle.weights_section(wq, dims)
+    text = f["text"].tobytes()
+    assert text.endswith(sec)
+    wr = oracle.read_weights_section(sec, dims)
+    assert np.array_equal(wr.view(np.uint32), f["w_read"].view(np.uint32))
+
+
+def test_oracle_model_codec_matches_reference_edge_cases(oracle):
+    """NaN / inf weights (index -1, singleton entries), constant matrices
+    (alpha = 0), 1x1 matrices (s = 1: binary levels), near-equal values."""
+    f = _model_fixture("generic")
+    dims = [tuple(int(v) for v in d) for d in f["dims"]]
+    for t in range(4):
+        wq = oracle.quantize(f[f"w{t}"], dims)
+        assert np.array_equal(wq.view(np.uint32), f[f"wq{t}"].view(np.uint32)), t
+        assert f[f"text{t}"].tobytes() == b"mojo01\n0\n0\n0\n" + oracle.weights_section(wq, dims), t
+
+
+def test_oracle_dictionary_tolerance_chains(oracle):
+    """float_vector_find's first-occurrence rule with the non-transitive
+    |a - b| < 1e-8 tolerance on values spaced below and above it."""
+    rng = np.random.default_rng(5)
+    base = rng.normal(0, 1e-6, 50).astype(np.float32)
+    w = np.concatenate([base + np.float32(k * 4e-9) for k in range(6)] + [base[::-1]]).astype(np.float32)
+    rng.shuffle(w)
+    d, idx = oracle.dictionary(w)
+    # pure-Python restatement of network.h:594-608 as the cross-check
+    ents = []
+    for x in w:
+        if not any(abs(np.float32(x - e)) < np.float32(1e-8) for e in ents):
+            ents.append(x)
+    exp_idx = [next(k for k, e in enumerate(ents) if abs(np.float32(x - e)) < np.float32(1e-8)) for x in w]
+    assert np.array_equal(d, np.array(ents, np.float32)) and idx.tolist() == exp_idx
+
+
+def test_live_reference_model_codec(oracle):
+    """Live check against the reference build when present (this container)."""
+    import pyoracle
+    try:
+        refm = pyoracle.ReferenceModel()
+    except FileNotFoundError:
+        pytest.skip("oracle/_ref not built (no /root/reference)")
+    rng = np.random.default_rng(9)
+    dims = [(4, 3, 5), (1, 1, 20), (9, 1, 2)]
+    n = sum(c * r * ch for c, r, ch in dims)
+    w = rng.normal(0, 0.1, n).astype(np.float32)
+    wq_ref, text = refm.quantize_params(w, dims)
+    wq = oracle.quantize(w, dims)
+    assert np.array_equal(wq.view(np.uint32), wq_ref.view(np.uint32))
+    assert text == b"mojo01\n0\n0\n0\n" + oracle.weights_section(wq, dims)
