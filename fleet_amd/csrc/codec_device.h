@@ -52,8 +52,10 @@ __device__ __forceinline__ void b64_tables_init(B64Tables* t) {
 #pragma unroll
   for (int i0 = 0; i0 < 256; i0 += NT) {
     const int i = i0 + tid;
-    t->from[i] = b64_from_value(i);
-    t->fromf[i] = b64_from_value_flag(i);
+    if (NT <= 256 || i < 256) {
+      t->from[i] = b64_from_value(i);
+      t->fromf[i] = b64_from_value_flag(i);
+    }
   }
   if (tid < 64) t->to[tid] = b64_to_value(tid);
   if (tid < 32) t->digits[tid] = dig[tid];

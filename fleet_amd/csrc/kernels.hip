@@ -365,12 +365,13 @@ __device__ __noinline__ float chain_general(const uint8_t* __restrict__ uploads,
   return A;
 }
 
-// Shared state of one tile of TG groups (E = 3*TG values) in LDS.
-template <int TG>
+// Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
+// of NW waves.
+template <int TG, int NW = 4>
 struct TileShared {
   static constexpr int E = 3 * TG;
   B64Tables tab;
-  uint32_t scratch[4][64 * 6];  // resolve_slow compaction, one list per wave
+  uint32_t scratch[NW][64 * 6];  // resolve_slow compaction, one list per wave
   int32_t last_codes[E];        // codes of the last upload (mergeFlatGradient's g)
   int32_t hmin[E], hmax[E];     // header-slot codes over all uploads (layout check)
   uint32_t hmask[TG];           // bit e = slot 3*g+e is a header slot
@@ -379,22 +380,22 @@ struct TileShared {
 
 // Tables, header slots of the tile (every thread checks one header position:
 // one independent load each, not a per-group binary search), min/max init.
-template <int TG>
-__device__ __forceinline__ void tile_init(TileShared<TG>& sh, const int32_t* __restrict__ hdr, int n_hdr,
+template <int TG, int NW>
+__device__ __forceinline__ void tile_init(TileShared<TG, NW>& sh, const int32_t* __restrict__ hdr, int n_hdr,
                                           int64_t g0, int ng) {
   constexpr int E = 3 * TG;
   const int tid = threadIdx.x;
   const int64_t v0 = 3 * g0, v1 = 3 * (g0 + ng);
   int32_t hp = -1;
   if (tid < n_hdr) hp = hdr[tid];
-  b64_tables_init(&sh.tab);
+  b64_tables_init<64 * NW>(&sh.tab);
   if (tid < TG) sh.hmask[tid] = 0u;
   if (tid < E) {
     sh.hmin[tid] = INT32_MAX;
     sh.hmax[tid] = INT32_MIN;
   }
   __syncthreads();
-  for (int i = tid; i < n_hdr; i += 256) {
+  for (int i = tid; i < n_hdr; i += 64 * NW) {
     if (i != tid) hp = hdr[i];
     if (hp >= v0 && hp < v1) atomicOr(&sh.hmask[(hp - v0) / 3], 1u << ((hp - v0) % 3));
   }
@@ -407,40 +408,55 @@ __device__ __forceinline__ void tile_init(TileShared<TG>& sh, const int32_t* __r
 // goes to pdst[cc*E + 3*gl + e]:
 //   p = Q(f32(f64(Q(int2float(code))) * d_c))   (CppNNUpdater.java:463-464)
 // Also: Base64 validity, the last upload's codes, header-slot min/max.
+// Split in two so a producer can issue the next pass's loads (tile_load)
+// before computing the current one (tile_compute).
 template <int TG, int IPT>
-__device__ __forceinline__ void tile_produce(TileShared<TG>& sh, const uint8_t* __restrict__ uploads, size_t pitch,
-                                             int M, const double* __restrict__ dampen, int64_t n_up, int64_t g0,
-                                             int ng, int c_base, int nitems, int it0, int stride,
+struct TileItems {
+  uint4 w[IPT];
+  int cc[IPT], gl[IPT], c_base;
+  bool live[IPT];
+};
+
+template <int TG, int IPT>
+__device__ __forceinline__ void tile_load(TileItems<TG, IPT>& it, const uint8_t* __restrict__ uploads, size_t pitch,
+                                          int64_t g0, int ng, int c_base, int nitems, int it0, int stride) {
+  it.c_base = c_base;
+#pragma unroll
+  for (int h = 0; h < IPT; ++h) {
+    const int item = it0 + h * stride;
+    it.live[h] = item < nitems && (item % TG) < ng;
+    it.cc[h] = it.live[h] ? item / TG : 0;
+    it.gl[h] = it.live[h] ? item % TG : 0;
+    it.w[h] = *reinterpret_cast<const uint4*>(uploads + (size_t)(c_base + it.cc[h]) * pitch + 16 * (g0 + it.gl[h]));
+  }
+}
+
+template <int TG, int IPT, int NW>
+__device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileItems<TG, IPT>& it, int M,
+                                             const double* __restrict__ dampen, int64_t n_up, int64_t g0,
                                              float* __restrict__ pdst, uint32_t& badacc) {
   constexpr int E = 3 * TG, S = 3 * IPT;
   const int lane = threadIdx.x & 63;
   uint32_t* ws = sh.scratch[threadIdx.x >> 6];
   int32_t codes[S];
-  int cc[IPT], gl[IPT];
-  bool live[IPT];
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
-    const int item = it0 + h * stride;
-    live[h] = item < nitems && (item % TG) < ng;
-    cc[h] = live[h] ? item / TG : 0;
-    gl[h] = live[h] ? item % TG : 0;
-    const uint4 w = *reinterpret_cast<const uint4*>(uploads + (size_t)(c_base + cc[h]) * pitch + 16 * (g0 + gl[h]));
-    const int r = (int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * (g0 + gl[h])));
+    const int r = (int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * (g0 + it.gl[h])));
     uint32_t b;
     if (r == 3)
-      b = b64_decode_group_full(w, &sh.tab, codes + 3 * h);
+      b = b64_decode_group_full(it.w[h], &sh.tab, codes + 3 * h);
     else
-      b = b64_decode_group(w, &sh.tab, codes + 3 * h) & needed_chars_mask(r);
-    if (live[h]) {
+      b = b64_decode_group(it.w[h], &sh.tab, codes + 3 * h) & needed_chars_mask(r);
+    if (it.live[h]) {
       badacc |= b;
-      if (c_base + cc[h] == M - 1)
-        for (int e = 0; e < 3; ++e) sh.last_codes[3 * gl[h] + e] = codes[3 * h + e];
-      const uint32_t hm = sh.hmask[gl[h]];
+      if (it.c_base + it.cc[h] == M - 1)
+        for (int e = 0; e < 3; ++e) sh.last_codes[3 * it.gl[h] + e] = codes[3 * h + e];
+      const uint32_t hm = sh.hmask[it.gl[h]];
       if (hm) {
         for (int e = 0; e < 3; ++e)
           if ((hm >> e) & 1u) {
-            atomicMin(&sh.hmin[3 * gl[h] + e], codes[3 * h + e]);
-            atomicMax(&sh.hmax[3 * gl[h] + e], codes[3 * h + e]);
+            atomicMin(&sh.hmin[3 * it.gl[h] + e], codes[3 * h + e]);
+            atomicMax(&sh.hmax[3 * it.gl[h] + e], codes[3 * h + e]);
           }
       }
     }
@@ -474,24 +490,34 @@ __device__ __forceinline__ void tile_produce(TileShared<TG>& sh, const uint8_t* 
   float r[S], p[S];
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
-    const double d = dampen[c_base + cc[h]];
+    const double d = dampen[it.c_base + it.cc[h]];
 #pragma unroll
     for (int e = 0; e < 3; ++e) r[3 * h + e] = (float)((double)y[3 * h + e] * d);
   }
   q_stage<S>(p, r, sh.tab.digits, ws, lane);
 #pragma unroll
   for (int h = 0; h < IPT; ++h)
-    if (live[h])
+    if (it.live[h])
 #pragma unroll
-      for (int e = 0; e < 3; ++e) pdst[cc[h] * E + 3 * gl[h] + e] = p[3 * h + e];
+      for (int e = 0; e < 3; ++e) pdst[it.cc[h] * E + 3 * it.gl[h] + e] = p[3 * h + e];
+}
+
+template <int TG, int IPT, int NW>
+__device__ __forceinline__ void tile_produce(TileShared<TG, NW>& sh, const uint8_t* __restrict__ uploads, size_t pitch,
+                                             int M, const double* __restrict__ dampen, int64_t n_up, int64_t g0,
+                                             int ng, int c_base, int nitems, int it0, int stride,
+                                             float* __restrict__ pdst, uint32_t& badacc) {
+  TileItems<TG, IPT> it;
+  tile_load<TG, IPT>(it, uploads, pitch, g0, ng, c_base, nitems, it0, stride);
+  tile_compute<TG, IPT, NW>(sh, it, M, dampen, n_up, g0, pdst, badacc);
 }
 
 // Final values of the tile (vals[0..E)) -> merged Base64 (+ fp32), layout
 // check. One thread per value computes its merged code (the longest part),
 // then one thread per group assembles the 16 Base64 chars. Call from every
 // thread of the block (contains a barrier).
-template <int TG>
-__device__ __forceinline__ void tile_epilogue(TileShared<TG>& sh, const float* __restrict__ vals, double inv_avg,
+template <int TG, int NW>
+__device__ __forceinline__ void tile_epilogue(TileShared<TG, NW>& sh, const float* __restrict__ vals, double inv_avg,
                                               int64_t n_up, int64_t walk_end, int64_t g0, int ng,
                                               uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
                                               int* __restrict__ err) {
@@ -546,7 +572,7 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
   const int tid = threadIdx.x;
   const int64_t g0 = g_begin + (int64_t)blockIdx.x * TG;
   const int ng = (int)min<int64_t>(TG, g_end - g0);
-  tile_init<TG>(sh, hdr_block + 4, hdr_block[1], g0, ng);
+  tile_init(sh, hdr_block + 4, hdr_block[1], g0, ng);
   FLEET_TSTAMP(1);
 
   float A = 0.f;  // phase-2 value: element tid of the tile (tid < E)
@@ -585,21 +611,26 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
   }
   if (tid < E) ptile[tid] = A;
   __syncthreads();
-  tile_epilogue<TG>(sh, ptile, inv_avg, n_up, hdr_block[2], g0, ng, merged, merged_f32, err);
+  tile_epilogue(sh, ptile, inv_avg, n_up, hdr_block[2], g0, ng, merged, merged_f32, err);
   FLEET_TSTAMP(5);
 }
 
-// Pipelined tile variant (E = 3*TG <= 64): waves 1-3 produce p for passes of
-// CPP clients into an LDS ring of RING passes while wave 0 consumes them in
-// client order (the serial A = Q(A + p_c)), so the client-independent work
-// and the serial accumulation overlap instead of running back to back.
-// Hand-off through LDS: a producer wave publishes "passes done" with a
-// workgroup release after its p writes; the consumer acquires the minimum
-// over the three producer waves before reading a pass, and publishes "passes
-// consumed" so producers never overwrite a ring slot still being read. Every
-// wait has a partner that always makes progress, so the grid drains.
-template <int TG, int IPT>
-__global__ void __launch_bounds__(256) k_update_pipe(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+// Pipelined tile variant (E = 3*TG <= 64): producer waves compute p for passes
+// of clients into an LDS ring while wave 0 consumes them in client order (the
+// serial A = Q(A + p_c)), so the client-independent work and the serial
+// accumulation overlap instead of running back to back.
+//   WP = 0: a pass is shared by all producer waves (IPT items per thread);
+//   WP = 1: a pass belongs to ONE producer wave (passes dealt round-robin), so
+//           a pass is ready after one wave's work -- the consumer starts
+//           early -- while the NW-1 producer waves work on successive passes
+//           in parallel.
+// Hand-off through LDS: a producer wave publishes its count of finished passes
+// with a workgroup release after its p writes; the consumer acquires it before
+// reading a pass, and publishes "passes consumed" so producers never overwrite
+// a ring slot still being read. Every wait has a partner that always makes
+// progress, so the grid drains.
+template <int TG, int IPT, int NW, int WP = 0>
+__global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                      const double* __restrict__ dampen, double inv_avg,
                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
                                                      const int32_t* __restrict__ hdr_block,
@@ -607,39 +638,47 @@ __global__ void __launch_bounds__(256) k_update_pipe(const uint8_t* __restrict__
                                                      int* __restrict__ err) {
   constexpr int E = 3 * TG;
   static_assert(E <= 64, "one consumer wave");
-  constexpr int NPW = 3;                       // producer waves
-  constexpr int CPP = (NPW * 64 * IPT) / TG;   // clients per pass: IPT items per producer thread
+  constexpr int NPW = NW - 1;                                // producer waves
+  constexpr int CPP = ((WP ? 1 : NPW) * 64 * IPT) / TG;      // clients per pass
   constexpr int RING = (6144 / E) / CPP > 0 ? (6144 / E) / CPP : 1;  // passes in LDS (~24 KiB)
   FLEET_TSTAMP(0);
-  __shared__ TileShared<TG> sh;
+  __shared__ TileShared<TG, NW> sh;
   __shared__ float ptile[RING * CPP * E];
   __shared__ float finals[E];
-  __shared__ int prog[NPW];  // passes completed by each producer wave
-  __shared__ int consumed;   // passes completed by the consumer
+  __shared__ int prog[NPW];  // passes finished by each producer wave
+  __shared__ int consumed;   // passes finished by the consumer
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int64_t g0 = g_begin + (int64_t)blockIdx.x * TG;
   const int ng = (int)min<int64_t>(TG, g_end - g0);
   if (tid < NPW) prog[tid] = 0;
   if (tid == 0) consumed = 0;
-  tile_init<TG>(sh, hdr_block + 4, hdr_block[1], g0, ng);
+  tile_init(sh, hdr_block + 4, hdr_block[1], g0, ng);
   FLEET_TSTAMP(1);
   const int npass = (M + CPP - 1) / CPP;
   uint32_t badacc = 0;
 
   if (wave > 0) {  // ---------------------------------------------- producers
-    const int pt = tid - 64;
-    for (int pass = 0; pass < npass; ++pass) {
+    const int w = wave - 1;
+    const int step = WP ? NPW : 1;
+    const int it0 = WP ? lane : tid - 64, stride = WP ? 64 : NPW * 64;
+    int done = 0;
+    int pass = WP ? w : 0;
+    TileItems<TG, IPT> nxt;  // the next pass's groups, loaded one pass ahead
+    if (pass < npass) tile_load<TG, IPT>(nxt, uploads, pitch, g0, ng, pass * CPP, min(CPP, M - pass * CPP) * TG, it0,
+                                         stride);
+    for (; pass < npass; pass += step) {
+      const TileItems<TG, IPT> cur = nxt;
+      const int np = pass + step;
+      if (np < npass) tile_load<TG, IPT>(nxt, uploads, pitch, g0, ng, np * CPP, min(CPP, M - np * CPP) * TG, it0,
+                                         stride);
       if (pass >= RING) {  // ring slot free once the consumer finished pass - RING
         while (__hip_atomic_load(&consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < pass - RING + 1)
           __builtin_amdgcn_s_sleep(1);
       }
-      const int c_base = pass * CPP;
-      const int cm = min(CPP, M - c_base);
-      tile_produce<TG, IPT>(sh, uploads, pitch, M, dampen, n_up, g0, ng, c_base, cm * TG, pt, NPW * 64,
-                            ptile + (pass % RING) * CPP * E, badacc);
+      tile_compute<TG, IPT, NW>(sh, cur, M, dampen, n_up, g0, ptile + (pass % RING) * CPP * E, badacc);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      if (lane == 0) __hip_atomic_store(&prog[wave - 1], pass + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (pass == 0) FLEET_TSTAMP(2);
+      ++done;
+      if (lane == 0) __hip_atomic_store(&prog[w], done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   } else {  // ---------------------------------------------------- consumer
     float A = 0.f;
@@ -647,11 +686,18 @@ __global__ void __launch_bounds__(256) k_update_pipe(const uint8_t* __restrict__
     const int col = tid < E ? tid : 0;
     for (int pass = 0; pass < npass; ++pass) {
       for (;;) {
-        int m = __hip_atomic_load(&prog[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        bool ready;
+        if (WP) {
+          ready = __hip_atomic_load(&prog[pass % NPW], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >
+                  pass / NPW;
+        } else {
+          int m = __hip_atomic_load(&prog[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 #pragma unroll
-        for (int w = 1; w < NPW; ++w)
-          m = min(m, __hip_atomic_load(&prog[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-        if (m > pass) break;
+          for (int v = 1; v < NPW; ++v)
+            m = min(m, __hip_atomic_load(&prog[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          ready = m > pass;
+        }
+        if (ready) break;
         __builtin_amdgcn_s_sleep(1);
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -684,7 +730,7 @@ __global__ void __launch_bounds__(256) k_update_pipe(const uint8_t* __restrict__
   FLEET_TSTAMP(4);
   if (badacc) atomicOr(err, FLEET_ERRBIT_BASE64);
   __syncthreads();
-  tile_epilogue<TG>(sh, finals, inv_avg, n_up, hdr_block[2], g0, ng, merged, merged_f32, err);
+  tile_epilogue(sh, finals, inv_avg, n_up, hdr_block[2], g0, ng, merged, merged_f32, err);
   FLEET_TSTAMP(5);
 }
 
@@ -949,12 +995,16 @@ static bool use_tiled(int64_t groups) {
 // overrides for experiments: FLEET_UPDATE_MODE=stream|tiled, FLEET_TILE_G,
 // FLEET_UPDATE_PIPE=0, FLEET_UPDATE_K).
 struct UpdatePlan {
-  int kind;  // 0 stream k_update<k>, 1 k_update_tiled<tg>, 2 k_update_pipe<tg, ipt>
-  int tg, k, ipt;
+  int kind;  // 0 stream k_update<k>, 1 k_update_tiled<tg>, 2 k_update_pipe<tg, ipt, nw, wp>
+  int tg, k, ipt, nw, wp;
 };
 static UpdatePlan plan_update(int64_t groups) {
-  UpdatePlan p{0, 0, 1, 1};
+  // measured best on MNIST-64 (scripts/ubench_tiled.hip): 4 waves, block-wide passes, 1 item per thread
+  UpdatePlan p{0, 0, 1, 1, 4, 0};
+  if (const char* e = getenv("FLEET_PIPE_WAVEPASS")) p.wp = atoi(e) != 0;
   if (const char* e = getenv("FLEET_PIPE_IPT")) p.ipt = atoi(e) == 2 ? 2 : 1;
+  if (const char* e = getenv("FLEET_PIPE_WAVES")) p.nw = atoi(e) == 8 ? 8 : 4;
+  if (p.ipt == 2) p.nw = 4, p.wp = 0;
   if (use_tiled(groups)) {
     // widest tile that still gives >= 4 blocks per CU; the narrow tiles are
     // pipelined (producer waves + one consumer wave)
@@ -976,7 +1026,7 @@ const char* update_kernel_name(int64_t groups) {
   if (p.kind == 0)
     snprintf(buf, sizeof buf, "k_update<%d>", p.k);
   else if (p.kind == 2)
-    snprintf(buf, sizeof buf, "k_update_pipe<%d, %d>", p.tg, p.ipt);
+    snprintf(buf, sizeof buf, "k_update_pipe<%d, %d, %d, %d>", p.tg, p.ipt, p.nw, p.wp);
   else
     snprintf(buf, sizeof buf, "k_update_tiled<%d>", p.tg);
   return buf;
@@ -992,13 +1042,29 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
   hipLaunchKernelGGL(KERNEL, dim3((unsigned)((groups + (PER_BLOCK)-1) / (PER_BLOCK))), dim3(256), 0, s, uploads, \
                      pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
   if (p.kind == 2) {
-    if (p.ipt == 2) {
-      if (p.tg == 8) FLEET_LAUNCH((k_update_pipe<8, 2>), 8);
-      else FLEET_LAUNCH((k_update_pipe<16, 2>), 16);
+#define FLEET_LAUNCH_PIPE(TG, IPT, NW, WP)                                                                       \
+  hipLaunchKernelGGL((k_update_pipe<TG, IPT, NW, WP>), dim3((unsigned)((groups + TG - 1) / TG)), dim3(64 * NW), 0, \
+                     s, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged,           \
+                     merged_f32, d_err)
+    if (p.wp) {
+      if (p.nw == 8) {
+        if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 8, 1);
+        else FLEET_LAUNCH_PIPE(16, 1, 8, 1);
+      } else {
+        if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 4, 1);
+        else FLEET_LAUNCH_PIPE(16, 1, 4, 1);
+      }
+    } else if (p.nw == 8) {
+      if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 8, 0);
+      else FLEET_LAUNCH_PIPE(16, 1, 8, 0);
+    } else if (p.ipt == 2) {
+      if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 2, 4, 0);
+      else FLEET_LAUNCH_PIPE(16, 2, 4, 0);
     } else {
-      if (p.tg == 8) FLEET_LAUNCH((k_update_pipe<8, 1>), 8);
-      else FLEET_LAUNCH((k_update_pipe<16, 1>), 16);
+      if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 4, 0);
+      else FLEET_LAUNCH_PIPE(16, 1, 4, 0);
     }
+#undef FLEET_LAUNCH_PIPE
   } else if (p.kind == 1) {
     if (p.tg == 8) FLEET_LAUNCH(k_update_tiled<8>, 8);
     else if (p.tg == 16) FLEET_LAUNCH(k_update_tiled<16>, 16);

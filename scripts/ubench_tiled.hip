@@ -9,11 +9,11 @@
 
 using namespace fleet;
 
-template <int TG, bool PIPE, int IPT = 1>
+template <int TG, bool PIPE, int IPT = 1, int NW = 4, int WP = 0>
 static void launch(unsigned blocks, const uint8_t* text, size_t pitch, int M, const double* damp, int64_t n_up,
                    int64_t groups, const int32_t* hdr, uint8_t* merged, float* mf, int* err) {
   if constexpr (PIPE)
-    hipLaunchKernelGGL((k_update_pipe<TG, IPT>), dim3(blocks), dim3(256), 0, 0, text, pitch, M, damp, 1.0 / M, n_up,
+    hipLaunchKernelGGL((k_update_pipe<TG, IPT, NW, WP>), dim3(blocks), dim3(64 * NW), 0, 0, text, pitch, M, damp, 1.0 / M, n_up,
                        (int64_t)0, groups, hdr, merged, mf, err);
   else
     hipLaunchKernelGGL(k_update_tiled<TG>, dim3(blocks), dim3(256), 0, 0, text, pitch, M, damp, 1.0 / M, n_up,
@@ -45,7 +45,7 @@ static int64_t layout(std::vector<int> w, std::vector<int> b) {
   return p;
 }
 
-template <int TG, bool PIPE = false, int IPT = 1>
+template <int TG, bool PIPE = false, int IPT = 1, int NW = 4, int WP = 0>
 void run(int64_t n_up, int M, int reps = 1) {
   const int64_t groups = (n_up + 2) / 3;
   const size_t pitch = 16 * groups, vpitch = 3 * groups;
@@ -84,13 +84,13 @@ void run(int64_t n_up, int M, int reps = 1) {
   launch_encode_f32(vals, n_up, vpitch, M, text, pitch, 0);
   const unsigned blocks = (unsigned)((groups + TG - 1) / TG);
   for (int rep = 0; rep < 3; ++rep)
-    launch<TG, PIPE, IPT>(blocks, text, pitch, M, damp, n_up, groups, hdr, merged, mf, err);
+    launch<TG, PIPE, IPT, NW, WP>(blocks, text, pitch, M, damp, n_up, groups, hdr, merged, mf, err);
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
   hipEventRecord(a);
   for (int r = 0; r < reps; ++r)
-    launch<TG, PIPE, IPT>(blocks, text, pitch, M, damp, n_up, groups, hdr, merged, mf, err);
+    launch<TG, PIPE, IPT, NW, WP>(blocks, text, pitch, M, damp, n_up, groups, hdr, merged, mf, err);
   hipEventRecord(b);
   hipEventSynchronize(b);
   float ms;
@@ -114,9 +114,9 @@ void run(int64_t n_up, int M, int reps = 1) {
       segmax[k] = std::max(segmax[k], v);
     }
   }
-  printf("%s%d TG=%d n=%ld M=%d blocks=%u: event %.1f us, span %.1f us | init %.2f/%.2f | pass0 %.2f/%.2f | "
+  printf("%s%d/%dw/wp%d TG=%d n=%ld M=%d blocks=%u: event %.1f us, span %.1f us | init %.2f/%.2f | pass0 %.2f/%.2f | "
          "rest of phase1 %.2f/%.2f | phase2 %.2f/%.2f (%.0f ns/client) | epilogue %.2f/%.2f  (avg/max us)\n",
-         PIPE ? "pipe" : "tiled", PIPE ? IPT : 2, TG, (long)n_up, M, blocks, ms * 1e3, (t5 - t0) * 0.01, seg[0] / blocks, segmax[0], seg[1] / blocks,
+         PIPE ? "pipe" : "tiled", PIPE ? IPT : 2, NW, WP, TG, (long)n_up, M, blocks, ms * 1e3, (t5 - t0) * 0.01, seg[0] / blocks, segmax[0], seg[1] / blocks,
          segmax[1], seg[2] / blocks, segmax[2], seg[3] / blocks, segmax[3], seg[3] / blocks * 1e3 / M,
          seg[4] / blocks, segmax[4]);
   hipFree(vals);
@@ -153,22 +153,13 @@ static void time_encode(int64_t n_up, int M, int reps) {
 }
 
 int main() {
-  time_encode(22961, 64, 50);
-  time_encode(22961, 1, 50);
-  for (int M : {16, 64}) {
-    run<16, true, 1>(22961, M, 20);
-    run<16, true, 2>(22961, M, 20);
-  }
-  run<16>(22961, 64, 20);
   const int64_t n = layout({200, 0, 128, 19200, 0, 1920}, {784, 0, 512, 0, 0, 192, 10});
   printf("MNIST layout n_up=%ld headers=%zu\n", (long)n, g_hpos.size());
-  run<16>(n, 64, 20);
-  run<16, true, 1>(n, 64, 20);
-  run<16, true, 2>(n, 64, 20);
-  run<8, true, 1>(n, 64, 20);
-  run<16, true, 1>(n, 256, 10);
-  g_hpos.clear();
-  g_hval.clear();
-  run<64>(313867, 256, 3);
+  for (int M : {16, 64, 256}) {
+    run<16, true, 1, 4, 0>(n, M, 20);
+    run<16, true, 1, 4, 1>(n, M, 20);
+    run<16, true, 1, 8, 1>(n, M, 20);
+    run<8, true, 1, 8, 1>(n, M, 20);
+  }
   return 0;
 }

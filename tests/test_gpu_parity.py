@@ -208,6 +208,8 @@ def test_update_groups_per_lane_variants(codec, oracle, monkeypatch, K):
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "8", "FLEET_UPDATE_PIPE": "0"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_UPDATE_PIPE": "0"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_PIPE_IPT": "2"},
+                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_PIPE_WAVES": "8"},
+                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_PIPE_WAVEPASS": "1"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "32"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "64"},
                                  {"FLEET_UPDATE_MODE": "stream", "FLEET_UPDATE_K": "1"},
@@ -235,7 +237,8 @@ def test_update_large_magnitudes_slow_path(codec, oracle, monkeypatch, env):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm) == oracle.update_faithful(ups, d)
 
 
-@pytest.mark.parametrize("mode", ["tiled", "tiled-nopipe", "tiled-wide", "tiled-ipt2", "stream"])
+@pytest.mark.parametrize("mode", ["tiled", "tiled-nopipe", "tiled-wide", "tiled-ipt2", "tiled-8waves",
+                                  "tiled-wavepass", "stream"])
 def test_update_modes(codec, oracle, monkeypatch, mode):
     """Every aggregation kernel (pipelined and two-phase tiles for small
     buckets, streaming for large ones) on ragged tiles, client counts that wrap
@@ -247,6 +250,10 @@ def test_update_modes(codec, oracle, monkeypatch, mode):
         monkeypatch.setenv("FLEET_TILE_G", "64")
     if mode == "tiled-ipt2":
         monkeypatch.setenv("FLEET_PIPE_IPT", "2")
+    if mode == "tiled-8waves":
+        monkeypatch.setenv("FLEET_PIPE_WAVES", "8")
+    if mode == "tiled-wavepass":
+        monkeypatch.setenv("FLEET_PIPE_WAVEPASS", "1")
     for lay, M in ((MNIST, 70), (synthetic(1000), 1), (synthetic(3001), 129), (synthetic(5002), 2),
                    (synthetic(700), 300), (CIFAR10, 3)):
         ups = uploads_for(oracle, lay, M, seed=M)
