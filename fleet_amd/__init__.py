@@ -97,6 +97,9 @@ def lib() -> C.CDLL:
         "fleet_update": (i32, [vp, vp, vp, i32, vp, vp, sz, szp, vp]),
         "fleet_update_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, sz, sz, vp, vp, vp]),
         "fleet_update_kernel": (C.c_char_p, [sz]),
+        "fleet_model_quantize_index": (i32, [vp, vp, vp, i32, vp, vp, vp, vp]),
+        "fleet_model_weights_text": (i32, [vp, vp, vp, i32, vp, sz, szp]),
+        "fleet_model_read_weights": (i32, [vp, vp, sz, vp, i32, vp]),
         "fleet_encode_device": (i32, [vp, vp, sz, sz, i32, vp, sz, vp]),
         "fleet_decode_device": (i32, [vp, vp, sz, sz, i32, vp, sz, vp]),
         "fleet_synth_device": (i32, [vp, C.c_uint64, i32, i32, vp, vp, i32, sz, vp, sz, vp]),
@@ -374,6 +377,54 @@ class Codec:
 
     def sync(self, stream=None):
         self._check(self._L.fleet_sync(self._h, _stream(stream)))
+
+    # -- DISTILLATION_MODE=1 model codec ----------------
+    @staticmethod
+    def _model_args(weights, dims):
+        w = np.ascontiguousarray(weights, dtype=np.float32).reshape(-1)
+        d = np.ascontiguousarray(dims, dtype=np.int32).reshape(-1)
+        if len(d) % 3:
+            raise ValueError("dims: (cols, rows, chans) per matrix")
+        n = int(sum(int(d[k]) * int(d[k + 1]) * int(d[k + 2]) for k in range(0, len(d), 3)))
+        if len(w) != n:
+            raise ValueError(f"{len(w)} weights for a model of {n}")
+        return w, d, n
+
+    def model_quantize_index(self, weights, dims):
+        """quantization_weight_model + getParams' dictionary and selected-index set
+        (network.h:594-692, 1683-1774): (quantised weights, dictionary, indices)."""
+        w, d, n = self._model_args(weights, dims)
+        wq = np.empty(n, np.float32)
+        dic = np.empty(max(1, n), np.float32)
+        idx = np.empty(n, np.int32)
+        U = C.c_int(0)
+        self._check(self._L.fleet_model_quantize_index(self._h, w.ctypes.data, d.ctypes.data, len(d) // 3,
+                                                       wq.ctypes.data, dic.ctypes.data, C.byref(U), idx.ctypes.data))
+        return wq, dic[: U.value].copy(), idx
+
+    def model_weights_text(self, weights, dims) -> bytes:
+        """getParams' DISTILLATION_MODE=1 weights section for these (unquantised) weights."""
+        w, d, n = self._model_args(weights, dims)
+        need = C.c_size_t(0)
+        rc = self._L.fleet_model_weights_text(self._h, w.ctypes.data, d.ctypes.data, len(d) // 3, None, 0,
+                                              C.byref(need))
+        if rc not in (0, FLEET_ERR_CAPACITY):
+            self._check(rc)
+        buf = np.empty(max(1, need.value), np.uint8)
+        self._check(self._L.fleet_model_weights_text(self._h, w.ctypes.data, d.ctypes.data, len(d) // 3,
+                                                     buf.ctypes.data, need.value, C.byref(need)))
+        return buf[: need.value].tobytes()
+
+    def model_read_weights(self, text, dims) -> np.ndarray:
+        """network::read's DISTILLATION_MODE=1 branch: weights section -> weights."""
+        t = _as_bytes(text)
+        d = np.ascontiguousarray(dims, dtype=np.int32).reshape(-1)
+        n = int(sum(int(d[k]) * int(d[k + 1]) * int(d[k + 2]) for k in range(0, len(d), 3)))
+        out = np.empty(n, np.float32)
+        self._check(self._L.fleet_model_read_weights(self._h, t, len(t), d.ctypes.data, len(d) // 3,
+                                                     out.ctypes.data))
+        return out
+
 
 
 class ByteVec:

@@ -16,6 +16,7 @@
 
 #include "../../include/fleet_codec.h"
 #include "kernels.h"
+#include "model_codec.h"
 
 #define FLEET_VERSION "fleet-mi355x 0.1.0 (gfx950)"
 
@@ -547,6 +548,163 @@ int fleet_synth_device(fleet_ctx* c, uint64_t seed, int M, int client0, const in
   HIP_TRY(c, hipStreamSynchronize(s));
   if (d_pos) (void)hipFree(d_pos);
   if (d_val) (void)hipFree(d_val);
+  return FLEET_OK;
+}
+
+// ------------------------------------------------- mode-1 model codec
+
+namespace {
+
+int model_total(fleet_ctx* c, const int32_t* dims, int n_mats, size_t* n) {
+  if (n_mats < 0 || (n_mats && !dims)) return fail(c, FLEET_ERR_ARG, "bad dims");
+  size_t t = 0;
+  for (int j = 0; j < n_mats; ++j) {
+    if (dims[3 * j] < 0 || dims[3 * j + 1] < 0 || dims[3 * j + 2] < 0) return fail(c, FLEET_ERR_ARG, "negative dim");
+    t += (size_t)dims[3 * j] * dims[3 * j + 1] * dims[3 * j + 2];
+  }
+  if (t > (size_t)INT32_MAX) return fail(c, FLEET_ERR_ARG, "model too large for int32 indices");
+  *n = t;
+  return FLEET_OK;
+}
+
+struct DevMem {
+  void* p = nullptr;
+  ~DevMem() {
+    if (p) (void)hipFree(p);
+  }
+};
+
+// quantize + dictionary on the device; leaves d_index and the dictionary on the host
+int model_run(fleet_ctx* c, const float* weights, const int32_t* dims, int n_mats, size_t n, float* quantized,
+              std::vector<float>* dict_host, int32_t* U, DevMem* d_index_keep) {
+  DevMem dw, dq, dd;
+  if (n) {
+    HIP_TRY(c, hipMalloc(&dw.p, n * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&dq.p, n * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&dd.p, n * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&d_index_keep->p, n * sizeof(int32_t)));
+    HIP_TRY(c, hipMemcpyAsync(dw.p, weights, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  }
+  HIP_TRY(c, fleet::model_quantize_index((const float*)dw.p, dims, n_mats, (float*)dq.p, (float*)dd.p,
+                                         (int32_t*)d_index_keep->p, U, c->stream));
+  if (quantized && n) HIP_TRY(c, hipMemcpyAsync(quantized, dq.p, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  dict_host->resize((size_t)*U);
+  if (*U) HIP_TRY(c, hipMemcpyAsync(dict_host->data(), dd.p, (size_t)*U * sizeof(float), hipMemcpyDeviceToHost,
+                                    c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return FLEET_OK;
+}
+
+}  // namespace
+
+int fleet_model_quantize_index(fleet_ctx* c, const float* weights, const int32_t* dims, int n_mats,
+                               float* quantized, float* dict, int* n_dict, int32_t* index) {
+  if (!c) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  size_t n = 0;
+  int rc = model_total(c, dims, n_mats, &n);
+  if (rc) return rc;
+  if (n && !weights) return FLEET_ERR_ARG;
+  std::vector<float> dh;
+  int32_t U = 0;
+  DevMem di;
+  if ((rc = model_run(c, weights, dims, n_mats, n, quantized, &dh, &U, &di))) return rc;
+  if (dict && U) std::memcpy(dict, dh.data(), sizeof(float) * (size_t)U);
+  if (n_dict) *n_dict = U;
+  if (index && n) {
+    HIP_TRY(c, hipMemcpy(index, di.p, n * sizeof(int32_t), hipMemcpyDeviceToHost));
+  }
+  return FLEET_OK;
+}
+
+int fleet_model_weights_text(fleet_ctx* c, const float* weights, const int32_t* dims, int n_mats, char* out,
+                             size_t cap, size_t* out_len) {
+  if (!c) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  size_t n = 0;
+  int rc = model_total(c, dims, n_mats, &n);
+  if (rc) return rc;
+  if (n && !weights) return FLEET_ERR_ARG;
+  std::vector<float> dh;
+  int32_t U = 0;
+  DevMem di;
+  if ((rc = model_run(c, weights, dims, n_mats, n, nullptr, &dh, &U, &di))) return rc;
+  // header and dictionary lines: `ostream << int` / `ostream << float` (precision 6 == %g),
+  // U lines of host formatting; the n index tokens are formatted on the device
+  std::string head;
+  char buf[64];
+  snprintf(buf, sizeof buf, "%zu\n%d\n", n, U);
+  head += buf;
+  for (int32_t k = 0; k < U; ++k) {
+    snprintf(buf, sizeof buf, "%d\n%g\n", k, (double)dh[(size_t)k]);
+    head += buf;
+  }
+  std::vector<char> body;
+  HIP_TRY(c, fleet::model_index_text((const int32_t*)di.p, dims, n_mats, &body, c->stream));
+  const size_t total = head.size() + body.size();
+  if (out_len) *out_len = total;
+  if (cap < total) return fail(c, FLEET_ERR_CAPACITY, "output capacity %zu < %zu", cap, total);
+  std::memcpy(out, head.data(), head.size());
+  if (!body.empty()) std::memcpy(out + head.size(), body.data(), body.size());
+  return FLEET_OK;
+}
+
+int fleet_model_read_weights(fleet_ctx* c, const char* text, size_t len, const int32_t* dims, int n_mats,
+                             float* weights_out) {
+  if (!c || (!text && len)) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  size_t n = 0;
+  int rc = model_total(c, dims, n_mats, &n);
+  if (rc) return rc;
+  if (n && !weights_out) return FLEET_ERR_ARG;
+  // header: loop_counter and U lines (getcleanline + atoi), then U pairs read
+  // with `>>` (int, float = strtof); the std::map keeps the first value of a key
+  std::string t(text, len);
+  const char* p = t.c_str();
+  char* e = nullptr;
+  (void)strtol(p, &e, 10);
+  if (e == p) return fail(c, FLEET_ERR_ARG, "weights section: no loop counter");
+  p = e;
+  const long U = strtol(p, &e, 10);
+  if (e == p || U < 0) return fail(c, FLEET_ERR_ARG, "weights section: no dictionary size");
+  p = e;
+  std::vector<std::pair<int32_t, float>> kv;
+  kv.reserve((size_t)U);
+  for (long k = 0; k < U; ++k) {
+    const long key = strtol(p, &e, 10);
+    if (e == p) return fail(c, FLEET_ERR_ARG, "weights section: bad dictionary index %ld", k);
+    p = e;
+    const float v = strtof(p, &e);
+    if (e == p) return fail(c, FLEET_ERR_ARG, "weights section: bad dictionary value %ld", k);
+    p = e;
+    kv.emplace_back((int32_t)key, v);
+  }
+  std::stable_sort(kv.begin(), kv.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<int32_t> keys;
+  std::vector<float> vals;
+  for (size_t k = 0; k < kv.size(); ++k)
+    if (k == 0 || kv[k].first != kv[k - 1].first) keys.push_back(kv[k].first), vals.push_back(kv[k].second);
+  const size_t body = (size_t)(p - t.c_str());
+  const size_t blen = len - body;
+  DevMem dt, dk, dv, dw;
+  if (blen) HIP_TRY(c, hipMalloc(&dt.p, blen));
+  HIP_TRY(c, hipMalloc(&dk.p, sizeof(int32_t) * (keys.size() + 1)));
+  HIP_TRY(c, hipMalloc(&dv.p, sizeof(float) * (vals.size() + 1)));
+  if (n) HIP_TRY(c, hipMalloc(&dw.p, sizeof(float) * n));
+  if (blen) HIP_TRY(c, hipMemcpyAsync(dt.p, text + body, blen, hipMemcpyHostToDevice, c->stream));
+  if (!keys.empty()) {
+    HIP_TRY(c, hipMemcpyAsync(dk.p, keys.data(), sizeof(int32_t) * keys.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(dv.p, vals.data(), sizeof(float) * vals.size(), hipMemcpyHostToDevice, c->stream));
+  }
+  int status = 0;
+  HIP_TRY(c, fleet::model_read_index((const uint8_t*)dt.p, (int64_t)blen, (int64_t)n, (const int32_t*)dk.p,
+                                     (const float*)dv.p, (int32_t)keys.size(), (float*)dw.p, &status, c->stream));
+  if (status == 1) return fail(c, FLEET_ERR_ARG, "weights section: malformed index token");
+  if (status == 2) return fail(c, FLEET_ERR_LAYOUT, "weights section: index count differs from the model size");
+  if (n) HIP_TRY(c, hipMemcpy(weights_out, dw.p, sizeof(float) * n, hipMemcpyDeviceToHost));
   return FLEET_OK;
 }
 

@@ -1,0 +1,23 @@
+// fleet_amd/csrc/model_codec.h -- internal launchers of the DISTILLATION_MODE=1
+// model codec (model_codec.hip <-> fleet_codec.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+namespace fleet {
+// quantization_weight_model + dictionary + selected-index set on the device.
+// d_w: n weights (n = sum of cols*rows*chans over h_dims); outputs d_wq[n],
+// d_dict[n] (first *h_U entries used), d_index[n] (nullable). Synchronous.
+hipError_t model_quantize_index(const float* d_w, const int32_t* h_dims, int n_mats, float* d_wq, float* d_dict,
+                                int32_t* d_index, int32_t* h_U, hipStream_t s);
+// the index lines of getParams' mode-1 section, formatted on the device
+hipError_t model_index_text(const int32_t* d_index, const int32_t* h_dims, int n_mats, std::vector<char>* out,
+                            hipStream_t s);
+// parse the index lines (device text) into weights: w[t] = value of key token t
+// (std::map semantics: 0.0f for an absent key). *h_status: 0 ok, 1 malformed
+// token, 2 token count != n_w.
+hipError_t model_read_index(const uint8_t* d_text, int64_t len, int64_t n_w, const int32_t* d_keys,
+                            const float* d_vals, int32_t n_keys, float* d_w, int* h_status, hipStream_t s);
+}  // namespace fleet

@@ -160,6 +160,30 @@ int fleet_check(fleet_ctx* ctx, void* stream);
  * computed on the GPU; compare with the oracle's digests. */
 int fleet_selftest_digest(fleet_ctx* ctx, int fn, uint64_t* out);
 
+/* DISTILLATION_MODE=1 model codec -- host buffers ----
+ * `weights` = the model's W matrices concatenated in W order, `dims` =
+ * n_mats x {cols, rows, chans} (W matrices are not channel-aligned: each is
+ * cols*rows*chans floats). */
+/* network::quantization_weight_model (commonLib/cppNN/network.h:1683-1774,
+ * core_math.h:881-912) on a copy of the weights, then getParams' first-occurrence
+ * dictionary (float_vector_find, network.h:594-608, |a-b| < 1e-8f) and the
+ * selected-index set (network.h:641-692). Outputs, each nullable: quantized[n]
+ * (the weights the text describes), dict[n] (entries in creation order, *n_dict
+ * of them), index[n] (the printed index; -1 for NaN/inf weights). */
+int fleet_model_quantize_index(fleet_ctx* ctx, const float* weights, const int32_t* dims, int n_mats,
+                               float* quantized, float* dict, int* n_dict, int32_t* index);
+/* The DISTILLATION_MODE=1 weights section of getParams (network.h:641-692) for
+ * these weights: "n\nU\n", U pairs "k\nvalue\n" (value as `ostream << float`,
+ * i.e. %g), one line of "index " per matrix -- the bytes the reference emits
+ * after the bias lines (getParametersNative, Server/.../cppNN_backend.cpp:244-280). */
+int fleet_model_weights_text(fleet_ctx* ctx, const float* weights, const int32_t* dims, int n_mats, char* out,
+                             size_t cap, size_t* out_len);
+/* network::read's DISTILLATION_MODE=1 weights branch (network.h:958-997): such a
+ * section back to weights (W[i] = value of the index's dictionary key; a key
+ * the dictionary lacks gives 0.0f, std::map::operator[]). */
+int fleet_model_read_weights(fleet_ctx* ctx, const char* text, size_t len, const int32_t* dims, int n_mats,
+                             float* weights_out);
+
 /* Name of the aggregation kernel fleet_update / fleet_update_device launch for
  * an upload of `len` Base64 bytes (or a group window of that many bytes):
  * "k_update<K>", "k_update_tiled<TG>" or "k_update_pipe<TG>" (profiling aid). */

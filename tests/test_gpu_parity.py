@@ -294,3 +294,72 @@ def test_device_window_update(codec, oracle):
     assert b"".join(parts) == exp
     # the single-rank driver (no process group): same bytes
     assert ShardedUpdater(codec).update(ups, d) == exp
+
+
+# ---- DISTILLATION_MODE=1 model codec ---------------------------------
+
+def _model_fixture(name):
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", f"model_{name}.npz"))
+
+
+@pytest.mark.parametrize("name", ["mnist_init", "mnist_seeded"])
+def test_model_codec_matches_reference_fixtures(codec, name):
+    """quantised weights, the weights section of getParams and network::read's
+    weights, bit-exact against the reference's own mojo network (fixtures)."""
+    f = _model_fixture(name)
+    dims = [tuple(int(v) for v in d) for d in f["dims"]]
+    wq, dic, idx = codec.model_quantize_index(f["w"], dims)
+    assert np.array_equal(wq.view(np.uint32), f["wq"].view(np.uint32))
+    sec = codec.model_weights_text(f["w"], dims)
+    assert f["text"].tobytes().endswith(sec)
+    wr = codec.model_read_weights(sec, dims)
+    assert np.array_equal(wr.view(np.uint32), f["w_read"].view(np.uint32))
+
+
+def test_model_codec_edge_cases(codec, oracle):
+    """NaN/inf (index -1), constant matrices (alpha = 0 -> NaN), s = 1 matrices."""
+    f = _model_fixture("generic")
+    dims = [tuple(int(v) for v in d) for d in f["dims"]]
+    for t in range(4):
+        wq, dic, idx = codec.model_quantize_index(f[f"w{t}"], dims)
+        assert np.array_equal(wq.view(np.uint32), f[f"wq{t}"].view(np.uint32)), t
+        assert b"mojo01\n0\n0\n0\n" + codec.model_weights_text(f[f"w{t}"], dims) == f[f"text{t}"].tobytes(), t
+        od, oi = oracle.dictionary(wq)
+        assert np.array_equal(dic.view(np.uint32), od.view(np.uint32)) and np.array_equal(idx, oi), t
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_model_dictionary_tolerance_chains(codec, oracle, seed):
+    """Long tolerance chains (levels closer than 1e-8 across and within
+    matrices), ties, +-0, against the oracle's sequential float_vector_find."""
+    rng = np.random.default_rng(seed)
+    dims = [(40, 30, 2), (1, 1, 300), (25, 4, 7), (7, 1, 1)]
+    n = sum(c * r * ch for c, r, ch in dims)
+    kinds = [rng.normal(0, 1e-7, n), rng.integers(-5, 6, n) * 4e-9 + rng.normal(0, 2e-9, n),
+             np.where(rng.random(n) < 0.5, 0.0, -0.0) + rng.integers(0, 3, n) * 1e-9]
+    w = kinds[seed].astype(np.float32)
+    wq, dic, idx = codec.model_quantize_index(w, dims)
+    owq = oracle.quantize(w, dims)
+    assert np.array_equal(wq.view(np.uint32), owq.view(np.uint32))
+    od, oi = oracle.dictionary(owq)
+    assert np.array_equal(dic.view(np.uint32), od.view(np.uint32)) and np.array_equal(idx, oi)
+    sec = codec.model_weights_text(w, dims)
+    assert sec == oracle.weights_section(owq, dims)
+    wr = codec.model_read_weights(sec, dims)
+    assert np.array_equal(wr.view(np.uint32), oracle.read_weights_section(sec, dims).view(np.uint32))
+
+
+def test_model_codec_large_random(codec, oracle):
+    """A 167k-weight model (conv stacks with few levels, and a 20,000-level FC
+    matrix: U ~ 20k) of trained-like weights. The oracle is O(n*U), so the
+    model is sized for it, not for the GPU."""
+    rng = np.random.default_rng(11)
+    dims = [(3, 3, 4096), (3, 3, 4096), (5, 5, 1000), (1, 1, 20000), (200, 100, 1)]
+    n = sum(c * r * ch for c, r, ch in dims)
+    w = (rng.normal(0, 0.05, n) * np.exp(rng.normal(0, 1, n))).astype(np.float32)
+    sec = codec.model_weights_text(w, dims)
+    owq = oracle.quantize(w, dims)
+    assert sec == oracle.weights_section(owq, dims)
+    wr = codec.model_read_weights(sec, dims)
+    assert np.array_equal(wr.view(np.uint32), oracle.read_weights_section(sec, dims).view(np.uint32))
