@@ -16,6 +16,8 @@ namespace fleet {
 // Base64.cpp:56-68 `from_base64`, extended with 0xff for bytes >= 0x80
 // (the reference indexes out of bounds there; such text is rejected here).
 struct B64Tables {
+  MulEntry mt[16];        // step multipliers by digit count (codec_math.h)
+  VarEntry var[512];      // digit count by sign + biased exponent (codec_math.h)
   DigitEntry digits[32];  // numDigits by frexp exponent (codec_math.h)
   uint8_t from[256];      // Base64.cpp:56-68, 0xff = not in the alphabet
   uint8_t fromf[256];     // same, 0x40 = not in the alphabet
@@ -59,6 +61,12 @@ __device__ __forceinline__ void b64_tables_init(B64Tables* t) {
   }
   if (tid < 64) t->to[tid] = b64_to_value(tid);
   if (tid < 32) t->digits[tid] = dig[tid];
+  if (tid < 16) t->mt[tid] = mul_entry((uint32_t)tid);
+#pragma unroll
+  for (int i0 = 0; i0 < 512; i0 += NT) {
+    const int i = i0 + tid;
+    if (NT >= 512 || i < 512) t->var[i] = var_entry((uint32_t)i);
+  }
 }
 
 // One 16-char group -> 12 bytes -> 3 little-endian int32 codes.

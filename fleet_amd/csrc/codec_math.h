@@ -349,6 +349,134 @@ FLEET_HD float q_lat(float x) {
   return r;
 }
 
+// --------------------------------------- multiplier-table variable-length Q
+// The throughput form of q_gen. Measured on gfx950 (scripts/ubench3.hip): f32
+// mul/fma issue in ~2.4 cycles per wave64 instruction, integer/convert/select
+// ops in ~4, packed f32 ops in ~8 (slower than two scalar ops). So the step
+// selection is done with multiplications instead of selects: every value runs
+// the full 9-step chains, and a step that the reference does not take
+// multiplies by 1 (x10 chain) or computes fma(t, 1, t*0) = t (/10 chain), both
+// exact identities. The per-value step multipliers (groups of 2, 1, 2 and 4
+// steps, Steps) come from a 16-entry LDS table indexed by the digit count d;
+// d itself from a 512-entry table indexed by the top 9 bits of x (sign and
+// biased exponent) plus one compare with the power of ten inside that binade.
+struct alignas(16) MulEntry {
+  float m[4];  // x10 chain group multipliers: 10 (step taken) or 1
+  float h[4];  // /10 chain: fma(t, h, t*l) = div10(t) (taken) or t
+  float l[4];
+};
+FLEET_HD MulEntry mul_entry(uint32_t d) {  // d = numDigits; d > 9 (slow marker): identity
+  MulEntry e;
+  const bool ok = d <= 9u;
+  const Steps s = steps_of(ok ? 9u - d : 0u);
+  const bool g[4] = {ok && s.e, ok && s.b0, ok && s.b1, ok && s.b2};
+  for (int i = 0; i < 4; ++i) {
+    e.m[i] = g[i] ? 10.0f : 1.0f;
+    e.h[i] = g[i] ? kTenthHi : 1.0f;
+    e.l[i] = g[i] ? kTenthLo : 0.0f;
+  }
+  return e;
+}
+
+// Digit table entry i = (sign << 8) | biased exponent of x: byte 0 = d for
+// |x| < thr, byte 1 = d for |x| >= thr; d = 15 marks values outside the q_gen
+// domain (-1e8 < x < 1e9), NaN and inf (callers send those through the
+// general codec). The byte is stored pre-multiplied for the MulEntry index.
+struct alignas(8) VarEntry {
+  float thr;
+  uint32_t info;
+};
+constexpr uint32_t kSlowDigits = 15u;
+FLEET_HD VarEntry var_entry(uint32_t i) {
+  constexpr DigitEntry dig[32] = FLEET_DIGIT_TABLE;
+  const uint32_t neg = (i >> 8) & 1u;
+  const int e = (int)(i & 255u) - 126;  // |x| in [2^(e-1), 2^e) for normal x
+  if (e <= 0) return VarEntry{__builtin_inff(), 0u};  // |x| < 1: (int)x == 0, d = 0
+  const DigitEntry t = dig[e > 31 ? 31 : e];
+  uint32_t dlo = t.base + neg, dhi = t.base + 1u + neg;  // '-' counts (Base64.cpp:73-82)
+  dlo = dlo > 9u ? kSlowDigits : dlo;
+  dhi = dhi > 9u ? kSlowDigits : dhi;
+  return VarEntry{t.thr, dlo | (dhi << 8)};
+}
+
+// numDigits((int)x) on the q_gen domain, kSlowDigits outside it
+FLEET_HD uint32_t var_digits(float x, const VarEntry* vt) {
+  const VarEntry v = vt[f2u(x) >> 23];
+  return (v.info >> (__builtin_fabsf(x) >= v.thr ? 8u : 0u)) & 0xffu;
+}
+
+FLEET_HD float mul10_mt(float X, const MulEntry& e) {
+  X = X * e.m[0];
+  X = X * e.m[0];
+  X = X * e.m[1];
+  X = X * e.m[2];
+  X = X * e.m[2];
+  X = X * e.m[3];
+  X = X * e.m[3];
+  X = X * e.m[3];
+  return X * e.m[3];
+}
+FLEET_HD float div10_mt(float t, const MulEntry& e) {
+  t = __builtin_fmaf(t, e.h[0], t * e.l[0]);
+  t = __builtin_fmaf(t, e.h[0], t * e.l[0]);
+  t = __builtin_fmaf(t, e.h[1], t * e.l[1]);
+  t = __builtin_fmaf(t, e.h[2], t * e.l[2]);
+  t = __builtin_fmaf(t, e.h[2], t * e.l[2]);
+  t = __builtin_fmaf(t, e.h[3], t * e.l[3]);
+  t = __builtin_fmaf(t, e.h[3], t * e.l[3]);
+  t = __builtin_fmaf(t, e.h[3], t * e.l[3]);
+  return __builtin_fmaf(t, e.h[3], t * e.l[3]);
+}
+
+// |code| = 10*floor(n/10) + d, n = trunc(X): floor(n/10) = mulhi(n, ceil(2^32/10))
+// for n < 2^30 (error n*0.4/2^32 < 0.1); the sign of x goes on the float.
+FLEET_HD uint32_t div10_u30(uint32_t n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umulhi(n, 0x1999999Au);
+#else
+  return (uint32_t)(((uint64_t)n * 0x1999999Au) >> 32);
+#endif
+}
+FLEET_HD float code_float_mt(float X, uint32_t d, float x) {
+  const uint32_t c = div10_u30((uint32_t)X) * 10u + d;
+  return u2f(f2u((float)c) | (f2u(x) & 0x80000000u));
+}
+
+// Q(x) on the q_gen domain (d = var_digits(x) <= 9)
+FLEET_HD float q_mt_d(float x, uint32_t d, const MulEntry* mt) {
+  const MulEntry e = mt[d];
+  return div10_mt(code_float_mt(mul10_mt(__builtin_fabsf(x), e), d, x), e);
+}
+FLEET_HD float q_mt(float x, const VarEntry* vt, const MulEntry* mt) { return q_mt_d(x, var_digits(x, vt), mt); }
+// float2int(x) on the q_gen domain
+FLEET_HD int32_t enc_mt(float x, const VarEntry* vt, const MulEntry* mt) {
+  const uint32_t d = var_digits(x, vt);
+  const uint32_t c = div10_u30((uint32_t)mul10_mt(__builtin_fabsf(x), mt[d])) * 10u + d;
+  return x < 0.0f ? -(int32_t)c : (int32_t)c;
+}
+// int2float(c) for every code: k = 9 - |c % 10| steps, flags from the last digit
+FLEET_HD uint32_t last_digit_u(uint32_t a) {  // a % 10 for every uint32
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t q = __umulhi(a, 0xCCCCCCCDu) >> 3;
+#else
+  const uint32_t q = (uint32_t)(((uint64_t)a * 0xCCCCCCCDu) >> 35);
+#endif
+  return a - q * 10u;
+}
+FLEET_HD float dec_mt_r(int32_t c, uint32_t r, const MulEntry* mt) { return div10_mt((float)c, mt[r]); }
+FLEET_HD float dec_mt(int32_t c, const MulEntry* mt) {
+  return dec_mt_r(c, last_digit_u(c < 0 ? 0u - (uint32_t)c : (uint32_t)c), mt);
+}
+
+// Q(x) for |x| < 1 (the fixed 9-step chains), scalar: cheaper than q_fast2
+FLEET_HD float q_fast1(float x) {
+  float X = __builtin_fabsf(x);
+#pragma unroll
+  for (int j = 0; j < 9; ++j) X = X * 10.0f;
+  const uint32_t c = div10_u30((uint32_t)X) * 10u;
+  return d9(u2f(f2u((float)c) | (f2u(x) & 0x80000000u)));
+}
+
 // int2float(c) for every code (k = 9 - |c % 10| in [0, 9]) -- total.
 FLEET_HD uint32_t last_digit(int32_t c) {
   uint32_t a = c < 0 ? 0u - (uint32_t)c : (uint32_t)c;

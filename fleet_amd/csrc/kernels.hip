@@ -124,38 +124,52 @@ __device__ __forceinline__ void resolve_slow(float (&out)[S], const uint32_t (&i
 }
 
 // out[i] = Q(x[i]) for a stage of S values: fixed 9-step chains when the
-// whole wave is in |x| < 1, else the variable chains; resolve_slow for the rest.
+// whole wave is in |x| < 1, else the multiplier-table chains (codec_math.h:
+// no selects, no packed ops -- the cheap encodings on gfx950); resolve_slow for
+// the values outside the q_gen domain.
 template <int S>
-__device__ __forceinline__ void q_stage(float (&out)[S], const float (&x)[S], const DigitEntry* dig,
+__device__ __forceinline__ void q_stage(float (&out)[S], const float (&x)[S], const B64Tables* tab,
                                         uint32_t* __restrict__ ws, int lane) {
   bool all_fast = true;
 #pragma unroll
   for (int i = 0; i < S; ++i) all_fast &= q_ok(x[i]);
-  uint32_t slow = 0;
   if (__ballot(!all_fast) == 0) {
 #pragma unroll
-    for (int i = 0; i + 1 < S; i += 2) {
-      const f2 v = q_fast2(f2{x[i], x[i + 1]});
-      out[i] = v.x;
-      out[i + 1] = v.y;
-    }
-    if (S & 1) out[S - 1] = q_fast(x[S - 1]);
+    for (int i = 0; i < S; ++i) out[i] = q_fast1(x[i]);
     return;
   }
-#pragma unroll
-  for (int i = 0; i + 1 < S; i += 2) {
-    const f2 v = q_gen2(f2{x[i], x[i + 1]}, dig);
-    out[i] = v.x;
-    out[i + 1] = v.y;
-  }
-  if (S & 1) out[S - 1] = q_gen(x[S - 1], dig);
+  uint32_t slow = 0;
   uint32_t in[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    slow |= (uint32_t)!q_gen_ok(x[i]) << i;
+    const uint32_t d = var_digits(x[i], tab->var);
+    slow |= (uint32_t)(d == kSlowDigits) << i;
+    out[i] = q_mt_d(x[i], d, tab->mt);
     in[i] = f2u(x[i]);
   }
   resolve_slow<S, 1>(out, in, slow, ws, lane);
+}
+
+// out[i] = int2float(codes[i]) (Base64.cpp:116-139): fixed 9-step chains when
+// every code of the wave ends in 0 (|value| < 1), else step multipliers from
+// the last digit. Total: no fallback needed.
+template <int S>
+__device__ __forceinline__ void dec_stage(float (&out)[S], const int32_t (&codes)[S], const B64Tables* tab) {
+  uint32_t r[S];
+  bool any = false;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const uint32_t a = codes[i] < 0 ? 0u - (uint32_t)codes[i] : (uint32_t)codes[i];
+    r[i] = last_digit_u(a);
+    any |= r[i] != 0u;
+  }
+  if (__ballot(any) == 0) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) out[i] = dec_fast(codes[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < S; ++i) out[i] = dec_mt_r(codes[i], r[i], tab->mt);
+  }
 }
 
 // Single value per thread on a latency-bound serial chain: same as q_stage<1>
@@ -178,12 +192,13 @@ __device__ __forceinline__ void q_stage_lat(float (&out)[1], const float (&x)[1]
 // Q(f32(f64(A) * inv)). Variable-length chains on their domain, the general
 // codec for the rest (divergent, rare).
 __device__ __forceinline__ int32_t merged_code(float A, double inv, int32_t last_code, bool keep_last,
-                                               const DigitEntry* dig) {
+                                               const B64Tables* tab) {
   if (keep_last) return enc(dec(last_code));
   const float r = (float)((double)A * inv);
-  if (q_gen_ok(r)) {
-    const float y = q_gen(r, dig);
-    if (q_gen_ok(y)) return enc_gen(y, dig);
+  const uint32_t d = var_digits(r, tab->var);
+  if (d != kSlowDigits) {
+    const float y = q_mt_d(r, d, tab->mt);
+    if (var_digits(y, tab->var) != kSlowDigits) return enc_mt(y, tab->var, tab->mt);
   }
   return enc(q(r));
 }
@@ -284,36 +299,15 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
     // general codec via resolve_slow (|x| >= 1e7: never for gradients).
     // stage A: y = Q(int2float(code))
     float y0[S], y[S];
-    {
-      bool all9 = true;
-#pragma unroll
-      for (int i = 0; i < S; ++i) all9 &= dec9_ok(codes[i]);
-      if (__ballot(!all9) == 0) {
-#pragma unroll
-        for (int i = 0; i + 1 < S; i += 2) {
-          const f2 v = dec_fast2(codes[i], codes[i + 1]);
-          y0[i] = v.x;
-          y0[i + 1] = v.y;
-        }
-        if (S & 1) y0[S - 1] = dec_fast(codes[S - 1]);
-      } else {
-#pragma unroll
-        for (int i = 0; i + 1 < S; i += 2) {
-          const f2 v = dec_gen2(codes[i], codes[i + 1]);
-          y0[i] = v.x;
-          y0[i + 1] = v.y;
-        }
-        if (S & 1) y0[S - 1] = dec_gen(codes[S - 1]);
-      }
-    }
-    q_stage<S>(y, y0, tab.digits, ws, lane);
+    dec_stage<S>(y0, codes, &tab);
+    q_stage<S>(y, y0, &tab, ws, lane);
 
     // stage B: p = Q((float)((double)y * d))
     const double d = dampen[c];
     float r[S], p[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) r[i] = (float)((double)y[i] * d);
-    q_stage<S>(p, r, tab.digits, ws, lane);
+    q_stage<S>(p, r, &tab, ws, lane);
 
     // stage C: A = Q(A + p)
     if (c == 0) {
@@ -323,7 +317,7 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
       float sm[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) sm[i] = acc[i] + p[i];
-      q_stage<S>(acc, sm, tab.digits, ws, lane);
+      q_stage<S>(acc, sm, &tab, ws, lane);
     }
   }
 
@@ -338,12 +332,12 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
       const bool keep_last = ((hbits >> (3 * k + e)) & 1u) || p0 + e >= walk_end;
-      const int32_t o = merged_code(acc[3 * k + e], inv_avg, codes[3 * k + e], keep_last, tab.digits);
+      const int32_t o = merged_code(acc[3 * k + e], inv_avg, codes[3 * k + e], keep_last, &tab);
       out[e] = e < r ? o : 0;
     }
     *reinterpret_cast<uint4*>(merged + 16 * g[k]) = pad_group(b64_encode_group(out, &tab), r);
     if (merged_f32) {
-      for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec_gen(out[e]);
+      for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec_mt(out[e], tab.mt);
     }
   }
 }
@@ -463,29 +457,8 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileI
   }
   // stage A: y = Q(int2float(code))
   float y0[S], y[S];
-  {
-    bool all9 = true;
-#pragma unroll
-    for (int i = 0; i < S; ++i) all9 &= dec9_ok(codes[i]);
-    if (__ballot(!all9) == 0) {
-#pragma unroll
-      for (int i = 0; i + 1 < S; i += 2) {
-        const f2 v = dec_fast2(codes[i], codes[i + 1]);
-        y0[i] = v.x;
-        y0[i + 1] = v.y;
-      }
-      if (S & 1) y0[S - 1] = dec_fast(codes[S - 1]);
-    } else {
-#pragma unroll
-      for (int i = 0; i + 1 < S; i += 2) {
-        const f2 v = dec_gen2(codes[i], codes[i + 1]);
-        y0[i] = v.x;
-        y0[i + 1] = v.y;
-      }
-      if (S & 1) y0[S - 1] = dec_gen(codes[S - 1]);
-    }
-  }
-  q_stage<S>(y, y0, sh.tab.digits, ws, lane);
+  dec_stage<S>(y0, codes, &sh.tab);
+  q_stage<S>(y, y0, &sh.tab, ws, lane);
   // stage B: p = Q(f32(f64(y) * d)), per-item client
   float r[S], p[S];
 #pragma unroll
@@ -494,7 +467,7 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileI
 #pragma unroll
     for (int e = 0; e < 3; ++e) r[3 * h + e] = (float)((double)y[3 * h + e] * d);
   }
-  q_stage<S>(p, r, sh.tab.digits, ws, lane);
+  q_stage<S>(p, r, &sh.tab, ws, lane);
 #pragma unroll
   for (int h = 0; h < IPT; ++h)
     if (it.live[h])
@@ -529,8 +502,8 @@ __device__ __forceinline__ void tile_epilogue(TileShared<TG, NW>& sh, const floa
     if (p < n_up) {
       const bool hdr = (sh.hmask[gl] >> e) & 1u;
       if (hdr && sh.hmin[tid] != sh.hmax[tid]) atomicOr(err, FLEET_ERRBIT_LAYOUT);
-      o = merged_code(vals[tid], inv_avg, sh.last_codes[tid], hdr || p >= walk_end, sh.tab.digits);
-      if (merged_f32) merged_f32[p] = dec_gen(o);
+      o = merged_code(vals[tid], inv_avg, sh.last_codes[tid], hdr || p >= walk_end, &sh.tab);
+      if (merged_f32) merged_f32[p] = dec_mt(o, sh.tab.mt);
     }
     sh.outcodes[tid] = o;
   }
@@ -756,7 +729,7 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
     for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
   } else {
 #pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_gen(x[e], tab.digits);
+    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab.var, tab.mt);
     if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
 #pragma unroll
       for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
@@ -1169,9 +1142,13 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 
 __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __restrict__ out) {
   __shared__ DigitEntry dig[32];
+  __shared__ VarEntry var[512];
+  __shared__ MulEntry mt[16];
   {
     constexpr DigitEntry init[32] = FLEET_DIGIT_TABLE;
     if (threadIdx.x < 32) dig[threadIdx.x] = init[threadIdx.x];
+    if (threadIdx.x < 16) mt[threadIdx.x] = mul_entry(threadIdx.x);
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) var[i] = var_entry((uint32_t)i);
     __syncthreads();
   }
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1208,6 +1185,13 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
                o = use ? (uint32_t)enc_fast(u2f(u)) : 0u; break;
       case 12: use = q_gen_ok(u2f(u));                                // select-chain Q (serial accumulation)
                o = use ? f2u(q_lat(u2f(u))) : 0u; break;
+      case 13: use = q_gen_ok(u2f(u));                                // multiplier-table Q (same digest as fn 6)
+               o = use ? f2u(q_mt(u2f(u), var, mt)) : 0u; break;
+      case 14: o = f2u(dec_mt((int32_t)u, mt)); break;                // multiplier-table int2float (as fn 7)
+      case 15: use = q_gen_ok(u2f(u));                                // multiplier-table float2int (as fn 10)
+               o = use ? (uint32_t)enc_mt(u2f(u), var, mt) : 0u; break;
+      case 16: use = (u & 0x7fffffffu) < 0x3f800000u;                 // scalar Q fast path (as fn 2)
+               o = use ? f2u(q_fast1(u2f(u))) : 0u; break;
       default: o = 0; use = false;
     }
     if (use) sum += splitmix64(((uint64_t)u << 32) | o);

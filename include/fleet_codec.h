@@ -157,6 +157,8 @@ int fleet_check(fleet_ctx* ctx, void* stream);
  *   fn 8: packed fn 6 on (x, -x/4)            fn 9: packed fn 7 on (c, c*2654435761)
  *   fn 10: variable-length float2int (-1e8 < x < 1e9)   fn 11: float2int fast path (|x| < 1)
  *   fn 12: select-chain Q of the serial accumulation (-1e8 < x < 1e9; same digest as fn 6)
+ *   fn 13: multiplier-table Q (as fn 6)   fn 14: multiplier-table int2float (as fn 7)
+ *   fn 15: multiplier-table float2int (as fn 10)   fn 16: scalar Q fast path (as fn 2)
  * computed on the GPU; compare with the oracle's digests. */
 int fleet_selftest_digest(fleet_ctx* ctx, int fn, uint64_t* out);
 

@@ -51,6 +51,30 @@ int main(int argc, char** argv) {
     report("q_lat (exhaustive)", b);
     return g_bad ? 1 : 0;
   }
+  if (argc > 1 && std::string(argv[1]) == "mt") {  // multiplier-table functions, every input
+    static VarEntry vt[512];
+    static MulEntry mt[16];
+    for (uint32_t i = 0; i < 512; ++i) vt[i] = var_entry(i);
+    for (uint32_t d = 0; d < 16; ++d) mt[d] = mul_entry(d);
+    long b = g_bad;
+    par_for(0, 1ull << 32, 1, [](uint64_t i) {
+      const float x = u2f((uint32_t)i);
+      const int32_t c = (int32_t)(uint32_t)i;
+      const uint32_t a = c < 0 ? 0u - (uint32_t)c : (uint32_t)c;
+      if (!same(dec_mt_r(c, last_digit_u(a), mt), fo_int2float(c))) g_bad++;
+      const uint32_t d = var_digits(x, vt);
+      if (!q_gen_ok(x)) {
+        if (d != kSlowDigits) g_bad++;
+        return;
+      }
+      if (d != (uint32_t)fo_num_digits(fo_cvtt(x))) g_bad++;
+      const int32_t e = fo_float2int(x);
+      if (!same(q_mt(x, vt, mt), fo_int2float(e)) || enc_mt(x, vt, mt) != e) g_bad++;
+      if (q_ok(x) && !same(q_fast1(x), fo_int2float(e))) g_bad++;
+    });
+    report("q_mt/enc_mt/dec_mt/var_digits/q_fast1 (exhaustive)", b);
+    return g_bad ? 1 : 0;
+  }
   const uint64_t s = exhaustive ? 1 : 97;  // sampling stride (odd, walks every residue class)
   long b0;
 
@@ -116,6 +140,38 @@ int main(int argc, char** argv) {
     if (!same(q_gen(x, tab), r) || !same(p.x, r) || !same(p.y, r2)) g_bad++;
   });
   report("q_gen/q_gen2", b0);
+
+  static VarEntry vt[512];
+  static MulEntry mt[16];
+  for (uint32_t i = 0; i < 512; ++i) vt[i] = var_entry(i);
+  for (uint32_t d = 0; d < 16; ++d) mt[d] = mul_entry(d);
+
+  b0 = g_bad;  // var_digits vs numDigits((int)x) on the q_gen domain, slow marker outside it
+  par_for(0, 1ull << 32, s, [](uint64_t i) {
+    float x = u2f((uint32_t)i);
+    const uint32_t d = var_digits(x, vt);
+    if (q_gen_ok(x) ? d != (uint32_t)fo_num_digits(fo_cvtt(x)) : d != kSlowDigits) g_bad++;
+  });
+  report("var_digits", b0);
+
+  b0 = g_bad;  // multiplier-table Q / float2int / fixed scalar Q vs the oracle
+  par_for(0, 1ull << 32, s, [](uint64_t i) {
+    float x = u2f((uint32_t)i);
+    if (!q_gen_ok(x)) return;
+    if (!same(q_mt(x, vt, mt), fo_int2float(fo_float2int(x)))) g_bad++;
+    if (enc_mt(x, vt, mt) != fo_float2int(x)) g_bad++;
+    if (q_ok(x) && !same(q_fast1(x), fo_int2float(fo_float2int(x)))) g_bad++;
+  });
+  report("q_mt/enc_mt/q_fast1", b0);
+
+  b0 = g_bad;  // multiplier-table int2float, every code
+  par_for(0, 1ull << 32, s, [](uint64_t i) {
+    int32_t c = (int32_t)(uint32_t)i;
+    const uint32_t a = c < 0 ? 0u - (uint32_t)c : (uint32_t)c;
+    if (last_digit_u(a) != a % 10u) g_bad++;
+    if (!same(dec_mt_r(c, last_digit_u(a), mt), fo_int2float(c))) g_bad++;
+  });
+  report("dec_mt/last_digit_u", b0);
 
   b0 = g_bad;  // dec_gen (+ packed) vs int2float, every code
   par_for(0, 1ull << 32, s, [](uint64_t i) {

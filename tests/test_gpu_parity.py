@@ -182,14 +182,18 @@ def test_device_synth_and_encode(codec, oracle):
         assert np.array_equal(b[c, : lay.n_up].view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
 
 
-@pytest.mark.parametrize("fn", range(13))
+# fn 13-16 compute the same functions as fn 6, 7, 10, 2 by other arithmetic
+SAME_DIGEST = {13: 6, 14: 7, 15: 10, 16: 2}
+
+
+@pytest.mark.parametrize("fn", range(17))
 def test_device_codec_exhaustive_digest(codec, fn):
     """Every input of each device codec function's domain (2^32 codes / bit
     patterns), digested on the GPU, equals the oracle's digest."""
     import json
     import os
     ref = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "digests.json")))
-    assert f"{codec.selftest_digest(fn):016x}" == ref[f"fn{fn}"]
+    assert f"{codec.selftest_digest(fn):016x}" == ref[f"fn{SAME_DIGEST.get(fn, fn)}"]
 
 
 @pytest.mark.parametrize("K", [1, 2, 4])
