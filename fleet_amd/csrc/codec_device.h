@@ -15,16 +15,17 @@ namespace fleet {
 
 // Base64.cpp:56-68 `from_base64`, extended with 0xff for bytes >= 0x80
 // (the reference indexes out of bounds there; such text is rejected here).
+// Every kernel copies this block of tables into LDS at start (b64_tables_init).
 struct B64Tables {
-  MulEntry mt[16];        // step multipliers by digit count (codec_math.h)
-  VarEntry var[512];      // digit count by sign + biased exponent (codec_math.h)
-  DigitEntry digits[32];  // numDigits by frexp exponent (codec_math.h)
-  uint8_t from[256];      // Base64.cpp:56-68, 0xff = not in the alphabet
-  uint8_t fromf[256];     // same, 0x40 = not in the alphabet
+  MulEntry mt[16];    // step multipliers by digit count (codec_math.h)
+  VarEntry var[512];  // digit count by sign + biased exponent (codec_math.h)
+  uint8_t from[256];  // Base64.cpp:56-68, 0xff = not in the alphabet
+  uint8_t fromf[256]; // same, 0x40 = not in the alphabet
   uint8_t to[64];
 };
+static_assert(sizeof(B64Tables) % 16 == 0, "copied as uint4");
 
-__device__ __forceinline__ uint8_t b64_from_value(int ch) {
+FLEET_HDC uint8_t b64_from_value(int ch) {
   if (ch >= 'A' && ch <= 'Z') return (uint8_t)(ch - 'A');
   if (ch >= 'a' && ch <= 'z') return (uint8_t)(ch - 'a' + 26);
   if (ch >= '0' && ch <= '9') return (uint8_t)(ch - '0' + 52);
@@ -35,37 +36,40 @@ __device__ __forceinline__ uint8_t b64_from_value(int ch) {
 
 // 0..63, or 0x40 for a byte outside the alphabet (one flag bit, so a group's
 // validity is the OR of its sextets)
-__device__ __forceinline__ uint8_t b64_from_value_flag(int ch) {
+FLEET_HDC uint8_t b64_from_value_flag(int ch) {
   const uint8_t v = b64_from_value(ch);
   return v == 0xff ? 0x40 : v;
 }
 
-__device__ __forceinline__ uint8_t b64_to_value(int s) {
+FLEET_HDC uint8_t b64_to_value(int s) {
   return (uint8_t)(s < 26 ? 'A' + s : s < 52 ? 'a' + s - 26 : s < 62 ? '0' + s - 52 : s == 62 ? '+' : '/');
 }
 
-// Fill the block's LDS tables (call from every thread of an NT-thread block,
-// then __syncthreads()). NT is a compile-time constant so the fill is a
-// straight-line pass, not a loop the compiler vectorises over unknown strides.
+FLEET_HDC B64Tables make_b64_tables() {
+  B64Tables t{};
+  for (int d = 0; d < 16; ++d) t.mt[d] = mul_entry((uint32_t)d);
+  for (int i = 0; i < 512; ++i) t.var[i] = var_entry((uint32_t)i);
+  for (int i = 0; i < 256; ++i) {
+    t.from[i] = b64_from_value(i);
+    t.fromf[i] = b64_from_value_flag(i);
+  }
+  for (int i = 0; i < 64; ++i) t.to[i] = b64_to_value(i);
+  return t;
+}
+// built at compile time; one copy per code object
+static __constant__ B64Tables g_b64_tables = make_b64_tables();
+
+// Copy the tables into the block's LDS (call from every thread of an NT-thread
+// block, then __syncthreads()): 340 16-byte loads from an L2-resident image.
 template <int NT = 256>
 __device__ __forceinline__ void b64_tables_init(B64Tables* t) {
-  constexpr DigitEntry dig[32] = FLEET_DIGIT_TABLE;
-  const int tid = threadIdx.x;
+  constexpr int n16 = (int)(sizeof(B64Tables) / 16);
+  const uint4* src = reinterpret_cast<const uint4*>(&g_b64_tables);
+  uint4* dst = reinterpret_cast<uint4*>(t);
 #pragma unroll
-  for (int i0 = 0; i0 < 256; i0 += NT) {
-    const int i = i0 + tid;
-    if (NT <= 256 || i < 256) {
-      t->from[i] = b64_from_value(i);
-      t->fromf[i] = b64_from_value_flag(i);
-    }
-  }
-  if (tid < 64) t->to[tid] = b64_to_value(tid);
-  if (tid < 32) t->digits[tid] = dig[tid];
-  if (tid < 16) t->mt[tid] = mul_entry((uint32_t)tid);
-#pragma unroll
-  for (int i0 = 0; i0 < 512; i0 += NT) {
-    const int i = i0 + tid;
-    if (NT >= 512 || i < 512) t->var[i] = var_entry((uint32_t)i);
+  for (int i0 = 0; i0 < n16; i0 += NT) {
+    const int i = i0 + (int)threadIdx.x;
+    if (i < n16) dst[i] = src[i];
   }
 }
 

@@ -14,6 +14,8 @@
 #else
 #define FLEET_HD static inline __attribute__((always_inline))
 #endif
+// compile-time evaluable (table images, codec_device.h)
+#define FLEET_HDC FLEET_HD constexpr
 
 namespace fleet {
 
@@ -164,7 +166,7 @@ FLEET_HD bool q_ok(float x) { return __builtin_fabsf(x) < 1.0f; }
 struct Steps {
   bool e, b0, b1, b2;
 };
-FLEET_HD Steps steps_of(uint32_t k) {
+FLEET_HDC Steps steps_of(uint32_t k) {
   const bool e = k >= 8u;
   const uint32_t r = k - (e ? 2u : 0u);
   return Steps{e, (r & 1u) != 0, (r & 2u) != 0, (r & 4u) != 0};
@@ -309,6 +311,17 @@ FLEET_HD f2 q_gen2(f2 x, const DigitEntry* tab) {
   return steps_div10x2(t, s0, s1);
 }
 
+// 10*floor(n/10) + d as a signed float, n < 2^30: floor(n/10) = mulhi(n, ceil(2^32/10))
+// (error n*0.4/2^32 < 0.1) -- one dependent op less than n/10u.
+FLEET_HD float code_float_lat(uint32_t n, uint32_t d, float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t q = __umulhi(n, 0x1999999Au);
+#else
+  const uint32_t q = (uint32_t)(((uint64_t)n * 0x1999999Au) >> 32);
+#endif
+  return u2f(f2u((float)(q * 10u + d)) | (f2u(x) & 0x80000000u));
+}
+
 // Q(x) on the q_gen domain for the serial accumulation (one value per lane, a
 // single wave: bound by issue slots AND the dependent chain, so both are cut).
 //   * sign folding: w = 10|x| when x <= -1 ('-' counts as a digit), else |x|;
@@ -337,7 +350,7 @@ FLEET_HD float q_lat(float x) {
     X = X * 10.0f;
     t = big[9 - j] ? t : X;
   }
-  const float cf = signed_code_float((uint32_t)t, d, x);
+  const float cf = code_float_lat((uint32_t)t, (uint32_t)d, x);
   float U = cf, a = cf * kTenthLo, r = cf;
 #pragma unroll
   for (int j = 1; j <= 9; ++j) {
@@ -365,8 +378,8 @@ struct alignas(16) MulEntry {
   float h[4];  // /10 chain: fma(t, h, t*l) = div10(t) (taken) or t
   float l[4];
 };
-FLEET_HD MulEntry mul_entry(uint32_t d) {  // d = numDigits; d > 9 (slow marker): identity
-  MulEntry e;
+FLEET_HDC MulEntry mul_entry(uint32_t d) {  // d = numDigits; d > 9 (slow marker): identity
+  MulEntry e{};
   const bool ok = d <= 9u;
   const Steps s = steps_of(ok ? 9u - d : 0u);
   const bool g[4] = {ok && s.e, ok && s.b0, ok && s.b1, ok && s.b2};
@@ -387,7 +400,7 @@ struct alignas(8) VarEntry {
   uint32_t info;
 };
 constexpr uint32_t kSlowDigits = 15u;
-FLEET_HD VarEntry var_entry(uint32_t i) {
+FLEET_HDC VarEntry var_entry(uint32_t i) {
   constexpr DigitEntry dig[32] = FLEET_DIGIT_TABLE;
   const uint32_t neg = (i >> 8) & 1u;
   const int e = (int)(i & 255u) - 126;  // |x| in [2^(e-1), 2^e) for normal x

@@ -620,7 +620,9 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   __shared__ float finals[E];
   __shared__ int prog[NPW];  // passes finished by each producer wave
   __shared__ int consumed;   // passes finished by the consumer
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // wave index made wave-uniform (readfirstlane), so the producer/consumer
+  // split below is a scalar branch and the consumer's s_setprio is its own
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   const int64_t g0 = g_begin + (int64_t)blockIdx.x * TG;
   const int ng = (int)min<int64_t>(TG, g_end - g0);
   if (tid < NPW) prog[tid] = 0;
@@ -654,6 +656,10 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
       if (lane == 0) __hip_atomic_store(&prog[w], done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   } else {  // ---------------------------------------------------- consumer
+    // the serial chain is the block's critical path: win VALU issue
+    // arbitration against co-resident producer waves (MI355X_MICROARCH.md,
+    // two waves per SIMD, item 4)
+    __builtin_amdgcn_s_setprio(3);
     float A = 0.f;
     uint32_t off_domain = 0;
     const int col = tid < E ? tid : 0;
@@ -1142,15 +1148,15 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 
 __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __restrict__ out) {
   __shared__ DigitEntry dig[32];
-  __shared__ VarEntry var[512];
-  __shared__ MulEntry mt[16];
+  __shared__ B64Tables tab;
   {
     constexpr DigitEntry init[32] = FLEET_DIGIT_TABLE;
     if (threadIdx.x < 32) dig[threadIdx.x] = init[threadIdx.x];
-    if (threadIdx.x < 16) mt[threadIdx.x] = mul_entry(threadIdx.x);
-    for (int i = threadIdx.x; i < 512; i += blockDim.x) var[i] = var_entry((uint32_t)i);
+    b64_tables_init(&tab);
     __syncthreads();
   }
+  const VarEntry* var = tab.var;
+  const MulEntry* mt = tab.mt;
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t nthreads = (uint64_t)gridDim.x * blockDim.x;
   uint64_t sum = 0;
