@@ -7,6 +7,7 @@
 // 420-509); a wave reads 1 KiB contiguous per client row (global_load_dwordx4).
 #include "kernels.h"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -715,19 +716,10 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
 
 // ----------------------------------------------------------------------------
 // Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
-__global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ values, int64_t n, size_t vpitch,
-                                                    uint8_t* __restrict__ out, size_t pitch, int64_t groups) {
-  __shared__ B64Tables tab;
-  b64_tables_init(&tab);
-  __syncthreads();
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= groups) return;
-  const int64_t row_id = blockIdx.y;
-  const float* v = values + row_id * vpitch + 3 * g;
-  const int r = (int)min<int64_t>(3, n - 3 * g);
-  float x[3];
-#pragma unroll
-  for (int e = 0; e < 3; ++e) x[e] = e < r ? v[e] : 0.0f;
+// One group (3 values) of one row: float2int (fixed chains when the wave is
+// in |x| < 1, multiplier-table chains otherwise, the general codec for values
+// outside the q_gen domain) and the 16 Base64 chars.
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
   int32_t codes[3];
   const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
   if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
@@ -735,13 +727,42 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
     for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
   } else {
 #pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab.var, tab.mt);
+    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab->var, tab->mt);
     if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
 #pragma unroll
       for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
     }
   }
-  *reinterpret_cast<uint4*>(out + row_id * pitch + 16 * g) = pad_group(b64_encode_group(codes, &tab), r);
+  return pad_group(b64_encode_group(codes, tab), r);
+}
+
+// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
+// Block (bx, by) encodes groups [256*bx, 256*bx+256) of rows [rpb*by, rpb*by+rpb):
+// a lane walks its group down rpb rows (next row's floats loaded while the
+// current one is encoded), so the LDS table copy is paid once per rpb rows.
+__global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ values, int64_t n, size_t vpitch,
+                                                    uint8_t* __restrict__ out, size_t pitch, int64_t groups,
+                                                    int rows, int rpb) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= groups) return;
+  const int row0 = blockIdx.y * rpb, row1 = min(rows, row0 + rpb);
+  const int r = (int)min<int64_t>(3, n - 3 * g);
+  const float* v = values + (size_t)row0 * vpitch + 3 * g;
+  float nx[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) nx[e] = e < r ? v[e] : 0.0f;
+  for (int row = row0; row < row1; ++row) {
+    float x[3] = {nx[0], nx[1], nx[2]};
+    if (row + 1 < row1) {
+      v += vpitch;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) nx[e] = e < r ? v[e] : 0.0f;
+    }
+    *reinterpret_cast<uint4*>(out + (size_t)row * pitch + 16 * g) = encode_group(x, r, &tab);
+  }
 }
 
 // int32 codes -> Base64 (Base64::encode(vector<int>))
@@ -1062,8 +1083,11 @@ hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int 
                              hipStream_t s) {
   int64_t groups = (n + 2) / 3;
   if (groups == 0 || rows == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_encode_f32, dim3(blocks_for(groups, 256), rows), dim3(256), 0, s, values, n, vpitch, out,
-                     pitch, groups);
+  // rows per block: about 1,024 blocks in all (4 per CU), at least one row each
+  const int64_t gx = blocks_for(groups, 256);
+  const int rpb = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 1023) / 1024));
+  hipLaunchKernelGGL(k_encode_f32, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s, values, n,
+                     vpitch, out, pitch, groups, rows, rpb);
   return hipGetLastError();
 }
 

@@ -1,0 +1,7 @@
+set -u
+O=gpurun_out/r2f; mkdir -p $O
+timeout -k 10 120 ./scripts/ubench3 > $O/ubench3.txt 2>&1; echo "ubench rc=$?"; grep -E "mad|mul_lo|clock" $O/ubench3.txt
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest.log; [ $rc -ne 0 ] && exit 1
+timeout -k 10 300 python bench.py --no-cpu-baseline > $O/bench.json 2> $O/bench.err; echo "bench rc=$?"; python3 -c "
+import json; r=json.loads(open('$O/bench.json').read().strip().splitlines()[-1]); print('mnist64', r['value'], r['ms_per_step'], r['kernels'])
+for k,v in r['extra'].items(): print(k, v['gib_s'], v['ms_per_step'], v['update_kernel_ms'], v['encode_kernel_ms'])"

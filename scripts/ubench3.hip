@@ -53,6 +53,11 @@ VK(k_and_or, asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(u[i]) : "v"(ua), 
 VK(k_lshl_add, asm volatile("v_lshl_add_u32 %0, %0, 3, %1" : "+v"(u[i]) : "v"(ua)))
 VK(k_mulhi, asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(u[i]) : "v"(ua)))
 VK(k_mullo, asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(u[i]) : "v"(ua)))
+VK(k_mad64, {
+  unsigned long long r;
+  asm volatile("v_mad_u64_u32 %0, s[0:1], %1, %2, %3" : "=v"(r) : "v"(u[i]), "v"(ua), "v"((unsigned long long)ub) : "s0", "s1");
+  u[i] = (unsigned)r;
+})
 VK(k_add_u32, asm volatile("v_add_u32 %0, %0, %1" : "+v"(u[i]) : "v"(ua)))
 VK(k_and, asm volatile("v_and_b32 %0, %0, %1" : "+v"(u[i]) : "v"(ua)))
 VK(k_lshr, asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(u[i])))
@@ -158,6 +163,7 @@ int main() {
   run(k_lshl_add, "v_lshl_add_u32", 1);
   run(k_mulhi, "v_mul_hi_u32", 1);
   run(k_mullo, "v_mul_lo_u32", 1);
+  run(k_mad64, "v_mad_u64_u32", 1);
   run(k_add_u32, "v_add_u32", 1);
   run(k_and, "v_and_b32", 1);
   run(k_lshr, "v_lshrrev_b32", 1);
