@@ -568,11 +568,21 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
         A = ptile[tid];
         k = 1;
       }
+      if (TG <= 16) {  // few blocks: the serial chain is the critical path (select-chain Q)
 #pragma unroll 4
-      for (; k < cm; ++k) {
-        const float s = A + ptile[k * E + tid];
-        off_domain |= (uint32_t)!q_gen_ok(s);
-        A = q_lat(s);
+        for (; k < cm; ++k) {
+          const float s = A + ptile[k * E + tid];
+          off_domain |= (uint32_t)!q_gen_ok(s);
+          A = q_lat(s);
+        }
+      } else {  // many blocks: throughput (multiplier-table Q, fewer instructions)
+#pragma unroll 2
+        for (; k < cm; ++k) {
+          const float s = A + ptile[k * E + tid];
+          const uint32_t d = var_digits(s, sh.tab.var);
+          off_domain |= (uint32_t)(d == kSlowDigits);
+          A = q_mt_d(s, d, sh.tab.mt);
+        }
       }
     }
     __syncthreads();
