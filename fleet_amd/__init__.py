@@ -104,6 +104,8 @@ def lib() -> C.CDLL:
         "fleet_decode_device": (i32, [vp, vp, sz, sz, i32, vp, sz, vp]),
         "fleet_synth_device": (i32, [vp, C.c_uint64, i32, i32, vp, vp, i32, sz, vp, sz, vp]),
         "fleet_selftest_digest": (i32, [vp, i32, C.POINTER(C.c_uint64)]),
+        "fleet_descent_device": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, C.c_float, vp]),
+        "fleet_descent": (i32, [vp, vp, sz, vp, sz, vp, sz, vp, vp, i32, vp, vp, i32, C.c_float]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -425,6 +427,35 @@ class Codec:
                                                      out.ctypes.data))
         return out
 
+    # -- descentNative's model step ----------------------------
+    @staticmethod
+    def _layout_args(layout):
+        ws = np.ascontiguousarray(layout.w_sizes, dtype=np.int32)
+        wp = np.ascontiguousarray(layout.w_present(), dtype=np.uint8)
+        bs = np.ascontiguousarray(layout.b_sizes, dtype=np.int32)
+        fc = np.ascontiguousarray(layout.fc_flags(), dtype=np.uint8)
+        return ws, wp, bs, fc
+
+    def descent(self, weights, fc_bias, grad, layout, lr: float):
+        """network::descent(vector) with the sgd solver (cppNN_backend.cpp:336-352): returns the
+        updated (weights, fc_bias); `grad` = decodeFloat(merged) in the layout's gradients() order."""
+        w = np.array(weights, dtype=np.float32, copy=True).reshape(-1)
+        b = np.array(fc_bias, dtype=np.float32, copy=True).reshape(-1)
+        g = np.ascontiguousarray(grad, dtype=np.float32).reshape(-1)
+        ws, wp, bs, fc = self._layout_args(layout)
+        self._check(self._L.fleet_descent(self._h, w.ctypes.data, len(w), b.ctypes.data, len(b), g.ctypes.data,
+                                          len(g), ws.ctypes.data, wp.ctypes.data, len(ws), bs.ctypes.data,
+                                          fc.ctypes.data, len(bs), float(lr)))
+        return w, b
+
+    def descent_device(self, weights_f32, fc_bias_f32, grad_f32, layout, lr: float, stream=None):
+        """Device-resident model step: float32 CUDA tensors updated in place."""
+        ws, wp, bs, fc = self._layout_args(layout)
+        self._check(self._L.fleet_descent_device(self._h, weights_f32.data_ptr(),
+                                                 fc_bias_f32.data_ptr() if fc_bias_f32 is not None else None,
+                                                 grad_f32.data_ptr(), ws.ctypes.data, wp.ctypes.data, len(ws),
+                                                 bs.ctypes.data, fc.ctypes.data, len(bs), float(lr),
+                                                 _stream(stream)))
 
 
 class ByteVec:

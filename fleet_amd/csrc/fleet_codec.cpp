@@ -708,6 +708,118 @@ int fleet_model_read_weights(fleet_ctx* c, const char* text, size_t len, const i
   return FLEET_OK;
 }
 
+// ------------------------------------------ SGD epilogue (descentNative)
+
+namespace {
+
+// Segments of network::descent(vector)'s walk over the gradients() layout
+// (network.h:1185-1202): weight blocks of non-null W, bias blocks of the
+// fully-connected layers. Also the layout's total length and the model sizes.
+int descent_segments(fleet_ctx* c, const int32_t* w_sizes, const uint8_t* w_present, int n_w,
+                     const int32_t* b_sizes, const uint8_t* fc_layer, int n_b, size_t* n_up, size_t* n_weights,
+                     size_t* n_fc, std::vector<fleet::DescentSegs>* segs) {
+  if (n_w < 0 || n_b < 0 || (n_w && (!w_sizes || !w_present)) || (n_b && (!b_sizes || !fc_layer)))
+    return fail(c, FLEET_ERR_ARG, "bad descent layout arguments");
+  segs->clear();
+  auto add = [&](int kind, size_t g, size_t m, size_t len) {
+    if (segs->empty() || segs->back().n == fleet::kMaxDescentSegs) {
+      segs->emplace_back();
+      segs->back().n = 0;
+    }
+    fleet::DescentSegs& d = segs->back();
+    d.kind[d.n] = kind;
+    d.grad_off[d.n] = (int64_t)g;
+    d.model_off[d.n] = (int64_t)m;
+    d.len[d.n] = (int64_t)len;
+    ++d.n;
+  };
+  size_t idx = 1, wo = 0, bo = 0;
+  for (int i = 0; i < n_w; ++i) {
+    if (w_sizes[i] < 0) return fail(c, FLEET_ERR_ARG, "negative weight block size");
+    ++idx;
+    if (w_present[i] && w_sizes[i] > 0) add(0, idx, wo, (size_t)w_sizes[i]);
+    if (w_present[i]) wo += (size_t)w_sizes[i];
+    idx += (size_t)w_sizes[i];
+  }
+  ++idx;
+  for (int k = 0; k < n_b; ++k) {
+    if (b_sizes[k] < 0) return fail(c, FLEET_ERR_ARG, "negative bias block size");
+    ++idx;
+    if (fc_layer[k] && b_sizes[k] > 0) add(1, idx, bo, (size_t)b_sizes[k]);
+    if (fc_layer[k]) bo += (size_t)b_sizes[k];
+    idx += (size_t)b_sizes[k];
+  }
+  *n_up = idx;
+  *n_weights = wo;
+  *n_fc = bo;
+  return FLEET_OK;
+}
+
+}  // namespace
+
+int fleet_descent_device(fleet_ctx* c, float* d_weights, float* d_fc_bias, const float* d_grad,
+                         const int32_t* w_sizes, const uint8_t* w_present, int n_w, const int32_t* b_sizes,
+                         const uint8_t* fc_layer, int n_b, float lr, void* stream) {
+  if (!c || !d_grad) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  size_t n_up = 0, nw = 0, nf = 0;
+  std::vector<fleet::DescentSegs> segs;
+  int rc = descent_segments(c, w_sizes, w_present, n_w, b_sizes, fc_layer, n_b, &n_up, &nw, &nf, &segs);
+  if (rc) return rc;
+  if ((nw && !d_weights) || (nf && !d_fc_bias)) return FLEET_ERR_ARG;
+  for (const auto& sg : segs)
+    HIP_TRY(c, fleet::launch_descent(d_weights, d_fc_bias, d_grad, sg, lr, pick(c, stream)));
+  return FLEET_OK;
+}
+
+int fleet_descent(fleet_ctx* c, float* weights, size_t n_weights, float* fc_bias, size_t n_fc_bias,
+                  const float* grad, size_t n_grad, const int32_t* w_sizes, const uint8_t* w_present, int n_w,
+                  const int32_t* b_sizes, const uint8_t* fc_layer, int n_b, float lr) {
+  if (!c || !grad) return FLEET_ERR_ARG;
+  size_t n_up = 0, nw = 0, nf = 0;
+  std::vector<fleet::DescentSegs> segs;
+  int rc;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    rc = descent_segments(c, w_sizes, w_present, n_w, b_sizes, fc_layer, n_b, &n_up, &nw, &nf, &segs);
+  }
+  if (rc) return rc;
+  if (n_grad != n_up || n_weights != nw || n_fc_bias != nf || (nw && !weights) || (nf && !fc_bias))
+    return fail(c, FLEET_ERR_ARG, "descent: sizes do not match the layout (grad %zu/%zu, weights %zu/%zu, bias %zu/%zu)",
+                n_grad, n_up, n_weights, nw, n_fc_bias, nf);
+  // the header floats network::descent(vector) reads its block sizes from
+  size_t idx = 0;
+  bool ok = grad[idx++] == (float)n_w;
+  for (int i = 0; i < n_w && ok; ++i) {
+    ok = grad[idx++] == (float)w_sizes[i];
+    idx += (size_t)w_sizes[i];
+  }
+  ok = ok && grad[idx++] == (float)n_b;
+  for (int k = 0; k < n_b && ok; ++k) {
+    ok = grad[idx++] == (float)b_sizes[k];
+    idx += (size_t)b_sizes[k];
+  }
+  if (!ok) return fail(c, FLEET_ERR_LAYOUT, "descent: gradient header does not match the model layout");
+  DevMem dw, db, dg;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (nw) HIP_TRY(c, hipMalloc(&dw.p, nw * sizeof(float)));
+    if (nf) HIP_TRY(c, hipMalloc(&db.p, nf * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&dg.p, n_grad * sizeof(float)));
+    if (nw) HIP_TRY(c, hipMemcpyAsync(dw.p, weights, nw * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    if (nf) HIP_TRY(c, hipMemcpyAsync(db.p, fc_bias, nf * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(dg.p, grad, n_grad * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    for (const auto& sg : segs)
+      HIP_TRY(c, fleet::launch_descent((float*)dw.p, (float*)db.p, (const float*)dg.p, sg, lr, c->stream));
+    if (nw) HIP_TRY(c, hipMemcpyAsync(weights, dw.p, nw * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    if (nf) HIP_TRY(c, hipMemcpyAsync(fc_bias, db.p, nf * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
+  return FLEET_OK;
+}
+
 const char* fleet_update_kernel(size_t len) {
   return fleet::update_kernel_name((int64_t)groups_of(fleet_b64_count(len)));
 }

@@ -4,6 +4,16 @@
 #include <stdint.h>
 
 namespace fleet {
+// segments of descentNative's model step (k_descent): kind 0 = weight block,
+// 1 = fully-connected bias block; offsets in floats
+constexpr int kMaxDescentSegs = 64;
+struct DescentSegs {
+  int n;
+  int kind[kMaxDescentSegs];
+  int64_t grad_off[kMaxDescentSegs], model_off[kMaxDescentSegs], len[kMaxDescentSegs];
+};
+hipError_t launch_descent(float* weights, float* fc_bias, const float* grad, const DescentSegs& segs, float lr,
+                          hipStream_t s);
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s);

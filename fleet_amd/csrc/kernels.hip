@@ -979,6 +979,53 @@ __global__ void k_synth_headers(float* __restrict__ out, size_t vpitch, const in
   if (i < n_hdr) out[(size_t)blockIdx.y * vpitch + hpos[i]] = hval[i];
 }
 
+// ----------------------------------------------------------------------------
+// descentNative's model step: Server/src/main/c++/
+// cppNN_backend.cpp:336-352 -> network::descent(vector), commonLib/cppNN/
+// network.h:1185-1202,1334-1353. Per segment: a weight block (kind 0,
+// sgd::increment_w, solver.h:88-94: w -= lr*(dW + 0*w)) or a fully-connected
+// layer's bias block (kind 1, update_bias, layer.h:241-243: b -= db*lr), each
+// op one fp32 rounding as in the reference's SSE build (no contraction).
+// NaN results as the reference's x86 SSE build produces them (the GPU's own
+// canonical NaN is 0x7FC00000): a NaN operand propagates quieted, the
+// instruction's first operand winning; an invalid operation gives 0xFFC00000.
+__device__ __forceinline__ float x86_nan(float a, float b, float r) {
+  if (r == r) return r;
+  if (a != a) return u2f(f2u(a) | 0x00400000u);
+  if (b != b) return u2f(f2u(b) | 0x00400000u);
+  return u2f(0xFFC00000u);
+}
+
+__global__ void __launch_bounds__(256) k_descent(float* __restrict__ weights, float* __restrict__ fc_bias,
+                                                 const float* __restrict__ grad, DescentSegs segs, float lr) {
+  const int sg = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= segs.len[sg]) return;
+  const float g = grad[segs.grad_off[sg] + i];
+  if (segs.kind[sg] == 0) {
+    float* w = weights + segs.model_off[sg] + i;
+    const float x = *w;
+    const float t = x86_nan(0.0f, x, 0.0f * x);  // w_decay * w
+    const float u = x86_nan(t, g, t + g);        // dW + t (the product is the x86 first operand)
+    const float v = x86_nan(lr, u, lr * u);
+    *w = x86_nan(x, v, x - v);
+  } else {
+    float* b = fc_bias + segs.model_off[sg] + i;
+    const float v = x86_nan(g, lr, g * lr);
+    *b = x86_nan(*b, v, *b - v);
+  }
+}
+
+hipError_t launch_descent(float* weights, float* fc_bias, const float* grad, const DescentSegs& segs, float lr,
+                          hipStream_t s) {
+  int64_t mx = 0;
+  for (int k = 0; k < segs.n; ++k) mx = std::max(mx, segs.len[k]);
+  if (segs.n == 0 || mx == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_descent, dim3((unsigned)((mx + 255) / 256), (unsigned)segs.n), dim3(256), 0, s, weights,
+                     fc_bias, grad, segs, lr);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- launchers
 
 static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }

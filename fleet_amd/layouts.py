@@ -23,6 +23,25 @@ class Layout:
     name: str
     w_sizes: Tuple[int, ...]
     b_sizes: Tuple[int, ...]
+    # layers whose update_bias is not the base no-op (fully_connected_layer,
+    # commonLib/cppNN/layer.h:241-243): the biases descentNative updates
+    fc_layers: Tuple[int, ...] = ()
+
+    def w_present(self):
+        """W slot non-null (a weight block of size 0 is a layer-graph edge without
+        weights, e.g. into a pooling layer)."""
+        return tuple(s > 0 for s in self.w_sizes)
+
+    def fc_flags(self):
+        return tuple(k in self.fc_layers for k in range(len(self.b_sizes)))
+
+    @property
+    def n_weights(self) -> int:
+        return sum(self.w_sizes)
+
+    @property
+    def n_fc_bias(self) -> int:
+        return sum(self.b_sizes[k] for k in self.fc_layers)
 
     @property
     def n_up(self) -> int:
@@ -57,9 +76,11 @@ def synthetic(n_up: int) -> Layout:
     return Layout(f"synthetic{n_up}", (n_up - 3,), ())
 
 
-MNIST = Layout("mnist", (200, 0, 128, 19200, 0, 1920), (784, 0, 512, 0, 0, 192, 10))
-CIFAR10 = Layout("cifar10", (432, 0, 9216, 0, 221184, 73728, 1920), (3072, 0, 3136, 0, 576, 384, 192, 10))
-CIFAR100 = Layout("cifar100", (432, 0, 9216, 0, 221184, 73728, 19200), (3072, 0, 3136, 0, 576, 384, 192, 100))
+MNIST = Layout("mnist", (200, 0, 128, 19200, 0, 1920), (784, 0, 512, 0, 0, 192, 10), (6,))
+CIFAR10 = Layout("cifar10", (432, 0, 9216, 0, 221184, 73728, 1920), (3072, 0, 3136, 0, 576, 384, 192, 10),
+                 (5, 6, 7))
+CIFAR100 = Layout("cifar100", (432, 0, 9216, 0, 221184, 73728, 19200), (3072, 0, 3136, 0, 576, 384, 192, 100),
+                  (5, 6, 7))
 
 LAYOUTS = {
     "mnist": MNIST,

@@ -186,6 +186,30 @@ int fleet_model_weights_text(fleet_ctx* ctx, const float* weights, const int32_t
 int fleet_model_read_weights(fleet_ctx* ctx, const char* text, size_t len, const int32_t* dims, int n_mats,
                              float* weights_out);
 
+/* descentNative's model step -------------------------------
+ * Server/src/main/c++/cppNN_backend.cpp:336-352: network::descent(vector)
+ * (commonLib/cppNN/network.h:1185-1202) walks the gradients() layout of the
+ * merged gradient -- w_sizes[n_w] weight blocks, b_sizes[n_b] bias blocks -- and
+ * descent() (:1334-1353) applies
+ *   sgd::increment_w (solver.h:88-94):  w -= lr*(dW + 0*w)   per weight block i
+ *                                         with w_present[i] (W[i] non-null)
+ *   update_bias (layer.h:241-243):       b -= db*lr           per layer k with
+ *                                         fc_layer[k] (fully_connected_layer)
+ * in fp32, one rounding per operation. `weights` = the non-null W concatenated in
+ * slot order (the model codec's layout); `fc_bias` = the fully-connected layers'
+ * biases concatenated in layer order; `grad` = decodeFloat(merged) (fleet_update's
+ * merged_f32), n_up floats. lr = (float)lrates_vec[currEpoch].
+ * Device-resident (layout arrays on the host; the header values inside d_grad
+ * are not re-read: fleet_update already checked them against the layout). */
+int fleet_descent_device(fleet_ctx* ctx, float* d_weights, float* d_fc_bias, const float* d_grad,
+                         const int32_t* w_sizes, const uint8_t* w_present, int n_w, const int32_t* b_sizes,
+                         const uint8_t* fc_layer, int n_b, float lr, void* stream);
+/* Host buffers, updated in place; checks the header floats of grad against the
+ * layout as network::descent(vector) would read them (FLEET_ERR_LAYOUT). */
+int fleet_descent(fleet_ctx* ctx, float* weights, size_t n_weights, float* fc_bias, size_t n_fc_bias,
+                  const float* grad, size_t n_grad, const int32_t* w_sizes, const uint8_t* w_present, int n_w,
+                  const int32_t* b_sizes, const uint8_t* fc_layer, int n_b, float lr);
+
 /* Name of the aggregation kernel fleet_update / fleet_update_device launch for
  * an upload of `len` Base64 bytes (or a group window of that many bytes):
  * "k_update<K>", "k_update_tiled<TG>" or "k_update_pipe<TG>" (profiling aid). */

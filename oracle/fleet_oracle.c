@@ -611,3 +611,79 @@ bad:
   free(s);
   return -1;
 }
+
+/* --------------------------------------------------- SGD epilogue (f1) */
+
+/* descentNative's model step (Server/src/main/c++/cppNN_backend.cpp:336-352):
+ * network::descent(vector) (commonLib/cppNN/network.h:1185-1202) reads the
+ * dW / dbias blocks of the gradients() layout from g -- sizes are (int) of
+ * the decoded header floats -- then descent() (:1334-1353) applies, per
+ * weight slot i with a non-empty block and a non-null W[i] (w_present[i]),
+ * sgd::increment_w (solver.h:88-94):
+ *     w[s] -= lr * (dW[s] + 0.0f * w[s])          (fp32, one rounding per op)
+ * and, per layer k that is a fully_connected_layer (fc_layer[k]),
+ * update_bias (layer.h:241-243):
+ *     b[j] -= db[j] * lr
+ * Other layers' update_bias is the base no-op (layer.h:108). `weights` holds
+ * the non-null W concatenated in slot order; `fc_bias` the FC layers' biases
+ * in layer order. Returns 0, or -1 when g's header does not fit the model. */
+/* x86 SSE NaN results (Intel SDM vol. 1, 4.8.3.5), restated so they do not
+ * depend on how this file's compiler orders commutative operands: r = a OP b
+ * with a the instruction's first (destination) operand as the reference's
+ * -O0 build emits it -- a NaN operand propagates quieted, the first one
+ * winning; an invalid operation on non-NaN operands gives the default NaN
+ * 0xFFC00000. The operand orders below were read off the reference build
+ * (tests/golden/descent_mnist.npz case 2). */
+static float x86_nan(float a, float b, float r) {
+  union { float f; uint32_t u; } x;
+  if (r == r) return r;
+  if (a != a) { x.f = a; x.u |= 0x00400000u; return x.f; }
+  if (b != b) { x.f = b; x.u |= 0x00400000u; return x.f; }
+  x.u = 0xFFC00000u;
+  return x.f;
+}
+
+int fo_descent(float* weights, size_t n_weights, float* fc_bias, size_t n_fc_bias, const float* g, size_t n_g,
+               const uint8_t* w_present, int n_w_slots, const uint8_t* fc_layer, int n_layers, float lr) {
+  size_t idx = 0, wo = 0, bo = 0;
+  if (n_g < 1) return -1;
+  const int nw = (int)g[idx++];
+  if (nw != n_w_slots) return -1;
+  for (int i = 0; i < nw; ++i) {
+    if (idx >= n_g) return -1;
+    const int size = (int)g[idx++];
+    if (size < 0 || idx + (size_t)size > n_g) return -1;
+    if (w_present[i] && size > 0) {
+      if (wo + (size_t)size > n_weights) return -1;
+      for (int s = 0; s < size; ++s) {
+        float* w = &weights[wo + (size_t)s];
+        const float x = *w, d = g[idx + (size_t)s];
+        const float t = x86_nan(0.0f, x, 0.0f * x); /* w_decay * w */
+        const float u = x86_nan(t, d, t + d);       /* dW + t: the product is the first operand */
+        const float v = x86_nan(lr, u, lr * u);
+        *w = x86_nan(x, v, x - v);
+      }
+    }
+    if (w_present[i]) wo += (size_t)size;
+    idx += (size_t)size;
+  }
+  if (idx >= n_g) return -1;
+  const int nb = (int)g[idx++];
+  if (nb != n_layers) return -1;
+  for (int k = 0; k < nb; ++k) {
+    if (idx >= n_g) return -1;
+    const int size = (int)g[idx++];
+    if (size < 0 || idx + (size_t)size > n_g) return -1;
+    if (fc_layer[k]) {
+      if (bo + (size_t)size > n_fc_bias) return -1;
+      for (int j = 0; j < size; ++j) {
+        const float d = g[idx + (size_t)j], b = fc_bias[bo + (size_t)j];
+        const float v = x86_nan(d, lr, d * lr);
+        fc_bias[bo + (size_t)j] = x86_nan(b, v, b - v);
+      }
+      bo += (size_t)size;
+    }
+    idx += (size_t)size;
+  }
+  return 0;
+}

@@ -87,6 +87,11 @@ size_t fo_weights_section(const float* w, const int32_t* dims, int n_mats, char*
 /* network::read's DISTILLATION_MODE=1 weights branch (network.h:958-997). */
 int fo_read_weights_section(const char* text, size_t len, const int32_t* dims, int n_mats, float* w_out);
 
+/* ---- SGD epilogue: descentNative's model step ---- */
+/* cppNN_backend.cpp:336-352 -> network.h:1185-1202,1334-1353 -> solver.h:88-94, layer.h:241-243 */
+int fo_descent(float* weights, size_t n_weights, float* fc_bias, size_t n_fc_bias, const float* g, size_t n_g,
+               const uint8_t* w_present, int n_w_slots, const uint8_t* fc_layer, int n_layers, float lr);
+
 #ifdef __cplusplus
 }
 #endif

@@ -111,6 +111,9 @@ class Oracle:
         L.fo_weights_section.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, sz]
         L.fo_read_weights_section.restype = C.c_int
         L.fo_read_weights_section.argtypes = [C.c_void_p, sz, C.c_void_p, C.c_int, C.c_void_p]
+        L.fo_descent.restype = C.c_int
+        L.fo_descent.argtypes = [C.c_void_p, sz, C.c_void_p, sz, C.c_void_p, sz, C.c_void_p, C.c_int, C.c_void_p,
+                                 C.c_int, C.c_float]
 
     # -- scalars / vectors ------------------------------------------------
     def float2int(self, x: np.ndarray) -> np.ndarray:
@@ -258,6 +261,19 @@ class Oracle:
             raise ValueError("malformed weights section")
         return out
 
+    def descent(self, weights, fc_bias, g, w_present, fc_layer, lr):
+        """descentNative's model step (fo_descent): returns the updated (weights, fc_bias)."""
+        w = np.array(weights, dtype=np.float32, copy=True)
+        b = np.array(fc_bias, dtype=np.float32, copy=True)
+        g = np.ascontiguousarray(g, dtype=np.float32)
+        wp = np.ascontiguousarray(w_present, dtype=np.uint8)
+        fl = np.ascontiguousarray(fc_layer, dtype=np.uint8)
+        rc = self.lib.fo_descent(w.ctypes.data, len(w), b.ctypes.data, len(b), g.ctypes.data, len(g), wp.ctypes.data,
+                                 len(wp), fl.ctypes.data, len(fl), float(lr))
+        if rc != 0:
+            raise ValueError("gradient header does not fit the model")
+        return w, b
+
     def philox(self, ctr, key):
         c = np.ascontiguousarray(ctr, dtype=np.uint32)
         k = np.ascontiguousarray(key, dtype=np.uint32)
@@ -384,6 +400,8 @@ class ReferenceModel:
         L.ref_mnist_roundtrip.restype = sz
         L.ref_mnist_roundtrip.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                           C.c_void_p, C.c_void_p, sz]
+        L.ref_mnist_descent.restype = C.c_int
+        L.ref_mnist_descent.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float] + [C.c_void_p] * 9
 
     def quantize_params(self, w, dims):
         """(quantised weights, getParams text) of a network whose W are the given matrices."""
@@ -413,3 +431,30 @@ class ReferenceModel:
         self.lib.ref_mnist_roundtrip(None if win is None else win.ctypes.data, C.byref(nm), None, w0.ctypes.data,
                                      wq.ctypes.data, wr.ctypes.data, buf.ctypes.data, n_text)
         return [tuple(int(v) for v in d) for d in dims], w0, wq, buf.tobytes(), wr
+
+    def mnist_descent(self, g=None, lr=0.01, w_in=None, b_in=None):
+        """descentNative's model step on the Driver's MNIST network (ref_mnist_descent):
+        dict with the gradients() layout (w_sizes, b_sizes), per layer the FC flag and
+        bias length (0 without use_bias()), the non-null W and the use_bias() biases
+        (concatenated in layer order) before (w0, b0) and after (w1, b1)."""
+        nw, nb = C.c_int(0), C.c_int(0)
+        ws, bs, fc = np.zeros(64, np.int32), np.zeros(64, np.int32), np.zeros(64, np.int32)
+        w0 = np.empty(1 << 16, np.float32)
+        b0 = np.empty(1 << 16, np.float32)
+        nl = self.lib.ref_mnist_descent(None, None, None, 0, 0.0, C.byref(nw), ws.ctypes.data, C.byref(nb),
+                                        bs.ctypes.data, w0.ctypes.data, b0.ctypes.data, None, None, fc.ctypes.data)
+        out = {"w_sizes": ws[: nw.value].copy(), "b_sizes": bs[: nb.value].copy(), "fc": fc[:nl] & 1,
+               "bias_len": fc[:nl] >> 1}
+        if g is None:
+            return out
+        g = np.ascontiguousarray(g, dtype=np.float32)
+        win = None if w_in is None else np.ascontiguousarray(w_in, dtype=np.float32)
+        bin_ = None if b_in is None else np.ascontiguousarray(b_in, dtype=np.float32)
+        w1 = np.empty_like(w0)
+        b1 = np.empty_like(b0)
+        self.lib.ref_mnist_descent(None if win is None else win.ctypes.data,
+                                   None if bin_ is None else bin_.ctypes.data, g.ctypes.data, len(g), float(lr),
+                                   None, None, None, None, w0.ctypes.data, b0.ctypes.data, w1.ctypes.data,
+                                   b1.ctypes.data, None)
+        out.update(w0=w0, b0=b0, w1=w1, b1=b1)
+        return out

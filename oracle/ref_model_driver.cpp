@@ -124,4 +124,69 @@ size_t ref_mnist_roundtrip(const float* w_in, int* n_mats, int* dims_out, float*
   return copy_out(params, text, cap);
 }
 
+// descentNative's model step on the Driver's MNIST network
+// (Server/src/main/c++/cppNN_backend.cpp:336-352: set_learning_rate, then
+// network::descent(vector), network.h:1185-1202 -> :1334-1353 -> sgd
+// solver.h:88-94 and fully_connected_layer::update_bias layer.h:241-243).
+// One train_class on a blank image first sizes dW_sets/dbias_sets, as
+// initUpdater does (:216-222). w_in (nullable) overwrites the non-null W in
+// order; b_in (nullable) the biases of every layer with use_bias(), in layer
+// order. Outputs (nullable): the gradients() layout sizes (w_sizes[n_w],
+// b_sizes[n_b]), the W and biases before (w0, b0) and after (w1, b1) the
+// step, and per layer fc[k] = (is a fully_connected_layer) | (bias size if
+// use_bias(), else 0) << 1.
+// g = the merged gradient (decodeFloat of mergeFlatGradient's output).
+int ref_mnist_descent(const float* w_in, const float* b_in, const float* g, int n_g, float lr, int* n_w,
+                      int* w_sizes, int* n_b, int* b_sizes, float* w0, float* b0, float* w1, float* b1, int* fc) {
+  mojo::network cnn("sgd");
+  cnn.push_back("I1", "input 28 28 1");
+  cnn.push_back("C1", "convolution 5 8 1 elu");
+  cnn.push_back("P1", "semi_stochastic_pool 3 3");
+  cnn.push_back("C2i", "convolution 1 16 1 elu");
+  cnn.push_back("C2", "convolution 5 48 1 elu");
+  cnn.push_back("P2", "semi_stochastic_pool 2 2");
+  cnn.push_back("FC2", "softmax 10");
+  cnn.connect_all();
+  cnn.start_epoch("cross_entropy");
+  std::vector<float> blank(28 * 28, 0.0f);
+  cnn.train_class(blank.data(), 3, NULL);
+  auto& layers = cnn.layer_sets[mojo::network::MAIN_LAYER_SET];
+  auto copy_w = [&](float* dst, const float* src) {
+    size_t o = 0;
+    for (auto* m : cnn.W)
+      if (m) {
+        if (src) std::memcpy(m->x, src + o, sizeof(float) * m->size());
+        if (dst) std::memcpy(dst + o, m->x, sizeof(float) * m->size());
+        o += m->size();
+      }
+  };
+  auto copy_b = [&](float* dst, const float* src) {
+    size_t o = 0;
+    for (auto* l : layers)
+      if (l->use_bias()) {
+        if (src) std::memcpy(l->bias.x, src + o, sizeof(float) * l->bias.size());
+        if (dst) std::memcpy(dst + o, l->bias.x, sizeof(float) * l->bias.size());
+        o += l->bias.size();
+      }
+  };
+  copy_w(w0, w_in);
+  copy_b(b0, b_in);
+  if (n_w) *n_w = (int)cnn.dW_sets[0].size();
+  if (w_sizes)
+    for (size_t i = 0; i < cnn.dW_sets[0].size(); ++i) w_sizes[i] = cnn.dW_sets[0][i].size();
+  if (n_b) *n_b = (int)cnn.dbias_sets[0].size();
+  if (b_sizes)
+    for (size_t i = 0; i < cnn.dbias_sets[0].size(); ++i) b_sizes[i] = cnn.dbias_sets[0][i].size();
+  if (fc)
+    for (size_t k = 0; k < layers.size(); ++k)
+      fc[k] = (dynamic_cast<mojo::fully_connected_layer*>(layers[k]) != NULL) |
+              ((layers[k]->use_bias() ? (int)layers[k]->bias.size() : 0) << 1);
+  if (!g) return (int)layers.size();
+  cnn.set_learning_rate(lr);
+  cnn.descent(std::vector<float>(g, g + n_g));
+  copy_w(w1, NULL);
+  copy_b(b1, NULL);
+  return (int)layers.size();
+}
+
 }  // extern "C"

@@ -367,3 +367,49 @@ def test_model_codec_large_random(codec, oracle):
     assert sec == oracle.weights_section(owq, dims)
     wr = codec.model_read_weights(sec, dims)
     assert np.array_equal(wr.view(np.uint32), oracle.read_weights_section(sec, dims).view(np.uint32))
+
+
+# ---- descentNative's model step --------------------------------------------
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_descent_matches_reference_fixture(codec, case):
+    """sgd increment_w + FC update_bias on the GPU vs the reference's own
+    network::descent (MNIST network, fixture from oracle/_ref), bitwise."""
+    import os
+    from test_oracle_golden import GOLDEN, descent_case
+    f = np.load(os.path.join(GOLDEN, "descent_mnist.npz"))
+    lay, w0, b0, g, lr, w1, b1 = descent_case(f, case)
+    w, b = codec.descent(w0, b0, g, lay, lr)
+    assert np.array_equal(w.view(np.uint32), w1.view(np.uint32))
+    assert np.array_equal(b.view(np.uint32), b1.view(np.uint32))
+
+
+def test_descent_device_after_update(codec, oracle):
+    """The device-resident server step: fused update -> merged_f32 stays in HBM ->
+    descent on the resident CIFAR-10 model, vs the oracle (update chain + fo_descent)."""
+    torch = pytest.importorskip("torch")
+    lay = CIFAR10
+    M = 4
+    ups = uploads_for(oracle, lay, M, seed=31)
+    d = policy("inverse", M)
+    merged, g = codec.update(ups, d, want_f32=True)
+    rng = np.random.default_rng(3)
+    w0 = rng.normal(0, 0.05, lay.n_weights).astype(np.float32)
+    b0 = rng.normal(0, 0.1, lay.n_fc_bias).astype(np.float32)
+    lr = np.float32(0.0123)
+    ew, eb = oracle.descent(w0, b0, oracle.decode_floats(merged), lay.w_present(), lay.fc_flags(), lr)
+    tw, tb, tg = (torch.from_numpy(x).cuda() for x in (w0, b0, g))
+    codec.descent_device(tw, tb, tg, lay, lr)
+    torch.cuda.synchronize()
+    assert np.array_equal(tw.cpu().numpy().view(np.uint32), ew.view(np.uint32))
+    assert np.array_equal(tb.cpu().numpy().view(np.uint32), eb.view(np.uint32))
+
+
+def test_descent_rejects_mismatched_header(codec):
+    g = np.zeros(MNIST.n_up, np.float32)
+    g[MNIST.header_positions()] = MNIST.header_values()
+    g[MNIST.header_positions()[3]] += 1  # one weight block size off
+    with pytest.raises(F.LayoutError):
+        codec.descent(np.zeros(MNIST.n_weights, np.float32), np.zeros(MNIST.n_fc_bias, np.float32), g, MNIST, 0.1)
+    with pytest.raises(F.FleetError):
+        codec.descent(np.zeros(5, np.float32), np.zeros(MNIST.n_fc_bias, np.float32), g, MNIST, 0.1)

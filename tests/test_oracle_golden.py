@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _text(a, n=None):
@@ -172,3 +173,72 @@ def test_live_reference_model_codec(oracle):
     wq = oracle.quantize(w, dims)
     assert np.array_equal(wq.view(np.uint32), wq_ref.view(np.uint32))
     assert text == b"mojo01\n0\n0\n0\n" + oracle.weights_section(wq, dims)
+
+
+# ---- descentNative's model step ------------------------------------------
+
+def _fc_slices(f):
+    """(start, len) of each fully-connected layer's bias inside the fixture's
+    use_bias() bias vector (layer order)."""
+    out, o = [], 0
+    for k, n in enumerate(f["bias_len"]):
+        if f["fc"][k]:
+            out.append((o, int(n)))
+        o += int(n)
+    return out
+
+
+def descent_case(f, case):
+    from fleet_amd.layouts import MNIST
+    assert tuple(f["w_sizes"]) == MNIST.w_sizes and tuple(f["b_sizes"]) == MNIST.b_sizes
+    assert tuple(np.flatnonzero(f["fc"])) == MNIST.fc_layers
+    sl = _fc_slices(f)
+    fc0 = np.concatenate([f[f"b0_{case}"][o:o + n] for o, n in sl])
+    fc1 = np.concatenate([f[f"b1_{case}"][o:o + n] for o, n in sl])
+    lr = f["lr"][0] if case == 0 else f[f"lr{case}"][0]
+    return MNIST, f[f"w0_{case}"], fc0, f[f"g{case}"], lr, f[f"w1_{case}"], fc1
+
+
+@pytest.mark.parametrize("case", [0, 1, 2])
+def test_oracle_descent_matches_reference(oracle, case):
+    """fo_descent (sgd increment_w + FC update_bias) vs the reference's own
+    network::descent on the MNIST network (fixture from oracle/_ref), bitwise,
+    including inf/NaN/-0/denormal weights and biases."""
+    f = np.load(os.path.join(GOLDEN, "descent_mnist.npz"))
+    lay, w0, b0, g, lr, w1, b1 = descent_case(f, case)
+    w, b = oracle.descent(w0, b0, g, lay.w_present(), lay.fc_flags(), lr)
+    assert np.array_equal(w.view(np.uint32), w1.view(np.uint32))
+    assert np.array_equal(b.view(np.uint32), b1.view(np.uint32))
+    # the other layers' biases (conv) never change (base update_bias is a no-op)
+    fcset = {o for o, _ in _fc_slices(f)}
+    o = 0
+    for k, n in enumerate(f["bias_len"]):
+        if n and o not in fcset:
+            assert np.array_equal(f[f"b0_{case}"][o:o + n].view(np.uint32), f[f"b1_{case}"][o:o + n].view(np.uint32))
+        o += int(n)
+
+
+def test_live_reference_descent(oracle):
+    """Random weights/biases/gradients through the live reference build."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libfleetref_model.so")):
+        pytest.skip("reference model build not available")
+    import pyoracle
+    from fleet_amd.layouts import MNIST
+    refm = pyoracle.ReferenceModel()
+    info = refm.mnist_descent()
+    nw, nb = int(sum(info["w_sizes"])), int(sum(info["bias_len"]))
+    rng = np.random.default_rng(9)
+    for t in range(3):
+        g = (rng.normal(0, 10.0 ** rng.integers(-6, 3), MNIST.n_up)).astype(np.float32)
+        g[MNIST.header_positions()] = MNIST.header_values()
+        w_in = rng.normal(0, 0.1, nw).astype(np.float32)
+        b_in = rng.normal(0, 0.1, nb).astype(np.float32)
+        lr = np.float32(rng.uniform(1e-4, 1.0))
+        r = refm.mnist_descent(g, lr, w_in, b_in)
+        f = {"bias_len": info["bias_len"], "fc": info["fc"]}
+        sl = _fc_slices(f)
+        fc0 = np.concatenate([b_in[o:o + n] for o, n in sl])
+        fc1 = np.concatenate([r["b1"][:nb][o:o + n] for o, n in sl])
+        w, b = oracle.descent(w_in, fc0, g, MNIST.w_present(), MNIST.fc_flags(), lr)
+        assert np.array_equal(w.view(np.uint32), r["w1"][:nw].view(np.uint32))
+        assert np.array_equal(b.view(np.uint32), fc1.view(np.uint32))
