@@ -1,0 +1,61 @@
+"""Host-side mirror of CppNNUpdater (fleet_amd/updater.py): getDampen policies,
+label similarity, and (GPU) a full M-softsync update + model step vs the oracle."""
+import math
+
+import numpy as np
+import pytest
+
+from fleet_amd.updater import FleetUpdater, get_dampen, similarity
+
+
+def test_get_dampen_policies():
+    # CppNNUpdater.java:300-327
+    assert get_dampen(0, 5) == 1.0
+    assert get_dampen(1, 0) == 1.0 and get_dampen(1, 2) == 1 / 3
+    assert get_dampen(2, 9, similarity=0.5, stale_size=4, has_outlier=True) == (1 / 10) / 0.5
+    assert get_dampen(2, 9, similarity=0.01, stale_size=4, has_outlier=True) == (1 / 10) / 0.1
+    assert get_dampen(2, 6, similarity=0.5, stale_size=4, has_outlier=True) == 1 / 7  # tau <= 1.5*staleSize
+    assert get_dampen(3, 7, stale_size=4, alpha=0.3) == math.exp(-0.3 * 4)
+    assert get_dampen(4, 9, similarity=0.25, stale_size=4, alpha=0.3, has_outlier=True) == math.exp(-0.3 * 4) / 0.25
+    assert math.isnan(get_dampen(2, 9, similarity=float("nan"), stale_size=4, has_outlier=True))
+
+
+def test_similarity():
+    assert similarity([1, 1], [2, 2]) == pytest.approx(1.0)
+    assert similarity([1, 0], [0, 1]) == 0.0
+    assert math.isnan(similarity([1, 2], [0, 0]))  # Java 0.0/0 -> NaN
+
+
+def test_staleness_simulation_not_rebuilt():
+    with pytest.raises(NotImplementedError):
+        FleetUpdater(None, None, 2, [0.1], [], [], stale_size=3)
+
+
+@pytest.mark.gpu
+def test_updater_two_rounds_vs_oracle(codec, oracle):
+    """Two M-softsync rounds (M=3, inverse dampening, stale epochs) through the
+    device path == the oracle's faithful per-op chain + fo_descent."""
+    from fleet_amd.layouts import MNIST
+    lay = MNIST
+    rng = np.random.default_rng(12)
+    w0 = rng.normal(0, 0.05, lay.n_weights).astype(np.float32)
+    b0 = rng.normal(0, 0.1, lay.n_fc_bias).astype(np.float32)
+    lrates = [0.05 / (1 + i) ** 0.3 for i in range(10)]
+    up = FleetUpdater(codec, lay, 3, lrates, w0, b0, policy=1)
+    ew, eb = w0.copy(), b0.copy()
+    epochs = [0, 0, 0, 1, 0, 1]
+    for r in range(2):
+        ups, damp = [], []
+        for k in range(3):
+            i = 3 * r + k
+            u = oracle.encode_floats(oracle.synth_upload(40 + i, i, list(lay.w_sizes), list(lay.b_sizes)))
+            out = up.update(u, [1] * 10, epochs[i], i)
+            assert (out is None) == (k < 2)
+            ups.append(u)
+            damp.append(1 / float(r - epochs[i] + 1))
+        merged = oracle.update_faithful(ups, damp)
+        assert out == merged
+        ew, eb = oracle.descent(ew, eb, oracle.decode_floats(merged), lay.w_present(), lay.fc_flags(),
+                                np.float32(lrates[r]))
+        assert np.array_equal(up.weights.view(np.uint32), ew.view(np.uint32))
+        assert np.array_equal(up.fc_bias.view(np.uint32), eb.view(np.uint32))
