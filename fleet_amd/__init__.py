@@ -106,6 +106,8 @@ def lib() -> C.CDLL:
         "fleet_selftest_digest": (i32, [vp, i32, C.POINTER(C.c_uint64)]),
         "fleet_descent_device": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, C.c_float, vp]),
         "fleet_descent": (i32, [vp, vp, sz, vp, sz, vp, sz, vp, vp, i32, vp, vp, i32, C.c_float]),
+        "fleet_model_params": (i32, [vp, vp, sz, vp, sz, i32, vp, sz, szp]),
+        "fleet_model_params_device": (i32, [vp, vp, sz, vp, sz, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -426,6 +428,15 @@ class Codec:
         self._check(self._L.fleet_model_read_weights(self._h, t, len(t), d.ctypes.data, len(d) // 3,
                                                      out.ctypes.data))
         return out
+
+    def getModelParametersNative(self, weights, biases, graph_edges: int) -> bytes:  # noqa: N802  (java:148)
+        """Base64 of network::getModelParams (cppNN_backend.cpp:227-242): the use_bias() biases repeated
+        graph_edges (= layer_graph.size()) times, then the non-null W."""
+        w = np.ascontiguousarray(weights, dtype=np.float32).reshape(-1)
+        b = np.ascontiguousarray(biases, dtype=np.float32).reshape(-1)
+        n = len(b) * int(graph_edges) + len(w)
+        return self._text_call(self._L.fleet_model_params, (w.ctypes.data, len(w), b.ctypes.data, len(b),
+                                                            int(graph_edges)), b64_len(n))
 
     # -- descentNative's model step (SURVEY.md §8 f1) ----------------------------
     @staticmethod

@@ -708,6 +708,45 @@ int fleet_model_read_weights(fleet_ctx* c, const char* text, size_t len, const i
   return FLEET_OK;
 }
 
+// ------------------------------------------ model parameters (getModelParametersNative)
+
+int fleet_model_params_device(fleet_ctx* c, const float* d_weights, size_t n_weights, const float* d_biases,
+                              size_t n_biases, int graph_edges, void* d_out, void* stream) {
+  if (!c || !d_out || graph_edges < 0 || (n_weights && !d_weights) || (n_biases && graph_edges && !d_biases))
+    return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, fleet::launch_encode_model_params(d_weights, (int64_t)n_weights, d_biases, (int64_t)n_biases,
+                                               n_biases ? (int64_t)graph_edges : 0, (uint8_t*)d_out,
+                                               pick(c, stream)));
+  return FLEET_OK;
+}
+
+int fleet_model_params(fleet_ctx* c, const float* weights, size_t n_weights, const float* biases, size_t n_biases,
+                       int graph_edges, char* out, size_t cap, size_t* out_len) {
+  if (!c || graph_edges < 0 || (n_weights && !weights) || (n_biases && !biases)) return FLEET_ERR_ARG;
+  const size_t n = n_biases * (size_t)graph_edges + n_weights;
+  const size_t len = fleet_b64_len(n);
+  if (out_len) *out_len = len;
+  if (cap < len || !out) return fail(c, FLEET_ERR_CAPACITY, "output capacity %zu < %zu", cap, len);
+  DevMem dw, db, dt;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    HIP_TRY(c, hipSetDevice(c->device));
+    if (n_weights) HIP_TRY(c, hipMalloc(&dw.p, n_weights * sizeof(float)));
+    if (n_biases) HIP_TRY(c, hipMalloc(&db.p, n_biases * sizeof(float)));
+    HIP_TRY(c, hipMalloc(&dt.p, 16 * groups_of(n) + 16));
+    if (n_weights) HIP_TRY(c, hipMemcpyAsync(dw.p, weights, n_weights * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    if (n_biases) HIP_TRY(c, hipMemcpyAsync(db.p, biases, n_biases * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, fleet::launch_encode_model_params((const float*)dw.p, (int64_t)n_weights, (const float*)db.p,
+                                                 (int64_t)n_biases, n_biases ? (int64_t)graph_edges : 0,
+                                                 (uint8_t*)dt.p, c->stream));
+    if (len) HIP_TRY(c, hipMemcpyAsync(out, dt.p, len, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
+  return FLEET_OK;
+}
+
 // ------------------------------------------ SGD epilogue (descentNative)
 
 namespace {

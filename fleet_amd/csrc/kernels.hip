@@ -775,6 +775,40 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
   }
 }
 
+// getModelParametersNative (Server/src/main/c++/cppNN_backend.cpp:227-242):
+// Base64::encode of network::getModelParams (commonLib/cppNN/network.h:708-723)
+// = the use_bias() biases repeated `reps` times (the bias loop sits inside the
+// loop over layer_graph) followed by the non-null W -- encoded straight from
+// the resident model, without materialising the vector.
+__global__ void __launch_bounds__(256) k_encode_model_params(const float* __restrict__ weights, int64_t n_w,
+                                                             const float* __restrict__ biases, int64_t n_b,
+                                                             int64_t reps, uint8_t* __restrict__ out,
+                                                             int64_t groups) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= groups) return;
+  const int64_t nbr = n_b * reps, n = nbr + n_w;
+  const int r = (int)min<int64_t>(3, n - 3 * g);
+  float x[3];
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    const int64_t v = 3 * g + e;
+    x[e] = e >= r ? 0.0f : v < nbr ? biases[v % n_b] : weights[v - nbr];
+  }
+  *reinterpret_cast<uint4*>(out + 16 * g) = encode_group(x, r, &tab);
+}
+
+hipError_t launch_encode_model_params(const float* weights, int64_t n_w, const float* biases, int64_t n_b, int64_t reps,
+                                      uint8_t* out, hipStream_t s) {
+  const int64_t groups = (n_b * reps + n_w + 2) / 3;
+  if (groups == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_encode_model_params, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, weights, n_w, biases,
+                     n_b, reps, out, groups);
+  return hipGetLastError();
+}
+
 // int32 codes -> Base64 (Base64::encode(vector<int>))
 __global__ void __launch_bounds__(256) k_encode_i32(const int32_t* __restrict__ codes_in, int64_t n,
                                                     uint8_t* __restrict__ out, int64_t groups) {

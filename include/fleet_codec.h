@@ -186,6 +186,17 @@ int fleet_model_weights_text(fleet_ctx* ctx, const float* weights, const int32_t
 int fleet_model_read_weights(fleet_ctx* ctx, const char* text, size_t len, const int32_t* dims, int n_mats,
                              float* weights_out);
 
+/* getModelParametersNative (Server/src/main/c++/cppNN_backend.cpp:227-242, SURVEY.md
+ * §8 a20): Base64::encode of network::getModelParams (commonLib/cppNN/network.h:
+ * 708-723) = the biases of every use_bias() layer (layer order) repeated
+ * graph_edges = layer_graph.size() times -- the bias loop sits inside the loop
+ * over layer_graph -- then the non-null W. Output: fleet_b64_len(n_biases *
+ * graph_edges + n_weights) bytes. */
+int fleet_model_params_device(fleet_ctx* ctx, const float* d_weights, size_t n_weights, const float* d_biases,
+                              size_t n_biases, int graph_edges, void* d_out, void* stream);
+int fleet_model_params(fleet_ctx* ctx, const float* weights, size_t n_weights, const float* biases, size_t n_biases,
+                       int graph_edges, char* out, size_t cap, size_t* out_len);
+
 /* descentNative's model step -------------------------------
  * Server/src/main/c++/cppNN_backend.cpp:336-352: network::descent(vector)
  * (commonLib/cppNN/network.h:1185-1202) walks the gradients() layout of the

@@ -400,6 +400,8 @@ class ReferenceModel:
         L.ref_mnist_roundtrip.restype = sz
         L.ref_mnist_roundtrip.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                           C.c_void_p, C.c_void_p, sz]
+        L.ref_mnist_model_params.restype = C.c_int
+        L.ref_mnist_model_params.argtypes = [C.c_void_p] * 4
         L.ref_mnist_descent.restype = C.c_int
         L.ref_mnist_descent.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float] + [C.c_void_p] * 9
 
@@ -458,3 +460,14 @@ class ReferenceModel:
                                    b1.ctypes.data, None)
         out.update(w0=w0, b0=b0, w1=w1, b1=b1)
         return out
+
+    def mnist_model_params(self, w_in=None, b_in=None):
+        """network::getModelParams of the MNIST network: (vector, layer_graph.size())."""
+        e = C.c_int(0)
+        n = self.lib.ref_mnist_model_params(None, None, None, C.byref(e))
+        out = np.empty(n, np.float32)
+        win = None if w_in is None else np.ascontiguousarray(w_in, dtype=np.float32)
+        bin_ = None if b_in is None else np.ascontiguousarray(b_in, dtype=np.float32)
+        self.lib.ref_mnist_model_params(None if win is None else win.ctypes.data,
+                                        None if bin_ is None else bin_.ctypes.data, out.ctypes.data, C.byref(e))
+        return out, e.value

@@ -189,4 +189,38 @@ int ref_mnist_descent(const float* w_in, const float* b_in, const float* g, int 
   return (int)layers.size();
 }
 
+// getModelParametersNative's vector (Server/src/main/c++/cppNN_backend.cpp:
+// 227-242 -> network::getModelParams, commonLib/cppNN/network.h:708-723) of the
+// Driver's MNIST network, optionally with its W / use_bias() biases overwritten
+// (w_in, b_in as in ref_mnist_descent). Returns the vector length; out nullable.
+// (The bias loop sits inside a loop over layer_graph, so the biases repeat
+// layer_graph.size() times before the weights.)
+int ref_mnist_model_params(const float* w_in, const float* b_in, float* out, int* graph_edges) {
+  mojo::network cnn("sgd");
+  cnn.push_back("I1", "input 28 28 1");
+  cnn.push_back("C1", "convolution 5 8 1 elu");
+  cnn.push_back("P1", "semi_stochastic_pool 3 3");
+  cnn.push_back("C2i", "convolution 1 16 1 elu");
+  cnn.push_back("C2", "convolution 5 48 1 elu");
+  cnn.push_back("P2", "semi_stochastic_pool 2 2");
+  cnn.push_back("FC2", "softmax 10");
+  cnn.connect_all();
+  size_t o = 0;
+  for (auto* m : cnn.W)
+    if (m) {
+      if (w_in) std::memcpy(m->x, w_in + o, sizeof(float) * m->size());
+      o += m->size();
+    }
+  o = 0;
+  for (auto* l : cnn.layer_sets[mojo::network::MAIN_LAYER_SET])
+    if (l->use_bias()) {
+      if (b_in) std::memcpy(l->bias.x, b_in + o, sizeof(float) * l->bias.size());
+      o += l->bias.size();
+    }
+  const std::vector<float> v = cnn.getModelParams();
+  if (out) std::memcpy(out, v.data(), sizeof(float) * v.size());
+  if (graph_edges) *graph_edges = (int)cnn.layer_graph.size();
+  return (int)v.size();
+}
+
 }  // extern "C"

@@ -413,3 +413,21 @@ def test_descent_rejects_mismatched_header(codec):
         codec.descent(np.zeros(MNIST.n_weights, np.float32), np.zeros(MNIST.n_fc_bias, np.float32), g, MNIST, 0.1)
     with pytest.raises(F.FleetError):
         codec.descent(np.zeros(5, np.float32), np.zeros(MNIST.n_fc_bias, np.float32), g, MNIST, 0.1)
+
+
+def test_model_params_matches_reference_fixture(codec):
+    """getModelParametersNative (a20) on the GPU: bytes of the reference's own
+    getModelParams + Base64::encode (fixture)."""
+    import os
+    from test_oracle_golden import GOLDEN
+    f = np.load(os.path.join(GOLDEN, "model_params_mnist.npz"))
+    assert codec.getModelParametersNative(f["w"], f["b"], int(f["graph_edges"][0])) == f["text"].tobytes()
+    # ragged lengths and large magnitudes (group boundaries inside the bias repeats)
+    rng = np.random.default_rng(1)
+    for nb, e, nw in ((7, 3, 11), (1, 1, 0), (0, 5, 4), (10, 6, 1000)):
+        b = (rng.normal(0, 1, nb) * 10.0 ** rng.integers(-8, 9, nb)).astype(np.float32)
+        w = (rng.normal(0, 1, nw) * 10.0 ** rng.integers(-8, 9, nw)).astype(np.float32)
+        from conftest import ROOT  # noqa: F401
+        import pyoracle
+        exp = pyoracle.Oracle().encode_floats(np.concatenate([np.tile(b, e), w]).astype(np.float32))
+        assert codec.getModelParametersNative(w, b, e) == exp, (nb, e, nw)

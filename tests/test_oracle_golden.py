@@ -242,3 +242,13 @@ def test_live_reference_descent(oracle):
         w, b = oracle.descent(w_in, fc0, g, MNIST.w_present(), MNIST.fc_flags(), lr)
         assert np.array_equal(w.view(np.uint32), r["w1"][:nw].view(np.uint32))
         assert np.array_equal(b.view(np.uint32), fc1.view(np.uint32))
+
+
+def test_model_params_fixture_pins_layout(oracle):
+    """getModelParams (a20): the reference's vector = biases x layer_graph.size(), then W
+    (fixture from oracle/_ref)."""
+    f = np.load(os.path.join(GOLDEN, "model_params_mnist.npz"))
+    e = int(f["graph_edges"][0])
+    exp = np.concatenate([np.tile(f["b"], e), f["w"]])
+    assert np.array_equal(exp.view(np.uint32), f["params"].view(np.uint32))
+    assert oracle.encode_floats(f["params"]) == f["text"].tobytes()
