@@ -392,9 +392,9 @@ FLEET_HDC MulEntry mul_entry(uint32_t d) {  // d = numDigits; d > 9 (slow marker
 }
 
 // Digit table entry i = (sign << 8) | biased exponent of x: byte 0 = d for
-// |x| < thr, byte 1 = d for |x| >= thr; d = 15 marks values outside the q_gen
+// |x| >= thr, byte 1 = d for |x| < thr; d = 15 marks values outside the q_gen
 // domain (-1e8 < x < 1e9), NaN and inf (callers send those through the
-// general codec). The byte is stored pre-multiplied for the MulEntry index.
+// general codec).
 struct alignas(8) VarEntry {
   float thr;
   uint32_t info;
@@ -409,13 +409,19 @@ FLEET_HDC VarEntry var_entry(uint32_t i) {
   uint32_t dlo = t.base + neg, dhi = t.base + 1u + neg;  // '-' counts (Base64.cpp:73-82)
   dlo = dlo > 9u ? kSlowDigits : dlo;
   dhi = dhi > 9u ? kSlowDigits : dhi;
-  return VarEntry{t.thr, dlo | (dhi << 8)};
+  return VarEntry{t.thr, dhi | (dlo << 8)};
 }
 
-// numDigits((int)x) on the q_gen domain, kSlowDigits outside it
+// numDigits((int)x) on the q_gen domain, kSlowDigits outside it. `ab` = the bits
+// of |x|: |x| < thr compares as integers (both non-negative), and the byte
+// shift comes from the sign of the difference -- no float compare, no select.
+FLEET_HD uint32_t var_digits_ab(uint32_t bits, uint32_t ab, const VarEntry* vt) {
+  const VarEntry v = vt[bits >> 23];
+  const uint32_t sh = ((ab - f2u(v.thr)) >> 28) & 8u;  // 8 when |x| < thr
+  return (v.info >> sh) & 0xffu;
+}
 FLEET_HD uint32_t var_digits(float x, const VarEntry* vt) {
-  const VarEntry v = vt[f2u(x) >> 23];
-  return (v.info >> (__builtin_fabsf(x) >= v.thr ? 8u : 0u)) & 0xffu;
+  return var_digits_ab(f2u(x), f2u(x) & 0x7fffffffu, vt);
 }
 
 FLEET_HD float mul10_mt(float X, const MulEntry& e) {

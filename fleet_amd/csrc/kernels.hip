@@ -131,24 +131,35 @@ __device__ __forceinline__ void resolve_slow(float (&out)[S], const uint32_t (&i
 template <int S>
 __device__ __forceinline__ void q_stage(float (&out)[S], const float (&x)[S], const B64Tables* tab,
                                         uint32_t* __restrict__ ws, int lane) {
-  bool all_fast = true;
+  // integer magnitude tests (an f32 compare with |.| is a 6-cycle e64 op):
+  // the whole wave is in |x| < 1 iff the largest |x| bit pattern is
+  uint32_t ab[S], amax = 0;
 #pragma unroll
-  for (int i = 0; i < S; ++i) all_fast &= q_ok(x[i]);
-  if (__ballot(!all_fast) == 0) {
+  for (int i = 0; i < S; ++i) {
+    ab[i] = f2u(x[i]) & 0x7fffffffu;
+    amax = max(amax, ab[i]);
+  }
+  if (__ballot(amax >= 0x3f800000u) == 0) {
 #pragma unroll
     for (int i = 0; i < S; ++i) out[i] = q_fast1(x[i]);
     return;
   }
-  uint32_t slow = 0;
-  uint32_t in[S];
+  uint32_t d[S], dmax = 0;
 #pragma unroll
   for (int i = 0; i < S; ++i) {
-    const uint32_t d = var_digits(x[i], tab->var);
-    slow |= (uint32_t)(d == kSlowDigits) << i;
-    out[i] = q_mt_d(x[i], d, tab->mt);
-    in[i] = f2u(x[i]);
+    d[i] = var_digits_ab(f2u(x[i]), ab[i], tab->var);
+    dmax = max(dmax, d[i]);
+    out[i] = q_mt_d(x[i], d[i], tab->mt);
   }
-  resolve_slow<S, 1>(out, in, slow, ws, lane);
+  if (__ballot(dmax > 9u) != 0) {  // values outside the q_gen domain (rare)
+    uint32_t slow = 0, in[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      slow |= (uint32_t)(d[i] == kSlowDigits) << i;
+      in[i] = f2u(x[i]);
+    }
+    resolve_slow<S, 1>(out, in, slow, ws, lane);
+  }
 }
 
 // out[i] = int2float(codes[i]) (Base64.cpp:116-139): fixed 9-step chains when
@@ -156,15 +167,14 @@ __device__ __forceinline__ void q_stage(float (&out)[S], const float (&x)[S], co
 // the last digit. Total: no fallback needed.
 template <int S>
 __device__ __forceinline__ void dec_stage(float (&out)[S], const int32_t (&codes)[S], const B64Tables* tab) {
-  uint32_t r[S];
-  bool any = false;
+  uint32_t r[S], rmax = 0;
 #pragma unroll
   for (int i = 0; i < S; ++i) {
     const uint32_t a = codes[i] < 0 ? 0u - (uint32_t)codes[i] : (uint32_t)codes[i];
     r[i] = last_digit_u(a);
-    any |= r[i] != 0u;
+    rmax = max(rmax, r[i]);
   }
-  if (__ballot(any) == 0) {
+  if (__ballot(rmax != 0u) == 0) {
 #pragma unroll
     for (int i = 0; i < S; ++i) out[i] = dec_fast(codes[i]);
   } else {
