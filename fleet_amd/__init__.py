@@ -26,7 +26,8 @@ from .layouts import LAYOUTS, Layout  # noqa: F401
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
-LIB_PATH = os.path.join(PKG, "libfleetcodec.so")
+# FLEET_CODEC_LIB: load another build of the same C-ABI (A/B experiments on one box)
+LIB_PATH = os.environ.get("FLEET_CODEC_LIB") or os.path.join(PKG, "libfleetcodec.so")
 HEADER_PATH = os.path.join(ROOT, "include", "fleet_codec.h")
 
 FLEET_OK = 0

@@ -236,8 +236,6 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
   constexpr int S = 3 * K;
   __shared__ B64Tables tab;
   __shared__ uint32_t scratch[4][64 * S];
-  b64_tables_init(&tab);
-  __syncthreads();
   const int lane = threadIdx.x & 63;
   uint32_t* ws = scratch[threadIdx.x >> 6];
 
@@ -281,6 +279,9 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
   uint4 nxt[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) nxt[k] = *reinterpret_cast<const uint4*>(rowp[k]);
+  // tables copied while the first client's groups are in flight
+  b64_tables_init(&tab);
+  __syncthreads();
   for (int c = 0; c < M; ++c) {
     uint4 cur[K];
 #pragma unroll
@@ -648,20 +649,21 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   const int ng = (int)min<int64_t>(TG, g_end - g0);
   if (tid < NPW) prog[tid] = 0;
   if (tid == 0) consumed = 0;
+  const int npass = (M + CPP - 1) / CPP;
+  // producers: the first pass's groups in flight while the tables are copied
+  const int w = wave - 1;
+  const int step = WP ? NPW : 1;
+  const int it0 = WP ? lane : tid - 64, stride = WP ? 64 : NPW * 64;
+  int pass = WP ? w : 0;
+  TileItems<TG, IPT> nxt;  // the next pass's groups, loaded one pass ahead
+  if (wave > 0 && pass < npass)
+    tile_load<TG, IPT>(nxt, uploads, pitch, g0, ng, pass * CPP, min(CPP, M - pass * CPP) * TG, it0, stride);
   tile_init(sh, hdr_block + 4, hdr_block[1], g0, ng);
   FLEET_TSTAMP(1);
-  const int npass = (M + CPP - 1) / CPP;
   uint32_t badacc = 0;
 
   if (wave > 0) {  // ---------------------------------------------- producers
-    const int w = wave - 1;
-    const int step = WP ? NPW : 1;
-    const int it0 = WP ? lane : tid - 64, stride = WP ? 64 : NPW * 64;
     int done = 0;
-    int pass = WP ? w : 0;
-    TileItems<TG, IPT> nxt;  // the next pass's groups, loaded one pass ahead
-    if (pass < npass) tile_load<TG, IPT>(nxt, uploads, pitch, g0, ng, pass * CPP, min(CPP, M - pass * CPP) * TG, it0,
-                                         stride);
     for (; pass < npass; pass += step) {
       const TileItems<TG, IPT> cur = nxt;
       const int np = pass + step;
@@ -1184,9 +1186,11 @@ hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int 
                              hipStream_t s) {
   int64_t groups = (n + 2) / 3;
   if (groups == 0 || rows == 0) return hipSuccess;
-  // rows per block: about 1,024 blocks in all (4 per CU), at least one row each
+  // rows per block: whole columns when the groups alone give >= 4 blocks per CU
+  // (fewest table copies); otherwise about 4,096 blocks in all. Measured
+  // (A/B on one box): 1M x 256 prefers whole columns, CIFAR/MNIST x 64-256 the split.
   const int64_t gx = blocks_for(groups, 256);
-  const int rpb = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 1023) / 1024));
+  const int rpb = gx >= 1024 ? rows : (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 4095) / 4096));
   hipLaunchKernelGGL(k_encode_f32, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s, values, n,
                      vpitch, out, pitch, groups, rows, rpb);
   return hipGetLastError();
