@@ -162,6 +162,32 @@ __device__ __forceinline__ void q_stage(float (&out)[S], const float (&x)[S], co
   }
 }
 
+// q_stage without the in-stage fallback: values outside the q_gen domain leave
+// their lane's results undefined and raise `dmax` above 9; the caller then
+// recomputes that lane's whole chain with the general codec (chain_general).
+// One max per value instead of the compaction machinery in every stage.
+template <int S>
+__device__ __forceinline__ void q_stage_off(float (&out)[S], const float (&x)[S], const B64Tables* tab,
+                                            uint32_t& dmax) {
+  uint32_t ab[S], amax = 0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    ab[i] = f2u(x[i]) & 0x7fffffffu;
+    amax = max(amax, ab[i]);
+  }
+  if (__ballot(amax >= 0x3f800000u) == 0) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) out[i] = q_fast1(x[i]);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const uint32_t d = var_digits_ab(f2u(x[i]), ab[i], tab->var);
+    dmax = max(dmax, d);
+    out[i] = q_mt_d(x[i], d, tab->mt);
+  }
+}
+
 // out[i] = int2float(codes[i]) (Base64.cpp:116-139): fixed 9-step chains when
 // every code of the wave ends in 0 (|value| < 1), else step multipliers from
 // the last digit. Total: no fallback needed.
@@ -214,6 +240,23 @@ __device__ __forceinline__ int32_t merged_code(float A, double inv, int32_t last
   return enc(q(r));
 }
 
+// The exact chain of one value recomputed from global memory with the general
+// codec: the fallback when the serial accumulation leaves the q_lat domain
+// (|A| >= 1e8; never for gradients). Per lane, divergent, slow, exact.
+__device__ __noinline__ float chain_general(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                            const double* __restrict__ dampen, int64_t g, int e,
+                                            const B64Tables* tab) {
+  float A = 0.f;
+  for (int c = 0; c < M; ++c) {
+    int32_t cc[3];
+    b64_decode_group(*reinterpret_cast<const uint4*>(uploads + (size_t)c * pitch + 16 * g), tab, cc);
+    const float y = q(dec(cc[e]));
+    const float p = q((float)((double)y * dampen[c]));
+    A = c == 0 ? p : q(A + p);
+  }
+  return A;
+}
+
 // ----------------------------------------------------------------------------
 // Fused update: CppNNUpdater.update's aggregation (java:420-509) for the
 // groups [g_begin, g_end). Per value and client c, in CppNNUpdater order:
@@ -235,9 +278,7 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
                                                 int* __restrict__ err) {
   constexpr int S = 3 * K;
   __shared__ B64Tables tab;
-  __shared__ uint32_t scratch[4][64 * S];
   const int lane = threadIdx.x & 63;
-  uint32_t* ws = scratch[threadIdx.x >> 6];
 
   // hdr_block = {status, n_headers, walk_end, 0, positions...} (k_layout_parse / host-built);
   // slots at or after walk_end are outside network::flatGrad's walk and, like
@@ -259,6 +300,7 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
   float acc[S];
   int32_t codes[S];
   uint32_t bad[K], need[K];
+  uint32_t dmax = 0;  // largest digit count seen (> 9: left the q_gen domain)
 #pragma unroll
   for (int k = 0; k < K; ++k) need[k] = needed_chars_mask((int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g[k])));
   // layout consistency (every upload carries the last one's header codes) is
@@ -312,14 +354,14 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
     // stage A: y = Q(int2float(code))
     float y0[S], y[S];
     dec_stage<S>(y0, codes, &tab);
-    q_stage<S>(y, y0, &tab, ws, lane);
+    q_stage_off<S>(y, y0, &tab, dmax);
 
     // stage B: p = Q((float)((double)y * d))
     const double d = dampen[c];
     float r[S], p[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) r[i] = (float)((double)y[i] * d);
-    q_stage<S>(p, r, &tab, ws, lane);
+    q_stage_off<S>(p, r, &tab, dmax);
 
     // stage C: A = Q(A + p)
     if (c == 0) {
@@ -329,7 +371,17 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
       float sm[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) sm[i] = acc[i] + p[i];
-      q_stage<S>(acc, sm, &tab, ws, lane);
+      q_stage_off<S>(acc, sm, &tab, dmax);
+    }
+  }
+  // a value left the q_gen domain somewhere in this lane's chains (|x| >= 1e8,
+  // inf, NaN -- never for gradients): recompute the lane's values exactly
+  if (__ballot(dmax > 9u) != 0) {
+    if (dmax > 9u) {
+#pragma unroll
+      for (int k = 0; k < K; ++k)
+        if (live[k])
+          for (int e = 0; e < 3; ++e) acc[3 * k + e] = chain_general(uploads, pitch, M, dampen, g[k], e, &tab);
     }
   }
 
@@ -352,23 +404,6 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
       for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec_mt(out[e], tab.mt);
     }
   }
-}
-
-// The exact chain of one value recomputed from global memory with the general
-// codec: the fallback when the serial accumulation leaves the q_lat domain
-// (|A| >= 1e8; never for gradients). Per lane, divergent, slow, exact.
-__device__ __noinline__ float chain_general(const uint8_t* __restrict__ uploads, size_t pitch, int M,
-                                            const double* __restrict__ dampen, int64_t g, int e,
-                                            const B64Tables* tab) {
-  float A = 0.f;
-  for (int c = 0; c < M; ++c) {
-    int32_t cc[3];
-    b64_decode_group(*reinterpret_cast<const uint4*>(uploads + (size_t)c * pitch + 16 * g), tab, cc);
-    const float y = q(dec(cc[e]));
-    const float p = q((float)((double)y * dampen[c]));
-    A = c == 0 ? p : q(A + p);
-  }
-  return A;
 }
 
 // Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
