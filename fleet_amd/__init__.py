@@ -108,6 +108,7 @@ def lib() -> C.CDLL:
         "fleet_descent_device": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, C.c_float, vp]),
         "fleet_descent": (i32, [vp, vp, sz, vp, sz, vp, sz, vp, vp, i32, vp, vp, i32, C.c_float]),
         "fleet_model_params": (i32, [vp, vp, sz, vp, sz, i32, vp, sz, szp]),
+        "fleet_model_version": (i32, [vp, vp, vp, i32, vp, sz, vp, vp]),
         "fleet_model_params_device": (i32, [vp, vp, sz, vp, sz, i32, vp, vp]),
     }
     for name, (res, args) in sig.items():
@@ -429,6 +430,17 @@ class Codec:
         self._check(self._L.fleet_model_read_weights(self._h, t, len(t), d.ctypes.data, len(d) // 3,
                                                      out.ctypes.data))
         return out
+
+    def model_version(self, weights, dims, biases):
+        """descentNative's mode-1 model copy: read(getParams()) of the unquantised model
+        (weights via the first-occurrence dictionary, %g/strtof round trips)."""
+        w, d, n = self._model_args(weights, dims)
+        b = np.ascontiguousarray(biases, dtype=np.float32).reshape(-1)
+        wo = np.empty(n, np.float32)
+        bo = np.empty(len(b), np.float32)
+        self._check(self._L.fleet_model_version(self._h, w.ctypes.data, d.ctypes.data, len(d) // 3, b.ctypes.data,
+                                                len(b), wo.ctypes.data, bo.ctypes.data))
+        return wo, bo
 
     def getModelParametersNative(self, weights, biases, graph_edges: int) -> bytes:  # noqa: N802  (java:148)
         """Base64 of network::getModelParams (cppNN_backend.cpp:227-242): the use_bias() biases repeated

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -856,6 +857,54 @@ int fleet_descent(fleet_ctx* c, float* weights, size_t n_weights, float* fc_bias
     if (nf) HIP_TRY(c, hipMemcpyAsync(fc_bias, db.p, nf * sizeof(float), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(c, hipStreamSynchronize(c->stream));
   }
+  return FLEET_OK;
+}
+
+// descentNative's model copy in DISTILLATION_MODE=1 (cppNN_backend.cpp:355-372):
+// cnnNew->read(cnn.getParams()) of the unquantised model. getParams prints the
+// biases and the first-occurrence dictionary values with `ostream << float`
+// (precision 6 = %g) and read() parses them back (strtof); every weight takes
+// its dictionary entry's value. Dictionary on the device (sort-based, no
+// O(n*U) scans); the U dictionary values and the biases are formatted and
+// parsed on the host (the same libc as the reference).
+int fleet_model_version(fleet_ctx* c, const float* weights, const int32_t* dims, int n_mats, const float* biases,
+                        size_t n_biases, float* weights_out, float* biases_out) {
+  if (!c || (n_biases && (!biases || !biases_out))) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  size_t n = 0;
+  int rc = model_total(c, dims, n_mats, &n);
+  if (rc) return rc;
+  if (n && (!weights || !weights_out)) return FLEET_ERR_ARG;
+  auto g6 = [](float v) {
+    char buf[48];
+    snprintf(buf, sizeof buf, "%g", (double)v);
+    return strtof(buf, nullptr);
+  };
+  for (size_t k = 0; k < n_biases; ++k) {
+    if (!std::isfinite(biases[k])) return fail(c, FLEET_ERR_ARG, "non-finite bias: the reference's text read fails");
+    biases_out[k] = g6(biases[k]);
+  }
+  if (!n) return FLEET_OK;
+  DevMem dw, dd, di, dv;
+  HIP_TRY(c, hipMalloc(&dw.p, n * sizeof(float)));
+  HIP_TRY(c, hipMalloc(&dd.p, n * sizeof(float)));
+  HIP_TRY(c, hipMalloc(&di.p, n * sizeof(int32_t)));
+  HIP_TRY(c, hipMemcpyAsync(dw.p, weights, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  int32_t U = 0;
+  HIP_TRY(c, fleet::model_quantize_index((const float*)dw.p, dims, n_mats, nullptr, (float*)dd.p, (int32_t*)di.p,
+                                         &U, c->stream, false));
+  std::vector<float> dict((size_t)U);
+  if (U) HIP_TRY(c, hipMemcpy(dict.data(), dd.p, (size_t)U * sizeof(float), hipMemcpyDeviceToHost));
+  for (float& v : dict) {
+    if (!std::isfinite(v)) return fail(c, FLEET_ERR_ARG, "non-finite weight: the reference's text read fails");
+    v = g6(v);
+  }
+  HIP_TRY(c, hipMalloc(&dv.p, ((size_t)U + 1) * sizeof(float)));
+  if (U) HIP_TRY(c, hipMemcpyAsync(dv.p, dict.data(), (size_t)U * sizeof(float), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, fleet::model_dict_gather((const int32_t*)di.p, (int64_t)n, (const float*)dv.p, (float*)dw.p, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(weights_out, dw.p, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
   return FLEET_OK;
 }
 

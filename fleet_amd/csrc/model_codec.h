@@ -10,8 +10,11 @@ namespace fleet {
 // quantization_weight_model + dictionary + selected-index set on the device.
 // d_w: n weights (n = sum of cols*rows*chans over h_dims); outputs d_wq[n],
 // d_dict[n] (first *h_U entries used), d_index[n] (nullable). Synchronous.
+// quantize = false: the dictionary of d_w itself (d_wq unused).
 hipError_t model_quantize_index(const float* d_w, const int32_t* h_dims, int n_mats, float* d_wq, float* d_dict,
-                                int32_t* d_index, int32_t* h_U, hipStream_t s);
+                                int32_t* d_index, int32_t* h_U, hipStream_t s, bool quantize = true);
+// w[i] = vals[index[i]] (0.0f for index -1)
+hipError_t model_dict_gather(const int32_t* d_index, int64_t n, const float* d_vals, float* d_w, hipStream_t s);
 // the index lines of getParams' mode-1 section, formatted on the device
 hipError_t model_index_text(const int32_t* d_index, const int32_t* h_dims, int n_mats, std::vector<char>* out,
                             hipStream_t s);

@@ -343,7 +343,7 @@ struct DevBuf {
 }  // namespace
 
 hipError_t model_quantize_index(const float* d_w, const int32_t* h_dims, int n_mats, float* d_wq, float* d_dict,
-                                int32_t* d_index, int32_t* h_U, hipStream_t s) {
+                                int32_t* d_index, int32_t* h_U, hipStream_t s, bool quantize) {
   std::vector<int64_t> off(n_mats + 1, 0);
   for (int j = 0; j < n_mats; ++j) off[j + 1] = off[j] + (int64_t)h_dims[3 * j] * h_dims[3 * j + 1] * h_dims[3 * j + 2];
   const int64_t n = off[n_mats];
@@ -357,9 +357,13 @@ hipError_t model_quantize_index(const float* d_w, const int32_t* h_dims, int n_m
   MC_TRY(d_prm.alloc(n_mats));
   MC_TRY(hipMemcpyAsync(d_off.p, off.data(), sizeof(int64_t) * (n_mats + 1), hipMemcpyHostToDevice, s));
   MC_TRY(hipMemcpyAsync(d_dims.p, h_dims, sizeof(int32_t) * 3 * n_mats, hipMemcpyHostToDevice, s));
-  hipLaunchKernelGGL(k_mm_minmax, dim3(n_mats), dim3(256), 0, s, d_w, d_off.p, d_dims.p, d_prm.p);
-  hipLaunchKernelGGL(k_mm_quantize, dim3(nb(n)), dim3(256), 0, s, d_w, n, d_off.p, n_mats, d_prm.p, d_wq);
-  MC_TRY(hipGetLastError());
+  if (quantize) {
+    hipLaunchKernelGGL(k_mm_minmax, dim3(n_mats), dim3(256), 0, s, d_w, d_off.p, d_dims.p, d_prm.p);
+    hipLaunchKernelGGL(k_mm_quantize, dim3(nb(n)), dim3(256), 0, s, d_w, n, d_off.p, n_mats, d_prm.p, d_wq);
+    MC_TRY(hipGetLastError());
+  } else {  // the dictionary of the weights as they are (descentNative's model copy)
+    d_wq = const_cast<float*>(d_w);
+  }
 
   // dictionary over the quantised weights
   DevBuf<uint32_t> key, key2;
@@ -410,6 +414,21 @@ hipError_t model_quantize_index(const float* d_w, const int32_t* h_dims, int n_m
   MC_TRY(hipStreamSynchronize(s));
   *h_U = last_rank + last_flag;
   return hipSuccess;
+}
+
+// w[i] = vals[index[i]] (index -1, a non-finite weight: 0.0f, std::map::operator[])
+__global__ void __launch_bounds__(256) k_dict_gather(const int32_t* __restrict__ index, int64_t n,
+                                                     const float* __restrict__ vals, float* __restrict__ w) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int32_t k = index[i];
+  w[i] = k >= 0 ? vals[k] : 0.0f;
+}
+
+hipError_t model_dict_gather(const int32_t* d_index, int64_t n, const float* d_vals, float* d_w, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_dict_gather, dim3(nb(n)), dim3(256), 0, s, d_index, n, d_vals, d_w);
+  return hipGetLastError();
 }
 
 hipError_t model_index_text(const int32_t* d_index, const int32_t* h_dims, int n_mats, std::vector<char>* out,

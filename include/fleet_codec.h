@@ -186,6 +186,16 @@ int fleet_model_weights_text(fleet_ctx* ctx, const float* weights, const int32_t
 int fleet_model_read_weights(fleet_ctx* ctx, const char* text, size_t len, const int32_t* dims, int n_mats,
                              float* weights_out);
 
+/* descentNative's DISTILLATION_MODE=1 model copy (Server/src/main/c++/
+ * cppNN_backend.cpp:355-372: cnnNew->read(cnn.getParams()) of the unquantised
+ * model, network.h:611-706 + 956-997): every weight becomes the %g/strtof
+ * round trip of its first-occurrence dictionary entry (|a-b| < 1e-8f), every
+ * bias the round trip of itself. The O(n*U) dictionary scans of the reference
+ * become a device sort. Non-finite weights or biases: FLEET_ERR_ARG (the
+ * reference's text parse fails on "nan"/"inf"). */
+int fleet_model_version(fleet_ctx* ctx, const float* weights, const int32_t* dims, int n_mats, const float* biases,
+                        size_t n_biases, float* weights_out, float* biases_out);
+
 /* getModelParametersNative (Server/src/main/c++/cppNN_backend.cpp:227-242, SURVEY.md
  * §8 a20): Base64::encode of network::getModelParams (commonLib/cppNN/network.h:
  * 708-723) = the biases of every use_bias() layer (layer order) repeated

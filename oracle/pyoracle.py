@@ -400,6 +400,8 @@ class ReferenceModel:
         L.ref_mnist_roundtrip.restype = sz
         L.ref_mnist_roundtrip.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                           C.c_void_p, C.c_void_p, sz]
+        L.ref_mnist_version_copy.restype = None
+        L.ref_mnist_version_copy.argtypes = [C.c_void_p] * 4
         L.ref_mnist_model_params.restype = C.c_int
         L.ref_mnist_model_params.argtypes = [C.c_void_p] * 4
         L.ref_mnist_descent.restype = C.c_int
@@ -471,3 +473,11 @@ class ReferenceModel:
         self.lib.ref_mnist_model_params(None if win is None else win.ctypes.data,
                                         None if bin_ is None else bin_.ctypes.data, out.ctypes.data, C.byref(e))
         return out, e.value
+
+    def mnist_version_copy(self, w_in, b_in):
+        """descentNative's mode-1 model copy: read(getParams()) of the MNIST network."""
+        w = np.ascontiguousarray(w_in, dtype=np.float32)
+        b = np.ascontiguousarray(b_in, dtype=np.float32)
+        wo, bo = np.empty_like(w), np.empty_like(b)
+        self.lib.ref_mnist_version_copy(w.ctypes.data, b.ctypes.data, wo.ctypes.data, bo.ctypes.data)
+        return wo, bo

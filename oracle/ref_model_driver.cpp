@@ -223,4 +223,45 @@ int ref_mnist_model_params(const float* w_in, const float* b_in, float* out, int
   return (int)v.size();
 }
 
+// descentNative's model copy (Server/src/main/c++/cppNN_backend.cpp:355-372):
+// a fresh network reads the MNIST network's getParams() text (unquantised, mode 1).
+void ref_mnist_version_copy(const float* w_in, const float* b_in, float* w_out, float* b_out) {
+  mojo::network cnn("sgd");
+  cnn.push_back("I1", "input 28 28 1");
+  cnn.push_back("C1", "convolution 5 8 1 elu");
+  cnn.push_back("P1", "semi_stochastic_pool 3 3");
+  cnn.push_back("C2i", "convolution 1 16 1 elu");
+  cnn.push_back("C2", "convolution 5 48 1 elu");
+  cnn.push_back("P2", "semi_stochastic_pool 2 2");
+  cnn.push_back("FC2", "softmax 10");
+  cnn.connect_all();
+  size_t o = 0;
+  for (auto* m : cnn.W)
+    if (m) {
+      if (w_in) std::memcpy(m->x, w_in + o, sizeof(float) * m->size());
+      o += m->size();
+    }
+  o = 0;
+  for (auto* l : cnn.layer_sets[mojo::network::MAIN_LAYER_SET])
+    if (l->use_bias()) {
+      if (b_in) std::memcpy(l->bias.x, b_in + o, sizeof(float) * l->bias.size());
+      o += l->bias.size();
+    }
+  mojo::network cnew("sgd");
+  std::istringstream ss(cnn.getParams());
+  cnew.read(ss);
+  o = 0;
+  for (auto* m : cnew.W)
+    if (m) {
+      std::memcpy(w_out + o, m->x, sizeof(float) * m->size());
+      o += m->size();
+    }
+  o = 0;
+  for (auto* l : cnew.layer_sets[mojo::network::MAIN_LAYER_SET])
+    if (l->use_bias()) {
+      std::memcpy(b_out + o, l->bias.x, sizeof(float) * l->bias.size());
+      o += l->bias.size();
+    }
+}
+
 }  // extern "C"

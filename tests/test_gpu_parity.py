@@ -431,3 +431,15 @@ def test_model_params_matches_reference_fixture(codec):
         import pyoracle
         exp = pyoracle.Oracle().encode_floats(np.concatenate([np.tile(b, e), w]).astype(np.float32))
         assert codec.getModelParametersNative(w, b, e) == exp, (nb, e, nw)
+
+
+def test_model_version_matches_reference_fixture(codec):
+    """descentNative's mode-1 model copy on the device dictionary == the
+    reference's read(getParams()) (fixture), bitwise."""
+    import os
+    from test_oracle_golden import GOLDEN
+    f = np.load(os.path.join(GOLDEN, "version_mnist.npz"))
+    dims = [tuple(int(v) for v in d) for d in f["dims"]]
+    w, b = codec.model_version(f["w"], dims, f["b"])
+    assert np.array_equal(w.view(np.uint32), f["w_out"].view(np.uint32))
+    assert np.array_equal(b.view(np.uint32), f["b_out"].view(np.uint32))

@@ -252,3 +252,24 @@ def test_model_params_fixture_pins_layout(oracle):
     exp = np.concatenate([np.tile(f["b"], e), f["w"]])
     assert np.array_equal(exp.view(np.uint32), f["params"].view(np.uint32))
     assert oracle.encode_floats(f["params"]) == f["text"].tobytes()
+
+
+def _g6_strtof(v):
+    """`ostream << float` (precision 6, %g) then strtof, through the C library."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    libc.strtof.restype = ctypes.c_float
+    libc.strtof.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    return np.array([libc.strtof(("%g" % float(x)).encode(), None) for x in v], np.float32)
+
+
+def test_oracle_model_version_matches_reference(oracle):
+    """descentNative's mode-1 model copy read(getParams()) (fixture from the
+    reference's own network): first-occurrence dictionary of the unquantised
+    weights + %g/strtof of the dictionary values and the biases."""
+    f = np.load(os.path.join(GOLDEN, "version_mnist.npz"))
+    d, idx = oracle.dictionary(f["w"])
+    vals = _g6_strtof(d)
+    w = np.where(idx >= 0, vals[np.maximum(idx, 0)], np.float32(0)).astype(np.float32)
+    assert np.array_equal(w.view(np.uint32), f["w_out"].view(np.uint32))
+    assert np.array_equal(_g6_strtof(f["b"]).view(np.uint32), f["b_out"].view(np.uint32))
