@@ -73,6 +73,29 @@ __device__ __forceinline__ void b64_tables_init(B64Tables* t) {
   }
 }
 
+// One-lookup latency Q entries (codec_math.h q_xl) for the serial consumer.
+struct XlTable {
+  XlEntry x[2 * kXlSpan];
+};
+static_assert(sizeof(XlTable) % 16 == 0, "copied as uint4");
+FLEET_HDC XlTable make_xl_table() {
+  XlTable t{};
+  for (uint32_t i = 0; i < 2 * kXlSpan; ++i) t.x[i] = xl_entry(i);
+  return t;
+}
+static __constant__ XlTable g_xl_table = make_xl_table();
+template <int NT = 256>
+__device__ __forceinline__ void xl_table_init(XlTable* t) {
+  constexpr int n16 = (int)(sizeof(XlTable) / 16);
+  const uint4* src = reinterpret_cast<const uint4*>(&g_xl_table);
+  uint4* dst = reinterpret_cast<uint4*>(t);
+#pragma unroll
+  for (int i0 = 0; i0 < n16; i0 += NT) {
+    const int i = i0 + (int)threadIdx.x;
+    if (i < n16) dst[i] = src[i];
+  }
+}
+
 // One 16-char group -> 12 bytes -> 3 little-endian int32 codes.
 // Returns a 16-bit mask of chars that are not in the alphabet (bit i = char i).
 __device__ __forceinline__ uint32_t b64_decode_group(uint4 w, const B64Tables* t, int32_t codes[3]) {

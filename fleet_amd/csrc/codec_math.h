@@ -496,6 +496,119 @@ FLEET_HD float q_fast1(float x) {
   return d9(u2f(f2u((float)c) | (f2u(x) & 0x80000000u)));
 }
 
+// ------------------------------------------- one-lookup latency Q (serial chain)
+// The serial accumulation A = Q(A + p) runs on ONE wave per tile: it is bound by
+// that wave's instruction issue, so the step count matters more than a table
+// load on the path. One LDS entry per (sign, biased exponent) of x, clamped to
+// 126..158 (|x| < 1 shares the 126 entry), holds everything the step needs:
+//   * the chains for k_hi = 9 - dhi steps (dhi = numDigits when |x| >= thr) as
+//     group multipliers (groups 2, 1, 2, 4: m = 10 or 1, h = RN(0.1) or 1);
+//   * ONE extra step taken iff |x| < thr and dlo = dhi - 1 (then k = k_hi + 1):
+//     both chains are order-free (identity steps are exact), so it goes last;
+//   * the /10 chain's small terms in the kTenthLo2 form of q_lat (one
+//     dependent fma per step): A_1 = U_0*c[0], A_j = U_{j-2}*c[j-1],
+//     c = kTenthLo after an identity step, kTenthLo2 after a taken one, 0 for
+//     an identity step itself (fma(U, 1, U'*0) = U exactly).
+// Entries of values outside the q_gen domain hold identity chains; callers
+// flag |x| >= 1e8 (max over the chain) and recompute such values exactly.
+constexpr uint32_t kXlSpan = 33;  // biased exponents 126..158 per sign
+struct alignas(16) XlEntry {
+  float m[4];     // x10 chain group multipliers
+  float thr;      // |x| < thr selects dlo and the extra step
+  uint32_t dhi, dlo;
+  float mx;       // extra x10 step: 10 if dlo + 1 == dhi, else 1
+  float c[10];    // small-term multipliers, c[9] for the extra step
+  float h[4];     // /10 chain group multipliers
+  float hx;       // extra /10 step: RN(0.1) or 1
+  float pad;
+};
+FLEET_HDC XlEntry xl_entry(uint32_t idx) {
+  XlEntry x{};
+  const uint32_t sign = idx / kXlSpan, be = 126u + idx % kXlSpan;
+  const VarEntry v = var_entry((sign << 8) | be);
+  uint32_t dhi = v.info & 0xffu, dlo = (v.info >> 8) & 0xffu;
+  const bool extra = dlo <= 9u && dlo + 1u == dhi;
+  if (dhi > 9u) dhi = 9u;  // off the domain: identity chains (flagged by the caller)
+  if (dlo > 9u) dlo = 9u;
+  const Steps s = steps_of(9u - dhi);
+  const bool g[4] = {s.e, s.b0, s.b1, s.b2};
+  bool taken[10] = {false, s.e, s.e, s.b0, s.b1, s.b1, s.b2, s.b2, s.b2, s.b2};  // taken[j], steps j = 1..9
+  for (int i = 0; i < 4; ++i) {
+    x.m[i] = g[i] ? 10.0f : 1.0f;
+    x.h[i] = g[i] ? kTenthHi : 1.0f;
+  }
+  x.thr = v.thr;
+  x.dhi = dhi;
+  x.dlo = extra ? dlo : dhi;
+  x.mx = extra ? 10.0f : 1.0f;
+  x.hx = extra ? kTenthHi : 1.0f;
+  x.c[0] = taken[1] ? kTenthLo : 0.0f;
+  for (int j = 2; j <= 9; ++j) x.c[j - 1] = taken[j] ? (taken[j - 1] ? kTenthLo2 : kTenthLo) : 0.0f;
+  x.c[9] = extra ? (taken[9] ? kTenthLo2 : kTenthLo) : 0.0f;
+  return x;
+}
+FLEET_HD uint32_t xl_index(float x) {
+  const uint32_t b = f2u(x);
+  uint32_t be = (b >> 23) & 0xffu;
+  be = be < 126u ? 126u : be > 158u ? 158u : be;
+  return (b >> 31) * kXlSpan + be - 126u;
+}
+// Q(x) for |x| < 1e8 (exact there; garbage, never a fault, elsewhere).
+// the entry's sign + clamped exponent: equal keys <=> same entry
+FLEET_HD uint32_t xl_key(float x) {
+  const uint32_t b = f2u(x);
+  uint32_t be = (b >> 23) & 0xffu;
+  be = be < 126u ? 126u : be > 158u ? 158u : be;
+  return (b & 0x80000000u) | be;
+}
+// the entry in registers: six 16-byte loads in flight together, and selects
+// between loaded values instead of loads under a condition
+FLEET_HD XlEntry xl_load(const XlEntry* xt, float x) {
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  typedef uint32_t u3 __attribute__((ext_vector_type(3)));
+  XlEntry e;
+  const u4* src = reinterpret_cast<const u4*>(xt + xl_index(x));
+  u4* dst = reinterpret_cast<u4*>(&e);
+#pragma unroll
+  for (int i = 0; i < 5; ++i) dst[i] = src[i];
+  // the last 16 bytes without the pad word: a loaded register nobody reads
+  // would be reused at once and stall on the load (write-after-write)
+  const u3 t = *reinterpret_cast<const u3*>(src + 5);
+  e.h[2] = u2f(t.x);
+  e.h[3] = u2f(t.y);
+  e.hx = u2f(t.z);
+  e.pad = 0.0f;
+  return e;
+}
+// Q(x) for |x| < 1e8 given x's entry (exact there; garbage, never a fault,
+// elsewhere).
+FLEET_HD float q_xl_e(float x, const XlEntry& e) {
+  const float ax = __builtin_fabsf(x);
+  const bool small = ax < e.thr;
+  float X = ax * e.m[0];
+  X = X * e.m[0];
+  X = X * e.m[1];
+  X = X * e.m[2];
+  X = X * e.m[2];
+  X = X * e.m[3];
+  X = X * e.m[3];
+  X = X * e.m[3];
+  X = X * e.m[3];
+  X = X * (small ? e.mx : 1.0f);
+  const uint32_t d = small ? e.dlo : e.dhi;
+  const float cf = code_float_mt(X, d, x);
+  const float H[9] = {e.h[0], e.h[0], e.h[1], e.h[2], e.h[2], e.h[3], e.h[3], e.h[3], e.h[3]};
+  float U = cf, a = cf * e.c[0];
+#pragma unroll
+  for (int j = 1; j <= 9; ++j) {
+    const float Un = __builtin_fmaf(U, H[j - 1], a);  // the only dependent op per step
+    a = U * (j < 9 ? e.c[j] : (small ? e.c[9] : 0.0f));
+    U = Un;
+  }
+  return __builtin_fmaf(U, small ? e.hx : 1.0f, a);
+}
+FLEET_HD float q_xl(float x, const XlEntry* xt) { return q_xl_e(x, xl_load(xt, x)); }
+
 // int2float(c) for every code (k = 9 - |c % 10| in [0, 9]) -- total.
 FLEET_HD uint32_t last_digit(int32_t c) {
   uint32_t a = c < 0 ? 0u - (uint32_t)c : (uint32_t)c;

@@ -597,6 +597,7 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
 
   float A = 0.f;  // phase-2 value: element tid of the tile (tid < E)
   uint32_t off_domain = 0;
+  float amax = 0.f;  // narrow tiles: max |A + p| (q_lat is exact below 1e8 for any sign)
   uint32_t badacc = 0;
   for (int c0 = 0; c0 < M; c0 += CM) {
     const int cm = min(CM, M - c0);
@@ -618,7 +619,7 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
 #pragma unroll 4
         for (; k < cm; ++k) {
           const float s = A + ptile[k * E + tid];
-          off_domain |= (uint32_t)!q_gen_ok(s);
+          amax = __builtin_fmaxf(amax, __builtin_fabsf(s));
           A = q_lat(s);
         }
       } else {  // many blocks: throughput (multiplier-table Q, fewer instructions)
@@ -635,6 +636,7 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
   }
   FLEET_TSTAMP(4);
   if (badacc) atomicOr(err, FLEET_ERRBIT_BASE64);
+  off_domain |= (uint32_t)!(amax < 1e8f);
   if (tid >= 3 * ng) off_domain = 0;  // columns past the last group hold no values
   if (__ballot(off_domain != 0)) {    // wave-uniform, never for gradients
     if (off_domain) A = chain_general(uploads, pitch, M, dampen, g0 + tid / 3, tid % 3, &sh.tab);
@@ -673,6 +675,7 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   constexpr int RING = (6144 / E) / CPP > 0 ? (6144 / E) / CPP : 1;  // passes in LDS (~24 KiB)
   FLEET_TSTAMP(0);
   __shared__ TileShared<TG, NW> sh;
+  __shared__ XlTable xl;  // the consumer's one-lookup Q
   __shared__ float ptile[RING * CPP * E];
   __shared__ float finals[E];
   __shared__ int prog[NPW];  // passes finished by each producer wave
@@ -718,10 +721,22 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
     // arbitration against co-resident producer waves (MI355X_MICROARCH.md,
     // two waves per SIMD, item 4)
     __builtin_amdgcn_s_setprio(3);
+    // the q_xl table is the consumer's alone: copied while pass 0 is produced,
+    // visible to this wave once its own LDS writes are done (no block barrier)
+    xl_table_init<64>(&xl);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes done
+    __builtin_amdgcn_wave_barrier();
     float A = 0.f;
-    uint32_t off_domain = 0;
+    float amax = 0.f;  // max |A + p| over the chain: q_xl is exact below 1e8
     const int col = tid < E ? tid : 0;
+#ifdef FLEET_TIMING
+    unsigned long long waited = 0, spun = 0;
+#endif
     for (int pass = 0; pass < npass; ++pass) {
+#ifdef FLEET_TIMING
+      const unsigned long long w0 = wall_clock64();
+      bool spin = false;
+#endif
       for (;;) {
         bool ready;
         if (WP) {
@@ -735,8 +750,21 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
           ready = m > pass;
         }
         if (ready) break;
+#ifdef FLEET_TIMING
+        spin = true;
+#endif
         __builtin_amdgcn_s_sleep(1);
       }
+#ifdef FLEET_TIMING
+      if (pass > 0) {  // slot 6: time the consumer waited for producers after the first pass
+        waited += wall_clock64() - w0;
+        spun += spin;
+      }
+      if (threadIdx.x == 0) {
+        g_fleet_timing[blockIdx.x * 8 + 6] = waited;
+        g_fleet_timing[blockIdx.x * 8 + 7] = spun;
+      }
+#endif
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       if (pass == 0) {
         FLEET_TSTAMP(2);
@@ -752,14 +780,18 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
 #pragma unroll 4
       for (; k < cm; ++k) {
         const float s = A + pt[k * E + col];
-        off_domain |= (uint32_t)!q_gen_ok(s);
-        A = q_lat(s);
+        amax = __builtin_fmaxf(amax, __builtin_fabsf(s));  // s is finite: p and A are Q outputs
+#ifdef FLEET_PIPE_TRIVIAL_CONSUMER  // dev experiment: producer-bound time
+        A = s * 0.5f;
+#else
+        A = q_xl(s, xl.x);
+#endif
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&consumed, pass + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if (tid >= 3 * ng) off_domain = 0;  // columns past the last group hold no values
-    if (__ballot(off_domain != 0)) {    // wave-uniform, never for gradients
+    const bool off_domain = tid < 3 * ng && !(amax < 1e8f);  // columns past the last group hold no values
+    if (__ballot(off_domain)) {                                // wave-uniform, never for gradients
       if (off_domain) A = chain_general(uploads, pitch, M, dampen, g0 + tid / 3, tid % 3, &sh.tab);
     }
     if (tid < E) finals[tid] = A;
@@ -1137,12 +1169,14 @@ struct UpdatePlan {
   int tg, k, ipt, nw, wp;
 };
 static UpdatePlan plan_update(int64_t groups) {
-  // measured best on MNIST-64 (scripts/ubench_tiled.hip): 4 waves, block-wide passes, 1 item per thread
-  UpdatePlan p{0, 0, 1, 1, 4, 0};
+  // measured best on MNIST-64 (scripts/ubench_tiled.hip, profiles/r01/ubench_tiled.log):
+  // 5 waves (4 producers keep ahead of the q_xl consumer), block-wide passes, 1 item per thread
+  UpdatePlan p{0, 0, 1, 1, 5, 0};
   if (const char* e = getenv("FLEET_PIPE_WAVEPASS")) p.wp = atoi(e) != 0;
   if (const char* e = getenv("FLEET_PIPE_IPT")) p.ipt = atoi(e) == 2 ? 2 : 1;
-  if (const char* e = getenv("FLEET_PIPE_WAVES")) p.nw = atoi(e) == 8 ? 8 : 4;
+  if (const char* e = getenv("FLEET_PIPE_WAVES")) p.nw = atoi(e) == 8 ? 8 : atoi(e) == 4 ? 4 : 5;
   if (p.ipt == 2) p.nw = 4, p.wp = 0;
+  if (p.wp && p.nw == 5) p.nw = 4;
   if (use_tiled(groups)) {
     // widest tile that still gives >= 4 blocks per CU; the narrow tiles are
     // pipelined (producer waves + one consumer wave)
@@ -1198,6 +1232,9 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
     } else if (p.ipt == 2) {
       if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 2, 4, 0);
       else FLEET_LAUNCH_PIPE(16, 2, 4, 0);
+    } else if (p.nw == 5) {
+      if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 5, 0);
+      else FLEET_LAUNCH_PIPE(16, 1, 5, 0);
     } else {
       if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 4, 0);
       else FLEET_LAUNCH_PIPE(16, 1, 4, 0);
@@ -1313,10 +1350,12 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __restrict__ out) {
   __shared__ DigitEntry dig[32];
   __shared__ B64Tables tab;
+  __shared__ XlTable xl;
   {
     constexpr DigitEntry init[32] = FLEET_DIGIT_TABLE;
     if (threadIdx.x < 32) dig[threadIdx.x] = init[threadIdx.x];
     b64_tables_init(&tab);
+    xl_table_init(&xl);
     __syncthreads();
   }
   const VarEntry* var = tab.var;
@@ -1362,6 +1401,9 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
                o = use ? (uint32_t)enc_mt(u2f(u), var, mt) : 0u; break;
       case 16: use = (u & 0x7fffffffu) < 0x3f800000u;                 // scalar Q fast path (as fn 2)
                o = use ? f2u(q_fast1(u2f(u))) : 0u; break;
+      case 17: { const float x = u2f(u);                              // one-lookup Q on |x| < 1e8 (as fn 6)
+               use = q_gen_ok(x);
+               o = use ? f2u(__builtin_fabsf(x) < 1e8f ? q_xl(x, xl.x) : q_lat(x)) : 0u; break; }
       default: o = 0; use = false;
     }
     if (use) sum += splitmix64(((uint64_t)u << 32) | o);

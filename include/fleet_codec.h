@@ -159,6 +159,7 @@ int fleet_check(fleet_ctx* ctx, void* stream);
  *   fn 12: select-chain Q of the serial accumulation (-1e8 < x < 1e9; same digest as fn 6)
  *   fn 13: multiplier-table Q (as fn 6)   fn 14: multiplier-table int2float (as fn 7)
  *   fn 15: multiplier-table float2int (as fn 10)   fn 16: scalar Q fast path (as fn 2)
+ *   fn 17: one-lookup latency Q (q_xl) on |x| < 1e8, fn 12 elsewhere (as fn 6)
  * computed on the GPU; compare with the oracle's digests. */
 int fleet_selftest_digest(fleet_ctx* ctx, int fn, uint64_t* out);
 

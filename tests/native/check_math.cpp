@@ -51,6 +51,18 @@ int main(int argc, char** argv) {
     report("q_lat (exhaustive)", b);
     return g_bad ? 1 : 0;
   }
+  if (argc > 1 && std::string(argv[1]) == "xl") {  // one-lookup latency Q, every input of |x| < 1e8
+    static XlEntry xt[2 * kXlSpan];
+    for (uint32_t i = 0; i < 2 * kXlSpan; ++i) xt[i] = xl_entry(i);
+    long b = g_bad;
+    par_for(0, 1ull << 32, 1, [](uint64_t i) {
+      const float x = u2f((uint32_t)i);
+      if (!(__builtin_fabsf(x) < 1e8f)) return;
+      if (!same(q_xl(x, xt), fo_int2float(fo_float2int(x)))) g_bad++;
+    });
+    report("q_xl (exhaustive)", b);
+    return g_bad ? 1 : 0;
+  }
   if (argc > 1 && std::string(argv[1]) == "mt") {  // multiplier-table functions, every input
     static VarEntry vt[512];
     static MulEntry mt[16];
@@ -163,6 +175,16 @@ int main(int argc, char** argv) {
     if (q_ok(x) && !same(q_fast1(x), fo_int2float(fo_float2int(x)))) g_bad++;
   });
   report("q_mt/enc_mt/q_fast1", b0);
+  b0 = g_bad;
+  {
+    static XlEntry xt[2 * kXlSpan];
+    for (uint32_t i = 0; i < 2 * kXlSpan; ++i) xt[i] = xl_entry(i);
+    par_for(0, 1ull << 32, s, [](uint64_t i) {
+      const float x = u2f((uint32_t)i);
+      if (__builtin_fabsf(x) < 1e8f && !same(q_xl(x, xt), fo_int2float(fo_float2int(x)))) g_bad++;
+    });
+  }
+  report("q_xl", b0);
 
   b0 = g_bad;  // multiplier-table int2float, every code
   par_for(0, 1ull << 32, s, [](uint64_t i) {

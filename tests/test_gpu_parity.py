@@ -183,10 +183,10 @@ def test_device_synth_and_encode(codec, oracle):
 
 
 # fn 13-16 compute the same functions as fn 6, 7, 10, 2 by other arithmetic
-SAME_DIGEST = {13: 6, 14: 7, 15: 10, 16: 2}
+SAME_DIGEST = {13: 6, 14: 7, 15: 10, 16: 2, 17: 6}
 
 
-@pytest.mark.parametrize("fn", range(17))
+@pytest.mark.parametrize("fn", range(18))
 def test_device_codec_exhaustive_digest(codec, fn):
     """Every input of each device codec function's domain (2^32 codes / bit
     patterns), digested on the GPU, equals the oracle's digest."""
@@ -213,6 +213,7 @@ def test_update_groups_per_lane_variants(codec, oracle, monkeypatch, K):
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_UPDATE_PIPE": "0"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_PIPE_IPT": "2"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_PIPE_WAVES": "8"},
+                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_PIPE_WAVES": "4"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_PIPE_WAVEPASS": "1"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "32"},
                                  {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "64"},
@@ -242,7 +243,7 @@ def test_update_large_magnitudes_slow_path(codec, oracle, monkeypatch, env):
 
 
 @pytest.mark.parametrize("mode", ["tiled", "tiled-nopipe", "tiled-wide", "tiled-ipt2", "tiled-8waves",
-                                  "tiled-wavepass", "stream"])
+                                  "tiled-4waves", "tiled-wavepass", "stream"])
 def test_update_modes(codec, oracle, monkeypatch, mode):
     """Every aggregation kernel (pipelined and two-phase tiles for small
     buckets, streaming for large ones) on ragged tiles, client counts that wrap
@@ -256,6 +257,8 @@ def test_update_modes(codec, oracle, monkeypatch, mode):
         monkeypatch.setenv("FLEET_PIPE_IPT", "2")
     if mode == "tiled-8waves":
         monkeypatch.setenv("FLEET_PIPE_WAVES", "8")
+    if mode == "tiled-4waves":
+        monkeypatch.setenv("FLEET_PIPE_WAVES", "4")
     if mode == "tiled-wavepass":
         monkeypatch.setenv("FLEET_PIPE_WAVEPASS", "1")
     for lay, M in ((MNIST, 70), (synthetic(1000), 1), (synthetic(3001), 129), (synthetic(5002), 2),
