@@ -18,6 +18,7 @@
 #include "../../include/fleet_codec.h"
 #include "kernels.h"
 #include "model_codec.h"
+#include "codec_device.h"
 
 #define FLEET_VERSION "fleet-mi355x 0.1.0 (gfx950)"
 
@@ -155,6 +156,124 @@ int finish_text(fleet_ctx* c, size_t out_len, char* out, size_t cap, size_t* out
   if (out_len) HIP_TRY(c, hipMemcpyAsync(out, c->d_out, out_len, hipMemcpyDeviceToHost, c->stream));
   int rc = read_err(c, c->stream);
   return rc;
+}
+
+// Copies the M uploads into the pinned staging rows (pitch apart, zero
+// padded) and queues ONE H2D of [rows | tail_bytes already written after the
+// rows] into d_a, in `pieces` parts, each queued as soon as its rows are
+// copied, so the DMA of a part overlaps the copy of the next (ingress
+// framing). Measured on MI355X (scripts/probe_e2e2.py, rocprofv3
+// memory-copy trace): 1 MiB H2D parts run at ~35 GB/s with ~9 us gaps, one
+// 7.8 MB copy at ~53 GB/s; three parts gave the shortest host-buffer update
+// (0.27 vs 0.32 ms for MNIST-64 with one part); copying with 2-4 threads did
+// not help consistently.
+int stage_uploads(fleet_ctx* c, const char* const* uploads, size_t len, size_t pitch, int M, size_t tail_bytes) {
+  int pieces = 3;
+  if (const char* e = getenv("FLEET_STAGE_PIECES")) pieces = std::max(1, atoi(e));
+  if (pitch * (size_t)M < (4u << 20)) pieces = 1;
+  pieces = std::min(pieces, M);
+  for (int k = 0; k < pieces; ++k) {
+    const int r0 = (int)((int64_t)M * k / pieces), r1 = (int)((int64_t)M * (k + 1) / pieces);
+    for (int i = r0; i < r1; ++i) {
+      uint8_t* row = c->h_stage + (size_t)i * pitch;
+      std::memcpy(row, uploads[i], len);
+      std::memset(row + len, 0, pitch - len);
+    }
+    const size_t off = (size_t)r0 * pitch;
+    const size_t bytes = (size_t)(r1 - r0) * pitch + (r1 == M ? tail_bytes : 0);
+    HIP_TRY(c, hipMemcpyAsync(c->d_a + off, c->h_stage + off, bytes, hipMemcpyHostToDevice, c->stream));
+  }
+  return FLEET_OK;
+}
+
+// network::flatGrad's header walk (network.h:1206-1223) over the last upload,
+// on the host from the caller's buffer -- the same walk as k_layout_parse:
+// words = {status (0 ok, 1 malformed), count, walk end, 0, positions...}.
+int32_t host_code_at(const char* text, int64_t p, bool* bad) {
+  static constexpr auto tab = [] {
+    struct T {
+      uint8_t v[256];
+    } t{};
+    for (int i = 0; i < 256; ++i) t.v[i] = fleet::b64_from_value(i);
+    return t;
+  }();
+  const uint8_t* g = reinterpret_cast<const uint8_t*>(text) + 16 * (p / 3);
+  const int e = (int)(p % 3);
+  const uint32_t carry[3] = {0x003fu, 0x07e0u, 0xfc00u};  // chars carrying bytes 4e..4e+3
+  uint8_t bytes[12];
+  for (int q = 0; q < 4; ++q) {
+    uint32_t w = 0;
+    for (int i = 0; i < 4; ++i) {
+      const uint8_t v = tab.v[g[4 * q + i]];
+      if (v == 0xff && ((carry[e] >> (4 * q + i)) & 1u)) *bad = true;
+      w = (w << 6) | (v & 63u);
+    }
+    bytes[3 * q] = (uint8_t)(w >> 16);
+    bytes[3 * q + 1] = (uint8_t)(w >> 8);
+    bytes[3 * q + 2] = (uint8_t)w;
+  }
+  uint32_t u = 0;
+  for (int i = 3; i >= 0; --i) u = (u << 8) | bytes[4 * e + i];
+  return (int32_t)u;
+}
+void host_layout_parse(const char* up, int64_t n, int cap, int32_t* out) {
+  int64_t idx = 0;
+  int nh = 0;
+  bool bad = false;
+  int status = 0;
+  for (int part = 0; part < 2 && !status; ++part) {
+    if (idx >= n || nh >= cap) {
+      status = 1;
+      break;
+    }
+    out[4 + nh++] = (int32_t)idx;
+    const int cnt = fleet::cvtt(fleet::dec(host_code_at(up, idx++, &bad)));
+    for (int i = 0; i < cnt; ++i) {
+      if (idx >= n || nh >= cap) {
+        status = 1;
+        break;
+      }
+      out[4 + nh++] = (int32_t)idx;
+      const int size = fleet::cvtt(fleet::dec(host_code_at(up, idx++, &bad)));
+      if (size < 0 || idx + size > n) {
+        status = 1;
+        break;
+      }
+      idx += size;
+    }
+  }
+  if (bad) status = 1;
+  out[0] = status;
+  out[1] = nh;
+  out[2] = (int32_t)idx;
+  out[3] = 0;
+}
+
+// fleet_update when the host walk of the last upload's header fails: the
+// device flow (parse kernel, update, error flags), so the error reported is
+// the same as a full device run's (Base64 errors anywhere take precedence).
+int update_host_fallback(fleet_ctx* c, const char* const* uploads, size_t len, int M, const double* dampen,
+                         char* merged, float* merged_f32) {
+  const size_t n = fleet_b64_count(len), groups = groups_of(n), pitch = round16(len), total = pitch * (size_t)M;
+  int rc;
+  if ((rc = grow_dev(c, &c->d_dampen, &c->d_dampen_cap, (size_t)M))) return rc;
+  if ((rc = grow_dev(c, &c->d_out, &c->d_out_cap, 16 * groups + 16))) return rc;
+  if (merged_f32 && (rc = grow_dev(c, &c->d_f32, &c->d_f32_cap, 3 * groups + 3))) return rc;
+  if ((rc = stage_uploads(c, uploads, len, pitch, M, 0))) return rc;
+  std::memcpy(c->h_stage + total, dampen, sizeof(double) * (size_t)M);
+  c->dev_params_valid = false;
+  HIP_TRY(c, hipMemcpyAsync(c->d_dampen, c->h_stage + total, sizeof(double) * (size_t)M, hipMemcpyHostToDevice,
+                            c->stream));
+  HIP_TRY(c, fleet::launch_layout_parse(c->d_a + (size_t)(M - 1) * pitch, (int64_t)n, FLEET_MAX_HEADERS, c->d_hdr,
+                                        c->stream));
+  HIP_TRY(c, fleet::launch_update(c->d_a, pitch, M, c->d_dampen, (double)1 / M, (int64_t)n, 0, (int64_t)groups,
+                                  c->d_hdr, c->d_out, merged_f32 ? c->d_f32 : nullptr, c->d_err, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(merged, c->d_out, len, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->h_hdr, c->d_hdr, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+  if ((rc = read_err(c, c->stream))) return rc;
+  if (c->h_hdr[0] != 0)
+    return fail(c, FLEET_ERR_LAYOUT, "last upload's header does not describe a gradient layout");
+  return FLEET_OK;  // not reached for a failed host walk (the device walk is the same)
 }
 
 }  // namespace
@@ -428,34 +547,35 @@ int fleet_update(fleet_ctx* c, const char* const* uploads, const size_t* lens, i
   const size_t groups = groups_of(n);
   const size_t pitch = round16(len);
   const size_t total = pitch * (size_t)M;
-  if ((rc = grow_pinned(c, total + sizeof(double) * (size_t)M + 64))) return rc;
-  if ((rc = grow_dev(c, &c->d_a, &c->d_a_cap, total + 16))) return rc;
-  if ((rc = grow_dev(c, &c->d_dampen, &c->d_dampen_cap, (size_t)M))) return rc;
-  if ((rc = grow_dev(c, &c->d_out, &c->d_out_cap, 16 * groups + 16))) return rc;
-  if (merged_f32 && (rc = grow_dev(c, &c->d_f32, &c->d_f32_cap, 3 * groups + 3))) return rc;
+  // one staging block, mirrored on the device in d_a:
+  //   [uploads M x pitch | dampen M doubles | header words | err | merged Base64 | merged fp32]
+  // one H2D up to err (inclusive, err = 0), one D2H from err on.
+  const size_t o_damp = total, o_hdr = round16(o_damp + sizeof(double) * (size_t)M);
+  const size_t o_err = round16(o_hdr + sizeof(int32_t) * kHdrWords), o_out = o_err + 16;
+  const size_t o_f32 = round16(o_out + 16 * groups + 16), o_end = o_f32 + sizeof(float) * (3 * groups + 3);
+  if ((rc = grow_pinned(c, o_end + 64))) return rc;
+  if ((rc = grow_dev(c, &c->d_a, &c->d_a_cap, o_end + 64))) return rc;
   HIP_TRY(c, hipStreamSynchronize(c->stream));  // staging buffer reuse
-  for (int i = 0; i < M; ++i) {
-    uint8_t* row = c->h_stage + (size_t)i * pitch;
-    std::memcpy(row, uploads[i], len);
-    std::memset(row + len, 0, pitch - len);
-  }
-  double* hd = (double*)(c->h_stage + total);
-  std::memcpy(hd, dampen, sizeof(double) * (size_t)M);
-  HIP_TRY(c, hipMemcpyAsync(c->d_a, c->h_stage, total, hipMemcpyHostToDevice, c->stream));
-  c->dev_params_valid = false;
-  HIP_TRY(c, hipMemcpyAsync(c->d_dampen, hd, sizeof(double) * (size_t)M, hipMemcpyHostToDevice, c->stream));
-  // layout of the last picked upload (mergeFlatGradient keeps its header)
-  HIP_TRY(c, fleet::launch_layout_parse(c->d_a + (size_t)(M - 1) * pitch, (int64_t)n, FLEET_MAX_HEADERS, c->d_hdr,
-                                        c->stream));
-  HIP_TRY(c, fleet::launch_update(c->d_a, pitch, M, c->d_dampen, (double)1 / M, (int64_t)n, 0, (int64_t)groups,
-                                  c->d_hdr, c->d_out, merged_f32 ? c->d_f32 : nullptr, c->d_err, c->stream));
-  HIP_TRY(c, hipMemcpyAsync(merged, c->d_out, len, hipMemcpyDeviceToHost, c->stream));
-  if (merged_f32) HIP_TRY(c, hipMemcpyAsync(merged_f32, c->d_f32, n * sizeof(float), hipMemcpyDeviceToHost,
-                                            c->stream));
-  HIP_TRY(c, hipMemcpyAsync(c->h_hdr, c->d_hdr, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-  if ((rc = read_err(c, c->stream))) return rc;
-  if (c->h_hdr[0] != 0)
-    return fail(c, FLEET_ERR_LAYOUT, "last upload's header does not describe a gradient layout");
+  // layout of the last picked upload (mergeFlatGradient keeps its header), walked on the host
+  int32_t* hw = reinterpret_cast<int32_t*>(c->h_stage + o_hdr);
+  host_layout_parse(uploads[M - 1], (int64_t)n, FLEET_MAX_HEADERS, hw);
+  if (hw[0] != 0) return update_host_fallback(c, uploads, len, M, dampen, merged, merged_f32);
+  std::memcpy(c->h_stage + o_damp, dampen, sizeof(double) * (size_t)M);
+  std::memset(c->h_stage + o_err, 0, 16);
+  if ((rc = stage_uploads(c, uploads, len, pitch, M, o_err + 16 - total))) return rc;
+  uint8_t* d = c->d_a;
+  HIP_TRY(c, fleet::launch_update(d, pitch, M, reinterpret_cast<const double*>(d + o_damp), (double)1 / M,
+                                  (int64_t)n, 0, (int64_t)groups, reinterpret_cast<const int32_t*>(d + o_hdr),
+                                  d + o_out, merged_f32 ? reinterpret_cast<float*>(d + o_f32) : nullptr,
+                                  reinterpret_cast<int*>(d + o_err), c->stream));
+  const size_t back = (merged_f32 ? o_f32 + sizeof(float) * n : o_out + len) - o_err;
+  HIP_TRY(c, hipMemcpyAsync(c->h_stage + o_err, d + o_err, back, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  const int e = *reinterpret_cast<const int*>(c->h_stage + o_err);
+  if (e & 1) return fail(c, FLEET_ERR_BASE64, "input is not Base64::encode output (alphabet/padding)");
+  if (e & 2) return fail(c, FLEET_ERR_LAYOUT, "uploads disagree on the gradient layout header slots");
+  std::memcpy(merged, c->h_stage + o_out, len);
+  if (merged_f32) std::memcpy(merged_f32, c->h_stage + o_f32, sizeof(float) * n);
   return FLEET_OK;
 }
 
