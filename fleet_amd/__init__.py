@@ -110,6 +110,9 @@ def lib() -> C.CDLL:
         "fleet_model_params": (i32, [vp, vp, sz, vp, sz, i32, vp, sz, szp]),
         "fleet_model_version": (i32, [vp, vp, vp, i32, vp, sz, vp, vp]),
         "fleet_model_params_device": (i32, [vp, vp, sz, vp, sz, i32, vp, vp]),
+        "fleet_minibatch_len": (sz, [i32, i32, i32, i32]),
+        "fleet_minibatch_device": (i32, [vp, vp, sz, i32, vp, vp, i32, vp, i32, vp, vp, vp]),
+        "fleet_minibatch": (i32, [vp, vp, sz, i32, vp, vp, i32, vp, i32, vp, vp, sz, szp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -450,6 +453,40 @@ class Codec:
         n = len(b) * int(graph_edges) + len(w)
         return self._text_call(self._L.fleet_model_params, (w.ctypes.data, len(w), b.ctypes.data, len(b),
                                                             int(graph_edges)), b64_len(n))
+
+    # -- getMiniBatch -------------------------------------------
+    def getMiniBatch(self, images, labels, idx, header, teacher=None) -> bytes:  # noqa: N802  (cppNN_backend.cpp:677)
+        """Base64 of the sampler's mini-batch vector (cppNN_backend.cpp:553-699) for the
+        sample indices `idx`: header (7 floats, fleet_amd.sampler.minibatch_header),
+        per sample its features, (mode 1) the teacher's probabilities, its label."""
+        x = np.ascontiguousarray(images, dtype=np.float32)
+        n_img, F = x.shape
+        lab = np.ascontiguousarray(labels, dtype=np.int32)
+        ix = np.ascontiguousarray(idx, dtype=np.int32)
+        h = np.ascontiguousarray(header, dtype=np.float32)
+        if len(h) != 7:
+            raise ValueError("header holds E, sigma, C, lr, batchSize, featureSize, numLabels")
+        t, nl = None, 0
+        if teacher is not None:
+            t = np.ascontiguousarray(teacher, dtype=np.float32)
+            nl = t.shape[1]
+            if t.shape[0] != len(ix):
+                raise ValueError("one teacher row per sample")
+        cap = self._L.fleet_minibatch_len(F, len(ix), nl, t is not None)
+        return self._text_call(self._L.fleet_minibatch, (x.ctypes.data, n_img, F, lab.ctypes.data, ix.ctypes.data,
+                                                         len(ix), t.ctypes.data if t is not None else None, nl,
+                                                         h.ctypes.data), cap)
+
+    def minibatch_device(self, images_f32, labels_i32, idx_i32, header, out_u8, teacher_f32=None, stream=None):
+        """Device-resident getMiniBatch: CUDA tensors images [N, F], labels [N], idx [B],
+        out uint8 [>= fleet_minibatch_len]. Index errors surface at check()."""
+        n_img, F = images_f32.shape
+        h = np.ascontiguousarray(header, dtype=np.float32)
+        nl = teacher_f32.shape[1] if teacher_f32 is not None else 0
+        self._check(self._L.fleet_minibatch_device(self._h, images_f32.data_ptr(), n_img, F, labels_i32.data_ptr(),
+                                                   idx_i32.data_ptr(), idx_i32.numel(),
+                                                   teacher_f32.data_ptr() if teacher_f32 is not None else None, nl,
+                                                   h.ctypes.data, out_u8.data_ptr(), _stream(stream)))
 
     # -- descentNative's model step (SURVEY.md §8 f1) ----------------------------
     @staticmethod

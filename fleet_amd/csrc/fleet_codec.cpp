@@ -134,6 +134,7 @@ int read_err(fleet_ctx* c, hipStream_t s) {
   }
   if (e & 1) return fail(c, FLEET_ERR_BASE64, "input is not Base64::encode output (alphabet/padding)");
   if (e & 2) return fail(c, FLEET_ERR_LAYOUT, "uploads disagree on the gradient layout header slots");
+  if (e & 4) return fail(c, FLEET_ERR_ARG, "sample index outside the dataset");
   return FLEET_OK;
 }
 
@@ -840,6 +841,67 @@ int fleet_model_params_device(fleet_ctx* c, const float* d_weights, size_t n_wei
   HIP_TRY(c, fleet::launch_encode_model_params(d_weights, (int64_t)n_weights, d_biases, (int64_t)n_biases,
                                                n_biases ? (int64_t)graph_edges : 0, (uint8_t*)d_out,
                                                pick(c, stream)));
+  return FLEET_OK;
+}
+
+size_t fleet_minibatch_len(int F, int B, int num_labels, int with_teacher) {
+  if (F < 0 || B < 0 || num_labels < 0) return 0;
+  const size_t n = 7 + (size_t)B * ((size_t)F + (with_teacher ? (size_t)num_labels : 0) + 1) + (with_teacher ? 1 : 0);
+  return fleet_b64_len(n);
+}
+
+int fleet_minibatch_device(fleet_ctx* c, const void* d_images, size_t n_images, int F, const void* d_labels,
+                           const void* d_idx, int B, const void* d_teacher, int num_labels, const float header[7],
+                           void* d_out, void* stream) {
+  if (!c || !d_out || !header || F < 0 || B < 0 || num_labels < 0 || (B && (!d_idx || !d_labels || !d_images)) ||
+      (d_teacher && num_labels == 0))
+    return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, fleet::launch_encode_minibatch((const float*)d_images, (int64_t)n_images, F, (const int32_t*)d_labels,
+                                            (const int32_t*)d_idx, B, (const float*)d_teacher, num_labels, header,
+                                            (uint8_t*)d_out, c->d_err, pick(c, stream)));
+  return FLEET_OK;
+}
+
+int fleet_minibatch(fleet_ctx* c, const float* images, size_t n_images, int F, const int32_t* labels,
+                    const int32_t* idx, int B, const float* teacher, int num_labels, const float header[7],
+                    char* out, size_t cap, size_t* out_len) {
+  if (!c || !header || F < 0 || B < 0 || num_labels < 0 || (B && (!idx || !labels || !images)) ||
+      (teacher && num_labels == 0))
+    return FLEET_ERR_ARG;
+  const size_t len = fleet_minibatch_len(F, B, num_labels, teacher != nullptr);
+  if (out_len) *out_len = len;
+  if (cap < len || !out) return fail(c, FLEET_ERR_CAPACITY, "output capacity %zu < %zu", cap, len);
+  for (int b = 0; b < B; ++b)
+    if (idx[b] < 0 || (size_t)idx[b] >= n_images)
+      return fail(c, FLEET_ERR_ARG, "sample %d: index %d outside the %zu images", b, idx[b], n_images);
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  // staging: [B x F features | B labels | 0..B-1 | B x NL teacher]; the device gathers nothing
+  const size_t nl = teacher ? (size_t)num_labels : 0;
+  const size_t o_lab = round16(sizeof(float) * (size_t)B * (size_t)F), o_idx = o_lab + round16(4 * (size_t)B);
+  const size_t o_tea = o_idx + round16(4 * (size_t)B), o_out = o_tea + round16(sizeof(float) * (size_t)B * nl);
+  const size_t o_end = o_out + round16(len) + 16;
+  int rc;
+  if ((rc = grow_pinned(c, o_end))) return rc;
+  if ((rc = grow_dev(c, &c->d_a, &c->d_a_cap, o_end))) return rc;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));  // staging buffer reuse
+  uint8_t* h = c->h_stage;
+  for (int b = 0; b < B; ++b) {
+    std::memcpy(h + sizeof(float) * (size_t)b * F, images + (size_t)idx[b] * F, sizeof(float) * (size_t)F);
+    reinterpret_cast<int32_t*>(h + o_lab)[b] = labels[idx[b]];
+    reinterpret_cast<int32_t*>(h + o_idx)[b] = b;
+  }
+  if (teacher) std::memcpy(h + o_tea, teacher, sizeof(float) * (size_t)B * nl);
+  uint8_t* d = c->d_a;
+  HIP_TRY(c, hipMemcpyAsync(d, h, o_out, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, fleet::launch_encode_minibatch((const float*)d, (int64_t)B, F, (const int32_t*)(d + o_lab),
+                                            (const int32_t*)(d + o_idx), B, teacher ? (const float*)(d + o_tea) : nullptr,
+                                            num_labels, header, d + o_out, c->d_err, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(h + o_out, d + o_out, len, hipMemcpyDeviceToHost, c->stream));
+  if ((rc = read_err(c, c->stream))) return rc;
+  std::memcpy(out, h + o_out, len);
   return FLEET_OK;
 }
 

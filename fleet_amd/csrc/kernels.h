@@ -21,6 +21,9 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
 const char* update_kernel_name(int64_t groups);
 hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int rows, uint8_t* out, size_t pitch,
                              hipStream_t s);
+hipError_t launch_encode_minibatch(const float* images, int64_t n_images, int F, const int32_t* labels,
+                                   const int32_t* idx, int B, const float* teacher, int NL, const float header[7],
+                                   uint8_t* out, int* err, hipStream_t s);
 hipError_t launch_encode_model_params(const float* weights, int64_t n_w, const float* biases, int64_t n_b, int64_t reps,
                                       uint8_t* out, hipStream_t s);
 hipError_t launch_encode_i32(const int32_t* codes, int64_t n, uint8_t* out, hipStream_t s);

@@ -18,6 +18,7 @@ namespace fleet {
 
 #define FLEET_ERRBIT_BASE64 1
 #define FLEET_ERRBIT_LAYOUT 2
+#define FLEET_ERRBIT_ARG 4
 
 // Dev-only phase timestamps (scripts/ubench_tiled.hip builds with FLEET_TIMING);
 // compiled out of the library.
@@ -877,6 +878,68 @@ __global__ void __launch_bounds__(256) k_encode_model_params(const float* __rest
     x[e] = e >= r ? 0.0f : v < nbr ? biases[v % n_b] : weights[v - nbr];
   }
   *reinterpret_cast<uint4*>(out + 16 * g) = encode_group(x, r, &tab);
+}
+
+// getMiniBatch (Server/src/main/c++/cppNN_backend.cpp:677-699): Base64::encode
+// of the vector uniformSample / nonIIDSample build (:553-675) -- 7 header
+// values, then per sample its F features, (mode 1) the teacher's NL class
+// probabilities, and its label as float; mode 1 ends with 1234567 --
+// encoded straight from the resident dataset by sample index, without
+// materialising the vector. An index outside [0, n_images) flags an argument
+// error and reads row 0.
+struct MiniBatchHeader {
+  float v[7];
+};
+__global__ void __launch_bounds__(256) k_encode_minibatch(const float* __restrict__ images, int64_t n_images, int F,
+                                                          const int32_t* __restrict__ labels,
+                                                          const int32_t* __restrict__ idx, int B,
+                                                          const float* __restrict__ teacher, int NL,
+                                                          MiniBatchHeader hdr, uint8_t* __restrict__ out,
+                                                          int64_t n, int64_t groups, int* __restrict__ err) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= groups) return;
+  const int per = F + (teacher ? NL : 0) + 1;
+  const int r = (int)min<int64_t>(3, n - 3 * g);
+  float x[3];
+  bool bad = false;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) {
+    const int64_t p = 3 * g + e;
+    float v = 0.0f;
+    if (e < r) {
+      if (p < 7) {
+        v = hdr.v[p];
+      } else {
+        const int64_t q = p - 7, b = q / per;
+        const int f = (int)(q - b * per);
+        if (b >= B) {
+          v = 1234567.0f;  // mode 1 end marker (:611)
+        } else {
+          int64_t row = idx[b];
+          if (row < 0 || row >= n_images) bad = true, row = 0;
+          v = f < F ? images[row * F + f] : (teacher && f < F + NL) ? teacher[b * NL + (f - F)] : (float)labels[row];
+        }
+      }
+    }
+    x[e] = v;
+  }
+  if (bad) atomicOr(err, FLEET_ERRBIT_ARG);
+  *reinterpret_cast<uint4*>(out + 16 * g) = encode_group(x, r, &tab);
+}
+
+hipError_t launch_encode_minibatch(const float* images, int64_t n_images, int F, const int32_t* labels,
+                                   const int32_t* idx, int B, const float* teacher, int NL, const float header[7],
+                                   uint8_t* out, int* err, hipStream_t s) {
+  const int64_t n = 7 + (int64_t)B * (F + (teacher ? NL : 0) + 1) + (teacher ? 1 : 0);
+  const int64_t groups = (n + 2) / 3;
+  MiniBatchHeader h;
+  for (int i = 0; i < 7; ++i) h.v[i] = header[i];
+  hipLaunchKernelGGL(k_encode_minibatch, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, images, n_images, F,
+                     labels, idx, B, teacher, NL, h, out, n, groups, err);
+  return hipGetLastError();
 }
 
 hipError_t launch_encode_model_params(const float* weights, int64_t n_w, const float* biases, int64_t n_b, int64_t reps,

@@ -1,0 +1,104 @@
+"""Mirror of the offline sampler's mini-batch request.
+
+CppNNOfflineSampler.getSample -> JNI getMiniBatch (Server/src/main/c++/
+cppNN_backend.cpp:677-699) draws batch_size*E sample indices -- uniformly with
+libc ``rand() % N`` (uniformSample, :553-634) or by walking the client's
+non-IID bucket with a cursor (nonIIDSample, :636-675) -- builds the float
+vector [E, sigma, C, lr, batchSize, featureSize, numLabels, per sample: features,
+(mode 1) teacher probabilities, label] and Base64-encodes it. The index draw is
+host logic and stays here; the gather + encode runs on the GPU
+(``Codec.getMiniBatch`` / ``Codec.minibatch_device``). The mode-1 teacher's
+forward pass (mojo network inference) is not rebuilt: its per-sample class
+probabilities are an input.
+
+Bucket construction (initSampler :409-470: label sort, 2-shard buckets,
+``std::random_shuffle``) is dataset plumbing outside the hot path; buckets are
+given.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+_libc = None
+
+
+def _rand() -> int:
+    """libc rand() -- the generator uniformSample draws from (srand(seed) in initSampler)."""
+    global _libc
+    if _libc is None:
+        _libc = ctypes.CDLL(None)
+        _libc.rand.restype = ctypes.c_int
+    return _libc.rand()
+
+
+def srand(seed: int) -> None:
+    """initSampler's srand(seed) (cppNN_backend.cpp:387)."""
+    global _libc
+    if _libc is None:
+        _libc = ctypes.CDLL(None)
+        _libc.rand.restype = ctypes.c_int
+    _libc.srand(ctypes.c_uint(seed))
+
+
+def minibatch_header(E: int, sigma: float, C: float, lr: float, batch_size: int, feature_size: int,
+                     num_labels: int) -> np.ndarray:
+    """The 7 leading values as push_back(float) converts them (:586-592): ints and the
+    doubles sigma, C rounded to float; lr is cnn.get_learning_rate() (a float)."""
+    return np.array([E, sigma, C, lr, batch_size, feature_size, num_labels], dtype=np.float64).astype(np.float32)
+
+
+def uniform_indices(n_images: int, count: int, rand=_rand) -> List[int]:
+    """uniformSample's draw (:559-563): index = 0 + rand() % (N - 1 - 0 + 1)."""
+    return [rand() % n_images for _ in range(count)]
+
+
+class NonIIDCursor:
+    """nonIIDSample's per-client cursor (:645-652): non-overlapping samples from the
+    client's bucket, wrapping around."""
+
+    def __init__(self, buckets: Sequence[Sequence[int]]):
+        self.buckets = [list(b) for b in buckets]
+        self.pos = [0] * len(self.buckets)
+
+    def take(self, client: int, count: int) -> List[int]:
+        b = self.buckets[client]
+        out = []
+        for _ in range(count):
+            out.append(b[self.pos[client]])
+            self.pos[client] = (self.pos[client] + 1) % len(b)
+        return out
+
+
+class OfflineSampler:
+    """CppNNOfflineSampler.getMiniBatch with the sampler state of cppNN_backend.cpp
+    (E, sigma, C, lr, iid, the client rotation currClientID, :691)."""
+
+    def __init__(self, codec, images, labels, E: int, sigma: float, C: float, lr: float = 0.01,
+                 num_labels: int = 10, iid: bool = False, buckets: Optional[Sequence[Sequence[int]]] = None):
+        self.codec = codec
+        self.images = np.ascontiguousarray(images, dtype=np.float32)
+        self.labels = np.ascontiguousarray(labels, dtype=np.int32)
+        self.E, self.sigma, self.C, self.lr = int(E), float(sigma), float(C), float(lr)
+        self.num_labels = int(num_labels)
+        self.iid = bool(iid)
+        if not self.iid and not buckets:
+            raise ValueError("the non-IID sampler needs the clients' buckets (initSampler)")
+        self.cursor = NonIIDCursor(buckets) if buckets else None
+        self.num_clients = len(buckets) if buckets else 1
+        self.curr_client = 0
+
+    def getMiniBatch(self, batch_size: int, teacher=None) -> bytes:  # noqa: N802  (cppNN_backend.cpp:677)
+        """``teacher(indices) -> [B, numLabels]`` supplies the mode-1 teacher's
+        probabilities for the IID path (uniformSample runs the teacher there)."""
+        B = batch_size * self.E
+        if self.iid:
+            idx = uniform_indices(len(self.images), B)
+        else:
+            idx = self.cursor.take(self.curr_client, B)
+        self.curr_client = (self.curr_client + 1) % self.num_clients
+        hdr = minibatch_header(self.E, self.sigma, self.C, self.lr, B, self.images.shape[1], self.num_labels)
+        probs = teacher(idx) if (teacher is not None and self.iid) else None
+        return self.codec.getMiniBatch(self.images, self.labels, idx, hdr, teacher=probs)

@@ -208,6 +208,29 @@ int fleet_model_params_device(fleet_ctx* ctx, const float* d_weights, size_t n_w
 int fleet_model_params(fleet_ctx* ctx, const float* weights, size_t n_weights, const float* biases, size_t n_biases,
                        int graph_edges, char* out, size_t cap, size_t* out_len);
 
+/* getMiniBatch (Server/src/main/c++/cppNN_backend.cpp:677-699):
+ * Base64::encode of the vector uniformSample / nonIIDSample build (:553-675) --
+ * header[7] = {E, sigma, C, lr, batchSize, featureSize, numLabels} as float (the
+ * caller converts as push_back does), then per sample idx[b] its F features,
+ * (DISTILLATION_MODE=1, teacher != NULL) the teacher's num_labels probabilities
+ * teacher[b*num_labels ..], and its label as float; with a teacher the vector
+ * ends with 1234567 (:611). The index draw (rand() % N, or the non-IID bucket
+ * cursor) stays with the caller (fleet_amd/sampler.py mirrors both); the
+ * teacher's forward pass is not rebuilt (its outputs are inputs).
+ * images: n_images x F fp32 rows; labels: n_images int32. Output:
+ * fleet_minibatch_len(F, B, num_labels, teacher != NULL) bytes. */
+size_t fleet_minibatch_len(int F, int B, int num_labels, int with_teacher);
+/* device-resident dataset, indices (d_idx[B]) and output; an index outside
+ * [0, n_images) is reported by fleet_check as FLEET_ERR_ARG */
+int fleet_minibatch_device(fleet_ctx* ctx, const void* d_images, size_t n_images, int F, const void* d_labels,
+                           const void* d_idx, int B, const void* d_teacher, int num_labels, const float header[7],
+                           void* d_out, void* stream);
+/* host buffers: the B sampled rows are gathered into pinned staging, encoded on
+ * the GPU and returned (synchronous); FLEET_ERR_ARG for an index outside the set */
+int fleet_minibatch(fleet_ctx* ctx, const float* images, size_t n_images, int F, const int32_t* labels,
+                    const int32_t* idx, int B, const float* teacher, int num_labels, const float header[7],
+                    char* out, size_t cap, size_t* out_len);
+
 /* descentNative's model step -------------------------------
  * Server/src/main/c++/cppNN_backend.cpp:336-352: network::descent(vector)
  * (commonLib/cppNN/network.h:1185-1202) walks the gradients() layout of the

@@ -309,6 +309,9 @@ class Reference:
         L.ref_update.restype = lng
         L.ref_update.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, lng,
                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, lng]
+        L.ref_minibatch_noniid.restype = lng
+        L.ref_minibatch_noniid.argtypes = [C.c_void_p, C.c_void_p, lng, C.c_int, C.c_void_p, lng, C.c_int,
+                                           C.c_double, C.c_double, C.c_int, C.c_int, C.c_void_p, lng]
 
     def float2int(self, x):
         x = np.ascontiguousarray(x, dtype=np.float32)
@@ -383,6 +386,38 @@ class Reference:
         if not intermediates:
             return out[:n].tobytes()
         return out[:n].tobytes(), inter
+
+
+    def minibatch_noniid(self, images, labels, bucket, E: int, sigma: float, Cc: float, num_labels: int,
+                         batch: int) -> bytes:
+        """getMiniBatch (cppNN_backend.cpp:677-699) on the non-IID path for one
+        client whose bucket is `bucket` (cursor at 0)."""
+        images = np.ascontiguousarray(images, dtype=np.float32)
+        labels = np.ascontiguousarray(labels, dtype=np.int32)
+        bucket = np.ascontiguousarray(bucket, dtype=np.int32)
+        n, F = images.shape
+        B = batch * E
+        cap = b64_len(7 + B * (F + 1)) + 64
+        return self._call_bytes(self.lib.ref_minibatch_noniid, images.ctypes.data, labels.ctypes.data, n, F,
+                                bucket.ctypes.data, len(bucket), E, sigma, Cc, num_labels, batch, cap=cap)
+
+
+def minibatch_vector(images, labels, idx, header, teacher=None) -> np.ndarray:
+    """The float vector uniformSample / nonIIDSample build (cppNN_backend.cpp:
+    553-675): the 7 header values, then per sample its F features, (mode 1) the
+    teacher's numLabels probabilities, and its label as float; mode 1 appends
+    1234567. `header` = (E, sigma, C, lr, batchSize, featureSize, numLabels)
+    already in float, as push_back converts them."""
+    images = np.asarray(images, dtype=np.float32)
+    parts = [np.asarray(header, dtype=np.float32)]
+    for b, i in enumerate(idx):
+        parts.append(images[i])
+        if teacher is not None:
+            parts.append(np.asarray(teacher[b], dtype=np.float32))
+        parts.append(np.array([labels[i]], dtype=np.float32))
+    if teacher is not None:
+        parts.append(np.array([1234567], dtype=np.float32))
+    return np.concatenate(parts)
 
 
 class ReferenceModel:

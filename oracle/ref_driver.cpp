@@ -39,7 +39,20 @@ jbyteArray Java_utils_ByteVec_scalarMulNative(JNIEnv*, jobject, jbyteArray, jdou
 jbyteArray Java_utils_ByteVec_addNative(JNIEnv*, jobject, jbyteArray, jbyteArray);
 jbyteArray Java_utils_ByteVec_subtractNative(JNIEnv*, jobject, jbyteArray, jbyteArray);
 double Java_utils_ByteVec_getNorm(JNIEnv*, jobject, jbyteArray);
+jbyteArray Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch(JNIEnv*, jobject, jint);
 }
+
+// the sampler's state in cppNN_backend.cpp (file-scope globals, :47-64)
+extern int E;
+extern double sigma, C;
+extern int numLabels;
+extern bool iid;
+extern int numClients;
+extern int currClientID;
+extern std::vector<std::vector<int>> buckets;
+extern std::vector<int> bucketIdx;
+extern std::vector<std::vector<float>> sorted_images;
+extern std::vector<int> sorted_labels;
 
 namespace {
 JNIEnv g_env;
@@ -200,3 +213,32 @@ long ref_update(const char* const* uploads, const long* lens, int M, const doubl
 }
 
 }  // extern "C"
+
+extern "C" {
+// getMiniBatch (cppNN_backend.cpp:677-699) on the non-IID path (nonIIDSample
+// :636-675; the IID path's uniformSample runs the mode-1 teacher's forward in
+// this DISTILLATION_MODE=1 build). One client whose bucket is `bucket`
+// (indices into the label-sorted images), cursor at 0; E, sigma, C,
+// numLabels as given; the learning rate is the backend's `cnn` default.
+long ref_minibatch_noniid(const float* images, const int32_t* labels, long n_images, int F, const int32_t* bucket,
+                          long bucket_len, int E_, double sigma_, double C_, int num_labels, int batch, char* out,
+                          long cap) {
+  Quiet q;
+  sorted_images.assign((size_t)n_images, std::vector<float>());
+  sorted_labels.assign((size_t)n_images, 0);
+  for (long i = 0; i < n_images; ++i) {
+    sorted_images[(size_t)i].assign(images + (size_t)i * F, images + (size_t)(i + 1) * F);
+    sorted_labels[(size_t)i] = labels[i];
+  }
+  buckets.assign(1, std::vector<int>(bucket, bucket + bucket_len));
+  bucketIdx.assign(1, 0);
+  iid = false;
+  numClients = 1;
+  currClientID = 0;
+  E = E_;
+  sigma = sigma_;
+  C = C_;
+  numLabels = num_labels;
+  return take(Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch(&g_env, &g_this, batch), out, cap);
+}
+}
