@@ -111,6 +111,7 @@ def lib() -> C.CDLL:
         "fleet_model_version": (i32, [vp, vp, vp, i32, vp, sz, vp, vp]),
         "fleet_model_params_device": (i32, [vp, vp, sz, vp, sz, i32, vp, vp]),
         "fleet_minibatch_len": (sz, [i32, i32, i32, i32]),
+        "fleet_kardam_grads": (i32, [vp, vp, vp, i32, vp, C.c_double, vp, vp, sz, szp, vp, vp]),
         "fleet_minibatch_device": (i32, [vp, vp, sz, i32, vp, vp, i32, vp, i32, vp, vp, vp]),
         "fleet_minibatch": (i32, [vp, vp, sz, i32, vp, vp, i32, vp, i32, vp, vp, sz, szp]),
     }
@@ -453,6 +454,33 @@ class Codec:
         n = len(b) * int(graph_edges) + len(w)
         return self._text_call(self._L.fleet_model_params, (w.ctypes.data, len(w), b.ctypes.data, len(b),
                                                             int(graph_edges)), b64_len(n))
+
+    # -- Kardam bookkeeping ------------------------------------
+    def kardam_grads(self, uploads: Sequence, dampen: Sequence[float], lr: float, prev=None):
+        """For the M picked uploads (CppNNUpdater.java:463-481): the texts
+        g_c = getFlatGradient(u_c).scalarMultiply(d_c).scalarMultiply(lr), their norms and,
+        where prev[c] is given, the norms of g_c.subtract(prev[c]) (else NaN)."""
+        ups = [_as_bytes(u) for u in uploads]
+        M = len(ups)
+        if M == 0 or len(dampen) != M:
+            raise ValueError("one dampening factor per upload")
+        arr = (C.c_char_p * M)(*ups)
+        lens = np.array([len(u) for u in ups], dtype=np.uint64)
+        d = np.ascontiguousarray(dampen, dtype=np.float64)
+        pv = None
+        if prev is not None:
+            if len(prev) != M:
+                raise ValueError("one previous gradient (or None) per upload")
+            pv = (C.c_char_p * M)(*[(_as_bytes(x) if x is not None else None) for x in prev])
+        pitch = len(ups[0]) + 16
+        g = np.empty((M, pitch), np.uint8)
+        glen = C.c_size_t(0)
+        ng = np.empty(M, np.float64)
+        nd = np.empty(M, np.float64)
+        self._check(self._L.fleet_kardam_grads(self._h, C.cast(arr, C.c_void_p), lens.ctypes.data, M, d.ctypes.data,
+                                               float(lr), C.cast(pv, C.c_void_p) if pv is not None else None,
+                                               g.ctypes.data, pitch, C.byref(glen), ng.ctypes.data, nd.ctypes.data))
+        return [g[c, : glen.value].tobytes() for c in range(M)], ng, nd
 
     # -- getMiniBatch (SURVEY.md §8 f4) -------------------------------------------
     def getMiniBatch(self, images, labels, idx, header, teacher=None) -> bytes:  # noqa: N802  (cppNN_backend.cpp:677)

@@ -844,6 +844,75 @@ int fleet_model_params_device(fleet_ctx* c, const float* d_weights, size_t n_wei
   return FLEET_OK;
 }
 
+int fleet_kardam_grads(fleet_ctx* c, const char* const* uploads, const size_t* lens, int M, const double* dampen,
+                       double lr, const char* const* prev, char* g_out, size_t g_pitch, size_t* g_len,
+                       double* norm_g, double* norm_diff) {
+  if (!c || !uploads || !lens || !dampen || M <= 0 || !norm_g || !norm_diff) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  const size_t len = lens[0];
+  int rc = check_text_len(c, len);
+  if (rc) return rc;
+  for (int i = 0; i < M; ++i)
+    if (!uploads[i] || lens[i] != len)
+      return fail(c, FLEET_ERR_ARG, "upload %d has length %zu, expected %zu (one model layout)", i, lens[i], len);
+  const size_t n = fleet_b64_count(len);
+  std::vector<int32_t> hw(kHdrWords);
+  host_layout_parse(uploads[M - 1], (int64_t)n, FLEET_MAX_HEADERS, hw.data());
+  if (hw[0] != 0) return fail(c, FLEET_ERR_LAYOUT, "last upload's header does not describe a gradient layout");
+  const int nh = hw[1];
+  const size_t n_flat = (size_t)hw[2] - (size_t)nh;  // flatGrad stops after the last bias block
+  const size_t glen = fleet_b64_len(n_flat), gpad = round16(glen) + 16;
+  if (g_len) *g_len = glen;
+  if (!g_out || g_pitch < glen) return fail(c, FLEET_ERR_CAPACITY, "g row pitch %zu < %zu", g_pitch, glen);
+  const size_t pitch = round16(len);
+  bool any_prev = false;
+  for (int i = 0; prev && i < M; ++i) any_prev |= prev[i] != nullptr;
+  // staging: [uploads | prev rows | has_prev | dampen | header positions]; device adds [g rows | partials]
+  const size_t o_prev = pitch * (size_t)M, o_has = o_prev + (any_prev ? gpad * (size_t)M : 0);
+  const size_t o_damp = round16(o_has + (size_t)M), o_hdr = round16(o_damp + sizeof(double) * (size_t)M);
+  const size_t o_g = round16(o_hdr + sizeof(int32_t) * (size_t)(nh + 1));
+  const int64_t groups = (int64_t)groups_of(n_flat);
+  const int nblk = (int)((groups + 255) / 256);
+  const size_t o_part = round16(o_g + gpad * (size_t)M), o_end = o_part + sizeof(double) * 2 * (size_t)M * (nblk + 1);
+  if ((rc = grow_pinned(c, o_end))) return rc;
+  if ((rc = grow_dev(c, &c->d_a, &c->d_a_cap, o_end))) return rc;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));  // staging buffer reuse
+  uint8_t* h = c->h_stage;
+  for (int i = 0; i < M; ++i) {
+    std::memcpy(h + (size_t)i * pitch, uploads[i], len);
+    std::memset(h + (size_t)i * pitch + len, 0, pitch - len);
+    h[o_has + i] = (uint8_t)(prev && prev[i]);
+    if (any_prev) {
+      uint8_t* row = h + o_prev + (size_t)i * gpad;
+      std::memset(row, 'A', gpad);
+      if (prev[i]) std::memcpy(row, prev[i], glen);
+    }
+  }
+  std::memcpy(h + o_damp, dampen, sizeof(double) * (size_t)M);
+  std::memcpy(h + o_hdr, hw.data() + 4, sizeof(int32_t) * (size_t)nh);
+  uint8_t* d = c->d_a;
+  HIP_TRY(c, hipMemcpyAsync(d, h, o_g, hipMemcpyHostToDevice, c->stream));
+  int nb = 0;
+  HIP_TRY(c, fleet::launch_kardam_grads(d, pitch, M, (const int32_t*)(d + o_hdr), nh, (int64_t)n_flat,
+                                        (const double*)(d + o_damp), lr, any_prev ? d + o_prev : nullptr, gpad,
+                                        d + o_has, d + o_g, gpad, (double*)(d + o_part), &nb, c->d_err, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(h + o_g, d + o_g, o_end - o_g, hipMemcpyDeviceToHost, c->stream));
+  if ((rc = read_err(c, c->stream))) return rc;
+  const double* part = (const double*)(h + o_part);
+  for (int i = 0; i < M; ++i) {
+    std::memcpy(g_out + (size_t)i * g_pitch, h + o_g + (size_t)i * gpad, glen);
+    double sg = 0, sd = 0;
+    for (int b = 0; b < nb; ++b) {  // block partials in index order
+      sg += part[(size_t)i * 2 * nb + b];
+      sd += part[(size_t)i * 2 * nb + nb + b];
+    }
+    norm_g[i] = std::sqrt(sg);
+    norm_diff[i] = (prev && prev[i]) ? std::sqrt(sd) : std::nan("");
+  }
+  return FLEET_OK;
+}
+
 size_t fleet_minibatch_len(int F, int B, int num_labels, int with_teacher) {
   if (F < 0 || B < 0 || num_labels < 0) return 0;
   const size_t n = 7 + (size_t)B * ((size_t)F + (with_teacher ? (size_t)num_labels : 0) + 1) + (with_teacher ? 1 : 0);

@@ -33,6 +33,10 @@ hipError_t launch_elementwise(const uint8_t* a, const uint8_t* b, int op, double
                               int* d_err, hipStream_t s);
 hipError_t launch_norm_partials(const uint8_t* a, int64_t n, double* partials, int* nblocks, int* d_err,
                                 hipStream_t s);
+hipError_t launch_kardam_grads(const uint8_t* uploads, size_t pitch, int M, const int32_t* d_hdr, int n_hdr,
+                               int64_t n_flat, const double* d_dampen, double lr, const uint8_t* prev,
+                               size_t prev_pitch, const uint8_t* d_has_prev, uint8_t* g_out, size_t g_pitch,
+                               double* partials, int* nblocks, int* d_err, hipStream_t s);
 hipError_t launch_flat(const uint8_t* up, const int32_t* d_hdr, int n_hdr, int64_t n_flat, uint8_t* out,
                        int* d_err, hipStream_t s);
 hipError_t launch_merge(const uint8_t* up, const uint8_t* flat, const int32_t* d_hdr, int n_hdr, int64_t walk_end,

@@ -1109,6 +1109,74 @@ __global__ void __launch_bounds__(256) k_merge(const uint8_t* __restrict__ up, c
   *reinterpret_cast<uint4*>(out + 16 * g) = pad_group(b64_encode_group(o, &tab), r);
 }
 
+// Kardam bookkeeping of CppNNUpdater.update (Server/src/main/java/apps/cppNN/
+// CppNNUpdater.java:463-481) for M picked uploads at once:
+//   pickedGrad_c = getFlatGradient(upload_c).scalarMultiply(dampen_c)
+//   g_c          = pickedGrad_c.scalarMultiply(lr)            -> text out (flat layout)
+//   ||g_c||, ||g_c.subtract(prev_c)||                           (Kardam.setGrad, Kardam.java:48-62)
+// per flat value i (pos(i) skips the header slots, k_flat):
+//   y = Q(dec(code)), p = Q(f32(f64(y) d)), g = enc(f32(f64(p) lr)), G = dec(g),
+//   D = dec(enc(G - dec(prev_i))); partial sums of (double)(G*G), (double)(D*D)
+// (getNorm, cppNN_backend.cpp:779-795: float products summed in double) per
+// block and client; the host adds the partials in index order. Exact general
+// codec throughout (side work: once per picked upload, only under staleness
+// simulation in the reference).
+__global__ void __launch_bounds__(256) k_kardam_grads(const uint8_t* __restrict__ uploads, size_t pitch,
+                                                      const int32_t* __restrict__ hdr, int n_hdr, int64_t n_flat,
+                                                      const double* __restrict__ dampen, double lr,
+                                                      const uint8_t* __restrict__ prev, size_t prev_pitch,
+                                                      const uint8_t* __restrict__ has_prev,
+                                                      uint8_t* __restrict__ g_out, size_t g_pitch,
+                                                      double* __restrict__ partials, int64_t groups,
+                                                      int* __restrict__ err) {
+  __shared__ B64Tables tab;
+  __shared__ double red[2][256];
+  b64_tables_init(&tab);
+  __syncthreads();
+  const int c = blockIdx.y;
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint8_t* up = uploads + (size_t)c * pitch;
+  const bool hp = prev && has_prev[c];
+  const double d = dampen[c];
+  double sg = 0.0, sd = 0.0;
+  if (g < groups) {
+    const int r = (int)min<int64_t>(3, n_flat - 3 * g);
+    int32_t o[3] = {0, 0, 0};
+    uint32_t bad = 0;
+    for (int e = 0; e < r; ++e) {
+      const int64_t i = 3 * g + e;
+      int64_t pos = i;
+      for (int h = 0; h < n_hdr; ++h)
+        if (hdr[h] <= pos) ++pos;
+      const float y = q(dec(code_at(up, pos, &tab, &bad)));
+      const float pv = q((float)((double)y * d));
+      o[e] = enc((float)((double)pv * lr));
+      const float G = dec(o[e]);
+      sg += (double)(G * G);
+      if (hp) {
+        const float D = q(G - dec(code_at(prev + (size_t)c * prev_pitch, i, &tab, &bad)));
+        sd += (double)(D * D);
+      }
+    }
+    if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
+    *reinterpret_cast<uint4*>(g_out + (size_t)c * g_pitch + 16 * g) = pad_group(b64_encode_group(o, &tab), r);
+  }
+  red[0][threadIdx.x] = sg;
+  red[1][threadIdx.x] = sd;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + w];
+      red[1][threadIdx.x] += red[1][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    partials[(size_t)c * 2 * gridDim.x + blockIdx.x] = red[0][0];
+    partials[(size_t)c * 2 * gridDim.x + gridDim.x + blockIdx.x] = red[1][0];
+  }
+}
+
 // network::flatGrad's header walk (network.h:1206-1223), one thread.
 // out[0] = status (0 ok, 1 malformed), out[1] = n_headers, out[2] = walk end,
 // out[4..] = header positions.
@@ -1362,6 +1430,19 @@ hipError_t launch_norm_partials(const uint8_t* a, int64_t n, double* partials, i
   *nblocks = (int)blocks_for(groups, 256);
   if (groups == 0) return hipSuccess;
   hipLaunchKernelGGL(k_norm_partials, dim3(*nblocks), dim3(256), 0, s, a, n, partials, groups, d_err);
+  return hipGetLastError();
+}
+
+hipError_t launch_kardam_grads(const uint8_t* uploads, size_t pitch, int M, const int32_t* d_hdr, int n_hdr,
+                               int64_t n_flat, const double* d_dampen, double lr, const uint8_t* prev,
+                               size_t prev_pitch, const uint8_t* d_has_prev, uint8_t* g_out, size_t g_pitch,
+                               double* partials, int* nblocks, int* d_err, hipStream_t s) {
+  const int64_t groups = (n_flat + 2) / 3;
+  *nblocks = (int)blocks_for(groups, 256);
+  if (groups == 0 || M == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_kardam_grads, dim3((unsigned)*nblocks, (unsigned)M), dim3(256), 0, s, uploads, pitch, d_hdr,
+                     n_hdr, n_flat, d_dampen, lr, prev, prev_pitch, d_has_prev, g_out, g_pitch, partials, groups,
+                     d_err);
   return hipGetLastError();
 }
 

@@ -68,6 +68,63 @@ def similarity(x: Sequence[int], y: Sequence[int]) -> float:
     return b
 
 
+class Kardam:
+    """utils/Kardam.java's bookkeeping (setGrad :48-62, setModel :93-106, updateLip
+    :190-203) with its O(N) vector work on the GPU: the gradient texts and norms of
+    all picked uploads come from one ``Codec.kardam_grads`` call,
+    the model-difference norm from ``subtractNative`` + ``getNorm``. ``checkByz``
+    is not rebuilt: CppNNUpdater bypasses it (``if (true || ...)``, :488)."""
+
+    def __init__(self, codec, workers: int = 10):
+        self.codec = codec
+        self.workers = workers
+        self.grads = {}           # worker -> (g text, epoch)
+        self.models = {}          # worker -> model text
+        self.model_diff_norm = {}
+        self.grad_diff_norm = {}
+        self.lips = {}
+
+    def set_grads(self, worker_ids, uploads, dampen, lr: float, epochs):
+        """setGrad for each picked upload: one device pass computes every g_c and its
+        difference norm to the worker's previous g. Returns the setGrad results."""
+        worker_ids = list(worker_ids)
+        if len(set(worker_ids)) < len(worker_ids):  # a worker twice in one batch: its pushes in order
+            out = []
+            for i in range(len(worker_ids)):
+                out += self.set_grads(worker_ids[i:i + 1], uploads[i:i + 1], dampen[i:i + 1], lr, epochs[i:i + 1])
+            return out
+        prev = [self.grads[w][0] if w in self.grads else None for w in worker_ids]
+        texts, _, diff = self.codec.kardam_grads(uploads, dampen, lr, prev)
+        out = []
+        for w, g, dn, ep in zip(worker_ids, texts, diff, epochs):
+            if w in self.grads:
+                if self.grads[w][1] == ep:  # same epoch as the previous push: ignored
+                    out.append(False)
+                    continue
+                self.grad_diff_norm[w] = float(dn)
+                self.grads[w] = (g, ep)
+                out.append(True)
+            else:
+                self.grads[w] = (g, ep)
+                out.append(False)
+        return out
+
+    def set_model(self, worker: int, model_text: bytes) -> None:
+        if worker in self.models:
+            norm = self.codec.getNorm(self.codec.subtractNative(model_text, self.models[worker]))
+            if norm == 0:  # same model as before: ignored
+                return
+            self.model_diff_norm[worker] = norm
+        self.models[worker] = model_text
+
+    def update_lip(self, worker: int) -> None:
+        lip = self.grad_diff_norm[worker] / self.model_diff_norm[worker]
+        lst = self.lips.setdefault(worker, [])
+        if len(lst) > 25:
+            lst.pop(0)
+        lst.append(lip)
+
+
 @dataclass
 class Pending:
     upload: bytes

@@ -220,6 +220,20 @@ int fleet_model_params(fleet_ctx* ctx, const float* weights, size_t n_weights, c
  * images: n_images x F fp32 rows; labels: n_images int32. Output:
  * fleet_minibatch_len(F, B, num_labels, teacher != NULL) bytes. */
 size_t fleet_minibatch_len(int F, int B, int num_labels, int with_teacher);
+
+/* Kardam bookkeeping of CppNNUpdater.update (Server/src/main/java/apps/cppNN/
+ * CppNNUpdater.java:463-481, utils/Kardam.java:48-62) for the M
+ * picked uploads in one call:
+ *   g_c = ByteVec(getFlatGradient(upload_c)).scalarMultiply(dampen_c).scalarMultiply(lr)
+ * (flat Base64, the text Kardam.setGrad stores), norm_g[c] = g_c.getNorm() and,
+ * when prev[c] != NULL (the worker's previous g, same length),
+ * norm_diff[c] = g_c.subtract(prev[c]).getNorm(), else NaN. The uploads share
+ * the last one's layout (as fleet_update enforces). g_out: M rows of g_pitch
+ * bytes (>= *g_len). Norms: partial sums of the reference's fp64 loop in a
+ * different order (1e-12 relative). */
+int fleet_kardam_grads(fleet_ctx* ctx, const char* const* uploads, const size_t* lens, int M, const double* dampen,
+                       double lr, const char* const* prev, char* g_out, size_t g_pitch, size_t* g_len,
+                       double* norm_g, double* norm_diff);
 /* device-resident dataset, indices (d_idx[B]) and output; an index outside
  * [0, n_images) is reported by fleet_check as FLEET_ERR_ARG */
 int fleet_minibatch_device(fleet_ctx* ctx, const void* d_images, size_t n_images, int F, const void* d_labels,

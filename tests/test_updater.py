@@ -1,6 +1,7 @@
 """Host-side mirror of CppNNUpdater (fleet_amd/updater.py): getDampen policies,
 label similarity, and (GPU) a full M-softsync update + model step vs the oracle."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -59,3 +60,63 @@ def test_updater_two_rounds_vs_oracle(codec, oracle):
                                 np.float32(lrates[r]))
         assert np.array_equal(up.weights.view(np.uint32), ew.view(np.uint32))
         assert np.array_equal(up.fc_bias.view(np.uint32), eb.view(np.uint32))
+
+
+# -- Kardam bookkeeping -------------------------------------------------
+KARDAM = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "kardam.npz")
+
+
+def _kardam_fixture():
+    z = np.load(KARDAM)
+    M = len(z["d"])
+    ups = [z[f"u{c}"].tobytes() for c in range(M)]
+    prev = [z[f"prev{c}"].tobytes() for c in range(M)]
+    return z, M, ups, prev
+
+
+def test_oracle_kardam_chain_matches_reference_fixture(oracle):
+    """The oracle's per-op chain (flat -> x d -> x lr, subtract, norm) against the
+    reference's own natives run through the same chain."""
+    z, M, ups, prev = _kardam_fixture()
+    lr = float(z["lr"][0])
+    for c in range(M):
+        g = oracle.scalar_mul(oracle.scalar_mul(oracle.flat_gradient(ups[c]), float(z["d"][c])), lr)
+        assert g == z[f"g{c}"].tobytes()
+        assert oracle.norm(g) == pytest.approx(float(z[f"norm_g{c}"][0]), rel=1e-12)
+        assert oracle.norm(oracle.subtract(g, prev[c])) == pytest.approx(float(z[f"norm_diff{c}"][0]), rel=1e-12)
+
+
+@pytest.mark.gpu
+def test_device_kardam_grads_match_reference_fixture(codec):
+    z, M, ups, prev = _kardam_fixture()
+    texts, ng, nd = codec.kardam_grads(ups, z["d"], float(z["lr"][0]), prev)
+    for c in range(M):
+        assert texts[c] == z[f"g{c}"].tobytes()
+        assert ng[c] == pytest.approx(float(z[f"norm_g{c}"][0]), rel=1e-12)
+        assert nd[c] == pytest.approx(float(z[f"norm_diff{c}"][0]), rel=1e-12)
+    texts2, ng2, nd2 = codec.kardam_grads(ups, z["d"], float(z["lr"][0]), [None, prev[1], None, prev[3]])
+    assert texts2 == texts and np.isnan(nd2[0]) and np.isnan(nd2[2]) and nd2[1] == nd[1]
+
+
+@pytest.mark.gpu
+def test_kardam_mirror_lips(codec):
+    """Kardam.setGrad / setModel / updateLip over two rounds: the Lipschitz value is
+    ||g - g_prev|| / ||model - model_prev|| from the device norms."""
+    from fleet_amd.updater import Kardam
+    z, M, ups, prev = _kardam_fixture()
+    k = Kardam(codec)
+    lr = float(z["lr"][0])
+    assert k.set_grads([0, 1], ups[:2], z["d"][:2], lr, [0, 0]) == [False, False]
+    assert k.set_grads([0, 1], ups[2:4], z["d"][2:4], lr, [1, 0]) == [True, False]  # worker 1: same epoch
+    m0 = codec.encode_floats(np.linspace(0, 1, 300, dtype=np.float32))
+    m1 = codec.encode_floats(np.linspace(0, 2, 300, dtype=np.float32))
+    k.set_model(0, m0)
+    k.set_model(0, m1)
+    k.update_lip(0)
+    g0 = codec.scalarMulNative(codec.scalarMulNative(codec.getFlatGradient(ups[0]), float(z["d"][0])), lr)
+    g2 = codec.scalarMulNative(codec.scalarMulNative(codec.getFlatGradient(ups[2]), float(z["d"][2])), lr)
+    want = codec.getNorm(codec.subtractNative(g2, g0)) / codec.getNorm(codec.subtractNative(m1, m0))
+    assert k.lips[0] == [pytest.approx(want, rel=1e-12)]
+    # a worker twice in one batch: its pushes in order
+    k2 = Kardam(codec)
+    assert k2.set_grads([5, 5], ups[:2], z["d"][:2], lr, [0, 1]) == [False, True]
