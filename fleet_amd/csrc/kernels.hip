@@ -77,61 +77,12 @@ __device__ __forceinline__ uint32_t header_bits(const int32_t* __restrict__ hdr,
   return (uint32_t)ih[0] | ((uint32_t)ih[1] << 1) | ((uint32_t)ih[2] << 2);
 }
 
-// ----------------------------------------------------------------------------
-// Rare-value compaction. The fast paths (codec_math.h) cover |value| < 1 and
-// upload codes whose last digit is 0 -- gradients, in practice. The other
-// values of a stage are gathered, across the whole wave, into a per-wave LDS
-// list, run through the general exact codec by consecutive lanes, and
-// scattered back: one general pass per wave and stage instead of one per
-// value slot, while the fast path stays branch-free for every lane.
-// KIND 0: in = upload code, out = Q(int2float(code)); KIND 1: in = x, out = Q(x);
-// KIND 2: in = code, out = int2float(code).
-template <int S, int KIND>
-__device__ __forceinline__ void resolve_slow(float (&out)[S], const uint32_t (&in)[S], uint32_t slow,
-                                             uint32_t* __restrict__ wscratch, int lane) {
-  if (__ballot(slow != 0) == 0) return;  // wave-uniform
-  uint32_t count = 0;
-  int pos[S];
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    const bool f = (slow >> i) & 1u;
-    const unsigned long long b = __ballot(f);
-    if (b) {
-      if (f) {
-        const int p = (int)count + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
-                                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-        wscratch[p] = in[i];
-        pos[i] = p;
-      }
-      count += (uint32_t)__popcll(b);
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  for (uint32_t base = 0; base < count; base += 64) {
-    const uint32_t idx = base + (uint32_t)lane;
-    if (idx < count) {
-      const uint32_t v = wscratch[idx];
-      const float r = KIND == 0 ? q(dec((int32_t)v)) : KIND == 1 ? q(u2f(v)) : dec((int32_t)v);
-      wscratch[idx] = f2u(r);
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-  for (int i = 0; i < S; ++i)
-    if ((slow >> i) & 1u) out[i] = u2f(wscratch[pos[i]]);
-}
-
 // out[i] = Q(x[i]) for a stage of S values: fixed 9-step chains when the
 // whole wave is in |x| < 1, else the multiplier-table chains (codec_math.h:
-// no selects, no packed ops -- the cheap encodings on gfx950); resolve_slow for
-// the values outside the q_gen domain.
+// no selects, no packed ops -- the cheap encodings on gfx950); the general
+// codec, per lane, for the values outside the q_gen domain.
 template <int S>
-__device__ __forceinline__ void q_stage(float (&out)[S], const float (&x)[S], const B64Tables* tab,
-                                        uint32_t* __restrict__ ws, int lane) {
+__device__ __forceinline__ void q_stage(float (&out)[S], const float (&x)[S], const B64Tables* tab) {
   // integer magnitude tests (an f32 compare with |.| is a 6-cycle e64 op):
   // the whole wave is in |x| < 1 iff the largest |x| bit pattern is
   uint32_t ab[S], amax = 0;
@@ -152,14 +103,10 @@ __device__ __forceinline__ void q_stage(float (&out)[S], const float (&x)[S], co
     dmax = max(dmax, d[i]);
     out[i] = q_mt_d(x[i], d[i], tab->mt);
   }
-  if (__ballot(dmax > 9u) != 0) {  // values outside the q_gen domain (rare)
-    uint32_t slow = 0, in[S];
+  if (__ballot(dmax > 9u) != 0) {  // values outside the q_gen domain (rare): the general codec, per lane
 #pragma unroll
-    for (int i = 0; i < S; ++i) {
-      slow |= (uint32_t)(d[i] == kSlowDigits) << i;
-      in[i] = f2u(x[i]);
-    }
-    resolve_slow<S, 1>(out, in, slow, ws, lane);
+    for (int i = 0; i < S; ++i)
+      if (d[i] == kSlowDigits) out[i] = q(x[i]);
   }
 }
 
@@ -210,18 +157,6 @@ __device__ __forceinline__ void dec_stage(float (&out)[S], const int32_t (&codes
   }
 }
 
-// Single value per thread on a latency-bound serial chain: same as q_stage<1>
-// but the digit count comes from compares (no LDS load inside the chain).
-__device__ __forceinline__ void q_stage_lat(float (&out)[1], const float (&x)[1], uint32_t* __restrict__ ws,
-                                            int lane) {
-  if (__ballot(!q_ok(x[0])) == 0) {
-    out[0] = q_fast(x[0]);
-    return;
-  }
-  out[0] = q_gen_lat(x[0]);
-  uint32_t in[1] = {f2u(x[0])};
-  resolve_slow<1, 1>(out, in, (uint32_t)!q_gen_ok(x[0]), ws, lane);
-}
 
 // ----------------------------------------------------------------------------
 // One merged slot (mergeFlatGradient, cppNN_backend.cpp:722-750, after
@@ -350,8 +285,8 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
 
     // Per stage and wave: if every value of the wave is inside the |x| < 1
     // fast domain, run the fixed 9-step chains; otherwise the 2+1+2+4-step
-    // variable chains (numDigits <= 7). Values outside both go through the
-    // general codec via resolve_slow (|x| >= 1e7: never for gradients).
+    // variable chains (numDigits <= 9). Values outside both are recomputed
+    // with the general codec at the end (|x| >= 1e8: never for gradients).
     // stage A: y = Q(int2float(code))
     float y0[S], y[S];
     dec_stage<S>(y0, codes, &tab);
@@ -413,7 +348,6 @@ template <int TG, int NW = 4>
 struct TileShared {
   static constexpr int E = 3 * TG;
   B64Tables tab;
-  uint32_t scratch[NW][64 * 6];  // resolve_slow compaction, one list per wave
   int32_t last_codes[E];        // codes of the last upload (mergeFlatGradient's g)
   int32_t hmin[E], hmax[E];     // header-slot codes over all uploads (layout check)
   uint32_t hmask[TG];           // bit e = slot 3*g+e is a header slot
@@ -478,8 +412,6 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileI
                                              const double* __restrict__ dampen, int64_t n_up, int64_t g0,
                                              float* __restrict__ pdst, uint32_t& badacc) {
   constexpr int E = 3 * TG, S = 3 * IPT;
-  const int lane = threadIdx.x & 63;
-  uint32_t* ws = sh.scratch[threadIdx.x >> 6];
   int32_t codes[S];
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
@@ -506,7 +438,7 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileI
   // stage A: y = Q(int2float(code))
   float y0[S], y[S];
   dec_stage<S>(y0, codes, &sh.tab);
-  q_stage<S>(y, y0, &sh.tab, ws, lane);
+  q_stage<S>(y, y0, &sh.tab);
   // stage B: p = Q(f32(f64(y) * d)), per-item client
   float r[S], p[S];
 #pragma unroll
@@ -515,7 +447,7 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileI
 #pragma unroll
     for (int e = 0; e < 3; ++e) r[3 * h + e] = (float)((double)y[3 * h + e] * d);
   }
-  q_stage<S>(p, r, &sh.tab, ws, lane);
+  q_stage<S>(p, r, &sh.tab);
 #pragma unroll
   for (int h = 0; h < IPT; ++h)
     if (it.live[h])
@@ -586,7 +518,13 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
                                                       int* __restrict__ err) {
   constexpr int E = 3 * TG;
   static_assert(E <= 256, "phase 2 is one thread per value");
-  constexpr int CM = 6144 / E;  // 24 KiB of p per chunk
+#ifndef FLEET_TILED_PT
+#define FLEET_TILED_PT 3072
+#endif
+  // p floats per chunk: 12 KiB (CM = 16 clients at TG = 64, so a chunk is two full
+  // 512-item passes); with the tables the block fits 7 per CU (measured: 24 KiB
+  // chunks 0.40 ms, 12 KiB 0.37, 8 KiB 0.50, 16 KiB 0.43 on cifar10_256)
+  constexpr int CM = FLEET_TILED_PT / E;
   FLEET_TSTAMP(0);
   __shared__ TileShared<TG> sh;
   __shared__ float ptile[CM * E];
