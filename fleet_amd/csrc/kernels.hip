@@ -1212,12 +1212,13 @@ hipError_t launch_descent(float* weights, float* fc_bias, const float* grad, con
 
 static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
 
-// groups per lane: as many as keep >= ~4 waves per SIMD busy (256 CUs x 4 SIMDs)
+// groups per lane of the stream kernel: 1 at every size measured -- 1M floats
+// x 256: 1.64 / 1.85 / 2.63 ms for K = 1 / 2 / 4 (before the multiplier-table
+// codec); 4M floats x 4096: 59.2 / 83.5 / 115.7 ms. More lanes in flight beat
+// fewer table copies (a lane walks all M clients, the copy is amortised anyway).
 int update_groups_per_lane(int64_t groups) {
+  (void)groups;
   if (const char* e = getenv("FLEET_UPDATE_K")) return atoi(e);
-  const int64_t lanes_for_4_waves = 256LL * 4 * 4 * 64;
-  if (groups >= 4 * lanes_for_4_waves) return 4;
-  if (groups >= 2 * lanes_for_4_waves) return 2;
   return 1;
 }
 
