@@ -36,6 +36,7 @@ WORKLOADS = {
     "synth4m_4096": ("synth4m", 4096, "configs[4]: synthetic 4M-float buckets x 4096 clients"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md:36
+HBM_COPY_GBS = 6290.0  # measured copy ceiling, same line (SURVEY.md §8d asks for both)
 
 
 def dampen_policy(M: int):
@@ -211,6 +212,17 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
     return res
 
 
+def sq_valu(workload: str, kernel: str):
+    """VALU lane-instructions per (client, value) of the profiled kernel
+    (profiles/r01/sq.json, SQ_INSTS_VALU pass), None when not profiled."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r01", "sq.json")) as f:
+            v = json.load(f)["workloads"][workload][kernel]["valu_lane_instr_per_element_client"]
+        return float(v)
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def pmc_traffic(workload: str, kernel: str = ""):
     """HBM bytes per k_update launch for `workload` from the newest committed
     rocprofv3 PMC summary (profiles/rNN/traffic.json, written by
@@ -287,6 +299,34 @@ def cpu_baseline(budget_s: float = 20.0):
             break
     per = t_total / reps
     value = M * MNIST.n_up * 4 / per / 2**30
+    # SURVEY.md §8d's other CPU legs, on the same sample (the aggregation chain only):
+    # the reference at -O2 on 1 core, the C restatement's fused chain on all the
+    # cores this process may use (OpenMP)
+    also = {}
+    ups = [o.encode_floats(v) for v in floats]
+
+    def rate(fn, budget=3.0):
+        n, t = 0, 0.0
+        while t < budget and n < 20:
+            t0 = time.perf_counter()
+            fn()
+            t += time.perf_counter() - t0
+            n += 1
+        return M * MNIST.n_up * 4 / (t / n) / 2**30, t / n
+    o2 = os.path.join(ROOT, "oracle", "_ref", "libfleetref_O2.so")
+    if os.path.exists(o2):
+        try:
+            r2 = pyoracle.Reference(o2)
+            v2, s2 = rate(lambda: r2.update(ups, d))
+            also["reference_O2_1core"] = {"value": v2, "unit": "GiB/s", "cores": 1, "s_per_update": s2}
+        except OSError:
+            pass
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
+    hm = o.header_mask(list(MNIST.w_sizes), list(MNIST.b_sizes))
+    vp, sp = rate(lambda: o.update_fused(ups, d, hm, threads=threads))
+    also["port_fused_openmp"] = {"value": vp, "unit": "GiB/s", "cores": threads, "s_per_update": sp}
+    also["note"] = "aggregation chain only (CppNNUpdater.update on pre-encoded uploads), same MNIST x 64 sample"
     import platform
     cpu = platform.processor() or "x86_64"
     try:
@@ -300,7 +340,7 @@ def cpu_baseline(budget_s: float = 20.0):
     return {"value": value, "unit": "GiB/s", "cores": 1, "kind": kind,
             "sample": f"MNIST layout (22,961 floats) x 64 clients: client encode + CppNNUpdater.update chain, "
                       f"{reps} rep(s), {per:.3f} s/rep, {'oracle/_ref -O0 (reference C++)' if kind == 'reference' else 'oracle faithful port -O2'}",
-            "cpu_model": cpu, "host_nproc": os.cpu_count()}
+            "cpu_model": cpu, "host_nproc": os.cpu_count(), "also": also}
 
 
 def main():
@@ -370,6 +410,8 @@ def main():
                    "dampening": "policy 1 inverse, tau = c mod 3"},
         "roofline": {"bound": "hbm", "kernel": r["update_kernel"], "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "frac_of_copy_ceiling": achieved / HBM_COPY_GBS,
+                     "valu_lane_instr_per_element_client": sq_valu(args.workload, r["update_kernel"]),
                      "traffic": traffic[0] if traffic else None,
                      "traffic_source": f"{traffic[2]} ({traffic[1]})" if traffic else None,
                      "bytes_per_launch": r["update_bytes"], "kernel_ms": r["update_kernel_ms"]},
