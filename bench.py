@@ -6,11 +6,13 @@ already resident in HBM:
   1. client-side encode  (Base64::encode(vector<float>) of every bucket; k_encode_f32)
   2. server aggregation  (CppNNUpdater.update's decode/dampen/sum/average/merge
                           chain, bit-exact; k_update) -> merged Base64 + fp32
-  3. N>1 only: all_gather of the merged element-range shards over RCCL.
 
 Multi-GPU: element-range sharding, weak scaling -- every rank owns
-a fixed slice of G 3-value groups of a model N times larger; no collective in
-the data path, one all_gather of the merged slices (the real exchange step).
+a fixed slice of G 3-value groups of a model N times larger. No collective in the
+data path: each rank's merged slice stays resident for its slice of the model
+step (fleet_descent_device), as the whole merged vector does at N=1; the
+all_gather of the slices (fleet_amd.shard, for a caller that needs the full
+vector) is timed separately and reported as `exchange_ms`, after the timed steps.
 
 Output: ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
 """
@@ -121,11 +123,11 @@ def steps_per_graph(steps: int, cap: int = 10) -> int:
 
 
 def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=True):
-    """Times `steps` steps. graph=True: the local part of a step (encode +
-    aggregation) is captured once into a HIP graph of G steps and replayed
-    steps/G times (the all_gather, N>1, stays eager after each replay);
+    """Times `steps` steps. graph=True: a step (encode + aggregation) is
+    captured once into a HIP graph of G steps and replayed steps/G times;
     graph=False: eager launches (host launch gaps between the small kernels
-    included). Both variants are reported."""
+    included). Both variants are reported. N>1: the all_gather of the merged
+    slices is timed after the steps, on its own (exchange_ms)."""
     import fleet_amd as F
     from fleet_amd.layouts import LAYOUTS
     lay_name, M, note = WORKLOADS[name]
@@ -141,7 +143,10 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
 
     def exchange():
         if world > 1:
-            dist.all_gather_into_tensor(gathered, sh.merged)
+            if dist.get_backend() == "gloo":  # CPU-collective rehearsal (FLEET_BENCH_BACKEND=gloo)
+                dist.all_gather(list(gathered.chunk(world)), sh.merged)
+            else:
+                dist.all_gather_into_tensor(gathered, sh.merged)
 
     def run_timed(body, count):
         torch.cuda.synchronize()
@@ -159,14 +164,10 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
 
     for _ in range(warmup):
         local()
-        exchange()
     torch.cuda.synchronize()
     codec.check()
 
-    def eager_step():
-        local()
-        exchange()
-    eager_elapsed = run_timed(eager_step, steps)
+    eager_elapsed = run_timed(local, steps)
     codec.check()
     eager_ms = eager_elapsed / steps * 1e3
 
@@ -183,17 +184,23 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
         for _ in range(max(1, warmup // G)):
             g.replay()
 
-        def graph_block():
-            g.replay()
-            for _ in range(G if world > 1 else 0):  # N>1: every step's all_gather, eager
-                exchange()
-        elapsed = run_timed(graph_block, steps // G)
+        elapsed = run_timed(g.replay, steps // G)
         codec.check()
         del g
+    exchange_ms = None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=sh.merged.device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        # the slices gathered once (RCCL all_gather over xGMI), timed on its own, and
+        # checked: this rank's slice of the gathered vector is its merged output
+        exchange()
+        xt = run_timed(exchange, 5) / 5
+        t = torch.tensor([xt], dtype=torch.float64, device=sh.merged.device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        exchange_ms = float(t.item()) * 1e3
+        if not torch.equal(gathered[rank * sh.pitch:(rank + 1) * sh.pitch], sh.merged):
+            raise RuntimeError("all_gather returned a different merged slice")
     ms = elapsed / steps * 1e3
     total_bytes_fp32 = world * M * sh.n_local * 4
     gib_s = total_bytes_fp32 / (elapsed / steps) / 2**30
@@ -201,7 +208,7 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
     res = {
         "workload": name, "note": note, "layout": lay_name, "clients": M, "n_up_per_rank": sh.n_local,
         "ms_per_step": ms, "gib_s": gib_s, "update_kernel_ms": upd_ms, "encode_kernel_ms": enc_ms,
-        "graph": graph, "steps_per_graph": G, "eager_ms_per_step": eager_ms,
+        "graph": graph, "steps_per_graph": G, "eager_ms_per_step": eager_ms, "exchange_ms": exchange_ms,
         "update_kernel": F.update_kernel(sh.L),
         "update_bytes": upd_b, "encode_bytes": enc_b,
         "update_gbs": upd_b / (upd_ms * 1e-3) / 1e9, "encode_gbs": enc_b / (enc_ms * 1e-3) / 1e9,
@@ -364,10 +371,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal of the N>1 path on a one-GPU box: every rank on device 0, gloo collectives
+    # (FLEET_BENCH_SAME_DEVICE=1 FLEET_BENCH_BACKEND=gloo); the driver's runs use one GPU per rank over RCCL
+    if os.environ.get("FLEET_BENCH_SAME_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("FLEET_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     import fleet_amd as F
     codec = F.Codec(local)
 
@@ -418,6 +433,9 @@ def main():
         "cpu_baseline": cpu,
         "timing": {"graph": bool(r["graph"]), "steps_per_graph": r["steps_per_graph"],
                    "eager_ms_per_step": r["eager_ms_per_step"],
+                   "exchange_ms": r["exchange_ms"],
+                   "exchange": "none in the timed steps (element shards stay resident); N>1: one all_gather of "
+                               "the merged slices timed separately (exchange_ms, max over ranks) and checked",
                    "kernel_ms": "HIP events around graph replays of 10 back-to-back launches"},
         "kernels": {"k_update_ms": r["update_kernel_ms"], "k_encode_f32_ms": r["encode_kernel_ms"],
                     "k_encode_gbs": r["encode_gbs"], "element_clients_per_s": r["element_clients_per_s"]},
