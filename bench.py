@@ -9,10 +9,10 @@ already resident in HBM:
 
 Multi-GPU: element-range sharding, weak scaling -- every rank owns
 a fixed slice of G 3-value groups of a model N times larger. No collective in the
-data path: each rank's merged slice stays resident for its slice of the model
-step (fleet_descent_device), as the whole merged vector does at N=1; the
-all_gather of the slices (fleet_amd.shard, for a caller that needs the full
-vector) is timed separately and reported as `exchange_ms`, after the timed steps.
+data path: each rank's merged slice (its share of the model delta) stays
+resident on its GPU, as the whole merged vector does at N=1; the all_gather of
+the slices (fleet_amd.shard, for a caller that needs the full vector) is timed
+separately and reported as `exchange_ms`, after the timed steps.
 
 Output: ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
 """
