@@ -39,6 +39,12 @@ WORKLOADS = {
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md:36
 HBM_COPY_GBS = 6290.0  # measured copy ceiling, same line (SURVEY.md §8d asks for both)
+# what actually bounds each aggregation kernel: none is HBM-bound
+LIMITER = {
+    "k_update_pipe": "latency of the serial client chain (one consumer wave per tile; DESIGN.md 4.2)",
+    "k_update_tiled": "VALU issue (exact chain, ~178 VALU instructions per client-value)",
+    "k_update": "VALU issue (exact chain, ~172 VALU instructions per client-value)",
+}
 
 
 def dampen_policy(M: int):
@@ -426,6 +432,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": r["update_kernel"], "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "frac_of_copy_ceiling": achieved / HBM_COPY_GBS,
+                     "limiter": LIMITER.get(r["update_kernel"].split("<")[0], "VALU issue"),
                      "valu_lane_instr_per_element_client": sq_valu(args.workload, r["update_kernel"]),
                      "traffic": traffic[0] if traffic else None,
                      "traffic_source": f"{traffic[2]} ({traffic[1]})" if traffic else None,
