@@ -121,6 +121,31 @@ def test_update_vs_elementwise_oracle(codec, oracle, layout, M):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
+def test_update_cifar100_layout(codec, oracle):
+    """configs[3]'s layout (CIFAR-100 cppNN, 17 header slots) on a few clients."""
+    from fleet_amd.layouts import CIFAR100
+    ups = uploads_for(oracle, CIFAR100, 3, seed=17)
+    d = policy("exp", 3)
+    hm = oracle.header_mask(list(CIFAR100.w_sizes), list(CIFAR100.b_sizes))
+    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
+
+
+def test_update_malformed_last_header(codec, oracle):
+    """The host walk of the last upload's header fails: the device flow reports the
+    same error a full device run would (layout, or Base64 when a char is invalid)."""
+    lay = synthetic(3000)
+    ups = uploads_for(oracle, lay, 3, seed=5)
+    v = oracle.decode_floats(ups[-1])
+    v[1] = 5000.0  # the first W block claims more values than the upload holds
+    bad_walk = oracle.encode_floats(v)
+    with pytest.raises(F.LayoutError):
+        codec.update([ups[0], ups[1], bad_walk], [1.0, 1.0, 1.0])
+    bad_char = bytearray(bad_walk)
+    bad_char[2] = ord("*")  # inside the first group: the header count itself
+    with pytest.raises(F.Base64Error):
+        codec.update([ups[0], ups[1], bytes(bad_char)], [1.0, 1.0, 1.0])
+
+
 def test_update_layout_mismatch_rejected(codec, oracle):
     a = uploads_for(oracle, synthetic(3000), 2, seed=3)
     b = uploads_for(oracle, Layout("x", (1000, 1996), ()), 1, seed=3)
