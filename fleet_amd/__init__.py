@@ -112,6 +112,7 @@ def lib() -> C.CDLL:
         "fleet_model_params_device": (i32, [vp, vp, sz, vp, sz, i32, vp, vp]),
         "fleet_minibatch_len": (sz, [i32, i32, i32, i32]),
         "fleet_kardam_grads": (i32, [vp, vp, vp, i32, vp, C.c_double, vp, vp, sz, szp, vp, vp]),
+        "fleet_descent_window_device": (i32, [vp, vp, vp, vp, sz, sz, vp, vp, i32, vp, vp, i32, C.c_float, vp]),
         "fleet_minibatch_device": (i32, [vp, vp, sz, i32, vp, vp, i32, vp, i32, vp, vp, vp]),
         "fleet_minibatch": (i32, [vp, vp, sz, i32, vp, vp, i32, vp, i32, vp, vp, sz, szp]),
     }
@@ -536,6 +537,17 @@ class Codec:
                                           len(g), ws.ctypes.data, wp.ctypes.data, len(ws), bs.ctypes.data,
                                           fc.ctypes.data, len(bs), float(lr)))
         return w, b
+
+    def descent_window_device(self, weights_f32, fc_bias_f32, grad_window_f32, value_begin: int, value_end: int,
+                              layout, lr: float, stream=None):
+        """The model step of one element shard: grad_window_f32 holds the merged fp32 values
+        [value_begin, value_end); only the parameters those positions cover are updated."""
+        ws, wp, bs, fc = self._layout_args(layout)
+        self._check(self._L.fleet_descent_window_device(self._h, weights_f32.data_ptr(),
+                                                        fc_bias_f32.data_ptr() if fc_bias_f32 is not None else None,
+                                                        grad_window_f32.data_ptr(), int(value_begin), int(value_end),
+                                                        ws.ctypes.data, wp.ctypes.data, len(ws), bs.ctypes.data,
+                                                        fc.ctypes.data, len(bs), float(lr), _stream(stream)))
 
     def descent_device(self, weights_f32, fc_bias_f32, grad_f32, layout, lr: float, stream=None):
         """Device-resident model step: float32 CUDA tensors updated in place."""

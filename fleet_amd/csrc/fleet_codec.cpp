@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdint>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -1006,13 +1007,21 @@ namespace {
 // Segments of network::descent(vector)'s walk over the gradients() layout
 // (network.h:1185-1202): weight blocks of non-null W, bias blocks of the
 // fully-connected layers. Also the layout's total length and the model sizes.
+// Segments of the model step; with [vb, ve) only the parts whose gradient
+// positions fall in that window of upload values (an element shard), with
+// gradient offsets relative to vb.
 int descent_segments(fleet_ctx* c, const int32_t* w_sizes, const uint8_t* w_present, int n_w,
                      const int32_t* b_sizes, const uint8_t* fc_layer, int n_b, size_t* n_up, size_t* n_weights,
-                     size_t* n_fc, std::vector<fleet::DescentSegs>* segs) {
+                     size_t* n_fc, std::vector<fleet::DescentSegs>* segs, size_t vb = 0, size_t ve = SIZE_MAX) {
   if (n_w < 0 || n_b < 0 || (n_w && (!w_sizes || !w_present)) || (n_b && (!b_sizes || !fc_layer)))
     return fail(c, FLEET_ERR_ARG, "bad descent layout arguments");
   segs->clear();
   auto add = [&](int kind, size_t g, size_t m, size_t len) {
+    const size_t lo = std::max(g, vb), hi = std::min(g + len, ve);
+    if (lo >= hi) return;
+    m += lo - g;
+    len = hi - lo;
+    g = lo - vb;
     if (segs->empty() || segs->back().n == fleet::kMaxDescentSegs) {
       segs->emplace_back();
       segs->back().n = 0;
@@ -1061,6 +1070,24 @@ int fleet_descent_device(fleet_ctx* c, float* d_weights, float* d_fc_bias, const
   if ((nw && !d_weights) || (nf && !d_fc_bias)) return FLEET_ERR_ARG;
   for (const auto& sg : segs)
     HIP_TRY(c, fleet::launch_descent(d_weights, d_fc_bias, d_grad, sg, lr, pick(c, stream)));
+  return FLEET_OK;
+}
+
+int fleet_descent_window_device(fleet_ctx* c, float* d_weights, float* d_fc_bias, const float* d_grad_window,
+                                size_t value_begin, size_t value_end, const int32_t* w_sizes,
+                                const uint8_t* w_present, int n_w, const int32_t* b_sizes, const uint8_t* fc_layer,
+                                int n_b, float lr, void* stream) {
+  if (!c || !d_grad_window || value_end < value_begin) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  size_t n_up = 0, nw = 0, nf = 0;
+  std::vector<fleet::DescentSegs> segs;
+  int rc = descent_segments(c, w_sizes, w_present, n_w, b_sizes, fc_layer, n_b, &n_up, &nw, &nf, &segs, value_begin,
+                            value_end);
+  if (rc) return rc;
+  if ((nw && !d_weights) || (nf && !d_fc_bias)) return FLEET_ERR_ARG;
+  for (const auto& sg : segs)
+    HIP_TRY(c, fleet::launch_descent(d_weights, d_fc_bias, d_grad_window, sg, lr, pick(c, stream)));
   return FLEET_OK;
 }
 

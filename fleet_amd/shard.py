@@ -84,6 +84,13 @@ class ShardedUpdater:
         self.codec.check()
         return merged
 
+    def local_step(self, weights, fc_bias, window_f32, begin: int, end: int, layout, lr: float):
+        """descentNative's model step on this rank's element shard: window_f32 is the
+        merged fp32 of groups [begin, end) (update_device's merged_f32 in window mode);
+        only the parameters those gradient positions cover are updated, in the
+        full-size resident model, so the ranks' steps are disjoint and need no exchange."""
+        self.codec.descent_window_device(weights, fc_bias, window_f32, 3 * begin, 3 * end, layout, lr)
+
     # -----------------------------------------------------------------------
     def update(self, uploads: Sequence[bytes], dampen: Sequence[float]) -> bytes:
         import torch

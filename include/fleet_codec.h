@@ -263,6 +263,16 @@ int fleet_minibatch(fleet_ctx* ctx, const float* images, size_t n_images, int F,
 int fleet_descent_device(fleet_ctx* ctx, float* d_weights, float* d_fc_bias, const float* d_grad,
                          const int32_t* w_sizes, const uint8_t* w_present, int n_w, const int32_t* b_sizes,
                          const uint8_t* fc_layer, int n_b, float lr, void* stream);
+/* The same model step on one element shard (fleet_amd.shard): d_grad_window holds
+ * the merged fp32 values [value_begin, value_end) of the upload positions (what
+ * fleet_update_device's window mode writes); only the weights and FC biases whose
+ * gradient positions fall in the window are updated, in the full-size model
+ * arrays -- so N ranks, each on its window, update disjoint parts with no
+ * exchange, and together do exactly fleet_descent_device's step. */
+int fleet_descent_window_device(fleet_ctx* ctx, float* d_weights, float* d_fc_bias, const float* d_grad_window,
+                                size_t value_begin, size_t value_end, const int32_t* w_sizes,
+                                const uint8_t* w_present, int n_w, const int32_t* b_sizes, const uint8_t* fc_layer,
+                                int n_b, float lr, void* stream);
 /* Host buffers, updated in place; checks the header floats of grad against the
  * layout as network::descent(vector) would read them (FLEET_ERR_LAYOUT). */
 int fleet_descent(fleet_ctx* ctx, float* weights, size_t n_weights, float* fc_bias, size_t n_fc_bias,

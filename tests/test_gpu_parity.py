@@ -433,6 +433,44 @@ def test_descent_device_after_update(codec, oracle):
     assert np.array_equal(tb.cpu().numpy().view(np.uint32), eb.view(np.uint32))
 
 
+def test_descent_window_shards_compose(codec, oracle):
+    """Element-sharded server step: each rank's window update writes merged_f32 of
+    its groups, fleet_descent_window_device steps the parameters those positions
+    cover; the ranks' steps (run one after another here, 1..4 ranks, ragged splits)
+    update disjoint parts and together equal the oracle's whole-model descent."""
+    torch = pytest.importorskip("torch")
+    from fleet_amd.shard import byte_range, group_range
+    lay = CIFAR10
+    M = 3
+    ups = uploads_for(oracle, lay, M, seed=37)
+    L = len(ups[0])
+    d = policy("inverse", M)
+    hp = lay.header_positions()
+    groups = (F.b64_count(L) + 2) // 3
+    merged = codec.update(ups, d)
+    rng = np.random.default_rng(4)
+    w0 = rng.normal(0, 0.05, lay.n_weights).astype(np.float32)
+    b0 = rng.normal(0, 0.1, lay.n_fc_bias).astype(np.float32)
+    lr = np.float32(0.021)
+    ew, eb = oracle.descent(w0, b0, oracle.decode_floats(merged), lay.w_present(), lay.fc_flags(), lr)
+    for world in (1, 2, 4):
+        tw, tb = torch.from_numpy(w0).cuda(), torch.from_numpy(b0).cuda()
+        for r in range(world):
+            gb, ge = group_range(groups, world, r)
+            b_0, b_1 = byte_range(L, gb, ge)
+            win = np.zeros((M, 16 * (ge - gb)), np.uint8)
+            for c, u in enumerate(ups):
+                win[c, : b_1 - b_0] = np.frombuffer(u, np.uint8)[b_0:b_1]
+            out = torch.zeros(16 * (ge - gb), dtype=torch.uint8, device="cuda")
+            f32 = torch.zeros(3 * (ge - gb), dtype=torch.float32, device="cuda")
+            codec.update_device(torch.from_numpy(win).cuda(), L, d, hp, out, f32, gb, ge, window=True)
+            codec.descent_window_device(tw, tb, f32, 3 * gb, 3 * ge, lay, lr)
+        torch.cuda.synchronize()
+        codec.check()
+        assert np.array_equal(tw.cpu().numpy().view(np.uint32), ew.view(np.uint32)), world
+        assert np.array_equal(tb.cpu().numpy().view(np.uint32), eb.view(np.uint32)), world
+
+
 def test_descent_rejects_mismatched_header(codec):
     g = np.zeros(MNIST.n_up, np.float32)
     g[MNIST.header_positions()] = MNIST.header_values()
