@@ -678,7 +678,7 @@ int fleet_synth_device(fleet_ctx* c, uint64_t seed, int M, int client0, const in
 
 namespace {
 
-int model_total(fleet_ctx* c, const int32_t* dims, int n_mats, size_t* n) {
+static int model_total(fleet_ctx* c, const int32_t* dims, int n_mats, size_t* n) {
   if (n_mats < 0 || (n_mats && !dims)) return fail(c, FLEET_ERR_ARG, "bad dims");
   size_t t = 0;
   for (int j = 0; j < n_mats; ++j) {
@@ -698,7 +698,7 @@ struct DevMem {
 };
 
 // quantize + dictionary on the device; leaves d_index and the dictionary on the host
-int model_run(fleet_ctx* c, const float* weights, const int32_t* dims, int n_mats, size_t n, float* quantized,
+static int model_run(fleet_ctx* c, const float* weights, const int32_t* dims, int n_mats, size_t n, float* quantized,
               std::vector<float>* dict_host, int32_t* U, DevMem* d_index_keep) {
   DevMem dw, dq, dd;
   if (n) {
@@ -1010,7 +1010,7 @@ namespace {
 // Segments of the model step; with [vb, ve) only the parts whose gradient
 // positions fall in that window of upload values (an element shard), with
 // gradient offsets relative to vb.
-int descent_segments(fleet_ctx* c, const int32_t* w_sizes, const uint8_t* w_present, int n_w,
+static int descent_segments(fleet_ctx* c, const int32_t* w_sizes, const uint8_t* w_present, int n_w,
                      const int32_t* b_sizes, const uint8_t* fc_layer, int n_b, size_t* n_up, size_t* n_weights,
                      size_t* n_fc, std::vector<fleet::DescentSegs>* segs, size_t vb = 0, size_t ve = SIZE_MAX) {
   if (n_w < 0 || n_b < 0 || (n_w && (!w_sizes || !w_present)) || (n_b && (!b_sizes || !fc_layer)))
