@@ -1,0 +1,76 @@
+"""Parity at BASELINE.json's full sizes (SURVEY.md §8d configs[2]-[4] and the 1 M-float
+north-star bucket), by sampled columns.
+
+The aggregation is element-wise (every value's chain runs over all M clients in
+client order and no other value enters it), so the merged text of any subset of
+3-value groups equals the oracle's fused update (oracle/fleet_oracle.c
+fo_update_fused, pinned to the reference by tests/test_oracle_golden.py) run on
+the uploads cut down to those groups. The full-size uploads are generated and
+encoded on the GPU (k_synth, k_encode_f32), aggregated by the kernel the launch
+plan picks at that size, and ~1,500 random groups plus the (padded) last group
+are checked byte for byte, with merged_f32 at the same positions bitwise."""
+import numpy as np
+import pytest
+
+import fleet_amd as F
+from fleet_amd.layouts import LAYOUTS
+
+pytestmark = pytest.mark.gpu
+
+# workload -> (layout, clients M, GiB of device memory the test holds at its peak)
+FULL = {
+    "cifar10_256": ("cifar10", 256, 1),
+    "cifar100_1024": ("cifar100", 1024, 4),
+    "synth1m_256": ("synth1m", 256, 3),
+    "synth4m_4096": ("synth4m", 4096, 152),
+}
+
+
+@pytest.mark.parametrize("name", sorted(FULL))
+def test_full_size_sampled_groups(codec, oracle, name):
+    torch = pytest.importorskip("torch")
+    lay_name, M, gib = FULL[name]
+    free, _ = torch.cuda.mem_get_info()
+    if free < (gib + 8) * 2**30:
+        pytest.skip(f"{name} needs ~{gib} GiB of free device memory")
+    lay = LAYOUTS[lay_name]
+    n = lay.n_up
+    groups = (n + 2) // 3
+    L = F.b64_len(n)
+    hp = np.asarray(lay.header_positions(), np.int32)
+    rng = np.random.default_rng(sum(map(ord, name)))
+    dampen = rng.uniform(0.05, 2.0, M)
+    dev = torch.device("cuda", 0)
+    values = torch.empty((M, 3 * groups), dtype=torch.float32, device=dev)
+    codec.synth_device(20261016, values, n, hp, lay.header_values())
+    text = torch.empty((M, 16 * groups), dtype=torch.uint8, device=dev)
+    codec.encode_device(values, n, text)
+    codec.check()
+    del values
+    torch.cuda.empty_cache()
+    merged = torch.zeros(16 * groups, dtype=torch.uint8, device=dev)
+    merged_f32 = torch.zeros(3 * groups, dtype=torch.float32, device=dev)
+    codec.update_device(text, L, dampen, hp, merged, merged_f32)
+    codec.check()
+
+    # sampled groups, the last (padded) group last, so the cut-down texts are valid Base64
+    sel = np.sort(rng.choice(groups - 1, size=min(1500, groups - 1), replace=False))
+    sel = np.append(sel, groups - 1)
+    tail = L - 16 * (groups - 1)  # bytes of the last group
+    cols = (16 * sel[:, None] + np.arange(16)[None, :]).reshape(-1)
+    cols = cols[: cols.size - (16 - tail)]
+    cols_t = torch.from_numpy(cols).to(dev)
+    sub = text.index_select(1, cols_t).cpu().numpy()
+    got = merged.index_select(0, cols_t).cpu().numpy().tobytes()
+    pos = (3 * sel[:, None] + np.arange(3)[None, :]).reshape(-1)
+    pos = pos[pos < n]
+    got_f32 = merged_f32.index_select(0, torch.from_numpy(pos).to(dev)).cpu().numpy()
+    del text
+    torch.cuda.empty_cache()
+
+    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))[pos]
+    ups = [sub[c].tobytes() for c in range(M)]
+    exp, exp_f32 = oracle.update_fused(ups, dampen, hm, threads=16, want_f32=True)
+    assert len(got) == 16 * (sel.size - 1) + tail and len(ups) == M
+    assert got == exp, name
+    assert np.array_equal(got_f32.view(np.uint32), exp_f32.view(np.uint32)), name
