@@ -1332,7 +1332,8 @@ hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int 
   // (fewest table copies); otherwise about 4,096 blocks in all. Measured
   // (A/B on one box): 1M x 256 prefers whole columns, CIFAR/MNIST x 64-256 the split.
   const int64_t gx = blocks_for(groups, 256);
-  const int rpb = gx >= 1024 ? rows : (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 4095) / 4096));
+  int rpb = gx >= 1024 ? rows : (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 4095) / 4096));
+  if (const char* e = getenv("FLEET_ENCODE_RPB")) rpb = std::max(1, std::min(rows, atoi(e)));  // experiments
   hipLaunchKernelGGL(k_encode_f32, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s, values, n,
                      vpitch, out, pitch, groups, rows, rpb);
   return hipGetLastError();
