@@ -1328,11 +1328,13 @@ hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int 
                              hipStream_t s) {
   int64_t groups = (n + 2) / 3;
   if (groups == 0 || rows == 0) return hipSuccess;
-  // rows per block: whole columns when the groups alone give >= 4 blocks per CU
-  // (fewest table copies); otherwise about 4,096 blocks in all. Measured
-  // (A/B on one box): 1M x 256 prefers whole columns, CIFAR/MNIST x 64-256 the split.
   const int64_t gx = blocks_for(groups, 256);
-  int rpb = gx >= 1024 ? rows : (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 4095) / 4096));
+  // rows per block: about 16,384 blocks in all (a lane walks its group down
+  // rpb rows, so the LDS table copy is paid once per rpb rows). Measured on
+  // one box (scripts/gpu_sweep.sh): synth1m_256 encodes in 480-500 us at 8-22
+  // rows per block against 525-545 us with whole columns (256 rows) and
+  // 510-525 us at 64; cifar10_256 and MNIST-64 are flat around 7 and 1.
+  int rpb = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 16383) / 16384));
   if (const char* e = getenv("FLEET_ENCODE_RPB")) rpb = std::max(1, std::min(rows, atoi(e)));  // experiments
   hipLaunchKernelGGL(k_encode_f32, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s, values, n,
                      vpitch, out, pitch, groups, rows, rpb);
