@@ -155,6 +155,9 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
                 dist.all_gather_into_tensor(gathered, sh.merged)
 
     def run_timed(body, count):
+        # barrier + synchronize on both sides; the clock stops when this rank's
+        # steps are done (before the closing barrier, whose latency is not step
+        # time) and the max over ranks is taken by the caller
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -163,10 +166,11 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
         for _ in range(count):
             body()
         torch.cuda.synchronize()
+        t1 = time.perf_counter()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        return time.perf_counter() - t0
+        return t1 - t0
 
     for _ in range(warmup):
         local()
