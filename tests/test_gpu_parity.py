@@ -121,6 +121,37 @@ def test_update_vs_elementwise_oracle(codec, oracle, layout, M):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
+@pytest.mark.parametrize("n_up", [3, 4, 5, 6, 7])
+@pytest.mark.parametrize("M", [1, 2, 3])
+def test_update_tiny_layouts(codec, oracle, n_up, M):
+    """The smallest uploads the layout allows (an empty weight block, one or two
+    values, one partial Base64 group) through the fused update, against the
+    faithful per-op chain; every tile/stream path sees one group."""
+    lay = synthetic(n_up)
+    ups = uploads_for(oracle, lay, M, seed=n_up * 10 + M)
+    d = policy("exp", M)
+    merged, f32 = codec.update(ups, d, want_f32=True)
+    exp = oracle.update_faithful(ups, d)
+    assert merged == exp
+    assert np.array_equal(f32.view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
+
+
+def test_empty_inputs(codec, oracle):
+    """Empty texts through the codec and the per-op natives; an update needs at
+    least one upload and a header to walk."""
+    empty = np.zeros(0, np.float32)
+    assert codec.encode_floats(empty) == oracle.encode_floats(empty) == b""
+    assert codec.decode_floats(b"").size == 0
+    assert codec.decode_ints(b"").size == 0
+    assert codec.scalarMulNative(b"", 0.5) == oracle.scalar_mul(b"", 0.5)
+    assert codec.addNative(b"", b"") == oracle.add(b"", b"")
+    assert codec.getNorm(b"") == 0.0
+    with pytest.raises((F.FleetError, ValueError)):
+        codec.update([], [])
+    with pytest.raises((F.FleetError, ValueError)):
+        codec.update([b"", b""], [1.0, 1.0])
+
+
 def test_update_cifar100_layout(codec, oracle):
     """configs[3]'s layout (CIFAR-100 cppNN, 17 header slots) on a few clients."""
     from fleet_amd.layouts import CIFAR100
