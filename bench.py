@@ -283,42 +283,33 @@ def end_to_end(torch, codec, name, reps=5):
 
 
 def cpu_baseline(budget_s: float = 20.0):
-    """The reference's own C++ (oracle/_ref, -O0 = Server/Makefile flags) if built,
-    else the C restatement's faithful per-op chain; single thread (update() is
-    synchronized in the reference). Sample: MNIST layout, 64 clients (= configs[1]),
-    client encode + CppNNUpdater.update chain, repeated while under budget."""
+    """The C restatement's faithful per-op chain (oracle/fleet_oracle.c, -O2), single
+    thread (update() is synchronized in the reference). The reference's own codec
+    and JNI backend (Base64.cpp, cppNN_backend.cpp) include <jni.h>, which the image
+    lacks, so there is no reference build to time (kind "port"). Sample: MNIST
+    layout, 64 clients (= configs[1]), client encode + CppNNUpdater.update chain,
+    repeated while under budget."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     from fleet_amd.layouts import MNIST
     o = pyoracle.Oracle()
-    kind, impl = "port", None
-    if os.path.exists(pyoracle.REF_SO):
-        try:
-            impl = pyoracle.Reference()
-            kind = "reference"
-        except OSError:
-            impl = None
+    kind = "port"
     M = 64
     floats = [o.synth_upload(1, c, list(MNIST.w_sizes), list(MNIST.b_sizes)) for c in range(M)]
     d = dampen_policy(M)
     reps, t_total = 0, 0.0
     while t_total < budget_s and reps < 10:
         t0 = time.perf_counter()
-        if impl is not None:
-            ups = [impl.encode_floats(v) for v in floats]
-            impl.update(ups, d)
-        else:
-            ups = [o.encode_floats(v) for v in floats]
-            o.update_faithful(ups, d)
+        ups = [o.encode_floats(v) for v in floats]
+        o.update_faithful(ups, d)
         t_total += time.perf_counter() - t0
         reps += 1
         if t_total > budget_s / 2:
             break
     per = t_total / reps
     value = M * MNIST.n_up * 4 / per / 2**30
-    # SURVEY.md §8d's other CPU legs, on the same sample (the aggregation chain only):
-    # the reference at -O2 on 1 core, the C restatement's fused chain on all the
-    # cores this process may use (OpenMP)
+    # SURVEY.md §8d's OpenMP leg on the same sample (the aggregation chain only):
+    # the C restatement's fused chain on all the cores this process may use
     also = {}
     ups = [o.encode_floats(v) for v in floats]
 
@@ -330,14 +321,6 @@ def cpu_baseline(budget_s: float = 20.0):
             t += time.perf_counter() - t0
             n += 1
         return M * MNIST.n_up * 4 / (t / n) / 2**30, t / n
-    o2 = os.path.join(ROOT, "oracle", "_ref", "libfleetref_O2.so")
-    if os.path.exists(o2):
-        try:
-            r2 = pyoracle.Reference(o2)
-            v2, s2 = rate(lambda: r2.update(ups, d))
-            also["reference_O2_1core"] = {"value": v2, "unit": "GiB/s", "cores": 1, "s_per_update": s2}
-        except OSError:
-            pass
     threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
     hm = o.header_mask(list(MNIST.w_sizes), list(MNIST.b_sizes))
@@ -356,7 +339,7 @@ def cpu_baseline(budget_s: float = 20.0):
         pass
     return {"value": value, "unit": "GiB/s", "cores": 1, "kind": kind,
             "sample": f"MNIST layout (22,961 floats) x 64 clients: client encode + CppNNUpdater.update chain, "
-                      f"{reps} rep(s), {per:.3f} s/rep, {'oracle/_ref -O0 (reference C++)' if kind == 'reference' else 'oracle faithful port -O2'}",
+                      f"{reps} rep(s), {per:.3f} s/rep, oracle faithful port -O2 (no reference build: Base64.cpp needs <jni.h>)",
             "cpu_model": cpu, "host_nproc": os.cpu_count(), "also": also}
 
 

@@ -70,7 +70,7 @@ def build_codec(force: bool = False) -> str:
 
 def build_jni(force: bool = False) -> str:
     """JNI shim. With JAVA_HOME set it builds against the real <jni.h>; otherwise
-    against the minimal test header (oracle/ref_jni) so tests can drive it."""
+    against the minimal test header (tests/native/jni) so tests can drive it."""
     src = os.path.join(CSRC, "jni_shim.cpp")
     if not os.path.exists(src):
         return ""
@@ -78,7 +78,7 @@ def build_jni(force: bool = False) -> str:
     if jh and os.path.exists(os.path.join(jh, "include", "jni.h")):
         inc = [f"-I{jh}/include", f"-I{jh}/include/linux"]
     else:
-        inc = [f"-I{os.path.join(ROOT, 'oracle', 'ref_jni')}"]
+        inc = [f"-I{os.path.join(ROOT, 'tests', 'native', 'jni')}"]
     if not force and not _newer(JNI_LIB, [src, LIB, os.path.join(INCLUDE, "fleet_codec.h")]):
         return JNI_LIB
     tmp = JNI_LIB + ".tmp"

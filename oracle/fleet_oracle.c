@@ -5,7 +5,7 @@
  * path. Compiled with -ffp-contract=off and no fast-math so every float op
  * is one IEEE-754 binary32/binary64 round-to-nearest-even operation, exactly
  * like the reference's x86-64 SSE build (Server/Makefile:2, -O0).
- * Parity with the reference's own compiled code: tests/test_oracle_golden.py.
+ * Parity status (unpinned for the codec/aggregation chain): fleet_oracle.h.
  */
 #include "fleet_oracle.h"
 

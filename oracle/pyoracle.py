@@ -2,9 +2,11 @@
 
 ctypes bindings for
   * ``liboracle.so``         -- the clean-room C restatement (fleet_oracle.c), and
-  * ``_ref/libfleetref.so``  -- the reference's own C++ compiled by oracle/Makefile
-                                (present only where /root/reference was available at
-                                build time; absent on a box that never built it).
+  * ``_ref/libfleetref_model.so`` -- the reference's own header-only mojo network
+                                (commonLib/cppNN) compiled by oracle/Makefile (present
+                                only where /root/reference was available at build time).
+The reference's codec (Base64.cpp) and JNI backend (cppNN_backend.cpp) include
+<jni.h>, which this image lacks: they have no reference build here.
 
 Only tests/, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of bench.py
 import this module. The product package (fleet_amd/) never does.
@@ -19,8 +21,6 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "liboracle.so")
-REF_SO = os.path.join(HERE, "_ref", "libfleetref.so")
-REF_O2_SO = os.path.join(HERE, "_ref", "libfleetref_O2.so")
 REF_MODEL_SO = os.path.join(HERE, "_ref", "libfleetref_model.so")
 
 _c_char_pp = C.POINTER(C.c_char_p)
@@ -30,7 +30,7 @@ def build(force: bool = False) -> None:
     """Compile liboracle.so (and the reference build when /root/reference exists)."""
     if force or not os.path.exists(ORACLE_SO):
         subprocess.check_call(["make", "-s", "liboracle.so"], cwd=HERE)
-    if os.path.isdir("/root/reference/Server") and (force or not os.path.exists(REF_SO)):
+    if os.path.isdir("/root/reference/Server") and (force or not os.path.exists(REF_MODEL_SO)):
         subprocess.check_call(["make", "-s", "ref"], cwd=HERE)
 
 
@@ -280,126 +280,6 @@ class Oracle:
         o = np.empty(4, np.uint32)
         self.lib.fo_philox4x32_10(c.ctypes.data, k.ctypes.data, o.ctypes.data)
         return o
-
-
-class Reference:
-    """The reference's own C++ (oracle/_ref), driven through its Java_* entry points."""
-
-    def __init__(self, path: str = REF_SO):
-        if not os.path.exists(path):
-            raise FileNotFoundError(path)
-        L = C.CDLL(path)
-        self.lib = L
-        lng = C.c_long
-        L.ref_float2int.restype = C.c_int
-        L.ref_float2int.argtypes = [C.c_void_p, lng, C.c_void_p]
-        L.ref_int2float.restype = C.c_int
-        L.ref_int2float.argtypes = [C.c_void_p, lng, C.c_void_p]
-        for name in ("ref_encode_floats", "ref_encode_ints", "ref_decode_floats", "ref_decode_ints",
-                     "ref_flat_gradient"):
-            getattr(L, name).restype = lng
-            getattr(L, name).argtypes = [C.c_void_p, lng, C.c_void_p, lng]
-        L.ref_scalar_mul.restype = lng
-        L.ref_scalar_mul.argtypes = [C.c_void_p, lng, C.c_double, C.c_void_p, lng]
-        for name in ("ref_add", "ref_subtract", "ref_merge_flat_gradient"):
-            getattr(L, name).restype = lng
-            getattr(L, name).argtypes = [C.c_void_p, lng, C.c_void_p, lng, C.c_void_p, lng]
-        L.ref_norm.restype = C.c_double
-        L.ref_norm.argtypes = [C.c_void_p, lng]
-        L.ref_update.restype = lng
-        L.ref_update.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, lng,
-                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, lng]
-        L.ref_minibatch_noniid.restype = lng
-        L.ref_minibatch_noniid.argtypes = [C.c_void_p, C.c_void_p, lng, C.c_int, C.c_void_p, lng, C.c_int,
-                                           C.c_double, C.c_double, C.c_int, C.c_int, C.c_void_p, lng]
-
-    def float2int(self, x):
-        x = np.ascontiguousarray(x, dtype=np.float32)
-        o = np.empty(len(x), np.int32)
-        assert self.lib.ref_float2int(x.ctypes.data, len(x), o.ctypes.data) == 0
-        return o
-
-    def int2float(self, c):
-        c = np.ascontiguousarray(c, dtype=np.int32)
-        o = np.empty(len(c), np.float32)
-        assert self.lib.ref_int2float(c.ctypes.data, len(c), o.ctypes.data) == 0
-        return o
-
-    def _call_bytes(self, fn, *args, cap):
-        out = np.empty(cap, np.uint8)
-        n = fn(*args, out.ctypes.data, cap)
-        assert 0 <= n <= cap
-        return out[:n].tobytes()
-
-    def encode_floats(self, v):
-        v = np.ascontiguousarray(v, dtype=np.float32)
-        return self._call_bytes(self.lib.ref_encode_floats, v.ctypes.data, len(v), cap=b64_len(len(v)) + 8)
-
-    def encode_ints(self, v):
-        v = np.ascontiguousarray(v, dtype=np.int32)
-        return self._call_bytes(self.lib.ref_encode_ints, v.ctypes.data, len(v), cap=b64_len(len(v)) + 8)
-
-    def decode_floats(self, s: bytes):
-        out = np.empty(len(s) // 4 * 3 + 4, np.float32)
-        n = self.lib.ref_decode_floats(s, len(s), out.ctypes.data, len(out))
-        return out[:n].copy()
-
-    def decode_ints(self, s: bytes):
-        out = np.empty(len(s) // 4 * 3 + 4, np.int32)
-        n = self.lib.ref_decode_ints(s, len(s), out.ctypes.data, len(out))
-        return out[:n].copy()
-
-    def flat_gradient(self, g: bytes) -> bytes:
-        return self._call_bytes(self.lib.ref_flat_gradient, g, len(g), cap=len(g) + 64)
-
-    def scalar_mul(self, v: bytes, a: float) -> bytes:
-        return self._call_bytes(self.lib.ref_scalar_mul, v, len(v), a, cap=len(v) + 64)
-
-    def add(self, a: bytes, b: bytes) -> bytes:
-        return self._call_bytes(self.lib.ref_add, a, len(a), b, len(b), cap=len(a) + 64)
-
-    def subtract(self, a: bytes, b: bytes) -> bytes:
-        return self._call_bytes(self.lib.ref_subtract, a, len(a), b, len(b), cap=len(a) + 64)
-
-    def merge_flat_gradient(self, g: bytes, flat: bytes) -> bytes:
-        return self._call_bytes(self.lib.ref_merge_flat_gradient, g, len(g), flat, len(flat), cap=len(g) + 64)
-
-    def norm(self, v: bytes) -> float:
-        return self.lib.ref_norm(v, len(v))
-
-    def update(self, uploads, dampen, intermediates: bool = False):
-        M = len(uploads)
-        arr = (C.c_char_p * M)(*uploads)
-        lens = np.array([len(u) for u in uploads], dtype=np.int64)
-        d = np.ascontiguousarray(dampen, dtype=np.float64)
-        cap = max(len(u) for u in uploads) + 64
-        out = np.empty(cap, np.uint8)
-        inter = None
-        ptrs = [None, None, None, None]
-        if intermediates:
-            inter = [np.zeros((M, cap), np.uint8), np.zeros((M, cap), np.uint8), np.zeros((M, cap), np.uint8),
-                     np.zeros((1, cap), np.uint8)]
-            ptrs = [a.ctypes.data for a in inter]
-        n = self.lib.ref_update(C.cast(arr, C.c_void_p), lens.ctypes.data, M, d.ctypes.data, out.ctypes.data,
-                                cap, ptrs[0], ptrs[1], ptrs[2], ptrs[3], cap)
-        assert 0 <= n <= cap
-        if not intermediates:
-            return out[:n].tobytes()
-        return out[:n].tobytes(), inter
-
-
-    def minibatch_noniid(self, images, labels, bucket, E: int, sigma: float, Cc: float, num_labels: int,
-                         batch: int) -> bytes:
-        """getMiniBatch (cppNN_backend.cpp:677-699) on the non-IID path for one
-        client whose bucket is `bucket` (cursor at 0)."""
-        images = np.ascontiguousarray(images, dtype=np.float32)
-        labels = np.ascontiguousarray(labels, dtype=np.int32)
-        bucket = np.ascontiguousarray(bucket, dtype=np.int32)
-        n, F = images.shape
-        B = batch * E
-        cap = b64_len(7 + B * (F + 1)) + 64
-        return self._call_bytes(self.lib.ref_minibatch_noniid, images.ctypes.data, labels.ctypes.data, n, F,
-                                bucket.ctypes.data, len(bucket), E, sigma, Cc, num_labels, batch, cap=cap)
 
 
 def minibatch_vector(images, labels, idx, header, teacher=None) -> np.ndarray:

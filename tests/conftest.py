@@ -26,17 +26,6 @@ def oracle():
 
 
 @pytest.fixture(scope="session")
-def reference():
-    import pyoracle
-    if not os.path.exists(pyoracle.REF_SO):
-        if os.path.isdir("/root/reference/Server"):
-            pyoracle.build()
-        else:
-            pytest.skip("reference build (oracle/_ref) not available on this machine")
-    return pyoracle.Reference()
-
-
-@pytest.fixture(scope="session")
 def codec():
     import fleet_amd
     fleet_amd.build_if_needed = None

@@ -1,5 +1,5 @@
 """ctypes helpers for driving libfleet_native.so built against the test JNI
-header (oracle/ref_jni/jni.h): arrays are heap blocks {int32 len, int32 elem, payload}."""
+header (tests/native/jni/jni.h): arrays are heap blocks {int32 len, int32 elem, payload}."""
 import ctypes as C
 
 import numpy as np

@@ -1,21 +1,15 @@
 /*
- * oracle/ref_jni/jni.h -- TEST INFRASTRUCTURE ONLY (oracle harness).
+ * tests/native/jni/jni.h -- TEST INFRASTRUCTURE ONLY.
  *
- * A minimal stand-in for the JNI surface that the reference's native server
- * backend touches (/root/reference/Server/src/main/c++/cppNN_backend.cpp), so
- * that file can be compiled unmodified, by path, into oracle/_ref/ and driven
- * through its real Java_* entry points from oracle/ref_driver.cpp.
- *
- * Used surface (grep env-> in cppNN_backend.cpp): GetArrayLength,
- * Get/ReleaseByteArrayElements, NewByteArray, SetByteArrayRegion,
- * GetDoubleArrayElements, Get/ReleaseStringUTFChars, DeleteLocalRef; plus
- * GetObjectArrayElement / ReleaseDoubleArrayElements for the test build of
- * fleet_amd's JNI shim (jni_shim.cpp).
+ * A minimal JNI surface for building and testing fleet_amd's OWN JNI shim
+ * (fleet_amd/csrc/jni_shim.cpp) in an image without a JDK: tests/jnifake.py
+ * drives the shim's Java_* exports through it. It is never used to compile
+ * reference sources. On a server host the shim is built against the JDK's
+ * real <jni.h> (JAVA_HOME; fleet_amd/build.py).
  *
  * Arrays are heap blocks {len, payload}. GetByteArrayElements hands out a
- * NUL-terminated copy: the reference reads JVM arrays as C strings
- * (`std::string encoded = (char*)buffer`), which over-reads a real JVM
- * array; the terminator makes that read well defined here.
+ * NUL-terminated copy, so callers that read a byte[] as a C string (as the
+ * reference's natives do) see a terminated buffer.
  */
 #ifndef FLEET_ORACLE_FAKE_JNI_H
 #define FLEET_ORACLE_FAKE_JNI_H

@@ -4,7 +4,7 @@ north-star bucket), by sampled columns.
 The aggregation is element-wise (every value's chain runs over all M clients in
 client order and no other value enters it), so the merged text of any subset of
 3-value groups equals the oracle's fused update (oracle/fleet_oracle.c
-fo_update_fused, pinned to the reference by tests/test_oracle_golden.py) run on
+fo_update_fused, parity status in oracle/fleet_oracle.h) run on
 the uploads cut down to those groups. The full-size uploads are generated and
 encoded on the GPU (k_synth, k_encode_f32), aggregated by the kernel the launch
 plan picks at that size, and ~1,500 random groups plus the (padded) last group

@@ -1,7 +1,8 @@
 """HIP path vs the oracle (bit-exact), through the C-ABI (libfleetcodec.so).
 
-The oracle is the C restatement in oracle/ (itself pinned to the reference's
-own compiled C++ by tests/test_oracle_golden.py). Every comparison of Base64
+The oracle is the C restatement in oracle/ (model side pinned to the reference's
+own mojo network; codec/aggregation side unpinned beyond SURVEY.md §8c's known
+answers, see oracle/fleet_oracle.h). Every comparison of Base64
 output is byte-for-byte; decoded floats are compared bitwise. getNorm is the
 one floating-point reduction: the reference sums in index order in fp64, the
 GPU in a tree, so it is checked to 1e-12 relative (documented in DESIGN.md).

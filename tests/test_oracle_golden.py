@@ -1,10 +1,16 @@
-"""Pin the oracle (oracle/fleet_oracle.c, the C restatement) to the reference.
+"""Check the oracle (oracle/fleet_oracle.c, the C restatement).
 
-1. Against the committed golden fixtures in tests/golden/ -- outputs of the
-   reference's own C++ (Base64.cpp + Server cppNN_backend.cpp compiled
-   unmodified, driven through its Java_* natives; tests/golden/make_golden.py).
-2. Live against that reference build (oracle/_ref) on fresh random inputs,
-   when it is present on this machine.
+Model side (DISTILLATION_MODE=1 codec, descent, getModelParams, model version):
+pinned to the reference's own header-only mojo network, compiled unmodified
+into oracle/_ref/libfleetref_model.so -- committed fixtures plus live checks
+when that build is present.
+
+Codec / aggregation side: the reference's Base64.cpp and cppNN_backend.cpp
+#include <jni.h>, which this image lacks, so there is no reference build and
+no reference output for them (the reference ships no fixtures).
+They are checked against SURVEY.md §8c's known-answer values and against
+regression fixtures generated from the restatement itself
+(tests/golden/make_golden.py): parity unpinned beyond the known answers.
 CPU only.
 """
 import glob
@@ -43,7 +49,7 @@ def test_codec_text_matches_golden(oracle):
 
 
 def test_known_answers():
-    """Values quoted in SURVEY.md §8c, measured on the reference."""
+    """Known-answer values quoted in SURVEY.md §8c (the only reference-side pins of the codec)."""
     import pyoracle
     o = pyoracle.Oracle()
     assert o.lib.fo_float2int(1.0) == 100000001
@@ -79,7 +85,7 @@ def test_update_chain_matches_golden(oracle, path):
     assert oracle.update_faithful(ups, d) == merged
     hm = oracle.header_mask(w, b)
     assert oracle.update_fused(ups, d, hm, threads=2) == merged
-    if "flat" in g.files:  # per-op intermediates of the reference chain
+    if "flat" in g.files:  # per-op intermediates of the update chain
         for i in range(M):
             flat = oracle.flat_gradient(ups[i])
             assert flat == _text(g["flat"][i], len(flat))
@@ -92,20 +98,6 @@ def test_update_chain_matches_golden(oracle, path):
             assert acc == _text(g["acc"][i], len(acc))
         avg = oracle.scalar_mul(acc, 1.0 / M)
         assert avg == _text(g["avg"][0], len(avg))
-
-
-def test_oracle_vs_live_reference(oracle, reference):
-    rng = np.random.default_rng(12345)
-    x = np.concatenate([rng.normal(0, 1e-3, 5000), rng.normal(0, 3, 5000),
-                        np.exp(rng.uniform(-45, 21, 5000)) * rng.choice([-1, 1], 5000)]).astype(np.float32)
-    assert np.array_equal(oracle.float2int(x), reference.float2int(x))
-    c = rng.integers(-2**31, 2**31, 20000).astype(np.int32)
-    assert np.array_equal(oracle.int2float(c).view(np.uint32), reference.int2float(c).view(np.uint32))
-    w, b = [300, 0, 50], [200, 7]
-    ups = [oracle.encode_floats(oracle.synth_upload(99, k, w, b)) for k in range(5)]
-    d = [math.exp(-0.3 * k) for k in range(5)]
-    assert oracle.update_faithful(ups, d) == reference.update(ups, d)
-    assert oracle.norm(ups[0]) == reference.norm(ups[0])
 
 
 # ---- DISTILLATION_MODE=1 model codec ---------------------------------

@@ -76,7 +76,7 @@ def _kardam_fixture():
 
 def test_oracle_kardam_chain_matches_reference_fixture(oracle):
     """The oracle's per-op chain (flat -> x d -> x lr, subtract, norm) against the
-    reference's own natives run through the same chain."""
+    kardam.npz regression fixture (tests/golden/make_golden.py)."""
     z, M, ups, prev = _kardam_fixture()
     lr = float(z["lr"][0])
     for c in range(M):
