@@ -39,11 +39,21 @@ struct fleet_ctx {
   size_t d_f32_cap = 0;
   double* d_dampen = nullptr;
   size_t d_dampen_cap = 0;
-  std::vector<double> dev_dampen;    // what d_dampen holds (device-resident path)
-  std::vector<int32_t> dev_hdr;      // what d_hdr holds (device-resident path)
-  bool dev_params_valid = false;
   int32_t* d_hdr = nullptr;  // {status, count, walk_end, 0, positions[FLEET_MAX_HEADERS]}
   int* d_err = nullptr;
+  // Device-resident entry points (fleet_*_device) run on the CALLER's stream and
+  // may be captured into HIP graphs, so they own parameter buffers of their own:
+  // nothing the host-buffer entry points do on the context's stream touches
+  // them, and a buffer a captured graph may reference is never freed before
+  // fleet_destroy (a grown dampen buffer is retired, not freed).
+  double* d_dev_dampen = nullptr;
+  size_t d_dev_dampen_cap = 0;
+  int32_t* d_dev_hdr = nullptr;
+  int* d_dev_err = nullptr;           // read by fleet_check
+  std::vector<void*> retired;         // freed in fleet_destroy
+  std::vector<double> dev_dampen;     // what d_dev_dampen holds
+  std::vector<int32_t> dev_hdr;       // what d_dev_hdr holds
+  bool dev_params_valid = false;
   double* d_partials = nullptr;
   size_t d_partials_cap = 0;
   // pinned host staging
@@ -125,12 +135,13 @@ int check_text_len(fleet_ctx* c, size_t len) {
   return FLEET_OK;
 }
 
-int read_err(fleet_ctx* c, hipStream_t s) {
-  HIP_TRY(c, hipMemcpyAsync(c->h_err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, s));
+int read_err(fleet_ctx* c, hipStream_t s, int* d_errbuf = nullptr) {
+  if (!d_errbuf) d_errbuf = c->d_err;
+  HIP_TRY(c, hipMemcpyAsync(c->h_err, d_errbuf, sizeof(int), hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   int e = *c->h_err;
   if (e) {
-    HIP_TRY(c, hipMemsetAsync(c->d_err, 0, sizeof(int), s));
+    HIP_TRY(c, hipMemsetAsync(d_errbuf, 0, sizeof(int), s));
     HIP_TRY(c, hipStreamSynchronize(s));
   }
   if (e & 1) return fail(c, FLEET_ERR_BASE64, "input is not Base64::encode output (alphabet/padding)");
@@ -141,7 +152,6 @@ int read_err(fleet_ctx* c, hipStream_t s) {
 
 // Parse the layout of the upload at d_text (device) into c->d_hdr / c->h_hdr.
 int parse_layout(fleet_ctx* c, const uint8_t* d_text, size_t n_up, int* n_hdr, size_t* walk_end = nullptr) {
-  c->dev_params_valid = false;
   HIP_TRY(c, fleet::launch_layout_parse(d_text, (int64_t)n_up, FLEET_MAX_HEADERS, c->d_hdr, c->stream));
   HIP_TRY(c, hipMemcpyAsync(c->h_hdr, c->d_hdr, kHdrWords * sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -191,7 +201,11 @@ int stage_uploads(fleet_ctx* c, const char* const* uploads, size_t len, size_t p
 // network::flatGrad's header walk (network.h:1206-1223) over the last upload,
 // on the host from the caller's buffer -- the same walk as k_layout_parse:
 // words = {status (0 ok, 1 malformed), count, walk end, 0, positions...}.
-int32_t host_code_at(const char* text, int64_t p, bool* bad) {
+// The caller's buffer is exactly `len` bytes (a JVM array or Python bytes, no
+// padding): the group holding value p is copied into a zero-padded local, so a
+// short or truncated upload never reads past the end (bytes at or beyond len
+// decode as the device path's zero padding).
+int32_t host_code_at(const char* text, size_t len, int64_t p, bool* bad) {
   static constexpr auto tab = [] {
     struct T {
       uint8_t v[256];
@@ -199,7 +213,9 @@ int32_t host_code_at(const char* text, int64_t p, bool* bad) {
     for (int i = 0; i < 256; ++i) t.v[i] = fleet::b64_from_value(i);
     return t;
   }();
-  const uint8_t* g = reinterpret_cast<const uint8_t*>(text) + 16 * (p / 3);
+  uint8_t g[16] = {0};
+  const size_t g0 = 16 * (size_t)(p / 3);
+  if (g0 < len) std::memcpy(g, text + g0, std::min<size_t>(16, len - g0));
   const int e = (int)(p % 3);
   const uint32_t carry[3] = {0x003fu, 0x07e0u, 0xfc00u};  // chars carrying bytes 4e..4e+3
   uint8_t bytes[12];
@@ -218,7 +234,7 @@ int32_t host_code_at(const char* text, int64_t p, bool* bad) {
   for (int i = 3; i >= 0; --i) u = (u << 8) | bytes[4 * e + i];
   return (int32_t)u;
 }
-void host_layout_parse(const char* up, int64_t n, int cap, int32_t* out) {
+void host_layout_parse(const char* up, size_t len, int64_t n, int cap, int32_t* out) {
   int64_t idx = 0;
   int nh = 0;
   bool bad = false;
@@ -229,14 +245,14 @@ void host_layout_parse(const char* up, int64_t n, int cap, int32_t* out) {
       break;
     }
     out[4 + nh++] = (int32_t)idx;
-    const int cnt = fleet::cvtt(fleet::dec(host_code_at(up, idx++, &bad)));
+    const int cnt = fleet::cvtt(fleet::dec(host_code_at(up, len, idx++, &bad)));
     for (int i = 0; i < cnt; ++i) {
       if (idx >= n || nh >= cap) {
         status = 1;
         break;
       }
       out[4 + nh++] = (int32_t)idx;
-      const int size = fleet::cvtt(fleet::dec(host_code_at(up, idx++, &bad)));
+      const int size = fleet::cvtt(fleet::dec(host_code_at(up, len, idx++, &bad)));
       if (size < 0 || idx + size > n) {
         status = 1;
         break;
@@ -263,7 +279,6 @@ int update_host_fallback(fleet_ctx* c, const char* const* uploads, size_t len, i
   if (merged_f32 && (rc = grow_dev(c, &c->d_f32, &c->d_f32_cap, 3 * groups + 3))) return rc;
   if ((rc = stage_uploads(c, uploads, len, pitch, M, 0))) return rc;
   std::memcpy(c->h_stage + total, dampen, sizeof(double) * (size_t)M);
-  c->dev_params_valid = false;
   HIP_TRY(c, hipMemcpyAsync(c->d_dampen, c->h_stage + total, sizeof(double) * (size_t)M, hipMemcpyHostToDevice,
                             c->stream));
   HIP_TRY(c, fleet::launch_layout_parse(c->d_a + (size_t)(M - 1) * pitch, (int64_t)n, FLEET_MAX_HEADERS, c->d_hdr,
@@ -305,6 +320,9 @@ int fleet_create(int device, fleet_ctx** out) {
   if (hipMalloc((void**)&c->d_hdr, kHdrWords * sizeof(int32_t)) != hipSuccess) return bail(FLEET_ERR_NOMEM);
   if (hipMalloc((void**)&c->d_err, 64) != hipSuccess) return bail(FLEET_ERR_NOMEM);
   if (hipMemset(c->d_err, 0, 64) != hipSuccess) return bail(FLEET_ERR_HIP);
+  if (hipMalloc((void**)&c->d_dev_hdr, kHdrWords * sizeof(int32_t)) != hipSuccess) return bail(FLEET_ERR_NOMEM);
+  if (hipMalloc((void**)&c->d_dev_err, 64) != hipSuccess) return bail(FLEET_ERR_NOMEM);
+  if (hipMemset(c->d_dev_err, 0, 64) != hipSuccess) return bail(FLEET_ERR_HIP);
   if (hipHostMalloc((void**)&c->h_hdr, kHdrWords * sizeof(int32_t), hipHostMallocDefault) != hipSuccess)
     return bail(FLEET_ERR_NOMEM);
   if (hipHostMalloc((void**)&c->h_err, 64, hipHostMallocDefault) != hipSuccess) return bail(FLEET_ERR_NOMEM);
@@ -317,8 +335,10 @@ void fleet_destroy(fleet_ctx* c) {
   if (!c) return;
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (void* p : {(void*)c->d_a, (void*)c->d_b, (void*)c->d_out, (void*)c->d_f32, (void*)c->d_dampen,
-                  (void*)c->d_hdr, (void*)c->d_err, (void*)c->d_partials})
+                  (void*)c->d_hdr, (void*)c->d_err, (void*)c->d_partials, (void*)c->d_dev_dampen,
+                  (void*)c->d_dev_hdr, (void*)c->d_dev_err})
     if (p) (void)hipFree(p);
+  for (void* p : c->retired) (void)hipFree(p);
   for (void* p : {(void*)c->h_stage, (void*)c->h_hdr, (void*)c->h_err})
     if (p) (void)hipHostFree(p);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -337,7 +357,7 @@ int fleet_check(fleet_ctx* c, void* stream) {
   if (!c) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
-  return read_err(c, pick(c, stream));
+  return read_err(c, pick(c, stream), c->d_dev_err);
 }
 
 int fleet_layout_from_sizes(const int32_t* w_sizes, int n_w, const int32_t* b_sizes, int n_b, int32_t* header_pos,
@@ -560,7 +580,7 @@ int fleet_update(fleet_ctx* c, const char* const* uploads, const size_t* lens, i
   HIP_TRY(c, hipStreamSynchronize(c->stream));  // staging buffer reuse
   // layout of the last picked upload (mergeFlatGradient keeps its header), walked on the host
   int32_t* hw = reinterpret_cast<int32_t*>(c->h_stage + o_hdr);
-  host_layout_parse(uploads[M - 1], (int64_t)n, FLEET_MAX_HEADERS, hw);
+  host_layout_parse(uploads[M - 1], len, (int64_t)n, FLEET_MAX_HEADERS, hw);
   if (hw[0] != 0) return update_host_fallback(c, uploads, len, M, dampen, merged, merged_f32);
   std::memcpy(c->h_stage + o_damp, dampen, sizeof(double) * (size_t)M);
   std::memset(c->h_stage + o_err, 0, 16);
@@ -613,17 +633,22 @@ int fleet_update_device(fleet_ctx* c, const void* d_uploads, size_t pitch, size_
   // so steady-state calls are pure kernel launches
   if (!c->dev_params_valid || c->dev_hdr != hdr_words || c->dev_dampen.size() != (size_t)M ||
       std::memcmp(c->dev_dampen.data(), dampen, sizeof(double) * (size_t)M) != 0) {
-    if ((rc = grow_dev(c, &c->d_dampen, &c->d_dampen_cap, (size_t)M))) return rc;
     HIP_TRY(c, hipStreamSynchronize(s));
-    HIP_TRY(c, hipMemcpy(c->d_dampen, dampen, sizeof(double) * (size_t)M, hipMemcpyHostToDevice));
-    HIP_TRY(c, hipMemcpy(c->d_hdr, hdr_words.data(), sizeof(int32_t) * hdr_words.size(), hipMemcpyHostToDevice));
+    if ((size_t)M > c->d_dev_dampen_cap) {  // grow; the old buffer may sit in a captured graph: retire it
+      if (c->d_dev_dampen) c->retired.push_back(c->d_dev_dampen);
+      c->d_dev_dampen = nullptr;
+      c->d_dev_dampen_cap = 0;
+      if ((rc = grow_dev(c, &c->d_dev_dampen, &c->d_dev_dampen_cap, (size_t)M))) return rc;
+    }
+    HIP_TRY(c, hipMemcpy(c->d_dev_dampen, dampen, sizeof(double) * (size_t)M, hipMemcpyHostToDevice));
+    HIP_TRY(c, hipMemcpy(c->d_dev_hdr, hdr_words.data(), sizeof(int32_t) * hdr_words.size(), hipMemcpyHostToDevice));
     c->dev_dampen.assign(dampen, dampen + M);
     c->dev_hdr = hdr_words;
     c->dev_params_valid = true;
   }
-  HIP_TRY(c, fleet::launch_update((const uint8_t*)d_uploads, pitch, M, c->d_dampen, (double)1 / M, (int64_t)n,
-                                  (int64_t)group_begin, (int64_t)group_end, c->d_hdr, (uint8_t*)d_merged,
-                                  (float*)d_merged_f32, c->d_err, s));
+  HIP_TRY(c, fleet::launch_update((const uint8_t*)d_uploads, pitch, M, c->d_dev_dampen, (double)1 / M, (int64_t)n,
+                                  (int64_t)group_begin, (int64_t)group_end, c->d_dev_hdr, (uint8_t*)d_merged,
+                                  (float*)d_merged_f32, c->d_dev_err, s));
   return FLEET_OK;
 }
 
@@ -646,7 +671,7 @@ int fleet_decode_device(fleet_ctx* c, const void* d_text, size_t len, size_t pit
   int rc = check_text_len(c, len);
   if (rc) return rc;
   HIP_TRY(c, fleet::launch_decode((const uint8_t*)d_text, (int64_t)fleet_b64_count(len), pitch, M, d_values,
-                                  vpitch, 0, c->d_err, pick(c, stream)));
+                                  vpitch, 0, c->d_dev_err, pick(c, stream)));
   return FLEET_OK;
 }
 
@@ -859,7 +884,7 @@ int fleet_kardam_grads(fleet_ctx* c, const char* const* uploads, const size_t* l
       return fail(c, FLEET_ERR_ARG, "upload %d has length %zu, expected %zu (one model layout)", i, lens[i], len);
   const size_t n = fleet_b64_count(len);
   std::vector<int32_t> hw(kHdrWords);
-  host_layout_parse(uploads[M - 1], (int64_t)n, FLEET_MAX_HEADERS, hw.data());
+  host_layout_parse(uploads[M - 1], len, (int64_t)n, FLEET_MAX_HEADERS, hw.data());
   if (hw[0] != 0) return fail(c, FLEET_ERR_LAYOUT, "last upload's header does not describe a gradient layout");
   const int nh = hw[1];
   const size_t n_flat = (size_t)hw[2] - (size_t)nh;  // flatGrad stops after the last bias block
@@ -930,7 +955,7 @@ int fleet_minibatch_device(fleet_ctx* c, const void* d_images, size_t n_images, 
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, fleet::launch_encode_minibatch((const float*)d_images, (int64_t)n_images, F, (const int32_t*)d_labels,
                                             (const int32_t*)d_idx, B, (const float*)d_teacher, num_labels, header,
-                                            (uint8_t*)d_out, c->d_err, pick(c, stream)));
+                                            (uint8_t*)d_out, c->d_dev_err, pick(c, stream)));
   return FLEET_OK;
 }
 

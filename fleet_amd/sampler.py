@@ -76,12 +76,17 @@ class OfflineSampler:
     """CppNNOfflineSampler.getMiniBatch with the sampler state of cppNN_backend.cpp
     (E, sigma, C, lr, iid, the client rotation currClientID, :691)."""
 
-    def __init__(self, codec, images, labels, E: int, sigma: float, C: float, lr: float = 0.01,
+    def __init__(self, codec, images, labels, E: int, sigma: float, C: float, lr=0.01,
                  num_labels: int = 10, iid: bool = False, buckets: Optional[Sequence[Sequence[int]]] = None):
+        """``lr``: a number, or a callable / an object with an ``lr`` attribute (the
+        FleetUpdater) read at every request -- the reference pushes
+        cnn.get_learning_rate() when the request is built (:588, :658), and
+        descentNative moves it along lrates_vec every epoch (:345-348)."""
         self.codec = codec
         self.images = np.ascontiguousarray(images, dtype=np.float32)
         self.labels = np.ascontiguousarray(labels, dtype=np.int32)
-        self.E, self.sigma, self.C, self.lr = int(E), float(sigma), float(C), float(lr)
+        self.E, self.sigma, self.C = int(E), float(sigma), float(C)
+        self._lr = lr
         self.num_labels = int(num_labels)
         self.iid = bool(iid)
         if not self.iid and not buckets:
@@ -89,6 +94,16 @@ class OfflineSampler:
         self.cursor = NonIIDCursor(buckets) if buckets else None
         self.num_clients = len(buckets) if buckets else 1
         self.curr_client = 0
+
+    @property
+    def lr(self) -> float:
+        """The learning rate as of now (cnn.get_learning_rate(), a float)."""
+        src = self._lr
+        if callable(src):
+            src = src()
+        elif hasattr(src, "lr"):
+            src = src.lr
+        return float(np.float32(src))
 
     def getMiniBatch(self, batch_size: int, teacher=None) -> bytes:  # noqa: N802  (cppNN_backend.cpp:677)
         """``teacher(indices) -> [B, numLabels]`` supplies the mode-1 teacher's

@@ -143,9 +143,14 @@ int fleet_decode_device(fleet_ctx* ctx, const void* d_text, size_t len, size_t p
 int fleet_synth_device(fleet_ctx* ctx, uint64_t seed, int M, int client0, const int32_t* header_pos,
                        const float* header_val, int n_headers, size_t n_up, void* d_values, size_t vpitch,
                        void* stream);
-/* Returns FLEET_ERR_BASE64 / FLEET_ERR_LAYOUT if a device call since the last
- * check saw malformed text or a header that differs from the last upload's
- * (synchronises the stream), and clears the flag. */
+/* Returns FLEET_ERR_BASE64 / FLEET_ERR_LAYOUT if a device-resident call
+ * (fleet_*_device) since the last check saw malformed text or a header that
+ * differs from the last upload's (synchronises the stream), and clears the
+ * flag. Device-resident calls keep their parameters and error flag in buffers
+ * of their own, so host-buffer calls on the same context (its own stream) may
+ * be issued while device-resident work is still in flight, and a grown
+ * parameter buffer that a captured HIP graph may reference stays allocated
+ * until fleet_destroy. */
 int fleet_check(fleet_ctx* ctx, void* stream);
 
 /* Self-test of the device codec arithmetic over whole input domains: an

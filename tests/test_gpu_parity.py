@@ -214,6 +214,68 @@ def test_device_resident_update_sharded(codec, oracle):
     assert np.array_equal(f32.cpu().numpy()[: lay.n_up].view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
 
 
+def test_device_and_host_calls_interleaved(codec, oracle):
+    """A device-resident update left in flight on the caller's stream, then
+    host-buffer calls on the same context (its own stream: flat gradient, an
+    update with more clients, a merge) before any sync: the device call keeps its
+    own parameter and error buffers, so both results are exact."""
+    torch = pytest.importorskip("torch")
+    lay = synthetic(30001)
+    M = 4
+    ups = uploads_for(oracle, lay, M, seed=41)
+    L = len(ups[0])
+    pitch = (L + 15) // 16 * 16
+    host = np.zeros((M, pitch), np.uint8)
+    for i, u in enumerate(ups):
+        host[i, :L] = np.frombuffer(u, np.uint8)
+    dev = torch.from_numpy(host).cuda()
+    groups = (F.b64_count(L) + 2) // 3
+    out = torch.zeros(16 * groups, dtype=torch.uint8, device="cuda")
+    d = policy("inverse", M)
+    hp = lay.header_positions()
+    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+    for rep in range(2):
+        codec.update_device(dev, L, d, hp, out)
+        more = uploads_for(oracle, MNIST, 9, seed=42 + rep)
+        dm = policy("exp", 9)
+        assert codec.getFlatGradient(more[0]) == oracle.flat_gradient(more[0])
+        assert codec.update(more, dm) == oracle.update_fused(more, dm, oracle.header_mask(
+            list(MNIST.w_sizes), list(MNIST.b_sizes)))
+        codec.check()
+        torch.cuda.synchronize()
+        assert out.cpu().numpy()[:L].tobytes() == oracle.update_fused(ups, d, hm)
+        out.zero_()
+    # more clients after the first call grows the device parameter buffer (the old one is retired)
+    M2 = 11
+    ups2 = uploads_for(oracle, lay, M2, seed=43)
+    host2 = np.zeros((M2, pitch), np.uint8)
+    for i, u in enumerate(ups2):
+        host2[i, :L] = np.frombuffer(u, np.uint8)
+    d2 = policy("exp", M2)
+    codec.update_device(torch.from_numpy(host2).cuda(), L, d2, hp, out)
+    codec.check()
+    torch.cuda.synchronize()
+    assert out.cpu().numpy()[:L].tobytes() == oracle.update_fused(ups2, d2, hm)
+
+
+@pytest.mark.parametrize("text", [b"AAAAAA==", b"AAAAAAAAAAAAAAAAAAAAAA==", b"AAAAAAAAAAAAAAAAAAAAAAAA", b"AAAA"])
+def test_update_short_uploads(codec, oracle, text):
+    """Uploads shorter than a 16-char group or ending inside one: the host
+    header walk reads only the caller's bytes (no over-read past a JVM array);
+    the result is the oracle's layout verdict: LayoutError for a header that
+    runs off the upload, otherwise the faithful chain's bytes."""
+    ups = [text, text]
+    try:
+        exp = oracle.update_faithful(ups, [1.0, 1.0])
+    except Exception:
+        exp = None
+    if exp is None:
+        with pytest.raises(F.LayoutError):
+            codec.update(ups, [1.0, 1.0])
+    else:
+        assert codec.update(ups, [1.0, 1.0]) == exp
+
+
 def test_device_synth_and_encode(codec, oracle):
     torch = pytest.importorskip("torch")
     lay = synthetic(20002)

@@ -65,8 +65,36 @@ def test_sampler_rotation_and_header():
         OfflineSampler(FakeCodec(), img, np.arange(6), E=1, sigma=0, C=0)
 
 
+def test_sampler_reads_learning_rate_per_request():
+    """The header's lr is cnn.get_learning_rate() when the request is built
+    (cppNN_backend.cpp:588,658); descentNative moves it along lrates_vec
+    (:345-348), so a schedule change shows in the next request."""
+    calls = []
+
+    class FakeCodec:
+        def getMiniBatch(self, images, labels, idx, header, teacher=None):  # noqa: N802
+            calls.append(header.copy())
+            return b""
+
+    class Updater:  # the FleetUpdater attribute the sampler reads
+        lr = np.float32(0.05)
+
+    up = Updater()
+    img = np.zeros((4, 3), np.float32)
+    s = OfflineSampler(FakeCodec(), img, np.arange(4), E=1, sigma=0.0, C=1.0, lr=up, buckets=[[0, 1, 2, 3]])
+    s.getMiniBatch(1)
+    up.lr = np.float32(0.01)  # the epoch moved on
+    s.getMiniBatch(1)
+    schedule = iter([0.2, 0.3])
+    s2 = OfflineSampler(FakeCodec(), img, np.arange(4), E=1, sigma=0.0, C=1.0, lr=lambda: next(schedule),
+                        buckets=[[0, 1, 2, 3]])
+    s2.getMiniBatch(1)
+    s2.getMiniBatch(1)
+    assert [h[3] for h in calls] == [np.float32(0.05), np.float32(0.01), np.float32(0.2), np.float32(0.3)]
+
+
 @pytest.mark.gpu
-def test_device_minibatch_matches_reference_fixture(codec):
+def test_device_minibatch_matches_restatement_fixture(codec):
     z = _fixture()
     s = OfflineSampler(codec, z["images"], z["labels"], E=int(z["E"]), sigma=float(z["sigma"]), C=float(z["C"]),
                        num_labels=int(z["num_labels"]), buckets=[z["bucket"].tolist()])

@@ -74,7 +74,7 @@ def _kardam_fixture():
     return z, M, ups, prev
 
 
-def test_oracle_kardam_chain_matches_reference_fixture(oracle):
+def test_oracle_kardam_chain_matches_restatement_fixture(oracle):
     """The oracle's per-op chain (flat -> x d -> x lr, subtract, norm) against the
     kardam.npz regression fixture (tests/golden/make_golden.py)."""
     z, M, ups, prev = _kardam_fixture()
@@ -87,7 +87,7 @@ def test_oracle_kardam_chain_matches_reference_fixture(oracle):
 
 
 @pytest.mark.gpu
-def test_device_kardam_grads_match_reference_fixture(codec):
+def test_device_kardam_grads_match_restatement_fixture(codec):
     z, M, ups, prev = _kardam_fixture()
     texts, ng, nd = codec.kardam_grads(ups, z["d"], float(z["lr"][0]), prev)
     for c in range(M):
