@@ -5,20 +5,28 @@ One step = the hot path over one batch of M synthetic client gradient buckets
 already resident in HBM:
   1. client-side encode  (Base64::encode(vector<float>) of every bucket; k_encode_f32)
   2. server aggregation  (CppNNUpdater.update's decode/dampen/sum/average/merge
-                          chain, bit-exact; k_update) -> merged Base64 + fp32
+                          chain, bit-exact; k_update*) -> merged Base64 + fp32
 
-Multi-GPU: element-range sharding, weak scaling -- every rank owns
-a fixed slice of G 3-value groups of a model N times larger. No collective in the
-data path: each rank's merged slice (its share of the model delta) stays
-resident on its GPU, as the whole merged vector does at N=1; the all_gather of
-the slices (fleet_amd.shard, for a caller that needs the full vector) is timed
-separately and reported as `exchange_ms`, after the timed steps.
+Headline (N=1): synth1m_256, the north-star configuration (1 M-float buckets,
+C = 256 clients, 1.43 GB of Base64 >> the 256 MiB Infinity Cache).
+
+Multi-GPU (element-range sharding):
+  * `value` at N>1 is weak scaling -- every rank owns a full-size slice of a
+    model N times larger; no collective in the timed steps (each rank's merged
+    slice stays resident, as the whole merged vector does at N=1).
+  * the `strong` block (every N, including 1) splits ONE fixed problem over the
+    N ranks: configs[4] (synthetic 4 M floats x 4096 clients) device-resident,
+    timed with the all_gather of the merged slices inside the step and without
+    it; and configs[3] (CIFAR-100 x 1024) host-staged: pinned-host H2D of the
+    rank's column window + aggregation + D2H of its merged slice (+ the gather).
+  * --strong makes the strong configs[4] gather-inside line the `value`.
 
 Output: ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -42,8 +50,8 @@ HBM_COPY_GBS = 6290.0  # measured copy ceiling, same line (SURVEY.md §8d asks f
 # what actually bounds each aggregation kernel: none is HBM-bound
 LIMITER = {
     "k_update_pipe": "latency of the serial client chain (one consumer wave per tile; DESIGN.md 4.2)",
-    "k_update_tiled": "VALU issue (exact chain, ~178 VALU instructions per client-value)",
-    "k_update": "VALU issue (exact chain, ~172 VALU instructions per client-value)",
+    "k_update_tiled": "VALU issue (exact chain)",
+    "k_update": "VALU issue (exact chain)",
 }
 
 
@@ -52,47 +60,76 @@ def dampen_policy(M: int):
     return [1.0 / ((c % 3) + 1) for c in range(M)]
 
 
-class Shard:
-    """One rank's device-resident slice of a workload."""
+def group_range(groups: int, world: int, rank: int):
+    from fleet_amd.shard import group_range as gr
+    return gr(groups, world, rank)
 
-    def __init__(self, codec, torch, layout, M, rank, world, seed=1):
+
+class Shard:
+    """One rank's device-resident slice of a workload.
+
+    weak (default): a full-size bucket slice per rank.
+    strong: the rank's column window [gb, ge) of the ONE fixed problem; the
+    window's values are synthesised in place (same value mix), and the update
+    runs in window mode with the fixed problem's whole-upload coordinates."""
+
+    def __init__(self, codec, torch, layout, M, rank, world, seed=1, strong=False):
         import fleet_amd as F
         self.F = F
         self.torch = torch
         self.codec = codec
         self.M = M
-        n_up_rank = layout.n_up  # weak scaling: every rank owns one full-size bucket slice
-        groups = (n_up_rank + 2) // 3
-        self.groups = groups
-        self.n_local = n_up_rank
-        self.g0 = rank * groups  # global group offset of this slice
-        # global layout = the per-rank layout replicated world times; headers of
-        # this slice in local coordinates (the slice is one copy of the layout)
-        self.hpos = np.asarray(layout.header_positions(), dtype=np.int32)
-        self.hval = np.asarray(layout.header_values(), dtype=np.float32)
-        self.L = F.b64_len(self.n_local)
-        self.pitch = 16 * groups
-        self.vpitch = 3 * groups
+        self.strong = strong
+        hpos = np.asarray(layout.header_positions(), dtype=np.int32)
+        hval = np.asarray(layout.header_values(), dtype=np.float32)
+        if strong:
+            G = (layout.n_up + 2) // 3
+            self.gb, self.ge = group_range(G, world, rank)
+            self.groups = self.ge - self.gb
+            v0, v1 = 3 * self.gb, min(layout.n_up, 3 * self.ge)
+            self.n_local = max(0, v1 - v0)            # values of this window
+            self.L = F.b64_len(layout.n_up)           # the fixed problem's upload length
+            keep = (hpos >= v0) & (hpos < v1)
+            self.hpos_global = hpos
+            syn_pos, syn_val = hpos[keep] - v0, hval[keep]
+        else:
+            self.gb, self.ge = 0, (layout.n_up + 2) // 3
+            self.groups = self.ge
+            self.n_local = layout.n_up
+            self.L = F.b64_len(self.n_local)
+            self.hpos_global = hpos
+            syn_pos, syn_val = hpos, hval
+        self.pitch = 16 * max(1, self.groups)
+        self.vpitch = 3 * max(1, self.groups)
         dev = torch.device("cuda", torch.cuda.current_device())
         self.values = torch.empty((M, self.vpitch), dtype=torch.float32, device=dev)
-        self.text = torch.empty((M, self.pitch), dtype=torch.uint8, device=dev)
-        self.merged = torch.empty((self.pitch,), dtype=torch.uint8, device=dev)
+        self.text = torch.zeros((M, self.pitch), dtype=torch.uint8, device=dev)
+        self.merged = torch.zeros((self.pitch,), dtype=torch.uint8, device=dev)
         self.merged_f32 = torch.empty((self.vpitch,), dtype=torch.float32, device=dev)
-        codec.synth_device(seed + rank * 1000003, self.values, self.n_local, self.hpos, self.hval)
+        if self.n_local:
+            codec.synth_device(seed + rank * 1000003, self.values, self.n_local, syn_pos, syn_val)
         self.dampen = np.asarray(dampen_policy(M), dtype=np.float64)
         torch.cuda.synchronize()
 
     def encode(self):
-        self.codec.encode_device(self.values, self.n_local, self.text)
+        if self.n_local:
+            self.codec.encode_device(self.values, self.n_local, self.text)
 
     def aggregate(self):
-        self.codec.update_device(self.text, self.L, self.dampen, self.hpos, self.merged, self.merged_f32)
+        if not self.n_local:
+            return
+        if self.strong:
+            self.codec.update_device(self.text, self.L, self.dampen, self.hpos_global, self.merged, self.merged_f32,
+                                     self.gb, self.ge, window=True)
+        else:
+            self.codec.update_device(self.text, self.L, self.dampen, self.hpos_global, self.merged, self.merged_f32)
 
     def algorithmic_bytes(self):
         """Per launch: k_update reads M*L Base64, writes L Base64 + 4*n fp32;
-        k_encode_f32 reads 4*n*M fp32, writes M*L Base64."""
-        upd = self.M * self.L + self.L + 4 * self.n_local
-        enc = self.M * (4 * self.n_local + self.L)
+        k_encode_f32 reads 4*n*M fp32, writes M*L Base64 (L, n of this rank's slice)."""
+        L = self.F.b64_len(self.n_local)
+        upd = self.M * L + L + 4 * self.n_local
+        enc = self.M * (4 * self.n_local + L)
         return upd, enc
 
 
@@ -128,56 +165,63 @@ def steps_per_graph(steps: int, cap: int = 10) -> int:
     return max(d for d in range(1, min(cap, steps) + 1) if steps % d == 0)
 
 
+def run_timed(torch, dist, world, body, count):
+    """barrier + synchronize on both sides; the clock stops when this rank's
+    steps are done (before the closing barrier, whose latency is not step
+    time); returns the MAX over ranks."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(count):
+        body()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = t1 - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el
+
+
+def all_gather_fn(torch, dist, world, src, out):
+    def f():
+        if world > 1:
+            if dist.get_backend() == "gloo":  # CPU-collective rehearsal (FLEET_BENCH_BACKEND=gloo)
+                dist.all_gather(list(out.chunk(world)), src)
+            else:
+                dist.all_gather_into_tensor(out, src)
+    return f
+
+
 def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=True):
-    """Times `steps` steps. graph=True: a step (encode + aggregation) is
-    captured once into a HIP graph of G steps and replayed steps/G times;
-    graph=False: eager launches (host launch gaps between the small kernels
-    included). Both variants are reported. N>1: the all_gather of the merged
-    slices is timed after the steps, on its own (exchange_ms)."""
+    """Weak-scaling measurement of `name`: times `steps` steps. graph=True: a
+    step (encode + aggregation) is captured once into a HIP graph of G steps
+    and replayed steps/G times; graph=False: eager launches. N>1: the
+    all_gather of the merged slices is timed after the steps, on its own
+    (exchange_ms)."""
     import fleet_amd as F
     from fleet_amd.layouts import LAYOUTS
     lay_name, M, note = WORKLOADS[name]
     layout = LAYOUTS[lay_name]
     sh = Shard(codec, torch, layout, M, rank, world)
-    gathered = None
-    if world > 1:
-        gathered = torch.empty((world * sh.pitch,), dtype=torch.uint8, device=sh.merged.device)
+    gathered = torch.empty((world * sh.pitch,), dtype=torch.uint8, device=sh.merged.device) if world > 1 else None
 
     def local():
         sh.encode()
         sh.aggregate()
-
-    def exchange():
-        if world > 1:
-            if dist.get_backend() == "gloo":  # CPU-collective rehearsal (FLEET_BENCH_BACKEND=gloo)
-                dist.all_gather(list(gathered.chunk(world)), sh.merged)
-            else:
-                dist.all_gather_into_tensor(gathered, sh.merged)
-
-    def run_timed(body, count):
-        # barrier + synchronize on both sides; the clock stops when this rank's
-        # steps are done (before the closing barrier, whose latency is not step
-        # time) and the max over ranks is taken by the caller
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(count):
-            body()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        return t1 - t0
 
     for _ in range(warmup):
         local()
     torch.cuda.synchronize()
     codec.check()
 
-    eager_elapsed = run_timed(local, steps)
+    eager_elapsed = run_timed(torch, dist, world, local, steps)
     codec.check()
     eager_ms = eager_elapsed / steps * 1e3
 
@@ -193,22 +237,14 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
         g = graph_of(torch, local, G)
         for _ in range(max(1, warmup // G)):
             g.replay()
-
-        elapsed = run_timed(g.replay, steps // G)
+        elapsed = run_timed(torch, dist, world, g.replay, steps // G)
         codec.check()
         del g
     exchange_ms = None
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=sh.merged.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        # the slices gathered once (RCCL all_gather over xGMI), timed on its own, and
-        # checked: this rank's slice of the gathered vector is its merged output
+        exchange = all_gather_fn(torch, dist, world, sh.merged, gathered)
         exchange()
-        xt = run_timed(exchange, 5) / 5
-        t = torch.tensor([xt], dtype=torch.float64, device=sh.merged.device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        exchange_ms = float(t.item()) * 1e3
+        exchange_ms = run_timed(torch, dist, world, exchange, 5) / 5 * 1e3
         if not torch.equal(gathered[rank * sh.pitch:(rank + 1) * sh.pitch], sh.merged):
             raise RuntimeError("all_gather returned a different merged slice")
     ms = elapsed / steps * 1e3
@@ -229,15 +265,108 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
     return res
 
 
+def strong_device(torch, dist, codec, name, steps, warmup, rank, world):
+    """Strong scaling of ONE fixed problem split over the ranks (device-resident):
+    step = encode + aggregation of this rank's window; timed once with the
+    all_gather of the merged slices inside every step and once without it."""
+    from fleet_amd.layouts import LAYOUTS
+    lay_name, M, note = WORKLOADS[name]
+    layout = LAYOUTS[lay_name]
+    sh = Shard(codec, torch, layout, M, rank, world, strong=True)
+    # every rank's slice padded to the largest window (one RCCL call)
+    G = (layout.n_up + 2) // 3
+    wmax = max(b - a for a, b in (group_range(G, world, r) for r in range(world)))
+    src = torch.zeros(16 * wmax, dtype=torch.uint8, device=sh.merged.device)
+    out = torch.empty(world * 16 * wmax, dtype=torch.uint8, device=sh.merged.device)
+    gather = all_gather_fn(torch, dist, world, src, out)
+
+    def local():
+        sh.encode()
+        sh.aggregate()
+
+    def with_gather():
+        local()
+        src[: 16 * sh.groups].copy_(sh.merged[: 16 * sh.groups])
+        gather()
+
+    for _ in range(warmup):
+        with_gather()
+    torch.cuda.synchronize()
+    codec.check()
+    inside = run_timed(torch, dist, world, with_gather, steps) / steps
+    outside = run_timed(torch, dist, world, local, steps) / steps
+    codec.check()
+    if world > 1 and not torch.equal(out[rank * 16 * wmax: rank * 16 * wmax + 16 * sh.groups],
+                                     sh.merged[: 16 * sh.groups]):
+        raise RuntimeError("all_gather returned a different merged slice")
+    fp32 = M * layout.n_up * 4
+    res = {"workload": name, "note": note, "clients": M, "n_up_total": layout.n_up,
+           "groups_per_rank_max": wmax,
+           "gather_inside": {"ms_per_step": inside * 1e3, "gib_s": fp32 / inside / 2**30},
+           "gather_outside": {"ms_per_step": outside * 1e3, "gib_s": fp32 / outside / 2**30}}
+    del sh, src, out
+    torch.cuda.empty_cache()
+    return res
+
+
+def strong_host(torch, dist, codec, name, steps, rank, world):
+    """Strong scaling of ONE fixed problem with host buffers: every step H2Ds this
+    rank's column window of the M uploads from pinned host memory, aggregates it,
+    D2Hs its merged slice into pinned host memory and (N>1) all-gathers the slices
+    -- the PCIe- and gather-inclusive rate of the sharded path."""
+    import fleet_amd as F
+    from fleet_amd.layouts import LAYOUTS
+    lay_name, M, note = WORKLOADS[name]
+    layout = LAYOUTS[lay_name]
+    sh = Shard(codec, torch, layout, M, rank, world, strong=True)
+    sh.encode()
+    torch.cuda.synchronize()
+    host_up = torch.empty(sh.text.shape, dtype=torch.uint8).pin_memory()
+    host_up.copy_(sh.text)
+    host_out = torch.empty(sh.merged.shape, dtype=torch.uint8).pin_memory()
+    G = (layout.n_up + 2) // 3
+    wmax = max(b - a for a, b in (group_range(G, world, r) for r in range(world)))
+    src = torch.zeros(16 * wmax, dtype=torch.uint8, device=sh.merged.device)
+    out = torch.empty(world * 16 * wmax, dtype=torch.uint8, device=sh.merged.device)
+    gather = all_gather_fn(torch, dist, world, src, out)
+
+    def step():
+        sh.text.copy_(host_up, non_blocking=True)
+        sh.aggregate()
+        host_out.copy_(sh.merged, non_blocking=True)
+        src[: 16 * sh.groups].copy_(sh.merged[: 16 * sh.groups])
+        gather()
+
+    step()
+    torch.cuda.synchronize()
+    codec.check()
+    el = run_timed(torch, dist, world, step, steps) / steps
+    codec.check()
+    res = {"workload": name, "note": note, "clients": M, "n_up_total": layout.n_up,
+           "h2d_bytes_per_rank": M * sh.pitch, "ms_per_step": el * 1e3,
+           "gib_s": M * layout.n_up * 4 / el / 2**30,
+           "what": "pinned-host H2D of the rank's column window + aggregation + D2H of its merged slice + all_gather"}
+    del sh, host_up, host_out, src, out
+    torch.cuda.empty_cache()
+    return res
+
+
+def newest_profile(name: str):
+    """profiles/rNN/<name>, newest round first."""
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)), reverse=True)
+
+
 def sq_valu(workload: str, kernel: str):
-    """VALU lane-instructions per (client, value) of the profiled kernel
-    (profiles/r01/sq.json, SQ_INSTS_VALU pass), None when not profiled."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "r01", "sq.json")) as f:
-            v = json.load(f)["workloads"][workload][kernel]["valu_lane_instr_per_element_client"]
-        return float(v)
-    except (OSError, KeyError, ValueError):
-        return None
+    """VALU lane-instructions per (client, value) of the profiled kernel from the
+    newest committed SQ_INSTS_VALU pass (profiles/rNN/sq.json), None when absent."""
+    for path in newest_profile("sq.json"):
+        try:
+            with open(path) as f:
+                v = json.load(f)["workloads"][workload][kernel]["valu_lane_instr_per_element_client"]
+            return float(v), os.path.relpath(path, ROOT)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
 
 
 def pmc_traffic(workload: str, kernel: str = ""):
@@ -245,8 +374,7 @@ def pmc_traffic(workload: str, kernel: str = ""):
     rocprofv3 PMC summary (profiles/rNN/traffic.json, written by
     scripts/pmc_summary.py from separate --pmc FETCH_SIZE / WRITE_SIZE passes,
     FETCH_SIZE doubled per the gfx950 correction). None when absent."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+    for path in newest_profile("traffic.json"):
         try:
             with open(path) as f:
                 kern = json.load(f)["workloads"].get(workload, {})
@@ -258,10 +386,11 @@ def pmc_traffic(workload: str, kernel: str = ""):
     return None
 
 
-def end_to_end(torch, codec, name, reps=5):
-    """Host-buffer path (fleet_update: pinned staging, H2D of the M uploads, layout
-    parse, update, D2H of the merged Base64 + error check) on the same synthetic
-    uploads: the PCIe-inclusive rate the JNI shim sees. Not `value`."""
+def end_to_end(torch, codec, name, reps=3):
+    """Host-buffer path (fleet_update: host header walk, pinned staging, H2D of the
+    M uploads, update, D2H of the merged Base64 + error check) on the same
+    synthetic uploads: the PCIe-inclusive rate the JNI shim sees. Not `value`.
+    Beside it, the H2D floor: one pinned-host -> HBM copy of the same bytes."""
     import fleet_amd as F
     from fleet_amd.layouts import LAYOUTS
     lay_name, M, _ = WORKLOADS[name]
@@ -270,63 +399,100 @@ def end_to_end(torch, codec, name, reps=5):
     sh.encode()
     torch.cuda.synchronize()
     host = sh.text.cpu().numpy()
-    ups = [host[c, : sh.L].tobytes() for c in range(M)]
-    del sh
+    L = sh.L
+    ups = [host[c, :L].tobytes() for c in range(M)]
+    del host
+    # H2D floor: the same bytes in one pinned buffer, one copy on torch's stream
+    pin = torch.empty(M * L, dtype=torch.uint8).pin_memory()
+    dst = sh.text.view(-1)[: M * L]
+    dst.copy_(pin, non_blocking=True)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    h2d = []
+    for _ in range(3):
+        a.record()
+        dst.copy_(pin, non_blocking=True)
+        b.record()
+        b.synchronize()
+        h2d.append(a.elapsed_time(b) * 1e-3)
+    h2d_s = min(h2d)
+    del sh, pin, dst
+    torch.cuda.empty_cache()
     d = dampen_policy(M)
     codec.update(ups, d)  # warm (allocations, staging)
-    t0 = time.perf_counter()
+    times = []
     for _ in range(reps):
+        t0 = time.perf_counter()
         merged = codec.update(ups, d)
-    dt = (time.perf_counter() - t0) / reps
-    return {"workload": name, "ms": dt * 1e3, "gib_s": M * layout.n_up * 4 / dt / 2**30,
-            "h2d_bytes": M * F.b64_len(layout.n_up), "d2h_bytes": len(merged)}
+        times.append(time.perf_counter() - t0)
+    dt = min(times)
+    return {"workload": name, "ms": dt * 1e3, "ms_mean": float(np.mean(times)) * 1e3,
+            "gib_s": M * layout.n_up * 4 / dt / 2**30,
+            "h2d_bytes": M * L, "d2h_bytes": len(merged),
+            "h2d_floor_ms": h2d_s * 1e3, "h2d_floor_gbs": M * L / h2d_s / 1e9,
+            "pcie_gbs_achieved": M * L / dt / 1e9, "x_floor": dt / h2d_s}
 
 
-def cpu_baseline(budget_s: float = 20.0):
-    """The C restatement's faithful per-op chain (oracle/fleet_oracle.c, -O2), single
-    thread (update() is synchronized in the reference). The reference's own codec
-    and JNI backend (Base64.cpp, cppNN_backend.cpp) include <jni.h>, which the image
-    lacks, so there is no reference build to time (kind "port"). Sample: MNIST
-    layout, 64 clients (= configs[1]), client encode + CppNNUpdater.update chain,
-    repeated while under budget."""
+def cpu_threads():
+    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(threads, int(os.environ.get("OMP_NUM_THREADS", threads))))
+
+
+def cpu_baseline(workload: str, budget_s: float = 20.0, faithful_clients: int = 4):
+    """The reference C++ path's CPU cost on the GPU box's host, for the headline
+    workload (kind "port": the C restatement oracle/fleet_oracle.c; the
+    reference's own codec and JNI backend (Base64.cpp, cppNN_backend.cpp)
+    include <jni.h>, which the image lacks, so there is no reference build to
+    time).
+
+    value: the restatement's fused chain with OpenMP on every core this process
+           may use, over the FULL workload: client encode (threads over clients)
+           + CppNNUpdater.update's aggregation chain.
+    also:  the faithful per-op string chain (one JNI op at a time, re-encoding
+           between ops, single thread like the synchronized update()) at -O2
+           and at -O0 (the reference's own flags, Server/Makefile:2), on the
+           first `faithful_clients` clients of the same workload."""
+    from concurrent.futures import ThreadPoolExecutor
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
-    from fleet_amd.layouts import MNIST
-    o = pyoracle.Oracle()
-    kind = "port"
-    M = 64
-    floats = [o.synth_upload(1, c, list(MNIST.w_sizes), list(MNIST.b_sizes)) for c in range(M)]
+    from fleet_amd.layouts import LAYOUTS
+    lay_name, M, _ = WORKLOADS[workload]
+    lay = LAYOUTS[lay_name]
+    w, b = list(lay.w_sizes), list(lay.b_sizes)
+    o2 = pyoracle.Oracle()
+    threads = cpu_threads()
+    with ThreadPoolExecutor(threads) as ex:  # ctypes releases the GIL
+        floats = list(ex.map(lambda c: o2.synth_upload(1, c, w, b), range(M)))
+    hm = o2.header_mask(w, b)
     d = dampen_policy(M)
+    fp32 = M * lay.n_up * 4
+
     reps, t_total = 0, 0.0
-    while t_total < budget_s and reps < 10:
+    while reps < 3 and t_total < budget_s / 2:
         t0 = time.perf_counter()
-        ups = [o.encode_floats(v) for v in floats]
-        o.update_faithful(ups, d)
+        with ThreadPoolExecutor(threads) as ex:
+            ups = list(ex.map(o2.encode_floats, floats))
+        o2.update_fused(ups, d, hm, threads=threads)
         t_total += time.perf_counter() - t0
         reps += 1
-        if t_total > budget_s / 2:
-            break
     per = t_total / reps
-    value = M * MNIST.n_up * 4 / per / 2**30
-    # SURVEY.md §8d's OpenMP leg on the same sample (the aggregation chain only):
-    # the C restatement's fused chain on all the cores this process may use
-    also = {}
-    ups = [o.encode_floats(v) for v in floats]
+    value = fp32 / per / 2**30
+    del ups
 
-    def rate(fn, budget=3.0):
+    also = {}
+    Mf = min(faithful_clients, M)
+    for tag, path in (("faithful_O2_1core", pyoracle.ORACLE_SO), ("faithful_O0_1core", pyoracle.ORACLE_O0_SO)):
+        o = pyoracle.Oracle(path)
         n, t = 0, 0.0
-        while t < budget and n < 20:
+        while n < 3 and t < budget_s / 4:
             t0 = time.perf_counter()
-            fn()
+            sub = [o.encode_floats(v) for v in floats[:Mf]]
+            o.update_faithful(sub, d[:Mf])
             t += time.perf_counter() - t0
             n += 1
-        return M * MNIST.n_up * 4 / (t / n) / 2**30, t / n
-    threads = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = min(threads, int(os.environ.get("OMP_NUM_THREADS", threads)))
-    hm = o.header_mask(list(MNIST.w_sizes), list(MNIST.b_sizes))
-    vp, sp = rate(lambda: o.update_fused(ups, d, hm, threads=threads))
-    also["port_fused_openmp"] = {"value": vp, "unit": "GiB/s", "cores": threads, "s_per_update": sp}
-    also["note"] = "aggregation chain only (CppNNUpdater.update on pre-encoded uploads), same MNIST x 64 sample"
+        also[tag] = {"value": Mf * lay.n_up * 4 / (t / n) / 2**30, "unit": "GiB/s", "cores": 1,
+                     "s_per_update": t / n, "clients": Mf,
+                     "mfloat_per_s": Mf * lay.n_up / (t / n) / 1e6}
     import platform
     cpu = platform.processor() or "x86_64"
     try:
@@ -337,9 +503,10 @@ def cpu_baseline(budget_s: float = 20.0):
                     break
     except OSError:
         pass
-    return {"value": value, "unit": "GiB/s", "cores": 1, "kind": kind,
-            "sample": f"MNIST layout (22,961 floats) x 64 clients: client encode + CppNNUpdater.update chain, "
-                      f"{reps} rep(s), {per:.3f} s/rep, oracle faithful port -O2 (no reference build: Base64.cpp needs <jni.h>)",
+    return {"value": value, "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{workload} in full ({M} clients x {lay.n_up} floats): client encode (threads over clients) + "
+                      f"CppNNUpdater.update chain (fused restatement, OpenMP), {reps} rep(s), {per:.2f} s/rep; "
+                      f"no reference build (Base64.cpp needs <jni.h>)",
             "cpu_model": cpu, "host_nproc": os.cpu_count(), "also": also}
 
 
@@ -348,13 +515,19 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="mnist64", choices=sorted(WORKLOADS))
-    ap.add_argument("--extras", default="cifar10_256,synth1m_256",
+    ap.add_argument("--workload", default="synth1m_256", choices=sorted(WORKLOADS))
+    ap.add_argument("--extras", default="synth4m_4096,cifar10_256,cifar100_1024,mnist64",
                     help="comma list of extra workloads measured in the same run (N=1 only); '' for none")
+    ap.add_argument("--strong", action="store_true",
+                    help="value = strong scaling of configs[4] (one fixed problem split over the ranks, "
+                         "all_gather of the merged slices inside every step)")
+    ap.add_argument("--no-strong-block", action="store_true", help="skip the strong-scaling block")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=1,
                     help="1 (default): replay steps from a captured HIP graph; 0: eager launches")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (PCIe-inclusive) measurement")
+    ap.add_argument("--e2e", default="synth1m_256,cifar10_256,mnist64",
+                    help="workloads of the host-buffer (PCIe-inclusive) measurement (N=1)")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
 
@@ -385,9 +558,16 @@ def main():
         for w in [x for x in args.extras.split(",") if x and x != args.workload]:
             extras[w] = time_workload(torch, dist, codec, w, max(3, args.steps // 4), 2, rank, world, args.graph)
 
+    strong = None
+    if args.strong or not args.no_strong_block:
+        ssteps = max(3, args.steps // 4)
+        strong = {"scaling": "strong", "n_gpus": world,
+                  "device": strong_device(torch, dist, codec, "synth4m_4096", ssteps, 1, rank, world),
+                  "host_staged": strong_host(torch, dist, codec, "cifar100_1024", ssteps, rank, world)}
+
     e2e = None
     if world == 1 and not args.no_e2e:
-        e2e = end_to_end(torch, codec, args.workload)
+        e2e = {w: end_to_end(torch, codec, w) for w in args.e2e.split(",") if w}
 
     if rank != 0:
         if world > 1:
@@ -396,48 +576,62 @@ def main():
         return
     cpu = None
     if not args.no_cpu_baseline and world == 1:
-        cpu = cpu_baseline(args.cpu_budget)
+        cpu = cpu_baseline(args.workload, args.cpu_budget)
     r = main_res
     achieved = r["update_gbs"]
     traffic = pmc_traffic(args.workload, r["update_kernel"]) if world == 1 else None
+    sq = sq_valu(args.workload, r["update_kernel"])
+    value, ms, scaling = r["gib_s"], r["ms_per_step"], "weak"
+    config = {"workload": args.workload, "layout": r["layout"], "clients": r["clients"],
+              "n_up_per_rank": r["n_up_per_rank"], "parallelism": f"element-shard x{world}",
+              "dampening": "policy 1 inverse, tau = c mod 3"}
+    if args.strong:
+        sd = strong["device"]
+        value, ms, scaling = sd["gather_inside"]["gib_s"], sd["gather_inside"]["ms_per_step"], "strong"
+        config = {"workload": "synth4m_4096", "layout": "synth4m", "clients": sd["clients"],
+                  "n_up_total": sd["n_up_total"], "parallelism": f"element-shard x{world}, all_gather inside",
+                  "dampening": "policy 1 inverse, tau = c mod 3"}
     line = {
         "metric": "gradient GiB/s encode+decode+aggregate (device-resident); % HBM roofline",
-        "value": r["gib_s"],
+        "value": value,
         "unit": "GiB/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": r["ms_per_step"],
+        "ms_per_step": ms,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (Philox4x32-10 value mix, SURVEY.md §8d), device-resident",
-        "config": {"workload": args.workload, "layout": r["layout"], "clients": r["clients"],
-                   "n_up_per_rank": r["n_up_per_rank"], "parallelism": f"element-shard x{world}",
-                   "dampening": "policy 1 inverse, tau = c mod 3"},
+        "config": config,
         "roofline": {"bound": "hbm", "kernel": r["update_kernel"], "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "frac_of_copy_ceiling": achieved / HBM_COPY_GBS,
                      "limiter": LIMITER.get(r["update_kernel"].split("<")[0], "VALU issue"),
-                     "valu_lane_instr_per_element_client": sq_valu(args.workload, r["update_kernel"]),
+                     "valu_lane_instr_per_element_client": sq[0] if sq else None,
+                     "valu_source": sq[1] if sq else None,
                      "traffic": traffic[0] if traffic else None,
                      "traffic_source": f"{traffic[2]} ({traffic[1]})" if traffic else None,
-                     "bytes_per_launch": r["update_bytes"], "kernel_ms": r["update_kernel_ms"]},
+                     "bytes_per_launch": r["update_bytes"], "kernel_ms": r["update_kernel_ms"],
+                     "workload": args.workload},
         "cpu_baseline": cpu,
         "timing": {"graph": bool(r["graph"]), "steps_per_graph": r["steps_per_graph"],
                    "eager_ms_per_step": r["eager_ms_per_step"],
                    "exchange_ms": r["exchange_ms"],
-                   "exchange": "none in the timed steps (element shards stay resident); N>1: one all_gather of "
-                               "the merged slices timed separately (exchange_ms, max over ranks) and checked",
+                   "exchange": "weak-scaling value: none in the timed steps (element shards stay resident); N>1: one "
+                               "all_gather of the merged slices timed separately (exchange_ms, max over ranks) and "
+                               "checked; the strong block times it inside the step",
                    "kernel_ms": "HIP events around graph replays of 10 back-to-back launches"},
         "kernels": {"k_update_ms": r["update_kernel_ms"], "k_encode_f32_ms": r["encode_kernel_ms"],
                     "k_encode_gbs": r["encode_gbs"], "element_clients_per_s": r["element_clients_per_s"]},
+        "weak": {"gib_s": r["gib_s"], "ms_per_step": r["ms_per_step"]},
+        "strong": strong,
         "extra": extras,
         "end_to_end_host_buffers": e2e,
     }
     if cpu:
-        line["vs_cpu_baseline"] = r["gib_s"] / cpu["value"]
+        line["vs_cpu_baseline"] = value / cpu["value"]
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -21,6 +21,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "liboracle.so")
+ORACLE_O0_SO = os.path.join(HERE, "liboracle_O0.so")  # same source at -O0 (bench.py's faithful CPU leg)
 REF_MODEL_SO = os.path.join(HERE, "_ref", "libfleetref_model.so")
 
 _c_char_pp = C.POINTER(C.c_char_p)
@@ -28,8 +29,8 @@ _c_char_pp = C.POINTER(C.c_char_p)
 
 def build(force: bool = False) -> None:
     """Compile liboracle.so (and the reference build when /root/reference exists)."""
-    if force or not os.path.exists(ORACLE_SO):
-        subprocess.check_call(["make", "-s", "liboracle.so"], cwd=HERE)
+    if force or not os.path.exists(ORACLE_SO) or not os.path.exists(ORACLE_O0_SO):
+        subprocess.check_call(["make", "-s", "liboracle.so", "liboracle_O0.so"], cwd=HERE)
     if os.path.isdir("/root/reference/Server") and (force or not os.path.exists(REF_MODEL_SO)):
         subprocess.check_call(["make", "-s", "ref"], cwd=HERE)
 
@@ -58,7 +59,7 @@ class Oracle:
     """The C restatement (fleet_oracle.c)."""
 
     def __init__(self, path: str = ORACLE_SO):
-        if not os.path.exists(path):
+        if not os.path.exists(ORACLE_SO) or not os.path.exists(path):
             build()
         L = C.CDLL(path)
         self.lib = L
