@@ -96,6 +96,7 @@ def lib() -> C.CDLL:
         "fleet_subtract": (i32, [vp, vp, sz, vp, sz, vp, sz, szp]),
         "fleet_norm": (i32, [vp, vp, sz, C.POINTER(C.c_double)]),
         "fleet_update": (i32, [vp, vp, vp, i32, vp, vp, sz, szp, vp]),
+        "fleet_update_multi": (i32, [vp, i32, vp, vp, i32, vp, vp, sz, szp, vp]),
         "fleet_update_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, sz, sz, vp, vp, vp]),
         "fleet_update_kernel": (C.c_char_p, [sz]),
         "fleet_model_quantize_index": (i32, [vp, vp, vp, i32, vp, vp, vp, vp]),
@@ -557,6 +558,38 @@ class Codec:
                                                  grad_f32.data_ptr(), ws.ctypes.data, wp.ctypes.data, len(ws),
                                                  bs.ctypes.data, fc.ctypes.data, len(bs), float(lr),
                                                  _stream(stream)))
+
+
+def update_multi(codecs: Sequence["Codec"], uploads: Sequence, dampen: Sequence[float], want_f32: bool = False):
+    """Codec.update spread over several device contexts from one process
+    (fleet_update_multi): context k aggregates a contiguous range of the 3-value
+    groups of every upload and writes its slice of the output; byte-identical to
+    one context's update. The first context reports errors."""
+    if not codecs:
+        raise ValueError("no contexts")
+    ups = [_as_bytes(u) for u in uploads]
+    M = len(ups)
+    if M == 0:
+        raise ValueError("no uploads")
+    if len(dampen) != M:
+        raise ValueError("one dampening factor per upload")
+    L = lib()
+    arr = (C.c_char_p * M)(*ups)
+    lens = np.array([len(u) for u in ups], dtype=np.uint64)
+    d = np.ascontiguousarray(dampen, dtype=np.float64)
+    hs = (C.c_void_p * len(codecs))(*[c._h for c in codecs])
+    n_len = len(ups[0])
+    out = np.empty(n_len + 16, np.uint8)
+    n = C.c_size_t(0)
+    f32 = np.empty(b64_count(n_len) + 1, np.float32) if want_f32 else None
+    rc = L.fleet_update_multi(C.cast(hs, C.c_void_p), len(codecs), C.cast(arr, C.c_void_p), lens.ctypes.data, M,
+                              d.ctypes.data, out.ctypes.data, len(out), C.byref(n),
+                              f32.ctypes.data if want_f32 else None)
+    codecs[0]._check(rc)
+    merged = out[: n.value].tobytes()
+    if want_f32:
+        return merged, f32[: b64_count(n_len)].copy()
+    return merged
 
 
 class ByteVec:

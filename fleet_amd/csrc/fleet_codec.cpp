@@ -12,9 +12,13 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
+
+#include <sched.h>
 
 #include "../../include/fleet_codec.h"
 #include "kernels.h"
@@ -170,27 +174,64 @@ int finish_text(fleet_ctx* c, size_t out_len, char* out, size_t cap, size_t* out
   return rc;
 }
 
-// Copies the M uploads into the pinned staging rows (pitch apart, zero
-// padded) and queues ONE H2D of [rows | tail_bytes already written after the
-// rows] into d_a, in `pieces` parts, each queued as soon as its rows are
-// copied, so the DMA of a part overlaps the copy of the next (ingress
-// framing). Measured on MI355X (scripts/probe_e2e2.py, rocprofv3
-// memory-copy trace): 1 MiB H2D parts run at ~35 GB/s with ~9 us gaps, one
-// 7.8 MB copy at ~53 GB/s; three parts gave the shortest host-buffer update
-// (0.27 vs 0.32 ms for MNIST-64 with one part); copying with 2-4 threads did
-// not help consistently.
-int stage_uploads(fleet_ctx* c, const char* const* uploads, size_t len, size_t pitch, int M, size_t tail_bytes) {
+// Host staging copy workers: FLEET_STAGE_THREADS, else -- for copies large
+// enough to pay for threads -- the CPUs this process may run on, at most 8.
+int stage_threads(size_t bytes) {
+  if (const char* e = getenv("FLEET_STAGE_THREADS")) return std::max(1, atoi(e));
+  if (bytes < (32u << 20)) return 1;
+  int n = 1;
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+  return std::max(1, std::min(n, 8));
+}
+
+// f(i) for i in [0, n) on `threads` threads (the caller's thread included).
+template <class F>
+void parallel_for(int n, int threads, F&& f) {
+  threads = std::max(1, std::min(threads, n));
+  if (threads == 1) {
+    for (int i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<int> next{0};
+  auto work = [&] {
+    for (int i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) f(i);
+  };
+  std::vector<std::thread> ts;
+  ts.reserve((size_t)threads - 1);
+  for (int t = 1; t < threads; ++t) ts.emplace_back(work);
+  work();
+  for (auto& t : ts) t.join();
+}
+
+// Copies bytes [col0, col0 + width) of each of the M uploads into the pinned
+// staging rows (pitch apart, zero padded) and queues ONE H2D of [rows |
+// tail_bytes already written after the rows] into d_a, in parts, each queued as
+// soon as its rows are copied, so the DMA of a part overlaps the copy of the
+// next (ingress framing). col0 = 0, width = len stages whole
+// uploads; a column window is one GPU's element shard (fleet_update_multi).
+// Measured on MI355X (scripts/probe_e2e2.py, rocprofv3 memory-copy trace): 1 MiB
+// H2D parts run at ~35 GB/s with ~9 us gaps, one 7.8 MB copy at ~53 GB/s; three
+// parts gave the shortest host-buffer update for MNIST-64 (0.27 vs 0.32 ms with
+// one part). Large batches (the 1.43 GB north-star batch) copy each part with
+// `threads` workers: one thread's memcpy into pinned memory, not PCIe, bounded
+// the host-buffer update there.
+int stage_uploads(fleet_ctx* c, const char* const* uploads, size_t col0, size_t width, size_t pitch, int M,
+                  size_t tail_bytes, int threads) {
+  const size_t total = pitch * (size_t)M;
   int pieces = 3;
+  if (total >= (512u << 20)) pieces = (int)std::min<size_t>(16, total / (96u << 20));
   if (const char* e = getenv("FLEET_STAGE_PIECES")) pieces = std::max(1, atoi(e));
-  if (pitch * (size_t)M < (4u << 20)) pieces = 1;
+  if (total < (4u << 20)) pieces = 1;
   pieces = std::min(pieces, M);
   for (int k = 0; k < pieces; ++k) {
     const int r0 = (int)((int64_t)M * k / pieces), r1 = (int)((int64_t)M * (k + 1) / pieces);
-    for (int i = r0; i < r1; ++i) {
+    parallel_for(r1 - r0, threads, [&](int j) {
+      const int i = r0 + j;
       uint8_t* row = c->h_stage + (size_t)i * pitch;
-      std::memcpy(row, uploads[i], len);
-      std::memset(row + len, 0, pitch - len);
-    }
+      std::memcpy(row, uploads[i] + col0, width);
+      std::memset(row + width, 0, pitch - width);
+    });
     const size_t off = (size_t)r0 * pitch;
     const size_t bytes = (size_t)(r1 - r0) * pitch + (r1 == M ? tail_bytes : 0);
     HIP_TRY(c, hipMemcpyAsync(c->d_a + off, c->h_stage + off, bytes, hipMemcpyHostToDevice, c->stream));
@@ -277,7 +318,7 @@ int update_host_fallback(fleet_ctx* c, const char* const* uploads, size_t len, i
   if ((rc = grow_dev(c, &c->d_dampen, &c->d_dampen_cap, (size_t)M))) return rc;
   if ((rc = grow_dev(c, &c->d_out, &c->d_out_cap, 16 * groups + 16))) return rc;
   if (merged_f32 && (rc = grow_dev(c, &c->d_f32, &c->d_f32_cap, 3 * groups + 3))) return rc;
-  if ((rc = stage_uploads(c, uploads, len, pitch, M, 0))) return rc;
+  if ((rc = stage_uploads(c, uploads, 0, len, pitch, M, 0, stage_threads(total)))) return rc;
   std::memcpy(c->h_stage + total, dampen, sizeof(double) * (size_t)M);
   HIP_TRY(c, hipMemcpyAsync(c->d_dampen, c->h_stage + total, sizeof(double) * (size_t)M, hipMemcpyHostToDevice,
                             c->stream));
@@ -551,11 +592,11 @@ int fleet_norm(fleet_ctx* c, const char* v, size_t len, double* out) {
 
 // ------------------------------------------------------------ fused update
 
-int fleet_update(fleet_ctx* c, const char* const* uploads, const size_t* lens, int M, const double* dampen,
-                 char* merged, size_t cap, size_t* out_len, float* merged_f32) {
-  if (!c || !uploads || !lens || !dampen || M <= 0) return FLEET_ERR_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+namespace {
+
+// Validation shared by the host-buffer updates; on success *len = the common length.
+int check_update_args(fleet_ctx* c, const char* const* uploads, const size_t* lens, int M, size_t cap,
+                      size_t* out_len, size_t* len_out) {
   const size_t len = lens[0];
   int rc = check_text_len(c, len);
   if (rc) return rc;
@@ -565,40 +606,127 @@ int fleet_update(fleet_ctx* c, const char* const* uploads, const size_t* lens, i
   }
   if (out_len) *out_len = len;
   if (cap < len) return fail(c, FLEET_ERR_CAPACITY, "output capacity %zu < %zu", cap, len);
+  *len_out = len;
+  return FLEET_OK;
+}
+
+// The host-buffer update of the groups [gb, ge) on context c (lock held, device
+// set): the column window [16*gb, 16*ge) of every upload is staged into pinned
+// memory and sent to HBM, the exact chain runs on it, and its merged slice
+// (Base64 bytes [16*gb, min(len, 16*ge)), fp32 values [3*gb, min(n, 3*ge))) is
+// written into the caller's outputs -- disjoint ranges for disjoint windows.
+// hw = the host walk of the last upload's header (whole-upload coordinates).
+//   staging block, mirrored on the device in d_a:
+//   [window rows M x wpitch | dampen M doubles | header words | err | merged | fp32]
+//   one H2D up to err (inclusive, err = 0), one D2H from err on.
+int update_window(fleet_ctx* c, const char* const* uploads, size_t len, int M, const double* dampen,
+                  const int32_t* hw, size_t gb, size_t ge, char* merged, float* merged_f32, int threads) {
   const size_t n = fleet_b64_count(len);
-  const size_t groups = groups_of(n);
-  const size_t pitch = round16(len);
-  const size_t total = pitch * (size_t)M;
-  // one staging block, mirrored on the device in d_a:
-  //   [uploads M x pitch | dampen M doubles | header words | err | merged Base64 | merged fp32]
-  // one H2D up to err (inclusive, err = 0), one D2H from err on.
+  const size_t w = ge - gb;
+  if (w == 0) return FLEET_OK;
+  const size_t wpitch = 16 * w;
+  const size_t col0 = 16 * gb, width = std::min(len, 16 * ge) - col0;
+  const size_t total = wpitch * (size_t)M;
   const size_t o_damp = total, o_hdr = round16(o_damp + sizeof(double) * (size_t)M);
   const size_t o_err = round16(o_hdr + sizeof(int32_t) * kHdrWords), o_out = o_err + 16;
-  const size_t o_f32 = round16(o_out + 16 * groups + 16), o_end = o_f32 + sizeof(float) * (3 * groups + 3);
+  const size_t o_f32 = round16(o_out + wpitch + 16), o_end = o_f32 + sizeof(float) * (3 * w + 3);
+  int rc;
   if ((rc = grow_pinned(c, o_end + 64))) return rc;
   if ((rc = grow_dev(c, &c->d_a, &c->d_a_cap, o_end + 64))) return rc;
   HIP_TRY(c, hipStreamSynchronize(c->stream));  // staging buffer reuse
-  // layout of the last picked upload (mergeFlatGradient keeps its header), walked on the host
-  int32_t* hw = reinterpret_cast<int32_t*>(c->h_stage + o_hdr);
-  host_layout_parse(uploads[M - 1], len, (int64_t)n, FLEET_MAX_HEADERS, hw);
-  if (hw[0] != 0) return update_host_fallback(c, uploads, len, M, dampen, merged, merged_f32);
+  std::memcpy(c->h_stage + o_hdr, hw, sizeof(int32_t) * kHdrWords);
   std::memcpy(c->h_stage + o_damp, dampen, sizeof(double) * (size_t)M);
   std::memset(c->h_stage + o_err, 0, 16);
-  if ((rc = stage_uploads(c, uploads, len, pitch, M, o_err + 16 - total))) return rc;
+  if ((rc = stage_uploads(c, uploads, col0, width, wpitch, M, o_err + 16 - total, threads))) return rc;
   uint8_t* d = c->d_a;
-  HIP_TRY(c, fleet::launch_update(d, pitch, M, reinterpret_cast<const double*>(d + o_damp), (double)1 / M,
-                                  (int64_t)n, 0, (int64_t)groups, reinterpret_cast<const int32_t*>(d + o_hdr),
-                                  d + o_out, merged_f32 ? reinterpret_cast<float*>(d + o_f32) : nullptr,
+  // window mode: row and output pointers shifted back by the window's start
+  HIP_TRY(c, fleet::launch_update(d - col0, wpitch, M, reinterpret_cast<const double*>(d + o_damp), (double)1 / M,
+                                  (int64_t)n, (int64_t)gb, (int64_t)ge, reinterpret_cast<const int32_t*>(d + o_hdr),
+                                  d + o_out - col0,
+                                  merged_f32 ? reinterpret_cast<float*>(d + o_f32) - 3 * gb : nullptr,
                                   reinterpret_cast<int*>(d + o_err), c->stream));
-  const size_t back = (merged_f32 ? o_f32 + sizeof(float) * n : o_out + len) - o_err;
+  const size_t v0 = 3 * gb, v1 = std::min(n, 3 * ge);
+  const size_t back = (merged_f32 ? o_f32 + sizeof(float) * (v1 - v0) : o_out + width) - o_err;
   HIP_TRY(c, hipMemcpyAsync(c->h_stage + o_err, d + o_err, back, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   const int e = *reinterpret_cast<const int*>(c->h_stage + o_err);
   if (e & 1) return fail(c, FLEET_ERR_BASE64, "input is not Base64::encode output (alphabet/padding)");
   if (e & 2) return fail(c, FLEET_ERR_LAYOUT, "uploads disagree on the gradient layout header slots");
-  std::memcpy(merged, c->h_stage + o_out, len);
-  if (merged_f32) std::memcpy(merged_f32, c->h_stage + o_f32, sizeof(float) * n);
+  std::memcpy(merged + col0, c->h_stage + o_out, width);
+  if (merged_f32) std::memcpy(merged_f32 + v0, c->h_stage + o_f32, sizeof(float) * (v1 - v0));
   return FLEET_OK;
+}
+
+}  // namespace
+
+int fleet_update(fleet_ctx* c, const char* const* uploads, const size_t* lens, int M, const double* dampen,
+                 char* merged, size_t cap, size_t* out_len, float* merged_f32) {
+  if (!c || !uploads || !lens || !dampen || !merged || M <= 0) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  size_t len = 0;
+  int rc = check_update_args(c, uploads, lens, M, cap, out_len, &len);
+  if (rc) return rc;
+  const size_t n = fleet_b64_count(len);
+  // layout of the last picked upload (mergeFlatGradient keeps its header), walked on the host
+  std::vector<int32_t> hw(kHdrWords);
+  host_layout_parse(uploads[M - 1], len, (int64_t)n, FLEET_MAX_HEADERS, hw.data());
+  if (hw[0] != 0) return update_host_fallback(c, uploads, len, M, dampen, merged, merged_f32);
+  return update_window(c, uploads, len, M, dampen, hw.data(), 0, groups_of(n), merged, merged_f32,
+                       stage_threads(round16(len) * (size_t)M));
+}
+
+int fleet_update_multi(fleet_ctx* const* ctxs, int n_ctx, const char* const* uploads, const size_t* lens, int M,
+                       const double* dampen, char* merged, size_t cap, size_t* out_len, float* merged_f32) {
+  if (!ctxs || n_ctx <= 0 || !uploads || !lens || !dampen || !merged || M <= 0) return FLEET_ERR_ARG;
+  for (int k = 0; k < n_ctx; ++k) {
+    if (!ctxs[k]) return FLEET_ERR_ARG;
+    for (int j = 0; j < k; ++j)
+      if (ctxs[j] == ctxs[k]) return fail(ctxs[0], FLEET_ERR_ARG, "context %d is passed twice", k);
+  }
+  if (n_ctx == 1) return fleet_update(ctxs[0], uploads, lens, M, dampen, merged, cap, out_len, merged_f32);
+  fleet_ctx* c0 = ctxs[0];
+  size_t len = 0;
+  int rc;
+  {
+    std::lock_guard<std::mutex> lk(c0->mu);
+    if ((rc = check_update_args(c0, uploads, lens, M, cap, out_len, &len))) return rc;
+  }
+  const size_t n = fleet_b64_count(len), groups = groups_of(n);
+  std::vector<int32_t> hw(kHdrWords);
+  host_layout_parse(uploads[M - 1], len, (int64_t)n, FLEET_MAX_HEADERS, hw.data());
+  // a malformed header: the single-device flow reports the same error as a full device run
+  if (hw[0] != 0) return fleet_update(c0, uploads, lens, M, dampen, merged, cap, out_len, merged_f32);
+  const int threads = std::max(1, stage_threads(round16(len) * (size_t)M) / n_ctx);
+  std::vector<int> rcs((size_t)n_ctx, FLEET_OK);
+  std::vector<std::thread> ts;
+  ts.reserve((size_t)n_ctx);
+  for (int k = 0; k < n_ctx; ++k) {
+    // balanced contiguous split of the groups (fleet_amd.shard.group_range)
+    const size_t base = groups / (size_t)n_ctx, rem = groups % (size_t)n_ctx;
+    const size_t gb = (size_t)k * base + std::min((size_t)k, rem), ge = gb + base + ((size_t)k < rem ? 1 : 0);
+    ts.emplace_back([&, k, gb, ge] {
+      fleet_ctx* c = ctxs[k];
+      std::lock_guard<std::mutex> lk(c->mu);
+      if (hipSetDevice(c->device) != hipSuccess) {
+        rcs[(size_t)k] = fail(c, FLEET_ERR_HIP, "hipSetDevice(%d) failed", c->device);
+        return;
+      }
+      rcs[(size_t)k] = update_window(c, uploads, len, M, dampen, hw.data(), gb, ge, merged, merged_f32, threads);
+    });
+  }
+  for (auto& t : ts) t.join();
+  // the first failing shard's error (Base64 errors first, as one device reports them)
+  int first = -1;
+  for (int k = 0; k < n_ctx; ++k)
+    if (rcs[(size_t)k] != FLEET_OK && (first < 0 || (rcs[(size_t)k] == FLEET_ERR_BASE64 && rcs[(size_t)first] != FLEET_ERR_BASE64)))
+      first = k;
+  if (first < 0) return FLEET_OK;
+  if (first != 0) {
+    std::lock_guard<std::mutex> lk(c0->mu);
+    c0->err = ctxs[first]->err;
+  }
+  return rcs[(size_t)first];
 }
 
 // ---------------------------------------------------------- device-resident

@@ -114,6 +114,19 @@ int fleet_norm(fleet_ctx* ctx, const char* v, size_t len, double* out);
  * Base64::decodeFloat(merged), i.e. what descentNative decodes (:336). */
 int fleet_update(fleet_ctx* ctx, const char* const* uploads, const size_t* lens, int M, const double* dampen,
                  char* merged, size_t cap, size_t* out_len, float* merged_f32);
+/* The same update spread over the GPUs of a node from ONE host process
+ * (SURVEY.md §8e element sharding; the reference server is one JVM calling
+ * its natives under synchronized(acc), CppNNUpdater.java:333,420-509).
+ * ctxs = n_ctx distinct contexts, one per device. Context k takes a
+ * contiguous, balanced range of the 16-char / 3-value groups: on its own
+ * thread it copies that column window of every upload into its pinned
+ * staging, H2Ds it over its own PCIe link, runs the exact chain there and
+ * D2Hs its merged slice straight into `merged` / `merged_f32` (disjoint byte
+ * ranges). No collective and no reduction crosses devices, so the output is
+ * byte-identical to fleet_update's. Errors are reported on ctxs[0]
+ * (fleet_last_error), Base64 errors first. */
+int fleet_update_multi(fleet_ctx* const* ctxs, int n_ctx, const char* const* uploads, const size_t* lens, int M,
+                       const double* dampen, char* merged, size_t cap, size_t* out_len, float* merged_f32);
 
 /* Device-resident entry points (all buffers are device pointers) ----------
  * Uploads are stored as M rows of `pitch` bytes (pitch >= 16*ceil(len/16),
