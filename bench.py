@@ -426,7 +426,22 @@ def end_to_end(torch, codec, name, reps=3):
         merged = codec.update(ups, d)
         times.append(time.perf_counter() - t0)
     dt = min(times)
-    return {"workload": name, "ms": dt * 1e3, "ms_mean": float(np.mean(times)) * 1e3,
+    multi = None
+    ndev = torch.cuda.device_count()
+    if ndev > 1:  # one process driving every visible GPU (fleet_update_multi): column windows per device
+        codecs = [codec] + [F.Codec(k) for k in range(1, ndev)]
+        F.update_multi(codecs, ups, d)
+        mt = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            if F.update_multi(codecs, ups, d) != merged:
+                raise RuntimeError("fleet_update_multi differs from fleet_update")
+            mt.append(time.perf_counter() - t0)
+        multi = {"devices": ndev, "ms": min(mt) * 1e3, "gib_s": M * layout.n_up * 4 / min(mt) / 2**30,
+                 "pcie_gbs_achieved": M * L / min(mt) / 1e9}
+        for cd in codecs[1:]:
+            cd.close()
+    return {"workload": name, "ms": dt * 1e3, "ms_mean": float(np.mean(times)) * 1e3, "multi_gpu": multi,
             "gib_s": M * layout.n_up * 4 / dt / 2**30,
             "h2d_bytes": M * L, "d2h_bytes": len(merged),
             "h2d_floor_ms": h2d_s * 1e3, "h2d_floor_gbs": M * L / h2d_s / 1e9,

@@ -13,6 +13,9 @@
 #include <cstdio>
 #include <cstring>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -26,6 +29,68 @@
 #include "codec_device.h"
 
 #define FLEET_VERSION "fleet-mi355x 0.1.0 (gfx950)"
+
+// Persistent host threads for the staging copies of large host-buffer updates
+// (one pool per context, created on first use): a thread per part and call
+// cost 50-100 us to start on the GPU boxes, more than a part's copy.
+class WorkerPool {
+ public:
+  explicit WorkerPool(int workers) {
+    for (int i = 0; i < workers; ++i) ts_.emplace_back([this] { loop(); });
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : ts_) t.join();
+  }
+  int workers() const { return (int)ts_.size(); }
+  // f(i) for every i in [0, n), on the pool's threads and the caller's
+  void run(int n, const std::function<void(int)>& f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      f_ = &f;
+      n_ = n;
+      next_.store(0, std::memory_order_relaxed);
+      pending_ = (int)ts_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return pending_ == 0; });
+    f_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (int i; (i = next_.fetch_add(1, std::memory_order_relaxed)) < n_;) (*f_)(i);
+  }
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> g(m_);
+    for (;;) {
+      cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      g.unlock();
+      work();
+      g.lock();
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> ts_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* f_ = nullptr;
+  int n_ = 0;
+  std::atomic<int> next_{0};
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
 
 struct fleet_ctx {
   int device = 0;
@@ -65,6 +130,7 @@ struct fleet_ctx {
   size_t h_stage_cap = 0;
   int32_t* h_hdr = nullptr;
   int* h_err = nullptr;
+  std::unique_ptr<WorkerPool> pool;  // staging copy threads (stage_uploads)
 };
 
 namespace {
@@ -174,34 +240,28 @@ int finish_text(fleet_ctx* c, size_t out_len, char* out, size_t cap, size_t* out
   return rc;
 }
 
-// Host staging copy workers: FLEET_STAGE_THREADS, else -- for copies large
-// enough to pay for threads -- the CPUs this process may run on, at most 8.
+// Host staging copy threads: FLEET_STAGE_THREADS, else one per ~2 MiB of
+// staging, at most 8 and at most the CPUs this process may run on.
 int stage_threads(size_t bytes) {
-  if (const char* e = getenv("FLEET_STAGE_THREADS")) return std::max(1, atoi(e));
-  if (bytes < (32u << 20)) return 1;
+  if (const char* e = getenv("FLEET_STAGE_THREADS")) return std::max(1, std::min(64, atoi(e)));
   int n = 1;
   cpu_set_t set;
   if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
-  return std::max(1, std::min(n, 8));
+  return (int)std::max<size_t>(1, std::min<size_t>({bytes >> 21, 8, (size_t)std::max(1, n)}));
 }
 
-// f(i) for i in [0, n) on `threads` threads (the caller's thread included).
-template <class F>
-void parallel_for(int n, int threads, F&& f) {
+// f(i) for i in [0, n) on `threads` threads (the caller's and the context's pool).
+void parallel_for(fleet_ctx* c, int n, int threads, const std::function<void(int)>& f) {
   threads = std::max(1, std::min(threads, n));
   if (threads == 1) {
     for (int i = 0; i < n; ++i) f(i);
     return;
   }
-  std::atomic<int> next{0};
-  auto work = [&] {
-    for (int i; (i = next.fetch_add(1, std::memory_order_relaxed)) < n;) f(i);
-  };
-  std::vector<std::thread> ts;
-  ts.reserve((size_t)threads - 1);
-  for (int t = 1; t < threads; ++t) ts.emplace_back(work);
-  work();
-  for (auto& t : ts) t.join();
+  if (!c->pool || c->pool->workers() != threads - 1) {
+    c->pool.reset();
+    c->pool.reset(new WorkerPool(threads - 1));
+  }
+  c->pool->run(n, f);
 }
 
 // Copies bytes [col0, col0 + width) of each of the M uploads into the pinned
@@ -213,20 +273,22 @@ void parallel_for(int n, int threads, F&& f) {
 // Measured on MI355X (scripts/probe_e2e2.py, rocprofv3 memory-copy trace): 1 MiB
 // H2D parts run at ~35 GB/s with ~9 us gaps, one 7.8 MB copy at ~53 GB/s; three
 // parts gave the shortest host-buffer update for MNIST-64 (0.27 vs 0.32 ms with
-// one part). Large batches (the 1.43 GB north-star batch) copy each part with
-// `threads` workers: one thread's memcpy into pinned memory, not PCIe, bounded
-// the host-buffer update there.
+// one part). Each part is copied by `threads` workers (the context's pool): one
+// thread's memcpy into pinned memory, not PCIe, bounded the host-buffer update
+// of large batches (synth1m_256: 56.7 -> 27.9 ms; H2D floor 25.1 ms), and 16
+// parts beat 3 there (cifar10_256, 8 threads: 9.37 -> 8.68 ms; floor 7.56 ms;
+// scripts/gpu_e2e_sweep.sh). MNIST-64: 4 threads 0.26 ms vs 1 thread 0.39 ms.
 int stage_uploads(fleet_ctx* c, const char* const* uploads, size_t col0, size_t width, size_t pitch, int M,
                   size_t tail_bytes, int threads) {
   const size_t total = pitch * (size_t)M;
   int pieces = 3;
-  if (total >= (512u << 20)) pieces = (int)std::min<size_t>(16, total / (96u << 20));
+  if (total >= (256u << 20)) pieces = (int)std::min<size_t>(16, total / (24u << 20));
   if (const char* e = getenv("FLEET_STAGE_PIECES")) pieces = std::max(1, atoi(e));
   if (total < (4u << 20)) pieces = 1;
   pieces = std::min(pieces, M);
   for (int k = 0; k < pieces; ++k) {
     const int r0 = (int)((int64_t)M * k / pieces), r1 = (int)((int64_t)M * (k + 1) / pieces);
-    parallel_for(r1 - r0, threads, [&](int j) {
+    parallel_for(c, r1 - r0, threads, [&](int j) {
       const int i = r0 + j;
       uint8_t* row = c->h_stage + (size_t)i * pitch;
       std::memcpy(row, uploads[i] + col0, width);
