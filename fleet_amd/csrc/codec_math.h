@@ -375,9 +375,15 @@ FLEET_HD float q_lat(float x) {
 // biased exponent) plus one compare with the power of ten inside that binade.
 struct alignas(16) MulEntry {
   float m[4];  // x10 chain group multipliers: 10 (step taken) or 1
-  float h[4];  // /10 chain: fma(t, h, t*l) = div10(t) (taken) or t
-  float l[4];
+  float h[4];  // /10 chain: fma(t, h, t*kTenthLo) = div10(t) (h = RN(0.1), taken) or t (h = 1)
 };
+// One small term for both kinds of /10 step: a taken step needs t*lo within
+// 40 % of t*(0.1 - RN(0.1)) (div10's 2^-27.3 midpoint margin, 2^-26 scale of
+// the term), and an identity step fma(t, 1, t*kTenthLo) = RN(t*(1 - 1.5e-9))
+// = t because |t*kTenthLo| < half an ulp of t (2^-25 |t| at least); t is never
+// +-0 in a chain with identity steps (codes there end in a digit count >= 1).
+// Checked over every input by the multiplier-table digests (fn 13-15) and
+// tests/native/check_math.cpp mt.
 FLEET_HDC MulEntry mul_entry(uint32_t d) {  // d = numDigits; d > 9 (slow marker): identity
   MulEntry e{};
   const bool ok = d <= 9u;
@@ -386,7 +392,6 @@ FLEET_HDC MulEntry mul_entry(uint32_t d) {  // d = numDigits; d > 9 (slow marker
   for (int i = 0; i < 4; ++i) {
     e.m[i] = g[i] ? 10.0f : 1.0f;
     e.h[i] = g[i] ? kTenthHi : 1.0f;
-    e.l[i] = g[i] ? kTenthLo : 0.0f;
   }
   return e;
 }
@@ -436,15 +441,15 @@ FLEET_HD float mul10_mt(float X, const MulEntry& e) {
   return X * e.m[3];
 }
 FLEET_HD float div10_mt(float t, const MulEntry& e) {
-  t = __builtin_fmaf(t, e.h[0], t * e.l[0]);
-  t = __builtin_fmaf(t, e.h[0], t * e.l[0]);
-  t = __builtin_fmaf(t, e.h[1], t * e.l[1]);
-  t = __builtin_fmaf(t, e.h[2], t * e.l[2]);
-  t = __builtin_fmaf(t, e.h[2], t * e.l[2]);
-  t = __builtin_fmaf(t, e.h[3], t * e.l[3]);
-  t = __builtin_fmaf(t, e.h[3], t * e.l[3]);
-  t = __builtin_fmaf(t, e.h[3], t * e.l[3]);
-  return __builtin_fmaf(t, e.h[3], t * e.l[3]);
+  t = __builtin_fmaf(t, e.h[0], t * kTenthLo);
+  t = __builtin_fmaf(t, e.h[0], t * kTenthLo);
+  t = __builtin_fmaf(t, e.h[1], t * kTenthLo);
+  t = __builtin_fmaf(t, e.h[2], t * kTenthLo);
+  t = __builtin_fmaf(t, e.h[2], t * kTenthLo);
+  t = __builtin_fmaf(t, e.h[3], t * kTenthLo);
+  t = __builtin_fmaf(t, e.h[3], t * kTenthLo);
+  t = __builtin_fmaf(t, e.h[3], t * kTenthLo);
+  return __builtin_fmaf(t, e.h[3], t * kTenthLo);
 }
 
 // |code| = 10*floor(n/10) + d, n = trunc(X): floor(n/10) = mulhi(n, ceil(2^32/10))
