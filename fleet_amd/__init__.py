@@ -116,6 +116,21 @@ def lib() -> C.CDLL:
         "fleet_descent_window_device": (i32, [vp, vp, vp, vp, sz, sz, vp, vp, i32, vp, vp, i32, C.c_float, vp]),
         "fleet_minibatch_device": (i32, [vp, vp, sz, i32, vp, vp, i32, vp, i32, vp, vp, vp]),
         "fleet_minibatch": (i32, [vp, vp, sz, i32, vp, vp, i32, vp, i32, vp, vp, sz, szp]),
+        "fleet_model_load": (i32, [vp, vp, sz, i32, C.POINTER(vp)]),
+        "fleet_model_destroy": (None, [vp]),
+        "fleet_model_last_error": (C.c_char_p, [vp]),
+        "fleet_model_init_updater": (i32, [vp, vp, i32]),
+        "fleet_model_descent": (i32, [vp, vp, sz, i32, i32]),
+        "fleet_model_count": (i32, [vp]),
+        "fleet_model_get_params": (i32, [vp, i32, vp, sz, szp]),
+        "fleet_model_get_model_params": (i32, [vp, i32, vp, sz, szp]),
+        "fleet_model_get_epoch": (i32, [vp]),
+        "fleet_model_set_epoch": (None, [vp, i32]),
+        "fleet_model_get_priority": (i32, [vp]),
+        "fleet_model_set_priority": (None, [vp, i32]),
+        "fleet_model_get_lrate": (C.c_double, [vp]),
+        "fleet_model_shape": (i32, [vp, szp, szp, C.POINTER(i32), C.POINTER(i32)]),
+        "fleet_model_export": (i32, [vp, i32, vp, sz, vp, sz]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -590,6 +605,91 @@ def update_multi(codecs: Sequence["Codec"], uploads: Sequence, dampen: Sequence[
     if want_f32:
         return merged, f32[: b64_count(n_len)].copy()
     return merged
+
+
+class Model:
+    """The server's resident model (fleet_model): the state the reference's updater
+    natives keep in libnative.so (cppNN_backend.cpp: cnn, models, lrates_vec,
+    currEpoch, priority), with the natives' names as methods."""
+
+    def __init__(self, codec: "Codec", params_text, distillation_mode: int = 1):
+        """fetchParamsNative (cppNN_backend.cpp:282-301): network::read of a getParams text."""
+        t = _as_bytes(params_text)
+        h = C.c_void_p()
+        rc = codec._L.fleet_model_load(codec._h, t, len(t), int(distillation_mode), C.byref(h))
+        if rc != FLEET_OK:
+            raise FleetError(rc, "fleet_model_load failed (see stderr): not a supported getParams text")
+        self._h, self._L, self.codec = h, codec._L, codec
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.fleet_model_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != FLEET_OK:
+            msg = self._L.fleet_model_last_error(self._h).decode(errors="replace")
+            raise (LayoutError if rc == FLEET_ERR_LAYOUT else Base64Error if rc == FLEET_ERR_BASE64 else FleetError)(rc, msg)
+
+    def _text(self, fn, version):
+        need = C.c_size_t(0)
+        rc = fn(self._h, int(version), None, 0, C.byref(need))
+        if rc not in (FLEET_OK, FLEET_ERR_CAPACITY):
+            self._check(rc)
+        out = np.empty(max(1, need.value), np.uint8)
+        self._check(fn(self._h, int(version), out.ctypes.data, need.value, C.byref(need)))
+        return out[: need.value].tobytes()
+
+    def initUpdater(self, lrates) -> None:  # noqa: N802  (cppNN_backend.cpp:161-225, model part)
+        lr = np.ascontiguousarray(lrates, dtype=np.float64)
+        self._check(self._L.fleet_model_init_updater(self._h, lr.ctypes.data, len(lr)))
+
+    def descentNative(self, merged, client_batch_size: int, stale_size: int) -> None:  # noqa: N802  (:329-383)
+        m = _as_bytes(merged)
+        self._check(self._L.fleet_model_descent(self._h, m, len(m), int(client_batch_size), int(stale_size)))
+
+    def modelsSize(self) -> int:  # noqa: N802  (:324-327)
+        return self._L.fleet_model_count(self._h)
+
+    def getParametersNative(self, priority: int) -> bytes:  # noqa: N802  (:244-280)
+        return self._text(self._L.fleet_model_get_params, priority)
+
+    def getModelParametersNative(self, priority: int) -> bytes:  # noqa: N802  (:227-242)
+        return self._text(self._L.fleet_model_get_model_params, priority)
+
+    def getCurrEpoch(self) -> int:  # noqa: N802
+        return self._L.fleet_model_get_epoch(self._h)
+
+    def setCurrEpoch(self, e: int) -> None:  # noqa: N802
+        self._L.fleet_model_set_epoch(self._h, int(e))
+
+    def getPriority(self) -> int:  # noqa: N802
+        return self._L.fleet_model_get_priority(self._h)
+
+    def setPriority(self, p: int) -> None:  # noqa: N802
+        self._L.fleet_model_set_priority(self._h, int(p))
+
+    def getLrate(self) -> float:  # noqa: N802
+        return self._L.fleet_model_get_lrate(self._h)
+
+    def shape(self):
+        nw, nb = C.c_size_t(0), C.c_size_t(0)
+        ge, nl = C.c_int(0), C.c_int(0)
+        self._check(self._L.fleet_model_shape(self._h, C.byref(nw), C.byref(nb), C.byref(ge), C.byref(nl)))
+        return nw.value, nb.value, ge.value, nl.value
+
+    def export(self, version: int = -1):
+        """(weights, biases) of models[version]; version -1 = the current model."""
+        nw, nb, _, _ = self.shape()
+        w, b = np.empty(nw, np.float32), np.empty(nb, np.float32)
+        self._check(self._L.fleet_model_export(self._h, int(version), w.ctypes.data, nw, b.ctypes.data, nb))
+        return w, b
 
 
 class ByteVec:

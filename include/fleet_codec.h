@@ -297,6 +297,49 @@ int fleet_descent(fleet_ctx* ctx, float* weights, size_t n_weights, float* fc_bi
                   const float* grad, size_t n_grad, const int32_t* w_sizes, const uint8_t* w_present, int n_w,
                   const int32_t* b_sizes, const uint8_t* fc_layer, int n_b, float lr);
 
+/* The server's resident model -----------------------
+ * The state the reference's updater natives keep in libnative.so globals
+ * (Server/src/main/c++/cppNN_backend.cpp: cnn, models, lrates_vec, currEpoch,
+ * priority), built on the entry points above. Errors: fleet_model_last_error.
+ * distillation_mode = the reference's compile-time DISTILLATION_MODE (1: the
+ * quantised dictionary / index-set text; 0: plain values). */
+typedef struct fleet_model fleet_model;
+/* fetchParamsNative (:282-301): network::read of a getParams text (mojo01 format,
+ * commonLib/cppNN/network.h:611-706, 840-1010). Layer types: input,
+ * convolution, max_pool, semi_stochastic_pool, fully_connected (FLeet's cppNN
+ * models); W shapes follow the layers' new_connection rules (layer.h). */
+int fleet_model_load(fleet_ctx* ctx, const char* text, size_t len, int distillation_mode, fleet_model** out);
+void fleet_model_destroy(fleet_model* m);
+const char* fleet_model_last_error(const fleet_model* m);
+/* initUpdater's model part (:161-194): lr = (float)lrates[0], the first version
+ * (read(getParams()) of the model) pushed, priority = epoch = 0. */
+int fleet_model_init_updater(fleet_model* m, const double* lrates, int n_lrates);
+/* descentNative (:329-383): decodeFloat(merged); lr = lrates[epoch] while epoch <
+ * n_lrates; network::descent (sgd w -= lr*dW, fully-connected biases b -= db*lr,
+ * fleet_descent); epoch++; the new version read(getParams()) appended and the
+ * oldest dropped beyond stale_size. The merged gradient's header must describe
+ * the model (FLEET_ERR_LAYOUT otherwise; the reference overruns). */
+int fleet_model_descent(fleet_model* m, const char* merged, size_t len, int client_batch_size, int stale_size);
+/* modelsSize (:324-327) */
+int fleet_model_count(fleet_model* m);
+/* getParametersNative(version) (:244-280): the full getParams text of
+ * models[version] -- header, bias lines (ostream precision 6), weights
+ * (mode 1: quantization_weight_model's dictionary and index set, the version
+ * itself left unquantised). */
+int fleet_model_get_params(fleet_model* m, int version, char* out, size_t cap, size_t* out_len);
+/* getModelParametersNative(version) (:227-242): Base64 of getModelParams. */
+int fleet_model_get_model_params(fleet_model* m, int version, char* out, size_t cap, size_t* out_len);
+/* getCurrEpoch/setCurrEpoch, getPriority/setPriority, getLrate (:129-159) */
+int fleet_model_get_epoch(fleet_model* m);
+void fleet_model_set_epoch(fleet_model* m, int epoch);
+int fleet_model_get_priority(fleet_model* m);
+void fleet_model_set_priority(fleet_model* m, int priority);
+double fleet_model_get_lrate(fleet_model* m);
+/* sizes: non-null W floats, use_bias() biases, layer-graph edges, layers */
+int fleet_model_shape(fleet_model* m, size_t* n_weights, size_t* n_biases, int* graph_edges, int* n_layers);
+/* weights / biases of models[version] (version -1: the current `cnn`) */
+int fleet_model_export(fleet_model* m, int version, float* weights, size_t n_weights, float* biases, size_t n_biases);
+
 /* Name of the aggregation kernel fleet_update / fleet_update_device launch for
  * an upload of `len` Base64 bytes (or a group window of that many bytes):
  * "k_update<K>", "k_update_tiled<TG>" or "k_update_pipe<TG>" (profiling aid). */

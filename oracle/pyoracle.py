@@ -320,6 +320,9 @@ class ReferenceModel:
         L.ref_mnist_version_copy.argtypes = [C.c_void_p] * 4
         L.ref_mnist_model_params.restype = C.c_int
         L.ref_mnist_model_params.argtypes = [C.c_void_p] * 4
+        L.ref_server_session.restype = sz
+        L.ref_server_session.argtypes = [C.c_char_p, sz, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                         C.c_int, C.c_void_p, sz]
         L.ref_mnist_descent.restype = C.c_int
         L.ref_mnist_descent.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float] + [C.c_void_p] * 9
 
@@ -389,6 +392,38 @@ class ReferenceModel:
         self.lib.ref_mnist_model_params(None if win is None else win.ctypes.data,
                                         None if bin_ is None else bin_.ctypes.data, out.ctypes.data, C.byref(e))
         return out, e.value
+
+    def server_session(self, text: bytes, lrates, grads, batch: int = 8, stale: int = 2):
+        """The updater's model natives replayed on the reference network
+        (ref_server_session): fetchParamsNative(text), initUpdater(lrates), one
+        descentNative per merged gradient (decoded floats). Returns
+        ([(newest_text, newest_params, oldest_text, oldest_params)] after init and
+        each step, models.size())."""
+        lr = np.ascontiguousarray(lrates, dtype=np.float64)
+        g = np.ascontiguousarray(np.stack(grads) if len(grads) else np.zeros((0, 1)), dtype=np.float32)
+        n_g = g.shape[1] if len(grads) else 0
+        args = (text, len(text), lr.ctypes.data, len(lr), g.ctypes.data, n_g, len(grads), batch, stale)
+        n = self.lib.ref_server_session(*args, None, 0)
+        buf = np.empty(n, np.uint8)
+        self.lib.ref_server_session(*args, buf.ctypes.data, n)
+        raw = buf.tobytes()
+        pos, states = 0, []
+
+        def take(kind):
+            nonlocal pos
+            k = int(np.frombuffer(raw, np.uint64, 1, pos)[0])
+            pos += 8
+            if kind == "text":
+                v = raw[pos:pos + k]
+                pos += k
+            else:
+                v = np.frombuffer(raw, np.float32, k, pos).copy()
+                pos += 4 * k
+            return v
+        for _ in range(len(grads) + 1):
+            states.append((take("text"), take("floats"), take("text"), take("floats")))
+        n_models = int(np.frombuffer(raw, np.uint64, 1, pos)[0])
+        return states, n_models
 
     def mnist_version_copy(self, w_in, b_in):
         """descentNative's mode-1 model copy: read(getParams()) of the MNIST network."""

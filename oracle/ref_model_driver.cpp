@@ -14,6 +14,9 @@
  *     cppNN_backend.cpp:109-117) with its own weight init, optionally
  *     overwritten; the same mode-1 getParams, then network::read of that text
  *     into a fresh network (the client/Driver side, network.h:840-997).
+ *   ref_server_session: the server's model natives replayed on a network read
+ *     from a getParams text (fetchParamsNative, initUpdater, descentNative,
+ *     getParametersNative, getModelParametersNative; cppNN_backend.cpp:161-383).
  */
 #include <cstdio>
 #include <cstring>
@@ -262,6 +265,95 @@ void ref_mnist_version_copy(const float* w_in, const float* b_in, float* w_out, 
       std::memcpy(b_out + o, l->bias.x, sizeof(float) * l->bias.size());
       o += l->bias.size();
     }
+}
+
+// The updater's model natives of Server/src/main/c++/cppNN_backend.cpp replayed
+// on the reference's own network code (DISTILLATION_MODE=1):
+//   fetchParamsNative(text)          :282-301  cnn.read; start_epoch("distillation")
+//   initUpdater(lrates)              :161-225  set_learning_rate(lrates[0]); models <- read(getParams());
+//                                              one train_class (blank input, label 0, uniform
+//                                              teacher probabilities) sizes dW_sets
+//   descentNative(g_i, batch, stale) :329-383  set_mini_batch_size; lr = lrates[epoch] while
+//                                              epoch < n; descent(g_i); epoch++; models <- read(getParams());
+//                                              oldest dropped beyond stale
+// g = n_steps merged gradients (decodeFloat of the merged Base64), n_g floats each.
+// After init and after every step, the newest and the oldest version's
+// getParametersNative text (save, quantize, getParams, restore) and getModelParams
+// vector are appended to `out` as records {u64 n, bytes} / {u64 n, floats}, then
+// models.size() as a u64. Returns the bytes needed (call with out == NULL to size it).
+size_t ref_server_session(const char* text, size_t len, const double* lrates, int n_lr, const float* g, int n_g,
+                          int n_steps, int batch, int stale, char* out, size_t cap) {
+  std::string buf;
+  auto put_text = [&](const std::string& t) {
+    const uint64_t n = t.size();
+    buf.append(reinterpret_cast<const char*>(&n), 8);
+    buf += t;
+  };
+  auto put_floats = [&](const std::vector<float>& v) {
+    const uint64_t n = v.size();
+    buf.append(reinterpret_cast<const char*>(&n), 8);
+    buf.append(reinterpret_cast<const char*>(v.data()), sizeof(float) * v.size());
+  };
+  auto quantized_text = [](mojo::network* net) {
+    std::vector<mojo::matrix*> unq;
+    net->save_model_weights(&unq);
+    net->quantization_weight_model();
+    const std::string t = net->getParams();
+    net->load_model_weights(unq);
+    return t;
+  };
+  mojo::network cnn("sgd");
+  {
+    std::istringstream ss(std::string(text, len));
+    cnn.start_epoch("distillation");
+    cnn.set_random_augmentation(1, 1, 0, 0, mojo::edge);
+    cnn.clear();
+    cnn.read(ss);
+  }
+  std::vector<mojo::network*> models;
+  auto push_version = [&]() {
+    mojo::network* nw = new mojo::network("sgd");
+    nw->start_epoch("distillation");
+    nw->set_random_augmentation(1, 1, 0, 0, mojo::edge);
+    std::istringstream ss(cnn.getParams());
+    nw->clear();
+    nw->read(ss);
+    models.push_back(nw);
+  };
+  auto record = [&]() {
+    for (mojo::network* v : {models.back(), models.front()}) {
+      put_text(quantized_text(v));
+      put_floats(v->getModelParams());
+    }
+  };
+  cnn.set_learning_rate(lrates[0]);
+  push_version();
+  {
+    auto& layers = cnn.layer_sets[mojo::network::MAIN_LAYER_SET];
+    const mojo::matrix& in = layers.front()->node;
+    std::vector<float> blank((size_t)in.cols * in.rows * in.chans, 0.0f);
+    const int n_out = layers.back()->node.size();
+    std::vector<float> teacher((size_t)n_out, 1.0f / (float)n_out);
+    cnn.train_class(blank.data(), 0, &teacher);
+  }
+  record();
+  int epoch = 0;
+  for (int i = 0; i < n_steps; ++i) {
+    cnn.set_mini_batch_size(batch);
+    if (epoch < n_lr) cnn.set_learning_rate(lrates[epoch]);
+    cnn.descent(std::vector<float>(g + (size_t)i * n_g, g + (size_t)(i + 1) * n_g));
+    ++epoch;
+    push_version();
+    if ((int)models.size() > stale) {
+      delete models.front();
+      models.erase(models.begin());
+    }
+    record();
+  }
+  const uint64_t nm = models.size();
+  buf.append(reinterpret_cast<const char*>(&nm), 8);
+  for (auto* v : models) delete v;
+  return copy_out(buf, out, cap);
 }
 
 }  // extern "C"
