@@ -97,6 +97,10 @@ def lib() -> C.CDLL:
         "fleet_norm": (i32, [vp, vp, sz, C.POINTER(C.c_double)]),
         "fleet_update": (i32, [vp, vp, vp, i32, vp, vp, sz, szp, vp]),
         "fleet_update_multi": (i32, [vp, i32, vp, vp, i32, vp, vp, sz, szp, vp]),
+        "fleet_update_rows": (i32, [vp, vp, sz, sz, i32, vp, vp, sz, szp, vp]),
+        "fleet_update_rows_multi": (i32, [vp, i32, vp, sz, sz, i32, vp, vp, sz, szp, vp]),
+        "fleet_host_register": (i32, [vp, vp, sz]),
+        "fleet_host_unregister": (i32, [vp, vp]),
         "fleet_update_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, sz, sz, vp, vp, vp]),
         "fleet_update_kernel": (C.c_char_p, [sz]),
         "fleet_model_quantize_index": (i32, [vp, vp, vp, i32, vp, vp, vp, vp]),
@@ -341,6 +345,18 @@ class Codec:
         if want_f32:
             return merged, f32[: b64_count(L)].copy()
         return merged
+
+    def update_rows(self, rows: np.ndarray, length: int, dampen: Sequence[float], want_f32: bool = False):
+        """fleet_update over a uint8 host array [M, row_pitch] whose row i holds upload i's
+        `length` Base64 chars; page-locked rows (register_host) go to HBM without a host copy."""
+        return update_rows([self], rows, length, dampen, want_f32)
+
+    def register_host(self, arr: np.ndarray):
+        """Page-lock a host array for copy-free ingress (fleet_host_register)."""
+        self._check(self._L.fleet_host_register(self._h, arr.ctypes.data, arr.nbytes))
+
+    def unregister_host(self, arr: np.ndarray):
+        self._check(self._L.fleet_host_unregister(self._h, arr.ctypes.data))
 
     # -- device-resident (torch tensors on this device) -----------------------
     def update_device(self, uploads_u8, length: int, dampen: Sequence[float], header_pos, merged_u8,
@@ -604,6 +620,35 @@ def update_multi(codecs: Sequence["Codec"], uploads: Sequence, dampen: Sequence[
     merged = out[: n.value].tobytes()
     if want_f32:
         return merged, f32[: b64_count(n_len)].copy()
+    return merged
+
+
+def update_rows(codecs: Sequence["Codec"], rows: np.ndarray, length: int, dampen: Sequence[float],
+                want_f32: bool = False):
+    """fleet_update_rows(_multi): the update over uploads stored as the rows of one host
+    array (rows[i, :length] = upload i), on one or several device contexts."""
+    if rows.ndim != 2 or rows.dtype != np.uint8 or not rows.flags.c_contiguous:
+        raise ValueError("rows: a C-contiguous uint8 array [M, row_pitch]")
+    M, pitch = rows.shape
+    if len(dampen) != M:
+        raise ValueError("one dampening factor per upload")
+    d = np.ascontiguousarray(dampen, dtype=np.float64)
+    out = np.empty(length + 16, np.uint8)
+    n = C.c_size_t(0)
+    f32 = np.empty(b64_count(length) + 1, np.float32) if want_f32 else None
+    L = lib()
+    if len(codecs) == 1:
+        rc = L.fleet_update_rows(codecs[0]._h, rows.ctypes.data, pitch, length, M, d.ctypes.data, out.ctypes.data,
+                                 len(out), C.byref(n), f32.ctypes.data if want_f32 else None)
+    else:
+        hs = (C.c_void_p * len(codecs))(*[c._h for c in codecs])
+        rc = L.fleet_update_rows_multi(C.cast(hs, C.c_void_p), len(codecs), rows.ctypes.data, pitch, length, M,
+                                       d.ctypes.data, out.ctypes.data, len(out), C.byref(n),
+                                       f32.ctypes.data if want_f32 else None)
+    codecs[0]._check(rc)
+    merged = out[: n.value].tobytes()
+    if want_f32:
+        return merged, f32[: b64_count(length)].copy()
     return merged
 
 

@@ -681,8 +681,14 @@ int check_update_args(fleet_ctx* c, const char* const* uploads, const size_t* le
 //   staging block, mirrored on the device in d_a:
 //   [window rows M x wpitch | dampen M doubles | header words | err | merged | fp32]
 //   one H2D up to err (inclusive, err = 0), one D2H from err on.
+// pinned_rows != NULL: the uploads are rows `row_pitch` apart in page-locked
+// memory (fleet_host_register, or allocated pinned): the window goes to HBM in
+// one 2D DMA straight from them, with no host copy (only the parameter words
+// are staged). Bytes past `len` in the last group of a row may hold anything:
+// the kernels ignore the chars that carry no value.
 int update_window(fleet_ctx* c, const char* const* uploads, size_t len, int M, const double* dampen,
-                  const int32_t* hw, size_t gb, size_t ge, char* merged, float* merged_f32, int threads) {
+                  const int32_t* hw, size_t gb, size_t ge, char* merged, float* merged_f32, int threads,
+                  const char* pinned_rows = nullptr, size_t row_pitch = 0) {
   const size_t n = fleet_b64_count(len);
   const size_t w = ge - gb;
   if (w == 0) return FLEET_OK;
@@ -699,7 +705,14 @@ int update_window(fleet_ctx* c, const char* const* uploads, size_t len, int M, c
   std::memcpy(c->h_stage + o_hdr, hw, sizeof(int32_t) * kHdrWords);
   std::memcpy(c->h_stage + o_damp, dampen, sizeof(double) * (size_t)M);
   std::memset(c->h_stage + o_err, 0, 16);
-  if ((rc = stage_uploads(c, uploads, col0, width, wpitch, M, o_err + 16 - total, threads))) return rc;
+  if (pinned_rows) {
+    HIP_TRY(c, hipMemcpy2DAsync(c->d_a, wpitch, pinned_rows + col0, row_pitch, width, (size_t)M,
+                                hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->d_a + total, c->h_stage + total, o_err + 16 - total, hipMemcpyHostToDevice,
+                              c->stream));
+  } else if ((rc = stage_uploads(c, uploads, col0, width, wpitch, M, o_err + 16 - total, threads))) {
+    return rc;
+  }
   uint8_t* d = c->d_a;
   // window mode: row and output pointers shifted back by the window's start
   HIP_TRY(c, fleet::launch_update(d - col0, wpitch, M, reinterpret_cast<const double*>(d + o_damp), (double)1 / M,
@@ -738,15 +751,26 @@ int fleet_update(fleet_ctx* c, const char* const* uploads, const size_t* lens, i
                        stage_threads(round16(len) * (size_t)M));
 }
 
-int fleet_update_multi(fleet_ctx* const* ctxs, int n_ctx, const char* const* uploads, const size_t* lens, int M,
-                       const double* dampen, char* merged, size_t cap, size_t* out_len, float* merged_f32) {
-  if (!ctxs || n_ctx <= 0 || !uploads || !lens || !dampen || !merged || M <= 0) return FLEET_ERR_ARG;
+namespace {
+
+// true when [p, p + bytes) is page-locked host memory the GPUs can DMA from
+bool is_pinned(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+int update_multi_impl(fleet_ctx* const* ctxs, int n_ctx, const char* const* uploads, const size_t* lens, int M,
+                      const double* dampen, char* merged, size_t cap, size_t* out_len, float* merged_f32,
+                      const char* pinned_rows, size_t row_pitch) {
   for (int k = 0; k < n_ctx; ++k) {
     if (!ctxs[k]) return FLEET_ERR_ARG;
     for (int j = 0; j < k; ++j)
       if (ctxs[j] == ctxs[k]) return fail(ctxs[0], FLEET_ERR_ARG, "context %d is passed twice", k);
   }
-  if (n_ctx == 1) return fleet_update(ctxs[0], uploads, lens, M, dampen, merged, cap, out_len, merged_f32);
   fleet_ctx* c0 = ctxs[0];
   size_t len = 0;
   int rc;
@@ -758,30 +782,40 @@ int fleet_update_multi(fleet_ctx* const* ctxs, int n_ctx, const char* const* upl
   std::vector<int32_t> hw(kHdrWords);
   host_layout_parse(uploads[M - 1], len, (int64_t)n, FLEET_MAX_HEADERS, hw.data());
   // a malformed header: the single-device flow reports the same error as a full device run
-  if (hw[0] != 0) return fleet_update(c0, uploads, lens, M, dampen, merged, cap, out_len, merged_f32);
+  if (hw[0] != 0) {
+    std::lock_guard<std::mutex> lk(c0->mu);
+    HIP_TRY(c0, hipSetDevice(c0->device));
+    return update_host_fallback(c0, uploads, len, M, dampen, merged, merged_f32);
+  }
   const int threads = std::max(1, stage_threads(round16(len) * (size_t)M) / n_ctx);
   std::vector<int> rcs((size_t)n_ctx, FLEET_OK);
-  std::vector<std::thread> ts;
-  ts.reserve((size_t)n_ctx);
-  for (int k = 0; k < n_ctx; ++k) {
+  auto run = [&](int k) {
     // balanced contiguous split of the groups (fleet_amd.shard.group_range)
     const size_t base = groups / (size_t)n_ctx, rem = groups % (size_t)n_ctx;
     const size_t gb = (size_t)k * base + std::min((size_t)k, rem), ge = gb + base + ((size_t)k < rem ? 1 : 0);
-    ts.emplace_back([&, k, gb, ge] {
-      fleet_ctx* c = ctxs[k];
-      std::lock_guard<std::mutex> lk(c->mu);
-      if (hipSetDevice(c->device) != hipSuccess) {
-        rcs[(size_t)k] = fail(c, FLEET_ERR_HIP, "hipSetDevice(%d) failed", c->device);
-        return;
-      }
-      rcs[(size_t)k] = update_window(c, uploads, len, M, dampen, hw.data(), gb, ge, merged, merged_f32, threads);
-    });
+    fleet_ctx* c = ctxs[k];
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (hipSetDevice(c->device) != hipSuccess) {
+      rcs[(size_t)k] = fail(c, FLEET_ERR_HIP, "hipSetDevice(%d) failed", c->device);
+      return;
+    }
+    rcs[(size_t)k] = update_window(c, uploads, len, M, dampen, hw.data(), gb, ge, merged, merged_f32,
+                                   n_ctx == 1 ? stage_threads(round16(len) * (size_t)M) : threads, pinned_rows,
+                                   row_pitch);
+  };
+  if (n_ctx == 1) {
+    run(0);
+  } else {
+    std::vector<std::thread> ts;
+    ts.reserve((size_t)n_ctx);
+    for (int k = 0; k < n_ctx; ++k) ts.emplace_back(run, k);
+    for (auto& t : ts) t.join();
   }
-  for (auto& t : ts) t.join();
   // the first failing shard's error (Base64 errors first, as one device reports them)
   int first = -1;
   for (int k = 0; k < n_ctx; ++k)
-    if (rcs[(size_t)k] != FLEET_OK && (first < 0 || (rcs[(size_t)k] == FLEET_ERR_BASE64 && rcs[(size_t)first] != FLEET_ERR_BASE64)))
+    if (rcs[(size_t)k] != FLEET_OK &&
+        (first < 0 || (rcs[(size_t)k] == FLEET_ERR_BASE64 && rcs[(size_t)first] != FLEET_ERR_BASE64)))
       first = k;
   if (first < 0) return FLEET_OK;
   if (first != 0) {
@@ -789,6 +823,54 @@ int fleet_update_multi(fleet_ctx* const* ctxs, int n_ctx, const char* const* upl
     c0->err = ctxs[first]->err;
   }
   return rcs[(size_t)first];
+}
+
+int update_rows_impl(fleet_ctx* const* ctxs, int n_ctx, const char* rows, size_t row_pitch, size_t len, int M,
+                     const double* dampen, char* merged, size_t cap, size_t* out_len, float* merged_f32) {
+  if (row_pitch < len) return fail(ctxs[0], FLEET_ERR_ARG, "row pitch %zu < upload length %zu", row_pitch, len);
+  std::vector<const char*> ptrs((size_t)M);
+  std::vector<size_t> lens((size_t)M, len);
+  for (int i = 0; i < M; ++i) ptrs[(size_t)i] = rows + (size_t)i * row_pitch;
+  const bool pinned = is_pinned(rows) && is_pinned(rows + (size_t)(M - 1) * row_pitch + (len ? len - 1 : 0));
+  return update_multi_impl(ctxs, n_ctx, ptrs.data(), lens.data(), M, dampen, merged, cap, out_len, merged_f32,
+                           pinned ? rows : nullptr, row_pitch);
+}
+
+}  // namespace
+
+int fleet_update_multi(fleet_ctx* const* ctxs, int n_ctx, const char* const* uploads, const size_t* lens, int M,
+                       const double* dampen, char* merged, size_t cap, size_t* out_len, float* merged_f32) {
+  if (!ctxs || n_ctx <= 0 || !uploads || !lens || !dampen || !merged || M <= 0) return FLEET_ERR_ARG;
+  if (n_ctx == 1) return fleet_update(ctxs[0], uploads, lens, M, dampen, merged, cap, out_len, merged_f32);
+  return update_multi_impl(ctxs, n_ctx, uploads, lens, M, dampen, merged, cap, out_len, merged_f32, nullptr, 0);
+}
+
+int fleet_update_rows(fleet_ctx* c, const char* rows, size_t row_pitch, size_t len, int M, const double* dampen,
+                      char* merged, size_t cap, size_t* out_len, float* merged_f32) {
+  if (!c || !rows || !dampen || !merged || M <= 0) return FLEET_ERR_ARG;
+  return update_rows_impl(&c, 1, rows, row_pitch, len, M, dampen, merged, cap, out_len, merged_f32);
+}
+
+int fleet_update_rows_multi(fleet_ctx* const* ctxs, int n_ctx, const char* rows, size_t row_pitch, size_t len, int M,
+                            const double* dampen, char* merged, size_t cap, size_t* out_len, float* merged_f32) {
+  if (!ctxs || n_ctx <= 0 || !ctxs[0] || !rows || !dampen || !merged || M <= 0) return FLEET_ERR_ARG;
+  return update_rows_impl(ctxs, n_ctx, rows, row_pitch, len, M, dampen, merged, cap, out_len, merged_f32);
+}
+
+int fleet_host_register(fleet_ctx* c, void* ptr, size_t bytes) {
+  if (!c || !ptr || !bytes) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipHostRegister(ptr, bytes, hipHostRegisterPortable));
+  return FLEET_OK;
+}
+
+int fleet_host_unregister(fleet_ctx* c, void* ptr) {
+  if (!c || !ptr) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipHostUnregister(ptr));
+  return FLEET_OK;
 }
 
 // ---------------------------------------------------------- device-resident

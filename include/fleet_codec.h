@@ -127,6 +127,20 @@ int fleet_update(fleet_ctx* ctx, const char* const* uploads, const size_t* lens,
  * (fleet_last_error), Base64 errors first. */
 int fleet_update_multi(fleet_ctx* const* ctxs, int n_ctx, const char* const* uploads, const size_t* lens, int M,
                        const double* dampen, char* merged, size_t cap, size_t* out_len, float* merged_f32);
+/* fleet_update / fleet_update_multi over uploads stored as M rows `row_pitch`
+ * bytes apart (row i = upload i, `len` Base64 chars): the ingress of a caller
+ * that deserialises the uploads into one buffer (a Java direct ByteBuffer,
+ * INTEGRATION.md). When that buffer is page-locked (fleet_host_register, or
+ * allocated pinned) every context DMAs its column window straight from it --
+ * no host copy at all; otherwise the rows are staged as in fleet_update. */
+int fleet_update_rows(fleet_ctx* ctx, const char* rows, size_t row_pitch, size_t len, int M, const double* dampen,
+                      char* merged, size_t cap, size_t* out_len, float* merged_f32);
+int fleet_update_rows_multi(fleet_ctx* const* ctxs, int n_ctx, const char* rows, size_t row_pitch, size_t len, int M,
+                            const double* dampen, char* merged, size_t cap, size_t* out_len, float* merged_f32);
+/* Page-lock (hipHostRegister, portable to every device) / release a long-lived
+ * host buffer, e.g. the upload rows of fleet_update_rows. */
+int fleet_host_register(fleet_ctx* ctx, void* ptr, size_t bytes);
+int fleet_host_unregister(fleet_ctx* ctx, void* ptr);
 
 /* Device-resident entry points (all buffers are device pointers) ----------
  * Uploads are stored as M rows of `pitch` bytes (pitch >= 16*ceil(len/16),

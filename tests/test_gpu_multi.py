@@ -85,3 +85,27 @@ def test_update_threaded_staging(contexts, oracle, monkeypatch, threads, pieces)
     expected = oracle.update_fused(ups, d, hm)
     assert contexts[0].update(ups, d) == expected
     assert F.update_multi(contexts[:2], ups, d) == expected
+
+
+@pytest.mark.parametrize("N", [1, 3])
+@pytest.mark.parametrize("pad", [0, 3, 16])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_update_rows(contexts, oracle, N, pad, pinned):
+    # uploads as the rows of one host buffer (a direct ByteBuffer's layout); page-locked
+    # rows are DMAed per context column window with no host copy
+    ups = uploads_for(oracle, MNIST, 5, seed=21 + pad)
+    d = [1.0 / ((c % 3) + 1) for c in range(5)]
+    L = len(ups[0])
+    rows = np.full((5, L + pad), ord("!"), np.uint8)  # bytes past len are never read as values
+    for i, u in enumerate(ups):
+        rows[i, :L] = np.frombuffer(u, np.uint8)
+    if pinned:
+        contexts[0].register_host(rows)
+    try:
+        merged, f32 = F.update_rows(contexts[:N], rows, L, d, want_f32=True)
+    finally:
+        if pinned:
+            contexts[0].unregister_host(rows)
+    expected = oracle.update_faithful(ups, d)
+    assert merged == expected
+    assert np.array_equal(f32.view(np.uint32), oracle.decode_floats(expected).view(np.uint32))
