@@ -1,36 +1,82 @@
-"""ctypes helpers for driving libfleet_native.so built against the test JNI
-header (tests/native/jni/jni.h): arrays are heap blocks {int32 len, int32 elem, payload}."""
+"""ctypes harness for driving libfleet_native.so through a JNI function table.
+
+tests/native/fakejvm.cpp (built here with g++ against tests/native/jni/jni.h,
+the JNI specification's table layout) is a small in-process JVM stand-in:
+fakejvm_env() is a JNIEnv* whose `functions` table the shim's calls dispatch
+through, and it counts the JNI-rule violations the shim must avoid (local
+reference overflow, JNI calls inside critical regions, unreleased array
+elements). TEST INFRASTRUCTURE ONLY."""
 import ctypes as C
+import os
+import subprocess
+import tempfile
 
 import numpy as np
 
-libc = C.CDLL(None)
-libc.calloc.restype = C.c_void_p
-libc.calloc.argtypes = [C.c_size_t, C.c_size_t]
-libc.free.argtypes = [C.c_void_p]
-
-HDR = 8
+HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
 
 
-def new_array(payload: bytes, elem: int = 1) -> int:
-    n = len(payload) // elem
-    p = libc.calloc(1, HDR + len(payload) + 1)
-    C.memmove(p, C.byref(C.c_int32(n)), 4)
-    C.memmove(p + 4, C.byref(C.c_int32(elem)), 4)
-    C.memmove(p + HDR, payload, len(payload))
-    return p
+def fakejvm():
+    global _lib
+    if _lib is not None:
+        return _lib
+    out = os.path.join(tempfile.mkdtemp(prefix="fakejvm"), "libfakejvm.so")
+    subprocess.check_call(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-fvisibility=hidden",
+                           "-I", os.path.join(HERE, "native", "jni"), os.path.join(HERE, "native", "fakejvm.cpp"),
+                           "-o", out])
+    L = C.CDLL(out)
+    vp = C.c_void_p
+    L.fakejvm_env.restype = vp
+    L.fakejvm_begin_call.restype = None
+    L.fakejvm_stat.restype = C.c_long
+    L.fakejvm_stat.argtypes = [C.c_char_p]
+    L.fakejvm_set_frame_limit.argtypes = [C.c_long]
+    L.fakejvm_new_array.restype = vp
+    L.fakejvm_new_array.argtypes = [C.c_int, vp, C.c_int]
+    L.fakejvm_new_object_array.restype = vp
+    L.fakejvm_new_object_array.argtypes = [vp, C.c_int]
+    L.fakejvm_new_direct.restype = vp
+    L.fakejvm_new_direct.argtypes = [vp, C.c_long]
+    L.fakejvm_array_len.restype = C.c_int
+    L.fakejvm_array_len.argtypes = [vp]
+    L.fakejvm_array_data.restype = vp
+    L.fakejvm_array_data.argtypes = [vp]
+    _lib = L
+    return L
+
+
+def env():
+    return fakejvm().fakejvm_env()
+
+
+def begin():
+    fakejvm().fakejvm_begin_call()
+
+
+def stat(name: str) -> int:
+    return fakejvm().fakejvm_stat(name.encode())
+
+
+def new_bytes(payload: bytes) -> int:
+    return fakejvm().fakejvm_new_array(1, payload, len(payload))
+
+
+def new_doubles(values) -> int:
+    a = np.ascontiguousarray(values, np.float64)
+    return fakejvm().fakejvm_new_array(4, a.ctypes.data, len(a))
 
 
 def new_object_array(ptrs) -> int:
     arr = (C.c_void_p * len(ptrs))(*ptrs)
-    return new_array(bytes(arr), elem=C.sizeof(C.c_void_p))
+    return fakejvm().fakejvm_new_object_array(arr, len(ptrs))
+
+
+def new_direct(buf: np.ndarray) -> int:
+    return fakejvm().fakejvm_new_direct(buf.ctypes.data, buf.nbytes)
 
 
 def read_bytes(p: int) -> bytes:
     assert p, "native returned null"
-    n = C.c_int32.from_address(p).value
-    return C.string_at(p + HDR, n)
-
-
-def new_doubles(values) -> int:
-    return new_array(np.ascontiguousarray(values, np.float64).tobytes(), elem=8)
+    L = fakejvm()
+    return C.string_at(L.fakejvm_array_data(p), L.fakejvm_array_len(p))

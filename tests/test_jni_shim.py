@@ -1,5 +1,8 @@
 """The JNI shim (libfleet_native.so): exports the reference's Java_* natives and
-returns, through the (test) JNI surface, exactly the bytes of the reference path."""
+returns, through a JNI function table (tests/native/jni/jni.h, the JNI
+specification's slot order; tests/native/fakejvm.cpp), exactly the bytes of the
+reference path -- while keeping the JNI rules a JVM enforces (local reference
+capacity, critical regions, released array elements)."""
 import ctypes as C
 import os
 
@@ -7,12 +10,21 @@ import numpy as np
 import pytest
 
 import fleet_amd as F
-from fleet_amd.layouts import MNIST, synthetic
+from fleet_amd.layouts import MNIST
 
 JNI = os.path.join(os.path.dirname(F.LIB_PATH), "libfleet_native.so")
-SYMBOLS = ["Java_apps_cppNN_CppNNUpdater_getFlatGradient", "Java_apps_cppNN_CppNNUpdater_mergeFlatGradient",
-           "Java_utils_ByteVec_scalarMulNative", "Java_utils_ByteVec_getNorm", "Java_utils_ByteVec_addNative",
-           "Java_utils_ByteVec_subtractNative", "Java_apps_cppNN_FleetUpdater_aggregateNative"]
+HERE = os.path.dirname(os.path.abspath(__file__))
+UPDATER = "Java_apps_cppNN_CppNNUpdater_"
+BYTES_OUT = {
+    UPDATER + "getFlatGradient": 1, UPDATER + "mergeFlatGradient": 2, "Java_utils_ByteVec_scalarMulNative": None,
+    "Java_utils_ByteVec_addNative": 2, "Java_utils_ByteVec_subtractNative": 2,
+    "Java_apps_cppNN_FleetUpdater_aggregateNative": 2, UPDATER + "getParametersNative": None,
+    UPDATER + "getModelParametersNative": None, "Java_apps_cppNN_FleetUpdater_aggregateDirectNative": None,
+}
+SYMBOLS = list(BYTES_OUT) + ["Java_utils_ByteVec_getNorm", UPDATER + "fetchParamsNative", UPDATER + "initUpdater",
+                             UPDATER + "descentNative", UPDATER + "modelsSize", UPDATER + "getPriority",
+                             UPDATER + "setPriority", UPDATER + "getCurrEpoch", UPDATER + "setCurrEpoch",
+                             UPDATER + "getLrate", "Java_apps_cppNN_FleetUpdater_registerDirectNative"]
 
 
 def load():
@@ -20,46 +32,163 @@ def load():
         pytest.skip("libfleet_native.so not built")
     F.lib()  # same HIP runtime as torch
     L = C.CDLL(JNI)
-    vp = C.c_void_p
-    for s in SYMBOLS:
-        getattr(L, s).restype = C.c_double if s.endswith("getNorm") else vp
-    L.Java_apps_cppNN_CppNNUpdater_getFlatGradient.argtypes = [vp, vp, vp]
-    L.Java_apps_cppNN_CppNNUpdater_mergeFlatGradient.argtypes = [vp, vp, vp, vp]
-    L.Java_utils_ByteVec_scalarMulNative.argtypes = [vp, vp, vp, C.c_double]
-    L.Java_utils_ByteVec_getNorm.argtypes = [vp, vp, vp]
-    L.Java_utils_ByteVec_addNative.argtypes = [vp, vp, vp, vp]
-    L.Java_utils_ByteVec_subtractNative.argtypes = [vp, vp, vp, vp]
-    L.Java_apps_cppNN_FleetUpdater_aggregateNative.argtypes = [vp, vp, vp, vp]
+    vp, i32, f64 = C.c_void_p, C.c_int32, C.c_double
+    for s in BYTES_OUT:
+        getattr(L, s).restype = vp
+    sig = {
+        UPDATER + "getFlatGradient": [vp, vp, vp], UPDATER + "mergeFlatGradient": [vp, vp, vp, vp],
+        "Java_utils_ByteVec_scalarMulNative": [vp, vp, vp, f64], "Java_utils_ByteVec_getNorm": [vp, vp, vp],
+        "Java_utils_ByteVec_addNative": [vp, vp, vp, vp], "Java_utils_ByteVec_subtractNative": [vp, vp, vp, vp],
+        "Java_apps_cppNN_FleetUpdater_aggregateNative": [vp, vp, vp, vp],
+        "Java_apps_cppNN_FleetUpdater_aggregateDirectNative": [vp, vp, vp, i32, i32, i32, vp],
+        "Java_apps_cppNN_FleetUpdater_registerDirectNative": [vp, vp, vp],
+        UPDATER + "fetchParamsNative": [vp, vp, vp], UPDATER + "initUpdater": [vp, vp, vp, i32, f64, f64],
+        UPDATER + "descentNative": [vp, vp, vp, i32, i32], UPDATER + "getParametersNative": [vp, vp, i32],
+        UPDATER + "getModelParametersNative": [vp, vp, i32], UPDATER + "modelsSize": [vp, vp],
+        UPDATER + "getCurrEpoch": [vp, vp], UPDATER + "setCurrEpoch": [vp, vp, i32],
+        UPDATER + "getPriority": [vp, vp], UPDATER + "setPriority": [vp, vp, i32], UPDATER + "getLrate": [vp, vp],
+    }
+    for s, a in sig.items():
+        getattr(L, s).argtypes = a
+    L.Java_utils_ByteVec_getNorm.restype = f64
+    L.Java_apps_cppNN_CppNNUpdater_getLrate.restype = f64
+    L.Java_apps_cppNN_FleetUpdater_registerDirectNative.restype = C.c_uint8
+    for s in ("modelsSize", "getCurrEpoch", "getPriority"):
+        getattr(L, UPDATER + s).restype = i32
     return L
 
 
 def test_shim_exports_reference_symbols():
     L = load()
     for s in SYMBOLS:
-        assert hasattr(L, s)
+        assert hasattr(L, s), s
+
+
+def test_fake_jvm_table_is_jni_shaped():
+    import jnifake as J
+    J.begin()
+    e = J.env()
+    table = C.cast(C.c_void_p.from_address(e).value, C.POINTER(C.c_void_p))
+    assert all(table[i] is None for i in range(4))          # reserved slots
+    assert table[171] and table[184] and table[222]         # GetArrayLength, GetByteArrayElements, critical
+    assert C.cast(table[4], C.CFUNCTYPE(C.c_int32, C.c_void_p))(e) == 0x00010008  # GetVersion
+
+
+def test_model_natives_without_a_model_are_inert():
+    # before fetchParamsNative the updater's state natives answer like an empty `models`
+    L = load()
+    import jnifake as J
+    J.begin()
+    assert L.Java_apps_cppNN_CppNNUpdater_modelsSize(J.env(), None) == 0
+    assert L.Java_apps_cppNN_CppNNUpdater_getParametersNative(J.env(), None, 0) is None
+    assert J.stat("critical_violations") == 0 and J.stat("overflows") == 0
+
+
+def check_rules(J):
+    assert J.stat("overflows") == 0, "local references beyond the frame's capacity"
+    assert J.stat("critical_violations") == 0, "JNI call inside a critical region"
+    assert J.stat("critical_depth") == 0, "critical region left open"
+    assert J.stat("pins") == 0, "array elements not released"
 
 
 @pytest.mark.gpu
-def test_shim_natives_match_oracle(oracle):
+def test_shim_per_op_natives_match_oracle(oracle):
     import jnifake as J
     L = load()
-    env = J.libc.calloc(1, 64)  # JNIEnv of the test header is stateless
+    env = J.env()
     ups = [oracle.encode_floats(oracle.synth_upload(4, c, list(MNIST.w_sizes), list(MNIST.b_sizes)))
            for c in range(3)]
-    a = J.new_array(ups[0])
+    J.begin()
+    a = J.new_bytes(ups[0])
     flat = J.read_bytes(L.Java_apps_cppNN_CppNNUpdater_getFlatGradient(env, None, a))
     assert flat == oracle.flat_gradient(ups[0])
     f1 = oracle.flat_gradient(ups[1])
-    assert J.read_bytes(L.Java_utils_ByteVec_scalarMulNative(env, None, J.new_array(f1), 1 / 3)) == \
+    assert J.read_bytes(L.Java_utils_ByteVec_scalarMulNative(env, None, J.new_bytes(f1), 1 / 3)) == \
         oracle.scalar_mul(f1, 1 / 3)
-    assert J.read_bytes(L.Java_utils_ByteVec_addNative(env, None, J.new_array(flat), J.new_array(f1))) == \
+    assert J.read_bytes(L.Java_utils_ByteVec_addNative(env, None, J.new_bytes(flat), J.new_bytes(f1))) == \
         oracle.add(flat, f1)
-    assert J.read_bytes(L.Java_utils_ByteVec_subtractNative(env, None, J.new_array(flat), J.new_array(f1))) == \
+    assert J.read_bytes(L.Java_utils_ByteVec_subtractNative(env, None, J.new_bytes(flat), J.new_bytes(f1))) == \
         oracle.subtract(flat, f1)
-    assert abs(L.Java_utils_ByteVec_getNorm(env, None, J.new_array(f1)) - oracle.norm(f1)) <= 1e-12 * oracle.norm(f1)
-    assert J.read_bytes(L.Java_apps_cppNN_CppNNUpdater_mergeFlatGradient(env, None, a, J.new_array(f1))) == \
+    assert abs(L.Java_utils_ByteVec_getNorm(env, None, J.new_bytes(f1)) - oracle.norm(f1)) <= 1e-12 * oracle.norm(f1)
+    assert J.read_bytes(L.Java_apps_cppNN_CppNNUpdater_mergeFlatGradient(env, None, a, J.new_bytes(f1))) == \
         oracle.merge_flat_gradient(ups[0], f1)
-    d = [1.0, 0.5, 1 / 3]
-    objs = J.new_object_array([J.new_array(u) for u in ups])
-    merged = J.read_bytes(L.Java_apps_cppNN_FleetUpdater_aggregateNative(env, None, objs, J.new_doubles(d)))
+    check_rules(J)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("frame_limit", [1 << 30, 8])
+def test_shim_aggregate_many_uploads(oracle, frame_limit):
+    # 40 uploads: more than the 16 local references JNI guarantees. With a JVM that
+    # grants EnsureLocalCapacity(40) the uploads are read in one critical region;
+    # with one that refuses (frame_limit 8) one reference at a time.
+    import jnifake as J
+    L = load()
+    env = J.env()
+    M = 40
+    ups = [oracle.encode_floats(oracle.synth_upload(6, c, list(MNIST.w_sizes), list(MNIST.b_sizes)))
+           for c in range(M)]
+    d = [1.0 / ((c % 3) + 1) for c in range(M)]
+    J.fakejvm().fakejvm_set_frame_limit(frame_limit)
+    try:
+        J.begin()
+        objs = J.new_object_array([J.new_bytes(u) for u in ups])
+        merged = J.read_bytes(L.Java_apps_cppNN_FleetUpdater_aggregateNative(env, None, objs, J.new_doubles(d)))
+        check_rules(J)
+        assert J.stat("max_live") <= (M + 1 if frame_limit > M else 16)
+        assert (J.stat("criticals") == M) == (frame_limit > M)
+    finally:
+        J.fakejvm().fakejvm_set_frame_limit(1 << 30)
     assert merged == oracle.update_faithful(ups, d)
+    # a null element: null result, every reference and critical region released
+    J.begin()
+    bad = J.new_object_array([J.new_bytes(ups[0]), None, J.new_bytes(ups[2])])
+    assert L.Java_apps_cppNN_FleetUpdater_aggregateNative(env, None, bad, J.new_doubles(d[:3])) is None
+    check_rules(J)
+
+
+@pytest.mark.gpu
+def test_shim_aggregate_direct_buffer(oracle):
+    import jnifake as J
+    L = load()
+    env = J.env()
+    M = 5
+    ups = [oracle.encode_floats(oracle.synth_upload(8, c, list(MNIST.w_sizes), list(MNIST.b_sizes)))
+           for c in range(M)]
+    d = [1.0, 0.5, 1 / 3, 1.0, 0.5]
+    Lb = len(ups[0])
+    pitch = Lb + 5
+    rows = np.zeros(M * pitch, np.uint8)
+    for i, u in enumerate(ups):
+        rows[i * pitch: i * pitch + Lb] = np.frombuffer(u, np.uint8)
+    J.begin()
+    buf = J.new_direct(rows)
+    assert L.Java_apps_cppNN_FleetUpdater_registerDirectNative(env, None, buf) == 1
+    out = J.read_bytes(L.Java_apps_cppNN_FleetUpdater_aggregateDirectNative(env, None, buf, M, Lb, pitch,
+                                                                             J.new_doubles(d)))
+    assert out == oracle.update_faithful(ups, d)
+    check_rules(J)
+
+
+@pytest.mark.gpu
+def test_shim_model_natives_match_reference_session(oracle):
+    # the updater's model natives through the table, against the reference's own
+    # network (tests/golden/session_mnist.npz, see test_gpu_model_state.py)
+    import jnifake as J
+    L = load()
+    env = J.env()
+    s = np.load(os.path.join(HERE, "golden", "session_mnist.npz"))
+    J.begin()
+    L.Java_apps_cppNN_CppNNUpdater_fetchParamsNative(env, None, J.new_bytes(bytes(s["init"])))
+    L.Java_apps_cppNN_CppNNUpdater_initUpdater(env, None, J.new_doubles(s["lrates"]), 1, 0.0, 0.0)
+    for step in range(4):
+        if step:
+            L.Java_apps_cppNN_CppNNUpdater_descentNative(env, None, J.new_bytes(bytes(s[f"merged{step - 1}"])),
+                                                         int(s["batch"]), int(s["stale"]))
+        newest = L.Java_apps_cppNN_CppNNUpdater_modelsSize(env, None) - 1
+        assert J.read_bytes(L.Java_apps_cppNN_CppNNUpdater_getParametersNative(env, None, newest)) == \
+            bytes(s[f"newest_text{step}"])
+        assert J.read_bytes(L.Java_apps_cppNN_CppNNUpdater_getModelParametersNative(env, None, 0)) == \
+            oracle.encode_floats(s[f"oldest_params{step}"])
+    assert L.Java_apps_cppNN_CppNNUpdater_getCurrEpoch(env, None) == 3
+    assert L.Java_apps_cppNN_CppNNUpdater_getLrate(env, None) == float(np.float32(s["lrates"][2]))
+    check_rules(J)
