@@ -594,16 +594,16 @@ def main():
         for w in [x for x in args.extras.split(",") if x and x != args.workload]:
             extras[w] = time_workload(torch, dist, codec, w, max(3, args.steps // 4), 2, rank, world, args.graph)
 
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        e2e = {w: end_to_end(torch, codec, w) for w in args.e2e.split(",") if w}
+
     strong = None
     if args.strong or not args.no_strong_block:
         ssteps = max(3, args.steps // 4)
         strong = {"scaling": "strong", "n_gpus": world,
                   "device": strong_device(torch, dist, codec, "synth4m_4096", ssteps, 1, rank, world),
                   "host_staged": strong_host(torch, dist, codec, "cifar100_1024", ssteps, rank, world)}
-
-    e2e = None
-    if world == 1 and not args.no_e2e:
-        e2e = {w: end_to_end(torch, codec, w) for w in args.e2e.split(",") if w}
 
     if rank != 0:
         if world > 1:
