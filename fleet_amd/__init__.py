@@ -102,6 +102,8 @@ def lib() -> C.CDLL:
         "fleet_host_register": (i32, [vp, vp, sz]),
         "fleet_host_unregister": (i32, [vp, vp]),
         "fleet_update_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, sz, sz, vp, vp, vp]),
+        "fleet_update_kardam_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, C.c_double, vp, vp, vp, sz, vp, vp,
+                                             vp, vp, vp]),
         "fleet_update_kernel": (C.c_char_p, [sz]),
         "fleet_model_quantize_index": (i32, [vp, vp, vp, i32, vp, vp, vp, vp]),
         "fleet_model_weights_text": (i32, [vp, vp, vp, i32, vp, sz, szp]),
@@ -384,6 +386,29 @@ class Codec:
                                          merged_f32.data_ptr() - shift_f if merged_f32 is not None else None,
                                          _stream(stream))
         self._check(rc)
+
+    def update_kardam_device(self, uploads_u8, length: int, dampen: Sequence[float], header_pos, lr: float,
+                             merged_u8, merged_f32=None, prev_f32=None, has_prev=None, g_out_f32=None, stream=None):
+        """update_device plus Kardam's per-client norms in the same pass (fleet_update_kardam_device):
+        returns (norm_g[M], norm_diff[M]); prev_f32 / g_out_f32: float32 CUDA tensors [M, vpitch]
+        of decoded Kardam gradients in upload coordinates."""
+        M, pitch = uploads_u8.shape
+        hp = np.ascontiguousarray(header_pos, dtype=np.int32)
+        d = np.ascontiguousarray(dampen, dtype=np.float64)
+        vpitch = (prev_f32 if prev_f32 is not None else g_out_f32).shape[1] if (
+            prev_f32 is not None or g_out_f32 is not None) else 0
+        hv = None
+        if prev_f32 is not None:
+            hv = np.ascontiguousarray(has_prev if has_prev is not None else np.ones(M), dtype=np.uint8)
+        ng, nd = np.empty(M, np.float64), np.empty(M, np.float64)
+        rc = self._L.fleet_update_kardam_device(
+            self._h, uploads_u8.data_ptr(), pitch, length, M, d.ctypes.data, hp.ctypes.data, len(hp), float(lr),
+            prev_f32.data_ptr() if prev_f32 is not None else None, hv.ctypes.data if hv is not None else None,
+            g_out_f32.data_ptr() if g_out_f32 is not None else None, vpitch, merged_u8.data_ptr(),
+            merged_f32.data_ptr() if merged_f32 is not None else None, ng.ctypes.data, nd.ctypes.data,
+            _stream(stream))
+        self._check(rc)
+        return ng, nd
 
     def encode_device(self, values_f32, n: int, out_u8, stream=None):
         """values_f32: float32 CUDA tensor [M, vpitch]; out_u8: uint8 [M, pitch]."""

@@ -875,36 +875,22 @@ int fleet_host_unregister(fleet_ctx* c, void* ptr) {
 
 // ---------------------------------------------------------- device-resident
 
-int fleet_update_device(fleet_ctx* c, const void* d_uploads, size_t pitch, size_t len, int M, const double* dampen,
-                        const int32_t* header_pos, int n_headers, size_t group_begin, size_t group_end,
-                        void* d_merged, void* d_merged_f32, void* stream) {
-  if (!c || !d_uploads || !dampen || M <= 0 || !d_merged || n_headers < 0 || n_headers > FLEET_MAX_HEADERS ||
-      (n_headers && !header_pos))
-    return FLEET_ERR_ARG;
-  std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
-  int rc = check_text_len(c, len);
-  if (rc) return rc;
-  const size_t n = fleet_b64_count(len);
-  const size_t groups = groups_of(n);
-  if (group_end > groups) group_end = groups;
-  if (group_begin > group_end) return FLEET_ERR_ARG;
-  // only columns [16*group_begin, 16*group_end) of each row are touched: rows
-  // must not overlap there (a full row, or a window of just those columns)
-  if (pitch % 16 != 0 || pitch < 16 * (group_end - group_begin))
-    return fail(c, FLEET_ERR_ARG, "pitch must be a multiple of 16 covering the selected groups");
-  hipStream_t s = pick(c, stream);
-  // {status, count, walk_end, 0, positions}: the caller's layout covers the whole upload
+namespace {
+
+// The device-resident update's parameters ({status, count, walk_end, 0, positions}
+// and dampen): kept resident in the context's own buffers and re-uploaded (one
+// sync) only when they change, so steady-state calls are pure kernel launches.
+int dev_params(fleet_ctx* c, hipStream_t s, size_t n, int M, const double* dampen, const int32_t* header_pos,
+               int n_headers) {
   std::vector<int32_t> hdr_words((size_t)n_headers + 4);
   hdr_words[0] = 0;
   hdr_words[1] = n_headers;
-  hdr_words[2] = (int32_t)n;
+  hdr_words[2] = (int32_t)n;  // the caller's layout covers the whole upload
   hdr_words[3] = 0;
   if (n_headers) std::memcpy(hdr_words.data() + 4, header_pos, sizeof(int32_t) * (size_t)n_headers);
-  // parameters stay resident between calls; re-upload (and sync once) only when they change,
-  // so steady-state calls are pure kernel launches
   if (!c->dev_params_valid || c->dev_hdr != hdr_words || c->dev_dampen.size() != (size_t)M ||
       std::memcmp(c->dev_dampen.data(), dampen, sizeof(double) * (size_t)M) != 0) {
+    int rc;
     HIP_TRY(c, hipStreamSynchronize(s));
     if ((size_t)M > c->d_dev_dampen_cap) {  // grow; the old buffer may sit in a captured graph: retire it
       if (c->d_dev_dampen) c->retired.push_back(c->d_dev_dampen);
@@ -918,9 +904,80 @@ int fleet_update_device(fleet_ctx* c, const void* d_uploads, size_t pitch, size_
     c->dev_hdr = hdr_words;
     c->dev_params_valid = true;
   }
+  return FLEET_OK;
+}
+
+int check_device_update(fleet_ctx* c, size_t pitch, size_t len, size_t* group_begin, size_t* group_end) {
+  int rc = check_text_len(c, len);
+  if (rc) return rc;
+  const size_t groups = groups_of(fleet_b64_count(len));
+  if (*group_end > groups) *group_end = groups;
+  if (*group_begin > *group_end) return FLEET_ERR_ARG;
+  // only columns [16*group_begin, 16*group_end) of each row are touched: rows
+  // must not overlap there (a full row, or a window of just those columns)
+  if (pitch % 16 != 0 || pitch < 16 * (*group_end - *group_begin))
+    return fail(c, FLEET_ERR_ARG, "pitch must be a multiple of 16 covering the selected groups");
+  return FLEET_OK;
+}
+
+}  // namespace
+
+int fleet_update_device(fleet_ctx* c, const void* d_uploads, size_t pitch, size_t len, int M, const double* dampen,
+                        const int32_t* header_pos, int n_headers, size_t group_begin, size_t group_end,
+                        void* d_merged, void* d_merged_f32, void* stream) {
+  if (!c || !d_uploads || !dampen || M <= 0 || !d_merged || n_headers < 0 || n_headers > FLEET_MAX_HEADERS ||
+      (n_headers && !header_pos))
+    return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  int rc = check_device_update(c, pitch, len, &group_begin, &group_end);
+  if (rc) return rc;
+  const size_t n = fleet_b64_count(len);
+  hipStream_t s = pick(c, stream);
+  if ((rc = dev_params(c, s, n, M, dampen, header_pos, n_headers))) return rc;
   HIP_TRY(c, fleet::launch_update((const uint8_t*)d_uploads, pitch, M, c->d_dev_dampen, (double)1 / M, (int64_t)n,
                                   (int64_t)group_begin, (int64_t)group_end, c->d_dev_hdr, (uint8_t*)d_merged,
                                   (float*)d_merged_f32, c->d_dev_err, s));
+  return FLEET_OK;
+}
+
+int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch, size_t len, int M,
+                               const double* dampen, const int32_t* header_pos, int n_headers, double lr,
+                               const void* d_prev, const uint8_t* has_prev, void* d_g_out, size_t vpitch,
+                               void* d_merged, void* d_merged_f32, double* norm_g, double* norm_diff, void* stream) {
+  if (!c || !d_uploads || !dampen || M <= 0 || !d_merged || !norm_g || !norm_diff || n_headers < 0 ||
+      n_headers > FLEET_MAX_HEADERS || (n_headers && !header_pos) || (d_prev && !has_prev))
+    return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  size_t gb = 0, ge = SIZE_MAX;
+  int rc = check_device_update(c, pitch, len, &gb, &ge);
+  if (rc) return rc;
+  const size_t n = fleet_b64_count(len);
+  if ((d_prev || d_g_out) && vpitch < n) return fail(c, FLEET_ERR_ARG, "vpitch %zu < %zu values", vpitch, n);
+  hipStream_t s = pick(c, stream);
+  if ((rc = dev_params(c, s, n, M, dampen, header_pos, n_headers))) return rc;
+  const size_t n_waves = 4 * ((ge + 255) / 256);
+  // scratch: [partials M x waves x 2 | norms M x 2 | has_prev M]; synchronous call (host outputs)
+  const size_t o_norm = sizeof(double) * 2 * (size_t)M * n_waves, o_has = o_norm + sizeof(double) * 2 * (size_t)M;
+  if ((rc = grow_dev(c, &c->d_b, &c->d_b_cap, o_has + (size_t)M + 64))) return rc;
+  HIP_TRY(c, hipStreamSynchronize(s));
+  double* d_part = reinterpret_cast<double*>(c->d_b);
+  double* d_norm = reinterpret_cast<double*>(c->d_b + o_norm);
+  uint8_t* d_has = c->d_b + o_has;
+  if (d_prev) HIP_TRY(c, hipMemcpy(d_has, has_prev, (size_t)M, hipMemcpyHostToDevice));
+  fleet::KardamOut kd{lr, (const float*)d_prev, d_prev ? d_has : nullptr, vpitch, (float*)d_g_out, d_part};
+  int nw = 0;
+  HIP_TRY(c, fleet::launch_update_kardam((const uint8_t*)d_uploads, pitch, M, c->d_dev_dampen, (double)1 / M,
+                                         (int64_t)n, 0, (int64_t)ge, c->d_dev_hdr, (uint8_t*)d_merged,
+                                         (float*)d_merged_f32, c->d_dev_err, kd, &nw, d_norm, s));
+  std::vector<double> norms(2 * (size_t)M);
+  HIP_TRY(c, hipMemcpyAsync(norms.data(), d_norm, sizeof(double) * norms.size(), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  for (int i = 0; i < M; ++i) {
+    norm_g[i] = std::sqrt(norms[2 * (size_t)i]);
+    norm_diff[i] = (d_prev && has_prev[i]) ? std::sqrt(norms[2 * (size_t)i + 1]) : std::nan("");
+  }
   return FLEET_OK;
 }
 

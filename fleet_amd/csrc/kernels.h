@@ -17,6 +17,24 @@ hipError_t launch_descent(float* weights, float* fc_bias, const float* grad, con
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s);
+// Kardam's side outputs of the fused update (k_update<1, true>): per client c and
+// flat value (upload positions that are neither header slots nor past the walk)
+//   G = Q(f32(f64(p) lr))            the decoded Kardam.setGrad text (p = stage B)
+//   D = Q(G - prev[c])               the decoded g.subtract(prev) text (has_prev[c])
+// partials[(c * n_waves + w) * 2 + {0, 1}] = per-wave sums of (double)(G*G), (double)(D*D);
+// g_out (nullable) = G in upload coordinates (M rows of vpitch floats).
+struct KardamOut {
+  double lr;
+  const float* prev;
+  const uint8_t* has_prev;
+  size_t vpitch;
+  float* g_out;
+  double* partials;
+};
+hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
+                                int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
+                                uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
+                                double* norms, hipStream_t s);
 // name of the aggregation kernel launch_update picks for `groups` groups
 const char* update_kernel_name(int64_t groups);
 hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int rows, uint8_t* out, size_t pitch,

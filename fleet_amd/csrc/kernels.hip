@@ -205,13 +205,18 @@ __device__ __noinline__ float chain_general(const uint8_t* __restrict__ uploads,
 // Layout: lane owns K groups (3K values) g = g_begin + (blockIdx*K + k)*256 + tid,
 // so every wave-wide load of a client row is 1 KiB contiguous; the next
 // client's K loads are in flight while the current one computes.
-template <int K>
+//
+// KD = true adds Kardam's bookkeeping of the same picked uploads (CppNNUpdater.java:
+// 463-481, Kardam.java:48-106) as side outputs of the client loop
+// (KardamOut), so it costs no second pass over the uploads; stages A and B then
+// use the exact in-stage fallback (their values feed the side outputs).
+template <int K, bool KD = false>
 __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                 const double* __restrict__ dampen, double inv_avg,
                                                 int64_t n_up, int64_t g_begin, int64_t g_end,
                                                 const int32_t* __restrict__ hdr_block,
                                                 uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                int* __restrict__ err) {
+                                                int* __restrict__ err, KardamOut kd = KardamOut{}) {
   constexpr int S = 3 * K;
   __shared__ B64Tables tab;
   const int lane = threadIdx.x & 63;
@@ -290,14 +295,53 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
     // stage A: y = Q(int2float(code))
     float y0[S], y[S];
     dec_stage<S>(y0, codes, &tab);
-    q_stage_off<S>(y, y0, &tab, dmax);
+    if constexpr (KD) q_stage<S>(y, y0, &tab);
+    else q_stage_off<S>(y, y0, &tab, dmax);
 
     // stage B: p = Q((float)((double)y * d))
     const double d = dampen[c];
     float r[S], p[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) r[i] = (float)((double)y[i] * d);
-    q_stage_off<S>(p, r, &tab, dmax);
+    if constexpr (KD) q_stage<S>(p, r, &tab);
+    else q_stage_off<S>(p, r, &tab, dmax);
+
+    if constexpr (KD) {
+      // Kardam.setGrad(id, pickedGrad.scalarMultiply(getLrate())) and updateLip's
+      // g.subtract(prev).getNorm() (getNorm: float products summed in double)
+      float rg[S], G[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) rg[i] = (float)((double)p[i] * kd.lr);
+      q_stage<S>(G, rg, &tab);
+      const bool hp = kd.prev && kd.has_prev[c];
+      double sg = 0.0, sd = 0.0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int e = 0; e < 3; ++e) {
+          const int64_t pos = 3 * g[k] + e;
+          const bool flat = live[k] && pos < n_up && pos < walk_end && !((hbits >> (3 * k + e)) & 1u);
+          const float Gv = G[3 * k + e];
+          if (flat) sg += (double)(Gv * Gv);
+          if (hp && flat) {
+            const float Dv = q(Gv - kd.prev[(size_t)c * kd.vpitch + pos]);
+            sd += (double)(Dv * Dv);
+          }
+          if (kd.g_out && live[k] && pos < n_up) kd.g_out[(size_t)c * kd.vpitch + pos] = flat ? Gv : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        sg += __shfl_xor(sg, o);
+        sd += __shfl_xor(sd, o);
+      }
+      if (lane == 0) {
+        const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
+        const size_t nw = (size_t)gridDim.x * (blockDim.x / 64);
+        kd.partials[((size_t)c * nw + w) * 2] = sg;
+        kd.partials[((size_t)c * nw + w) * 2 + 1] = sd;
+      }
+    }
 
     // stage C: A = Q(A + p)
     if (c == 0) {
@@ -1321,6 +1365,47 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
     else FLEET_LAUNCH(k_update<1>, 256);
   }
 #undef FLEET_LAUNCH
+  return hipGetLastError();
+}
+
+// per client: the wave partials of k_update<1, true> summed in a fixed order
+__global__ void __launch_bounds__(256) k_kardam_reduce(const double* __restrict__ partials, int64_t n_waves,
+                                                       double* __restrict__ norms) {
+  __shared__ double red[2][256];
+  const int c = blockIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int64_t w = threadIdx.x; w < n_waves; w += blockDim.x) {
+    a += partials[((size_t)c * n_waves + w) * 2];
+    b += partials[((size_t)c * n_waves + w) * 2 + 1];
+  }
+  red[0][threadIdx.x] = a;
+  red[1][threadIdx.x] = b;
+  __syncthreads();
+  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + s];
+      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    norms[2 * c] = red[0][0];
+    norms[2 * c + 1] = red[1][0];
+  }
+}
+
+hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
+                                int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
+                                uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
+                                double* norms, hipStream_t s) {
+  const int64_t groups = g_end - g_begin;
+  const unsigned blocks = (unsigned)((groups + 255) / 256);
+  *n_waves = (int)blocks * 4;
+  if (groups <= 0) return hipSuccess;
+  if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
+  hipLaunchKernelGGL((k_update<1, true>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
+                     g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd);
+  hipLaunchKernelGGL(k_kardam_reduce, dim3((unsigned)M), dim3(256), 0, s, kd.partials, (int64_t)*n_waves, norms);
   return hipGetLastError();
 }
 

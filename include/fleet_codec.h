@@ -157,6 +157,22 @@ int fleet_host_unregister(fleet_ctx* ctx, void* ptr);
 int fleet_update_device(fleet_ctx* ctx, const void* d_uploads, size_t pitch, size_t len, int M,
                         const double* dampen, const int32_t* header_pos, int n_headers, size_t group_begin,
                         size_t group_end, void* d_merged, void* d_merged_f32, void* stream);
+/* fleet_update_device plus Kardam's bookkeeping of the same picked uploads
+ * (CppNNUpdater.java:463-481, Kardam.java:48-106) as side
+ * outputs of the one pass over the uploads (no second read of them):
+ *   G_c = decodeFloat(getFlatGradient(u_c).scalarMultiply(dampen[c]).scalarMultiply(lr))
+ *   norm_g[c]    = G_c's getNorm
+ *   norm_diff[c] = getNorm(g_c.subtract(prev_c)) when has_prev[c] (else NaN)
+ * with prev_c = the worker's previous G (d_prev: M rows of vpitch floats in
+ * upload coordinates, header slots ignored; NULL = none) and, when d_g_out is
+ * given, this round's G written there in the same layout (the next round's
+ * prev). Whole uploads (all groups); synchronous (the norms are host outputs);
+ * not for graph capture. Norms: fixed-order partial sums of the reference's
+ * fp64 loop (1e-12 relative, like fleet_norm). */
+int fleet_update_kardam_device(fleet_ctx* ctx, const void* d_uploads, size_t pitch, size_t len, int M,
+                               const double* dampen, const int32_t* header_pos, int n_headers, double lr,
+                               const void* d_prev, const uint8_t* has_prev, void* d_g_out, size_t vpitch,
+                               void* d_merged, void* d_merged_f32, double* norm_g, double* norm_diff, void* stream);
 /* Client-side encode of M fp32 buckets (rows of `n` floats, `vpitch` floats
  * apart) into Base64 rows of `pitch` bytes: Base64::encode(vector<float>) per row. */
 int fleet_encode_device(fleet_ctx* ctx, const void* d_values, size_t n, size_t vpitch, int M, void* d_out,

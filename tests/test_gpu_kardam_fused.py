@@ -1,0 +1,68 @@
+"""Kardam's bookkeeping as side outputs of the fused update (fleet_update_kardam_device,
+SURVEY.md §8 f2: CppNNUpdater.java:463-481, Kardam.java:48-106) against the
+two-pass path (fleet_kardam_grads, itself checked against the oracle's per-op
+chain in test_updater.py): same merged bytes as the plain update, the same
+decoded Kardam gradients (bitwise), norms within 1e-12 relative (getNorm's fp64
+sum in another order, as for fleet_norm)."""
+import numpy as np
+import pytest
+import torch
+
+import fleet_amd as F
+from fleet_amd.layouts import MNIST, synthetic
+
+pytestmark = pytest.mark.gpu
+
+
+def scatter_flat(flat, layout):
+    """flat (getFlatGradient order) -> upload coordinates, header slots 0."""
+    out = np.zeros(layout.n_up, np.float32)
+    mask = np.ones(layout.n_up, bool)
+    mask[layout.header_positions()] = False
+    out[mask] = flat
+    return out
+
+
+@pytest.mark.parametrize("layout,M", [(MNIST, 6), (synthetic(3001), 4)])
+def test_kardam_side_outputs(codec, oracle, layout, M):
+    dev = torch.device("cuda", 0)
+    lr = 0.05
+    d = [1.0 / ((c % 3) + 1) for c in range(M)]
+    L = F.b64_len(layout.n_up)
+    pitch = 16 * ((L + 15) // 16)
+    vpitch = layout.n_up + 3
+    hpos = layout.header_positions()
+
+    def round_(seed, prev_texts, prev_dev, has):
+        ups = [oracle.encode_floats(oracle.synth_upload(seed, c, list(layout.w_sizes), list(layout.b_sizes)))
+               for c in range(M)]
+        host = np.zeros((M, pitch), np.uint8)
+        for c, u in enumerate(ups):
+            host[c, :L] = np.frombuffer(u, np.uint8)
+        t = torch.from_numpy(host).to(dev)
+        merged = torch.zeros(pitch, dtype=torch.uint8, device=dev)
+        g_out = torch.zeros((M, vpitch), dtype=torch.float32, device=dev)
+        ng, nd = codec.update_kardam_device(t, L, d, hpos, lr, merged, None, prev_dev, has, g_out)
+        codec.check()
+        torch.cuda.synchronize()
+        assert merged.cpu().numpy()[:L].tobytes() == codec.update(ups, d)
+        prev_arg = None if prev_texts is None else [p if h else None for p, h in zip(prev_texts, has)]
+        g_texts, eng, end = codec.kardam_grads(ups, d, lr, prev_arg)
+        G = g_out.cpu().numpy()[:, : layout.n_up]
+        for c in range(M):
+            want = scatter_flat(codec.decode_floats(g_texts[c]), layout)
+            assert np.array_equal(G[c].view(np.uint32), want.view(np.uint32))
+        np.testing.assert_allclose(ng, eng, rtol=1e-12, atol=0)
+        if prev_texts is None:
+            assert np.all(np.isnan(nd))
+        else:
+            for c in range(M):
+                if has[c]:
+                    np.testing.assert_allclose(nd[c], end[c], rtol=1e-12, atol=1e-300)
+                else:
+                    assert np.isnan(nd[c])
+        return g_texts, g_out
+
+    g1, g1_dev = round_(31, None, None, None)
+    has = [c % 2 == 0 for c in range(M)]
+    round_(32, g1, g1_dev, has)
