@@ -199,7 +199,7 @@ def all_gather_fn(torch, dist, world, src, out):
     return f
 
 
-def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=True, pipeline=False):
+def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=True):
     """Weak-scaling measurement of `name`: times `steps` steps. graph=True: a
     step (encode + aggregation) is captured once into a HIP graph of G steps
     and replayed steps/G times; graph=False: eager launches. N>1: the
@@ -240,36 +240,6 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
         elapsed = run_timed(torch, dist, world, g.replay, steps // G)
         codec.check()
         del g
-    # pipelined: the client encode of batch i+1 (its own stream) overlaps the aggregation
-    # of batch i (another stream), double-buffered uploads -- every step still encodes
-    # and aggregates one full batch
-    pipe_ms = None
-    if pipeline:
-        text2 = torch.empty_like(sh.text)
-        bufs = [sh.text, text2]
-        s_enc, s_agg = torch.cuda.Stream(), torch.cuda.Stream()
-        ev_enc = [torch.cuda.Event(), torch.cuda.Event()]
-        ev_agg = [torch.cuda.Event(), torch.cuda.Event()]
-        state = {"i": 0}
-
-        def pipe_step():
-            i = state["i"]
-            b = i % 2
-            if i >= 2:
-                s_enc.wait_event(ev_agg[b])
-            codec.encode_device(sh.values, sh.n_local, bufs[b], stream=s_enc.cuda_stream)
-            ev_enc[b].record(s_enc)
-            s_agg.wait_event(ev_enc[b])
-            codec.update_device(bufs[b], sh.L, sh.dampen, sh.hpos_global, sh.merged, sh.merged_f32,
-                                stream=s_agg.cuda_stream)
-            ev_agg[b].record(s_agg)
-            state["i"] = i + 1
-        for _ in range(max(2, warmup)):
-            pipe_step()
-        torch.cuda.synchronize()
-        pipe_ms = run_timed(torch, dist, world, pipe_step, steps) / steps * 1e3
-        codec.check()
-        del text2, bufs
     exchange_ms = None
     if world > 1:
         exchange = all_gather_fn(torch, dist, world, sh.merged, gathered)
@@ -285,7 +255,6 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
         "workload": name, "note": note, "layout": lay_name, "clients": M, "n_up_per_rank": sh.n_local,
         "ms_per_step": ms, "gib_s": gib_s, "update_kernel_ms": upd_ms, "encode_kernel_ms": enc_ms,
         "graph": graph, "steps_per_graph": G, "eager_ms_per_step": eager_ms, "exchange_ms": exchange_ms,
-        "pipelined_ms_per_step": pipe_ms,
         "update_kernel": F.update_kernel(sh.L),
         "update_bytes": upd_b, "encode_bytes": enc_b,
         "update_gbs": upd_b / (upd_ms * 1e-3) / 1e9, "encode_gbs": enc_b / (enc_ms * 1e-3) / 1e9,
@@ -619,8 +588,7 @@ def main():
     import fleet_amd as F
     codec = F.Codec(local)
 
-    main_res = time_workload(torch, dist, codec, args.workload, args.steps, args.warmup, rank, world, args.graph,
-                             pipeline=True)
+    main_res = time_workload(torch, dist, codec, args.workload, args.steps, args.warmup, rank, world, args.graph)
     extras = {}
     if world == 1 and args.extras:
         for w in [x for x in args.extras.split(",") if x and x != args.workload]:
