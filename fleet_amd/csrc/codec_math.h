@@ -396,34 +396,45 @@ FLEET_HDC MulEntry mul_entry(uint32_t d) {  // d = numDigits; d > 9 (slow marker
   return e;
 }
 
-// Digit table entry i = (sign << 8) | biased exponent of x: byte 0 = d for
-// |x| >= thr, byte 1 = d for |x| < thr; d = 15 marks values outside the q_gen
-// domain (-1e8 < x < 1e9), NaN and inf (callers send those through the
-// general codec).
+// Digit table entry i = (sign << 8) | biased exponent of x. The binade holds at
+// most one power of ten, thr: numDigits((int)x) is dlo for |x| < thr and dhi =
+// dlo + 1 for |x| >= thr ('-' counts, Base64.cpp:73-82). The entry keeps
+// base = dlo + 1, so d = base - (|x| < thr) is three integer ops (sub, shift,
+// sub) with no select or bit-field extract. d > 9 marks values outside the
+// q_gen domain (-1e8 < x < 1e9), NaN and inf (callers send those through the
+// general codec): base = 10 where only dhi leaves the domain (dlo = 9), 15
+// where both do.
 struct alignas(8) VarEntry {
   float thr;
-  uint32_t info;
+  uint32_t base;
 };
 constexpr uint32_t kSlowDigits = 15u;
-FLEET_HDC VarEntry var_entry(uint32_t i) {
+struct DigitPair {
+  float thr;
+  uint32_t dlo, dhi;  // kSlowDigits when > 9
+};
+FLEET_HDC DigitPair digit_pair(uint32_t i) {
   constexpr DigitEntry dig[32] = FLEET_DIGIT_TABLE;
   const uint32_t neg = (i >> 8) & 1u;
   const int e = (int)(i & 255u) - 126;  // |x| in [2^(e-1), 2^e) for normal x
-  if (e <= 0) return VarEntry{__builtin_inff(), 0u};  // |x| < 1: (int)x == 0, d = 0
+  if (e <= 0) return DigitPair{__builtin_inff(), 0u, 0u};  // |x| < 1: (int)x == 0, d = 0
   const DigitEntry t = dig[e > 31 ? 31 : e];
-  uint32_t dlo = t.base + neg, dhi = t.base + 1u + neg;  // '-' counts (Base64.cpp:73-82)
+  uint32_t dlo = t.base + neg, dhi = t.base + 1u + neg;
   dlo = dlo > 9u ? kSlowDigits : dlo;
   dhi = dhi > 9u ? kSlowDigits : dhi;
-  return VarEntry{t.thr, dhi | (dlo << 8)};
+  return DigitPair{t.thr, dlo, dhi};
+}
+FLEET_HDC VarEntry var_entry(uint32_t i) {
+  const DigitPair p = digit_pair(i);
+  return VarEntry{p.thr, p.dlo <= 9u ? p.dlo + 1u : kSlowDigits};
 }
 
-// numDigits((int)x) on the q_gen domain, kSlowDigits outside it. `ab` = the bits
-// of |x|: |x| < thr compares as integers (both non-negative), and the byte
-// shift comes from the sign of the difference -- no float compare, no select.
+// numDigits((int)x) on the q_gen domain, a value > 9 outside it. `ab` = the
+// bits of |x|: |x| < thr compares as integers (both non-negative, below 2^31),
+// the borrow of ab - thr is the comparison.
 FLEET_HD uint32_t var_digits_ab(uint32_t bits, uint32_t ab, const VarEntry* vt) {
   const VarEntry v = vt[bits >> 23];
-  const uint32_t sh = ((ab - f2u(v.thr)) >> 28) & 8u;  // 8 when |x| < thr
-  return (v.info >> sh) & 0xffu;
+  return v.base - ((ab - f2u(v.thr)) >> 31);
 }
 FLEET_HD uint32_t var_digits(float x, const VarEntry* vt) {
   return var_digits_ab(f2u(x), f2u(x) & 0x7fffffffu, vt);
@@ -530,8 +541,8 @@ struct alignas(16) XlEntry {
 FLEET_HDC XlEntry xl_entry(uint32_t idx) {
   XlEntry x{};
   const uint32_t sign = idx / kXlSpan, be = 126u + idx % kXlSpan;
-  const VarEntry v = var_entry((sign << 8) | be);
-  uint32_t dhi = v.info & 0xffu, dlo = (v.info >> 8) & 0xffu;
+  const DigitPair v = digit_pair((sign << 8) | be);
+  uint32_t dhi = v.dhi, dlo = v.dlo;
   const bool extra = dlo <= 9u && dlo + 1u == dhi;
   if (dhi > 9u) dhi = 9u;  // off the domain: identity chains (flagged by the caller)
   if (dlo > 9u) dlo = 9u;

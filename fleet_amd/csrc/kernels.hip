@@ -106,7 +106,7 @@ __device__ __forceinline__ void q_stage(float (&out)[S], const float (&x)[S], co
   if (__ballot(dmax > 9u) != 0) {  // values outside the q_gen domain (rare): the general codec, per lane
 #pragma unroll
     for (int i = 0; i < S; ++i)
-      if (d[i] == kSlowDigits) out[i] = q(x[i]);
+      if (d[i] > 9u) out[i] = q(x[i]);
   }
 }
 
@@ -169,9 +169,9 @@ __device__ __forceinline__ int32_t merged_code(float A, double inv, int32_t last
   if (keep_last) return enc(dec(last_code));
   const float r = (float)((double)A * inv);
   const uint32_t d = var_digits(r, tab->var);
-  if (d != kSlowDigits) {
+  if (d <= 9u) {
     const float y = q_mt_d(r, d, tab->mt);
-    if (var_digits(y, tab->var) != kSlowDigits) return enc_mt(y, tab->var, tab->mt);
+    if (var_digits(y, tab->var) <= 9u) return enc_mt(y, tab->var, tab->mt);
   }
   return enc(q(r));
 }
@@ -610,7 +610,7 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
         for (; k < cm; ++k) {
           const float s = A + ptile[k * E + tid];
           const uint32_t d = var_digits(s, sh.tab.var);
-          off_domain |= (uint32_t)(d == kSlowDigits);
+          off_domain |= (uint32_t)(d > 9u);
           A = q_mt_d(s, d, sh.tab.mt);
         }
       }
