@@ -122,6 +122,10 @@ def lib() -> C.CDLL:
         "fleet_descent_window_device": (i32, [vp, vp, vp, vp, sz, sz, vp, vp, i32, vp, vp, i32, C.c_float, vp]),
         "fleet_minibatch_device": (i32, [vp, vp, sz, i32, vp, vp, i32, vp, i32, vp, vp, vp]),
         "fleet_minibatch": (i32, [vp, vp, sz, i32, vp, vp, i32, vp, i32, vp, vp, sz, szp]),
+        "fleet_teacher_weight_count": (sz, []),
+        "fleet_teacher_bias_count": (sz, []),
+        "fleet_teacher_forward_device": (i32, [vp, vp, vp, vp, sz, i32, vp, i32, C.c_float, vp, vp]),
+        "fleet_teacher_forward": (i32, [vp, vp, sz, vp, sz, vp, sz, i32, vp, i32, C.c_float, vp]),
         "fleet_model_load": (i32, [vp, vp, sz, i32, C.POINTER(vp)]),
         "fleet_model_destroy": (None, [vp]),
         "fleet_model_last_error": (C.c_char_p, [vp]),
@@ -573,6 +577,40 @@ class Codec:
                                                    idx_i32.data_ptr(), idx_i32.numel(),
                                                    teacher_f32.data_ptr() if teacher_f32 is not None else None, nl,
                                                    h.ctypes.data, out_u8.data_ptr(), _stream(stream)))
+
+    # -- the sampler's mode-1 teacher forward ----------------
+    def teacher_forward(self, w, b, images, idx=None, temperature: float = 2.0) -> np.ndarray:
+        """uniformSample's teacher.forward(sample, TEMPERATURE, -1, 1) (cppNN_backend.cpp:603)
+        for images[idx] (all rows when idx is None): [B, 10] class probabilities of
+        initSampler's teacher network with weights w (non-null W in network order) and
+        biases b (use_bias() layers in layer order)."""
+        wv = np.ascontiguousarray(w, dtype=np.float32).reshape(-1)
+        bv = np.ascontiguousarray(b, dtype=np.float32).reshape(-1)
+        x = np.ascontiguousarray(images, dtype=np.float32)
+        if x.ndim == 1:
+            x = x.reshape(1, -1)
+        n_img, F = x.shape
+        ix = np.arange(n_img, dtype=np.int32) if idx is None else np.ascontiguousarray(idx, dtype=np.int32)
+        out = np.empty((len(ix), 10), np.float32)
+        self._check(self._L.fleet_teacher_forward(self._h, wv.ctypes.data, len(wv), bv.ctypes.data, len(bv),
+                                                  x.ctypes.data, n_img, F, ix.ctypes.data, len(ix),
+                                                  float(temperature), out.ctypes.data))
+        return out
+
+    def teacher_forward_device(self, w_f32, b_f32, images_f32, probs_f32, idx_i32=None, temperature: float = 2.0,
+                               stream=None):
+        """Device-resident teacher forward: CUDA tensors w [21448], b [82], images [N, F >= 784],
+        probs [B, 10] written for images[idx] (B = N rows when idx is None). Index errors at check()."""
+        n_img, F = images_f32.shape
+        if w_f32.numel() != self._L.fleet_teacher_weight_count() or b_f32.numel() != self._L.fleet_teacher_bias_count():
+            raise ValueError("teacher weights / biases of the wrong size")
+        B = idx_i32.numel() if idx_i32 is not None else n_img
+        if probs_f32.numel() < 10 * B:
+            raise ValueError("probs holds B x 10 floats")
+        self._check(self._L.fleet_teacher_forward_device(self._h, w_f32.data_ptr(), b_f32.data_ptr(),
+                                                         images_f32.data_ptr(), n_img, F,
+                                                         idx_i32.data_ptr() if idx_i32 is not None else None, B,
+                                                         float(temperature), probs_f32.data_ptr(), _stream(stream)))
 
     # -- descentNative's model step (SURVEY.md §8 f1) ----------------------------
     @staticmethod

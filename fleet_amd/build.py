@@ -27,7 +27,7 @@ ARCH = os.environ.get("FLEET_OFFLOAD_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", f"-I{INCLUDE}", f"-I{CSRC}"]
 
-SOURCES = [("kernels.hip", True), ("model_codec.hip", True), ("fleet_codec.cpp", True), ("model_state.cpp", True)]
+SOURCES = [("kernels.hip", True), ("model_codec.hip", True), ("fleet_codec.cpp", True), ("model_state.cpp", True), ("teacher.hip", True)]
 
 
 def _newer(target: str, deps) -> bool:
@@ -47,7 +47,7 @@ def _run(cmd):
 
 def build_codec(force: bool = False) -> str:
     srcs = [os.path.join(CSRC, s) for s, _ in SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in ("codec_device.h", "codec_math.h", "kernels.h", "model_codec.h")] + [
+    deps = srcs + [os.path.join(CSRC, h) for h in ("codec_device.h", "codec_math.h", "kernels.h", "model_codec.h", "teacher_math.h")] + [
         os.path.join(INCLUDE, "fleet_codec.h")]
     if not force and not _newer(LIB, deps):
         return LIB

@@ -1329,6 +1329,55 @@ int fleet_minibatch(fleet_ctx* c, const float* images, size_t n_images, int F, c
   return FLEET_OK;
 }
 
+size_t fleet_teacher_weight_count(void) { return (size_t)fleet::teacher_weight_count(); }
+size_t fleet_teacher_bias_count(void) { return (size_t)fleet::teacher_bias_count(); }
+
+int fleet_teacher_forward_device(fleet_ctx* c, const void* d_w, const void* d_b, const void* d_images, size_t n_images,
+                                 int F, const void* d_idx, int B, float temperature, void* d_probs, void* stream) {
+  if (!c || B < 0 || (B && (!d_w || !d_b || !d_images || !d_probs)) || F < 28 * 28) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, fleet::launch_teacher_forward((const float*)d_w, (const float*)d_b, (const float*)d_images,
+                                           (int64_t)n_images, F, (const int32_t*)d_idx, B, temperature,
+                                           (float*)d_probs, c->d_dev_err, pick(c, stream)));
+  return FLEET_OK;
+}
+
+int fleet_teacher_forward(fleet_ctx* c, const float* w, size_t n_w, const float* b, size_t n_b, const float* images,
+                          size_t n_images, int F, const int32_t* idx, int B, float temperature, float* probs) {
+  if (!c || B < 0 || F < 28 * 28 || (B && (!w || !b || !images || !idx || !probs))) return FLEET_ERR_ARG;
+  if (n_w != fleet_teacher_weight_count() || n_b != fleet_teacher_bias_count())
+    return fail(c, FLEET_ERR_ARG, "teacher: %zu weights and %zu biases, expected %zu and %zu", n_w, n_b,
+                fleet_teacher_weight_count(), fleet_teacher_bias_count());
+  for (int i = 0; i < B; ++i)
+    if (idx[i] < 0 || (size_t)idx[i] >= n_images)
+      return fail(c, FLEET_ERR_ARG, "sample %d: index %d outside the %zu images", i, idx[i], n_images);
+  if (B == 0) return FLEET_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  // staging: [w | b | B gathered rows | B x 10 probs]
+  const size_t o_b = round16(sizeof(float) * n_w), o_x = o_b + round16(sizeof(float) * n_b);
+  const size_t o_p = o_x + round16(sizeof(float) * (size_t)B * (size_t)F);
+  const size_t o_end = o_p + round16(sizeof(float) * (size_t)B * 10);
+  int rc;
+  if ((rc = grow_pinned(c, o_end))) return rc;
+  if ((rc = grow_dev(c, &c->d_a, &c->d_a_cap, o_end))) return rc;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));  // staging buffer reuse
+  uint8_t* h = c->h_stage;
+  std::memcpy(h, w, sizeof(float) * n_w);
+  std::memcpy(h + o_b, b, sizeof(float) * n_b);
+  for (int i = 0; i < B; ++i)
+    std::memcpy(h + o_x + sizeof(float) * (size_t)i * F, images + (size_t)idx[i] * F, sizeof(float) * (size_t)F);
+  uint8_t* d = c->d_a;
+  HIP_TRY(c, hipMemcpyAsync(d, h, o_p, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c, fleet::launch_teacher_forward((const float*)d, (const float*)(d + o_b), (const float*)(d + o_x), B, F,
+                                           nullptr, B, temperature, (float*)(d + o_p), c->d_err, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(h + o_p, d + o_p, sizeof(float) * (size_t)B * 10, hipMemcpyDeviceToHost, c->stream));
+  if ((rc = read_err(c, c->stream))) return rc;
+  std::memcpy(probs, h + o_p, sizeof(float) * (size_t)B * 10);
+  return FLEET_OK;
+}
+
 int fleet_model_params(fleet_ctx* c, const float* weights, size_t n_weights, const float* biases, size_t n_biases,
                        int graph_edges, char* out, size_t cap, size_t* out_len) {
   if (!c || graph_edges < 0 || (n_weights && !weights) || (n_biases && !biases)) return FLEET_ERR_ARG;
@@ -1545,7 +1594,7 @@ const char* fleet_update_kernel(size_t len) {
 }
 
 int fleet_selftest_digest(fleet_ctx* c, int fn, uint64_t* out) {
-  if (!c || !out || fn < 0 || fn > 17) return FLEET_ERR_ARG;
+  if (!c || !out || fn < 0 || fn > 18) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   unsigned long long* d = nullptr;

@@ -3,6 +3,11 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// device error bits (atomicOr into the context's error word, read back by fleet_check)
+#define FLEET_ERRBIT_BASE64 1
+#define FLEET_ERRBIT_LAYOUT 2
+#define FLEET_ERRBIT_ARG 4
+
 namespace fleet {
 // segments of descentNative's model step (k_descent): kind 0 = weight block,
 // 1 = fully-connected bias block; offsets in floats
@@ -42,6 +47,13 @@ hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int 
 hipError_t launch_encode_minibatch(const float* images, int64_t n_images, int F, const int32_t* labels,
                                    const int32_t* idx, int B, const float* teacher, int NL, const float header[7],
                                    uint8_t* out, int* err, hipStream_t s);
+// the sampler's mode-1 teacher forward (teacher.hip): probs[b*10 + j] for sample
+// idx[b] (idx == nullptr: sample b) of the n_images x F rows
+hipError_t launch_teacher_forward(const float* w, const float* b, const float* images, int64_t n_images, int F,
+                                  const int32_t* idx, int B, float temperature, float* probs, int* err,
+                                  hipStream_t s);
+int64_t teacher_weight_count();
+int64_t teacher_bias_count();
 hipError_t launch_encode_model_params(const float* weights, int64_t n_w, const float* biases, int64_t n_b, int64_t reps,
                                       uint8_t* out, hipStream_t s);
 hipError_t launch_encode_i32(const int32_t* codes, int64_t n, uint8_t* out, hipStream_t s);

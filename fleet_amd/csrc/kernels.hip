@@ -13,12 +13,9 @@
 #include <cstring>
 
 #include "codec_device.h"
+#include "teacher_math.h"
 
 namespace fleet {
-
-#define FLEET_ERRBIT_BASE64 1
-#define FLEET_ERRBIT_LAYOUT 2
-#define FLEET_ERRBIT_ARG 4
 
 // Dev-only phase timestamps (scripts/ubench_tiled.hip builds with FLEET_TIMING);
 // compiled out of the library.
@@ -823,15 +820,22 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
   const int row0 = blockIdx.y * rpb, row1 = min(rows, row0 + rpb);
   const int r = (int)min<int64_t>(3, n - 3 * g);
   const float* v = values + (size_t)row0 * vpitch + 3 * g;
-  float nx[3];
-#pragma unroll
-  for (int e = 0; e < 3; ++e) nx[e] = e < r ? v[e] : 0.0f;
+  // one 12-byte load per full group (a wave instruction spans 768 contiguous
+  // bytes once, instead of three dword loads over the same lines); two rows in
+  // flight ahead of the one being encoded
+  typedef float f3 __attribute__((ext_vector_type(3)));
+  auto load = [&](const float* p) -> f3 {
+    if (r == 3) return *reinterpret_cast<const f3*>(p);
+    return f3{p[0], r > 1 ? p[1] : 0.0f, 0.0f};
+  };
+  f3 n1 = load(v), n2 = f3{0.0f, 0.0f, 0.0f};
+  if (row0 + 1 < row1) n2 = load(v + vpitch);
   for (int row = row0; row < row1; ++row) {
-    float x[3] = {nx[0], nx[1], nx[2]};
-    if (row + 1 < row1) {
+    const float x[3] = {n1.x, n1.y, n1.z};
+    n1 = n2;
+    if (row + 2 < row1) {
       v += vpitch;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) nx[e] = e < r ? v[e] : 0.0f;
+      n2 = load(v + vpitch);
     }
     *reinterpret_cast<uint4*>(out + (size_t)row * pitch + 16 * g) = encode_group(x, r, &tab);
   }
@@ -1414,12 +1418,13 @@ hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int 
   int64_t groups = (n + 2) / 3;
   if (groups == 0 || rows == 0) return hipSuccess;
   const int64_t gx = blocks_for(groups, 256);
-  // rows per block: about 16,384 blocks in all (a lane walks its group down
+  // rows per block: about 65,536 blocks in all (a lane walks its group down
   // rpb rows, so the LDS table copy is paid once per rpb rows). Measured on
-  // one box (scripts/gpu_sweep.sh): synth1m_256 encodes in 480-500 us at 8-22
-  // rows per block against 525-545 us with whole columns (256 rows) and
-  // 510-525 us at 64; cifar10_256 and MNIST-64 are flat around 7 and 1.
-  int rpb = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 16383) / 16384));
+  // one box (scripts/gpu_encode_rpb.sh, two rows of loads in flight):
+  // synth1m_256 encodes in 478-480 us at 4-8 rows per block, 483 at 16, 501 at
+  // 2 and 32, 595 at 1; the same access pattern without the codec arithmetic
+  // (scripts/ubench_stream.hip, 12 B in / 16 B out per lane) runs 452-486 us.
+  int rpb = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 65535) / 65536));
   if (const char* e = getenv("FLEET_ENCODE_RPB")) rpb = std::max(1, std::min(rows, atoi(e)));  // experiments
   hipLaunchKernelGGL(k_encode_f32, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s, values, n,
                      vpitch, out, pitch, groups, rows, rpb);
@@ -1575,6 +1580,8 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
       case 17: { const float x = u2f(u);                              // one-lookup Q on |x| < 1e8 (as fn 6)
                use = q_gen_ok(x);
                o = use ? f2u(__builtin_fabsf(x) < 1e8f ? q_xl(x, xl.x) : q_lat(x)) : 0u; break; }
+      case 18: { const float e = glibc_expf(u2f(u));                 // the teacher's expf (libm's)
+               o = e != e ? 0x7fc00000u : f2u(e); break; }
       default: o = 0; use = false;
     }
     if (use) sum += splitmix64(((uint64_t)u << 32) | o);

@@ -8,8 +8,10 @@ vector [E, sigma, C, lr, batchSize, featureSize, numLabels, per sample: features
 (mode 1) teacher probabilities, label] and Base64-encodes it. The index draw is
 host logic and stays here; the gather + encode runs on the GPU
 (``Codec.getMiniBatch`` / ``Codec.minibatch_device``). The mode-1 teacher's
-forward pass (mojo network inference) is not rebuilt: its per-sample class
-probabilities are an input.
+forward pass (uniformSample's teacher.forward, :603) runs on the GPU too
+(``Teacher``: fleet_teacher_forward, bit-identical to the mojo network); its
+training in initSampler (:480-546: 300 rand()-drawn MNIST samples) is dataset
+plumbing and stays with the caller, who hands over the trained weights.
 
 Bucket construction (initSampler :409-470: label sort, 2-shard buckets,
 ``std::random_shuffle``) is dataset plumbing outside the hot path; buckets are
@@ -106,8 +108,8 @@ class OfflineSampler:
         return float(np.float32(src))
 
     def getMiniBatch(self, batch_size: int, teacher=None) -> bytes:  # noqa: N802  (cppNN_backend.cpp:677)
-        """``teacher(indices) -> [B, numLabels]`` supplies the mode-1 teacher's
-        probabilities for the IID path (uniformSample runs the teacher there)."""
+        """``teacher(indices) -> [B, numLabels]`` (e.g. a ``Teacher``) supplies the mode-1
+        teacher's probabilities for the IID path (uniformSample runs the teacher there)."""
         B = batch_size * self.E
         if self.iid:
             idx = uniform_indices(len(self.images), B)
@@ -117,3 +119,22 @@ class OfflineSampler:
         hdr = minibatch_header(self.E, self.sigma, self.C, self.lr, B, self.images.shape[1], self.num_labels)
         probs = teacher(idx) if (teacher is not None and self.iid) else None
         return self.codec.getMiniBatch(self.images, self.labels, idx, hdr, teacher=probs)
+
+
+class Teacher:
+    """The sampler's mode-1 teacher (initSampler's network, cppNN_backend.cpp:494-502)
+    with trained weights: ``teacher(idx)`` = teacher.forward(images[i], TEMPERATURE, -1, 1)
+    for each drawn index (uniformSample, :596-613), on the GPU (Codec.teacher_forward).
+    w: the network's non-null W in order (21448 floats), b: the use_bias() layers'
+    biases in layer order (82)."""
+
+    TEMPERATURE = 2.0  # commonLib/cppNN/network.h:53
+
+    def __init__(self, codec, w, b, images):
+        self.codec = codec
+        self.w = np.ascontiguousarray(w, dtype=np.float32).reshape(-1)
+        self.b = np.ascontiguousarray(b, dtype=np.float32).reshape(-1)
+        self.images = np.ascontiguousarray(images, dtype=np.float32)
+
+    def __call__(self, idx) -> np.ndarray:
+        return self.codec.teacher_forward(self.w, self.b, self.images, idx, self.TEMPERATURE)

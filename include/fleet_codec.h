@@ -208,6 +208,8 @@ int fleet_check(fleet_ctx* ctx, void* stream);
  *   fn 13: multiplier-table Q (as fn 6)   fn 14: multiplier-table int2float (as fn 7)
  *   fn 15: multiplier-table float2int (as fn 10)   fn 16: scalar Q fast path (as fn 2)
  *   fn 17: one-lookup latency Q (q_xl) on |x| < 1e8, fn 12 elsewhere (as fn 6)
+ *   fn 18: the teacher forward's expf (glibc 2.35 restated) over all 2^32 inputs,
+ *          NaN results as 0x7fc00000 (the libm expf digest of tests/native/digest_ref.cpp)
  * computed on the GPU; compare with the oracle's digests. */
 int fleet_selftest_digest(fleet_ctx* ctx, int fn, uint64_t* out);
 
@@ -268,6 +270,29 @@ int fleet_model_params(fleet_ctx* ctx, const float* weights, size_t n_weights, c
  * images: n_images x F fp32 rows; labels: n_images int32. Output:
  * fleet_minibatch_len(F, B, num_labels, teacher != NULL) bytes. */
 size_t fleet_minibatch_len(int F, int B, int num_labels, int with_teacher);
+
+/* The sampler's mode-1 teacher forward: uniformSample appends
+ * teacher.forward(sample, TEMPERATURE, -1, 1)'s 10 class probabilities per drawn
+ * sample (Server/src/main/c++/cppNN_backend.cpp:596-613) for the teacher network
+ * initSampler builds (:494-502: I1 28x28, C1 conv 5x5x8 elu, P1 semi-stochastic
+ * pool 3, C2i conv 1x1x16 elu, C2 conv 5x5x48 elu, P2 semi-stochastic pool 2,
+ * FC2 softmax 10), computed as commonLib/cppNN's network::forward does, bit for
+ * bit (expf = glibc 2.35's, fleet_amd/csrc/teacher_math.h). w: the network's
+ * non-null W in order (fleet_teacher_weight_count() floats), b: the use_bias()
+ * layers' biases in layer order (fleet_teacher_bias_count()); the first 784 of
+ * each image's F features are the input; temperature = TEMPERATURE (2,
+ * commonLib/cppNN/network.h:53). Replaces the teacher.forward calls; the
+ * teacher's training in initSampler stays with the caller. */
+size_t fleet_teacher_weight_count(void);
+size_t fleet_teacher_bias_count(void);
+/* device buffers: probs[b*10 + j] for image d_idx[b] (d_idx NULL: image b);
+ * an index outside [0, n_images) is reported by fleet_check as FLEET_ERR_ARG */
+int fleet_teacher_forward_device(fleet_ctx* ctx, const void* d_w, const void* d_b, const void* d_images,
+                                 size_t n_images, int F, const void* d_idx, int B, float temperature, void* d_probs,
+                                 void* stream);
+/* host buffers, synchronous: probs[B x 10] for images[idx[b]] */
+int fleet_teacher_forward(fleet_ctx* ctx, const float* w, size_t n_w, const float* b, size_t n_b, const float* images,
+                          size_t n_images, int F, const int32_t* idx, int B, float temperature, float* probs);
 
 /* Kardam bookkeeping of CppNNUpdater.update (Server/src/main/java/apps/cppNN/
  * CppNNUpdater.java:463-481, utils/Kardam.java:48-62) for the M

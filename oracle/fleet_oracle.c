@@ -687,3 +687,121 @@ int fo_descent(float* weights, size_t n_weights, float* fc_bias, size_t n_fc_bia
   }
   return 0;
 }
+
+/* ------------------------------------------------ mode-1 teacher forward */
+
+static float fo_elu(float x, float bias) { /* activation.h:172-176 */
+  if ((x + bias) < 0) return 0.1f * (expf(x + bias) - 1.f);
+  return x + bias;
+}
+
+/* layer.h:481-556 on a P x P window of a channel (row stride js) */
+static float fo_semi_pool(const float* top, int base, int js, int P) {
+  int max_i = base, max2_i = base;
+  float mx = top[base], mx2 = mx;
+  for (int jj = 0; jj < P; jj++)
+    for (int ii = 0; ii < P; ii++) {
+      const int index = base + ii + jj * js;
+      if (mx < top[index]) {
+        mx2 = mx;
+        max2_i = max_i;
+        mx = top[index];
+        max_i = index;
+      } else if (mx2 < top[index]) {
+        mx2 = top[index];
+        max2_i = index;
+      }
+    }
+  const int r = 34909 % 100;
+  const float denom = mx + mx2;
+  if (denom == 0) return top[max_i];
+  const int t1 = fo_cvtt(100 * mx / (mx + mx2));
+  return (r <= t1) ? top[max_i] : top[max2_i]; /* train == 1 */
+}
+
+void fo_teacher_forward(const float* w, const float* b, const float* x, float temperature, float* probs) {
+  static const int W1 = 0, W2i = 200, W2 = 328, Wfc = 328 + 19200;
+  static const int B1 = 0, B2i = 8, B2 = 24;
+  float c1[8 * 576], p1[8 * 64], c2i[16 * 64], c2[48 * 16], p2[192], fc[10];
+  /* C1 (the node is zeroed, then one running sum per output) */
+  for (int map = 0; map < 8; map++)
+    for (int y = 0; y < 24; y++)
+      for (int xx = 0; xx < 24; xx++) {
+        float c = 0;
+        for (int k = 0; k < 5; k++)
+          for (int m = 0; m < 5; m++) c += x[(y + k) * 28 + xx + m] * w[W1 + map * 25 + k * 5 + m];
+        c1[map * 576 + y * 24 + xx] = c;
+      }
+  for (int map = 0; map < 8; map++)
+    for (int i = 0; i < 576; i++) c1[map * 576 + i] = fo_elu(c1[map * 576 + i], b[B1 + map]);
+  /* P1 */
+  for (int k = 0, o = 0; k < 8; k++)
+    for (int j = 0; j <= 24 - 3; j += 3)
+      for (int i = 0; i <= 24 - 3; i += 3) p1[o++] = fo_semi_pool(c1, i + j * 24 + k * 576, 24, 3);
+  /* C2i: input channel outer, map, position */
+  for (int i = 0; i < 16 * 64; i++) c2i[i] = 0;
+  for (int k = 0; k < 8; k++)
+    for (int map = 0; map < 16; map++) {
+      const float cw = w[W2i + map + k * 16];
+      for (int j = 0; j < 64; j++) c2i[j + 64 * map] += p1[k * 64 + j] * cw;
+    }
+  for (int map = 0; map < 16; map++)
+    for (int i = 0; i < 64; i++) c2i[map * 64 + i] = fo_elu(c2i[map * 64 + i], b[B2i + map]);
+  /* C2: input channel outer, map, position, tap */
+  for (int i = 0; i < 48 * 16; i++) c2[i] = 0;
+  for (int k = 0; k < 16; k++)
+    for (int map = 0; map < 48; map++)
+      for (int y = 0; y < 4; y++)
+        for (int xx = 0; xx < 4; xx++) {
+          float* c = &c2[map * 16 + y * 4 + xx];
+          for (int t = 0; t < 25; t++)
+            *c += c2i[k * 64 + (y + t / 5) * 8 + xx + t % 5] * w[W2 + (k * 48 + map) * 25 + t];
+        }
+  for (int map = 0; map < 48; map++)
+    for (int i = 0; i < 16; i++) c2[map * 16 + i] = fo_elu(c2[map * 16 + i], b[B2 + map]);
+  /* P2 */
+  for (int k = 0, o = 0; k < 48; k++)
+    for (int j = 0; j <= 4 - 2; j += 2)
+      for (int i = 0; i <= 4 - 2; i += 2) p2[o++] = fo_semi_pool(c2, i + j * 4 + k * 16, 4, 2);
+  /* FC2 */
+  for (int j = 0; j < 10; j++) {
+    float v = 0;
+    for (int i = 0; i < 192; i++) v += p2[i] * w[Wfc + j * 192 + i];
+    fc[j] = 0;
+    fc[j] += v;
+  }
+  /* softmax */
+  float mx = fc[0];
+  for (int j = 1; j < 10; j++)
+    if (fc[j] > mx) mx = fc[j] / temperature;
+  float denom = 0;
+  for (int j = 0; j < 10; j++) denom += expf(fc[j] / temperature - mx);
+  for (int i = 0; i < 10; i++) probs[i] = expf(fc[i] / temperature - mx) / denom;
+}
+
+static uint64_t fo_splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+uint64_t fo_expf_digest(void) {
+  uint64_t sum = 0;
+#pragma omp parallel for reduction(+ : sum) schedule(static)
+  for (int64_t hi = 0; hi < 65536; ++hi) {
+    uint64_t part = 0;
+    for (uint32_t lo = 0; lo < 65536; ++lo) {
+      const uint32_t u = (uint32_t)(hi << 16) | lo;
+      float xv;
+      memcpy(&xv, &u, 4);
+      const float e = expf(xv);
+      uint32_t o;
+      memcpy(&o, &e, 4);
+      if (e != e) o = 0x7fc00000u;
+      part += fo_splitmix64(((uint64_t)u << 32) | o);
+    }
+    sum += part;
+  }
+  return sum;
+}

@@ -96,6 +96,22 @@ int fo_read_weights_section(const char* text, size_t len, const int32_t* dims, i
 
 /* ---- SGD epilogue: descentNative's model step ---- */
 /* cppNN_backend.cpp:336-352 -> network.h:1185-1202,1334-1353 -> solver.h:88-94, layer.h:241-243 */
+/* The sampler's mode-1 teacher forward, one sample:
+ * teacher.forward(x, TEMPERATURE, -1, 1) of initSampler's network
+ * (Server/src/main/c++/cppNN_backend.cpp:494-502, 603) restated from
+ * commonLib/cppNN: network.h:523-585 (forward), layer.h:805-887 (convolution
+ * accumulate, 5x5 via core_math.h unwrap_aligned_NxN/dotsum_unwrapped_NxN, 1x1),
+ * layer.h:481-556 (semi-stochastic pool, r = 9, train = 1), layer.h:200-238 +
+ * core_math.h dot (fully connected), activation.h:161-176 (elu) and :271-313
+ * (softmax), with the libm expf the reference calls (std::exp(float)).
+ * w: non-null W in network order (21448 floats), b: use_bias() biases in layer
+ * order (82), x: 784 floats, probs: 10. Pinned to the reference's own network
+ * (oracle/_ref ref_teacher_forward) by tests/test_teacher.py. */
+void fo_teacher_forward(const float* w, const float* b, const float* x, float temperature, float* probs);
+/* glibc expf over all 2^32 inputs: the order-independent digest of
+ * tests/native/digest_ref.cpp fn 18 (NaN results as 0x7fc00000) */
+uint64_t fo_expf_digest(void);
+
 int fo_descent(float* weights, size_t n_weights, float* fc_bias, size_t n_fc_bias, const float* g, size_t n_g,
                const uint8_t* w_present, int n_w_slots, const uint8_t* fc_layer, int n_layers, float lr);
 

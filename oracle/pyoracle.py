@@ -115,6 +115,10 @@ class Oracle:
         L.fo_descent.restype = C.c_int
         L.fo_descent.argtypes = [C.c_void_p, sz, C.c_void_p, sz, C.c_void_p, sz, C.c_void_p, C.c_int, C.c_void_p,
                                  C.c_int, C.c_float]
+        L.fo_teacher_forward.restype = None
+        L.fo_teacher_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_float, C.c_void_p]
+        L.fo_expf_digest.restype = C.c_uint64
+        L.fo_expf_digest.argtypes = []
 
     # -- scalars / vectors ------------------------------------------------
     def float2int(self, x: np.ndarray) -> np.ndarray:
@@ -275,6 +279,20 @@ class Oracle:
             raise ValueError("gradient header does not fit the model")
         return w, b
 
+    def teacher_forward(self, w, b, x, temperature: float = 2.0) -> np.ndarray:
+        """fo_teacher_forward per sample: [B, 784] inputs -> [B, 10] probabilities."""
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        b = np.ascontiguousarray(b, dtype=np.float32)
+        x = np.ascontiguousarray(x, dtype=np.float32).reshape(-1, 784)
+        out = np.empty((x.shape[0], 10), np.float32)
+        for i in range(x.shape[0]):
+            self.lib.fo_teacher_forward(w.ctypes.data, b.ctypes.data, x[i].ctypes.data, temperature, out[i].ctypes.data)
+        return out
+
+    def expf_digest(self) -> int:
+        """The libm expf digest over all 2^32 inputs (fn 18 of the device self-test)."""
+        return int(self.lib.fo_expf_digest())
+
     def philox(self, ctr, key):
         c = np.ascontiguousarray(ctr, dtype=np.uint32)
         k = np.ascontiguousarray(key, dtype=np.uint32)
@@ -323,6 +341,8 @@ class ReferenceModel:
         L.ref_server_session.restype = sz
         L.ref_server_session.argtypes = [C.c_char_p, sz, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                          C.c_int, C.c_void_p, sz]
+        L.ref_teacher_forward.restype = C.c_int
+        L.ref_teacher_forward.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
         L.ref_mnist_descent.restype = C.c_int
         L.ref_mnist_descent.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_float] + [C.c_void_p] * 9
 
@@ -424,6 +444,15 @@ class ReferenceModel:
             states.append((take("text"), take("floats"), take("text"), take("floats")))
         n_models = int(np.frombuffer(raw, np.uint64, 1, pos)[0])
         return states, n_models
+
+    def teacher_forward(self, w, b, x) -> np.ndarray:
+        """initSampler's teacher with these W / biases, forward(x_i, TEMPERATURE, -1, 1) per sample."""
+        w = np.ascontiguousarray(w, dtype=np.float32)
+        b = np.ascontiguousarray(b, dtype=np.float32)
+        x = np.ascontiguousarray(x, dtype=np.float32).reshape(-1, 784)
+        out = np.empty((x.shape[0], 10), np.float32)
+        self.lib.ref_teacher_forward(w.ctypes.data, b.ctypes.data, x.ctypes.data, x.shape[0], out.ctypes.data)
+        return out
 
     def mnist_version_copy(self, w_in, b_in):
         """descentNative's mode-1 model copy: read(getParams()) of the MNIST network."""

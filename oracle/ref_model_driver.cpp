@@ -17,6 +17,9 @@
  *   ref_server_session: the server's model natives replayed on a network read
  *     from a getParams text (fetchParamsNative, initUpdater, descentNative,
  *     getParametersNative, getModelParametersNative; cppNN_backend.cpp:161-383).
+ *   ref_teacher_forward: the sampler's mode-1 teacher (initSampler's network,
+ *     cppNN_backend.cpp:494-502) with the given W / biases, and uniformSample's
+ *     teacher.forward(sample, TEMPERATURE, -1, 1) per sample (:603).
  */
 #include <cstdio>
 #include <cstring>
@@ -357,3 +360,41 @@ size_t ref_server_session(const char* text, size_t len, const double* lrates, in
 }
 
 }  // extern "C"
+
+extern "C" {
+
+// w: the teacher's non-null W in network order, b: the use_bias() layers' biases
+// in layer order; x: B samples of 784 floats; probs: B x 10.
+int ref_teacher_forward(const float* w, const float* b, const float* x, int B, float* probs) {
+  mojo::network teacher("sgd");
+  teacher.set_smart_training(false);
+  teacher.set_learning_rate(0.01f);
+  teacher.push_back("I1", "input 28 28 1");
+  teacher.push_back("C1", "convolution 5 8 1 elu");
+  teacher.push_back("P1", "semi_stochastic_pool 3 3");
+  teacher.push_back("C2i", "convolution 1 16 1 elu");
+  teacher.push_back("C2", "convolution 5 48 1 elu");
+  teacher.push_back("P2", "semi_stochastic_pool 2 2");
+  teacher.push_back("FC2", "softmax 10");
+  teacher.connect_all();
+  size_t o = 0;
+  for (auto* m : teacher.W)
+    if (m) {
+      std::memcpy(m->x, w + o, sizeof(float) * m->size());
+      o += m->size();
+    }
+  size_t ob = 0;
+  for (auto* l : teacher.layer_sets[mojo::network::MAIN_LAYER_SET])
+    if (l->use_bias()) {
+      std::memcpy(l->bias.x, b + ob, sizeof(float) * l->bias.size());
+      ob += l->bias.size();
+    }
+  for (int i = 0; i < B; ++i) {
+    const float* out = teacher.forward(x + (size_t)i * 784, TEMPERATURE, -1, 1);
+    std::memcpy(probs + (size_t)i * 10, out, sizeof(float) * 10);
+  }
+  return (int)(o * 1000 + ob);
+}
+
+}  // extern "C"
+

@@ -1,8 +1,10 @@
 // tests/native/digest_ref.cpp -- the oracle's side of fleet_selftest_digest:
 // the same order-independent digests, computed with oracle/fleet_oracle.c over
-// the same whole input domains. Writes tests/golden/digests.json (~1 min, 8 cores).
+// the same whole input domains (fn 18: the libm expf the reference's mojo
+// network calls, against the device's glibc_expf restatement). Writes tests/golden/digests.json (~1 min, 8 cores).
 #include <atomic>
 #include <cstdio>
+#include <cmath>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -47,6 +49,7 @@ static uint64_t digest(int fn) {
           case 10: { float x = u2f(u); use = x < 1e9f && x > -1e8f; if (use) o = (uint32_t)fo_float2int(x); break; }
           case 11: use = (u & 0x7fffffffu) < 0x3f800000u; if (use) o = (uint32_t)fo_float2int(u2f(u)); break;
           case 12: { float x = u2f(u); use = x < 1e9f && x > -1e8f; if (use) o = f2u(Q(x)); break; }
+          case 18: { float e = expf(u2f(u)); o = e != e ? 0x7fc00000u : f2u(e); break; }  // libm expf
         }
         if (use) sum += splitmix64(((uint64_t)u << 32) | o);
       }
@@ -62,9 +65,12 @@ int main(int argc, char** argv) {
   const char* path = argc > 1 ? argv[1] : "tests/golden/digests.json";
   FILE* f = fopen(path, "w");
   fprintf(f, "{\n  \"generator\": \"tests/native/digest_ref.cpp over oracle/fleet_oracle.c\",\n");
-  for (int fn = 0; fn <= 12; ++fn) {
+  const int fns[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 18};
+  const int nf = (int)(sizeof fns / sizeof fns[0]);
+  for (int j = 0; j < nf; ++j) {
+    const int fn = fns[j];
     uint64_t d = digest(fn);
-    fprintf(f, "  \"fn%d\": \"%016llx\"%s\n", fn, (unsigned long long)d, fn < 12 ? "," : "");
+    fprintf(f, "  \"fn%d\": \"%016llx\"%s\n", fn, (unsigned long long)d, j < nf - 1 ? "," : "");
     printf("fn%d %016llx\n", fn, (unsigned long long)d);
     fflush(stdout);
   }

@@ -74,3 +74,71 @@ def test_full_size_sampled_groups(codec, oracle, name):
     assert len(got) == 16 * (sel.size - 1) + tail and len(ups) == M
     assert got == exp, name
     assert np.array_equal(got_f32.view(np.uint32), exp_f32.view(np.uint32)), name
+
+
+def test_full_size_host_ingress_paths(oracle):
+    """synth1m_256 through every host-side entry (fleet_update staged by the worker pool,
+    fleet_update_rows from page-locked rows, fleet_update_multi / _rows_multi over three
+    contexts) gives the device-resident update's bytes, which test_full_size_sampled_groups
+    pins to the oracle; plus the fused Kardam norms at full size vs fleet_kardam_grads
+    (rtol 1e-12 as in test_gpu_kardam_fused.py)."""
+    torch = pytest.importorskip("torch")
+    free, _ = torch.cuda.mem_get_info()
+    if free < 12 * 2**30:
+        pytest.skip("needs ~12 GiB of free device memory")
+    lay = LAYOUTS["synth1m"]
+    M = 256
+    n = lay.n_up
+    groups = (n + 2) // 3
+    L = F.b64_len(n)
+    hp = np.asarray(lay.header_positions(), np.int32)
+    rng = np.random.default_rng(7)
+    dampen = rng.uniform(0.05, 2.0, M)
+    dev = torch.device("cuda", 0)
+    cs = [F.Codec(0) for _ in range(3)]
+    try:
+        codec = cs[0]
+        values = torch.empty((M, 3 * groups), dtype=torch.float32, device=dev)
+        codec.synth_device(20261017, values, n, hp, lay.header_values())
+        text = torch.empty((M, 16 * groups), dtype=torch.uint8, device=dev)
+        codec.encode_device(values, n, text)
+        codec.check()
+        del values
+        merged = torch.zeros(16 * groups, dtype=torch.uint8, device=dev)
+        merged_f32 = torch.zeros(3 * groups, dtype=torch.float32, device=dev)
+        codec.update_device(text, L, dampen, hp, merged, merged_f32)
+        codec.check()
+        want = merged.cpu().numpy()[:L].tobytes()
+        want_f32 = merged_f32.cpu().numpy()[:n]
+        rows = np.ascontiguousarray(text.cpu().numpy())  # [M, 16*groups], rows[i, :L] = upload i
+        ups = [rows[i, :L].tobytes() for i in range(M)]
+
+        got, f32 = codec.update(ups, dampen, want_f32=True)
+        assert got == want
+        assert np.array_equal(f32[:n].view(np.uint32), want_f32.view(np.uint32))
+        assert F.update_multi(cs, ups, dampen) == want
+        del ups
+        codec.register_host(rows)
+        try:
+            assert codec.update_rows(rows, L, dampen) == want
+            assert F.update_rows(cs, rows, L, dampen) == want
+        finally:
+            codec.unregister_host(rows)
+        assert F.update_rows(cs[:2], rows, L, dampen) == want  # pageable rows: staged copy
+
+        # Kardam side outputs at full size on a 16-client slice (kardam_grads is host-paced)
+        K = 16
+        lr = 0.05
+        kd = dampen[:K]
+        kmerged = torch.zeros(16 * groups, dtype=torch.uint8, device=dev)
+        ng, nd = codec.update_kardam_device(text[:K].contiguous(), L, kd, hp, lr, kmerged,
+                                            g_out_f32=torch.zeros((K, n + 3), dtype=torch.float32, device=dev))
+        codec.check()
+        _, eng, _ = codec.kardam_grads([rows[i, :L].tobytes() for i in range(K)], kd, lr)
+        np.testing.assert_allclose(ng, eng, rtol=1e-12, atol=0)
+        assert np.all(np.isnan(nd))
+        assert kmerged.cpu().numpy()[:L].tobytes() == codec.update([rows[i, :L].tobytes() for i in range(K)], kd)
+    finally:
+        for c in cs:
+            c.close()
+        torch.cuda.empty_cache()

@@ -305,7 +305,7 @@ def test_device_synth_and_encode(codec, oracle):
 SAME_DIGEST = {13: 6, 14: 7, 15: 10, 16: 2, 17: 6}
 
 
-@pytest.mark.parametrize("fn", range(18))
+@pytest.mark.parametrize("fn", range(19))
 def test_device_codec_exhaustive_digest(codec, fn):
     """Every input of each device codec function's domain (2^32 codes / bit
     patterns), digested on the GPU, equals the oracle's digest."""
