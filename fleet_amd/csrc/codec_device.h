@@ -96,6 +96,32 @@ __device__ __forceinline__ void xl_table_init(XlTable* t) {
   }
 }
 
+// The throughput-Q tables of k_update (codec_math.h d16_entry / StepTables):
+// 8 KB of digit offsets by the top 13 bits of x, and the stride-16 step tables.
+struct alignas(16) D16Table {
+  StepTables st;
+  uint8_t d16[8192];
+};
+static_assert(sizeof(D16Table) % 16 == 0, "copied as uint4");
+FLEET_HDC D16Table make_d16_table() {
+  D16Table t{};
+  t.st = make_step_tables();
+  for (uint32_t i = 0; i < 8192; ++i) t.d16[i] = d16_entry(i);
+  return t;
+}
+static __constant__ D16Table g_d16_table = make_d16_table();
+template <int NT = 256>
+__device__ __forceinline__ void d16_table_init(D16Table* t) {
+  constexpr int n16 = (int)(sizeof(D16Table) / 16);
+  const uint4* src = reinterpret_cast<const uint4*>(&g_d16_table);
+  uint4* dst = reinterpret_cast<uint4*>(t);
+#pragma unroll
+  for (int i0 = 0; i0 < n16; i0 += NT) {
+    const int i = i0 + (int)threadIdx.x;
+    if (i < n16) dst[i] = src[i];
+  }
+}
+
 // One 16-char group -> 12 bytes -> 3 little-endian int32 codes.
 // Returns a 16-bit mask of chars that are not in the alphabet (bit i = char i).
 __device__ __forceinline__ uint32_t b64_decode_group(uint4 w, const B64Tables* t, int32_t codes[3]) {

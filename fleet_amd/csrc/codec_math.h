@@ -512,6 +512,61 @@ FLEET_HD float q_fast1(float x) {
   return d9(u2f(f2u((float)c) | (f2u(x) & 0x80000000u)));
 }
 
+// ------------------------------------- byte-table digit count (throughput Q)
+// The k_update stages' form of q_mt: the digit count comes from ONE byte load
+// indexed by the top 13 bits of x (sign, exponent, 4 mantissa bits; 8 KB), and
+// the byte is already the byte offset of the step tables' entry (16 * d), so
+// neither the compare against the power of ten nor an address computation
+// costs a VALU instruction. A 1/16-binade slice that holds a power of ten (the
+// one place where numDigits changes inside a binade) holds kD16Cmp instead: its
+// lanes take the compare (var_digits_ab) in a rare divergent fix-up. Values
+// outside the q_gen domain map to >= kD16Out (identity chains; the caller
+// recomputes them exactly).
+constexpr uint32_t kD16Out = 10u << 4;   // first out-of-domain offset
+constexpr uint32_t kD16Cmp = 14u << 4;   // the slice holds the power of ten: compare
+constexpr uint32_t kD16Slow = 15u << 4;  // numDigits > 9, inf, NaN
+FLEET_HDC uint8_t d16_entry(uint32_t i) {  // i = bits >> 19
+  const DigitPair p = digit_pair(i >> 4);
+  const uint32_t ab_lo = (i << 19) & 0x7fffffffu, ab_hi = ab_lo | 0x7ffffu;
+  const uint32_t thr = __builtin_bit_cast(uint32_t, p.thr);
+  const uint32_t d_lo = ab_lo < thr ? p.dlo : p.dhi, d_hi = ab_hi < thr ? p.dlo : p.dhi;
+  if (d_lo != d_hi) return (uint8_t)kD16Cmp;
+  return (uint8_t)(d_lo > 9u ? kD16Slow : d_lo << 4);
+}
+// step tables at a 16-byte stride, addressed by the d16 byte offset
+struct alignas(16) StepTables {
+  float m[16][4];     // x10 chain group multipliers (MulEntry::m)
+  float h[16][4];     // /10 chain group multipliers (MulEntry::h)
+  uint32_t d[16][4];  // d itself (the code's last digit), in .x
+};
+FLEET_HDC StepTables make_step_tables() {
+  StepTables t{};
+  for (uint32_t d = 0; d < 16; ++d) {
+    const MulEntry e = mul_entry(d);
+    for (int k = 0; k < 4; ++k) {
+      t.m[d][k] = e.m[k];
+      t.h[d][k] = e.h[k];
+      t.d[d][k] = d;
+    }
+  }
+  return t;
+}
+// the marker lanes' digit offset (the compare of var_digits_ab)
+FLEET_HD uint32_t d16_fix(float x, const VarEntry* vt) {
+  return var_digits_ab(f2u(x), f2u(x) & 0x7fffffffu, vt) << 4;
+}
+// Q(x) given e = 16 * numDigits((int)x) <= 144 (garbage, never a fault, for e >= kD16Out)
+FLEET_HD float q_d16(float x, uint32_t e, const StepTables* st) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  // e is a multiple of 16 (d16_entry, d16_fix): 16-byte loads at the byte offset itself
+  const char* base = reinterpret_cast<const char*>(st);
+  const f4 m = *static_cast<const f4*>(__builtin_assume_aligned(base + e, 16));
+  const f4 h = *static_cast<const f4*>(__builtin_assume_aligned(base + sizeof(st->m) + e, 16));
+  const uint32_t d = *static_cast<const uint32_t*>(__builtin_assume_aligned(base + sizeof(st->m) + sizeof(st->h) + e, 16));
+  const MulEntry me{{m.x, m.y, m.z, m.w}, {h.x, h.y, h.z, h.w}};
+  return div10_mt(code_float_mt(mul10_mt(__builtin_fabsf(x), me), d, x), me);
+}
+
 // ------------------------------------------- one-lookup latency Q (serial chain)
 // The serial accumulation A = Q(A + p) runs on ONE wave per tile: it is bound by
 // that wave's instruction issue, so the step count matters more than a table

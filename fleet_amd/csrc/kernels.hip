@@ -133,6 +133,32 @@ __device__ __forceinline__ void q_stage_off(float (&out)[S], const float (&x)[S]
   }
 }
 
+// q_stage_off with the byte-table digit count (codec_math.h q_d16): one byte
+// load per value gives the step tables' offset; lanes in a power-of-ten slice
+// (rare) take the compare; values outside the q_gen domain raise `dmax` to
+// >= kD16Out and leave their results undefined (the caller recomputes them).
+template <int S>
+__device__ __forceinline__ void q_stage_d16(float (&out)[S], const float (&x)[S], const D16Table* dt,
+                                            const VarEntry* vt, uint32_t& dmax) {
+  uint32_t e[S], emax = 0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    e[i] = dt->d16[f2u(x[i]) >> 19];
+    emax = max(emax, e[i]);
+  }
+  if (__ballot(emax >= kD16Out) != 0) {  // compare slices / out of domain (wave-uniform branch)
+    emax = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      if (e[i] == kD16Cmp) e[i] = d16_fix(x[i], vt);
+      emax = max(emax, e[i]);
+    }
+  }
+  dmax = max(dmax, emax);
+#pragma unroll
+  for (int i = 0; i < S; ++i) out[i] = q_d16(x[i], e[i], &dt->st);
+}
+
 // out[i] = int2float(codes[i]) (Base64.cpp:116-139): fixed 9-step chains when
 // every code of the wave ends in 0 (|value| < 1), else step multipliers from
 // the last digit. Total: no fallback needed.
@@ -216,6 +242,7 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
                                                 int* __restrict__ err, KardamOut kd = KardamOut{}) {
   constexpr int S = 3 * K;
   __shared__ B64Tables tab;
+  __shared__ D16Table dtab;
   const int lane = threadIdx.x & 63;
 
   // hdr_block = {status, n_headers, walk_end, 0, positions...} (k_layout_parse / host-built);
@@ -261,6 +288,7 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
   for (int k = 0; k < K; ++k) nxt[k] = *reinterpret_cast<const uint4*>(rowp[k]);
   // tables copied while the first client's groups are in flight
   b64_tables_init(&tab);
+  if constexpr (!KD) d16_table_init(&dtab);
   __syncthreads();
   for (int c = 0; c < M; ++c) {
     uint4 cur[K];
@@ -293,7 +321,7 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
     float y0[S], y[S];
     dec_stage<S>(y0, codes, &tab);
     if constexpr (KD) q_stage<S>(y, y0, &tab);
-    else q_stage_off<S>(y, y0, &tab, dmax);
+    else q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
 
     // stage B: p = Q((float)((double)y * d))
     const double d = dampen[c];
@@ -301,7 +329,7 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
 #pragma unroll
     for (int i = 0; i < S; ++i) r[i] = (float)((double)y[i] * d);
     if constexpr (KD) q_stage<S>(p, r, &tab);
-    else q_stage_off<S>(p, r, &tab, dmax);
+    else q_stage_d16<S>(p, r, &dtab, tab.var, dmax);
 
     if constexpr (KD) {
       // Kardam.setGrad(id, pickedGrad.scalarMultiply(getLrate())) and updateLip's
@@ -348,13 +376,16 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
       float sm[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) sm[i] = acc[i] + p[i];
-      q_stage_off<S>(acc, sm, &tab, dmax);
+      if constexpr (KD) q_stage_off<S>(acc, sm, &tab, dmax);
+      else q_stage_d16<S>(acc, sm, &dtab, tab.var, dmax);
     }
   }
   // a value left the q_gen domain somewhere in this lane's chains (|x| >= 1e8,
-  // inf, NaN -- never for gradients): recompute the lane's values exactly
-  if (__ballot(dmax > 9u) != 0) {
-    if (dmax > 9u) {
+  // inf, NaN -- never for gradients): recompute the lane's values exactly.
+  // dmax holds digit counts (KD: q_stage_off) or their table offsets (q_stage_d16).
+  const bool out_of_domain = KD ? dmax > 9u : dmax >= kD16Out;
+  if (__ballot(out_of_domain) != 0) {
+    if (out_of_domain) {
 #pragma unroll
       for (int k = 0; k < K; ++k)
         if (live[k])

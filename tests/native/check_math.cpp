@@ -87,6 +87,30 @@ int main(int argc, char** argv) {
     report("q_mt/enc_mt/dec_mt/var_digits/q_fast1 (exhaustive)", b);
     return g_bad ? 1 : 0;
   }
+  if (argc > 1 && std::string(argv[1]) == "d16") {  // byte-table digit count + stride-16 Q, every input
+    static VarEntry vt[512];
+    static uint8_t dt[8192];
+    static StepTables st = make_step_tables();
+    for (uint32_t i = 0; i < 512; ++i) vt[i] = var_entry(i);
+    for (uint32_t i = 0; i < 8192; ++i) dt[i] = d16_entry(i);
+    long b = g_bad;
+    par_for(0, 1ull << 32, 1, [](uint64_t i) {
+      const float x = u2f((uint32_t)i);
+      uint32_t e = dt[(uint32_t)i >> 19];
+      if (e == kD16Cmp) e = d16_fix(x, vt);
+      if (!q_gen_ok(x)) {
+        if (e < kD16Out) g_bad++;
+        return;
+      }
+      if (e != 16u * (uint32_t)fo_num_digits(fo_cvtt(x))) g_bad++;
+      if (!same(q_d16(x, e, &st), fo_int2float(fo_float2int(x)))) g_bad++;
+    });
+    long cmp_slices = 0;
+    for (uint32_t i = 0; i < 8192; ++i) cmp_slices += dt[i] == kD16Cmp;
+    printf("d16 table: %ld compare slices of 8192\n", cmp_slices);
+    report("d16 / q_d16 (exhaustive)", b);
+    return g_bad ? 1 : 0;
+  }
   const uint64_t s = exhaustive ? 1 : 97;  // sampling stride (odd, walks every residue class)
   long b0;
 
@@ -175,6 +199,37 @@ int main(int argc, char** argv) {
     if (q_ok(x) && !same(q_fast1(x), fo_int2float(fo_float2int(x)))) g_bad++;
   });
   report("q_mt/enc_mt/q_fast1", b0);
+  b0 = g_bad;  // byte-table digit offsets + stride-16 Q (k_update's stages) vs the oracle
+  {
+    static uint8_t dt[8192];
+    static StepTables st = make_step_tables();
+    for (uint32_t i = 0; i < 8192; ++i) dt[i] = d16_entry(i);
+    par_for(0, 1ull << 32, s, [](uint64_t i) {
+      const float x = u2f((uint32_t)i);
+      uint32_t e = dt[(uint32_t)i >> 19];
+      if (e == kD16Cmp) e = d16_fix(x, vt);
+      if (!q_gen_ok(x)) {
+        if (e < kD16Out) g_bad++;
+        return;
+      }
+      if (e != 16u * (uint32_t)fo_num_digits(fo_cvtt(x))) g_bad++;
+      if (!same(q_d16(x, e, &st), fo_int2float(fo_float2int(x)))) g_bad++;
+    });
+    // every power-of-ten slice, densely (where the compare decides)
+    for (uint32_t sl = 0; sl < 8192; ++sl)
+      if (dt[sl] == kD16Cmp)
+        par_for((uint64_t)sl << 19, (uint64_t)(sl + 1) << 19, 1, [](uint64_t i) {
+          const float x = u2f((uint32_t)i);
+          const uint32_t e = d16_fix(x, vt);
+          if (!q_gen_ok(x)) {
+            if (e < kD16Out) g_bad++;
+            return;
+          }
+          if (e != 16u * (uint32_t)fo_num_digits(fo_cvtt(x)) || !same(q_d16(x, e, &st), fo_int2float(fo_float2int(x))))
+            g_bad++;
+        });
+  }
+  report("d16/q_d16", b0);
   b0 = g_bad;
   {
     static XlEntry xt[2 * kXlSpan];
