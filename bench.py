@@ -591,14 +591,17 @@ def main():
     codec = F.Codec(local)
 
     main_res = time_workload(torch, dist, codec, args.workload, args.steps, args.warmup, rank, world, args.graph)
+    # the host-buffer paths before the extras: after the 150 GiB synth4m_4096 extra the
+    # process's small pinned-host copies run 2-3x slower (measured on MNIST-64: 0.81 vs
+    # 0.30 ms), an allocator-state effect that is not the path's
+    e2e = None
+    if world == 1 and not args.no_e2e:
+        e2e = {w: end_to_end(torch, codec, w) for w in args.e2e.split(",") if w}
+
     extras = {}
     if world == 1 and args.extras:
         for w in [x for x in args.extras.split(",") if x and x != args.workload]:
             extras[w] = time_workload(torch, dist, codec, w, max(3, args.steps // 4), 2, rank, world, args.graph)
-
-    e2e = None
-    if world == 1 and not args.no_e2e:
-        e2e = {w: end_to_end(torch, codec, w) for w in args.e2e.split(",") if w}
 
     strong = None
     if args.strong or not args.no_strong_block:

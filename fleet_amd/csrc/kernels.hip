@@ -1345,7 +1345,7 @@ const char* update_kernel_name(int64_t groups) {
   static thread_local char buf[48];
   const UpdatePlan p = plan_update(groups);
   if (p.kind == 0)
-    snprintf(buf, sizeof buf, "k_update<%d>", p.k);
+    snprintf(buf, sizeof buf, "k_update<%d, false>", p.k);  // as rocprofv3 names it
   else if (p.kind == 2)
     snprintf(buf, sizeof buf, "k_update_pipe<%d, %d, %d, %d>", p.tg, p.ipt, p.nw, p.wp);
   else
