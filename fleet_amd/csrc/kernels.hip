@@ -233,8 +233,8 @@ __device__ __noinline__ float chain_general(const uint8_t* __restrict__ uploads,
 // 463-481, Kardam.java:48-106) as side outputs of the client loop
 // (KardamOut), so it costs no second pass over the uploads; stages A and B then
 // use the exact in-stage fallback (their values feed the side outputs).
-template <int K, bool KD = false>
-__global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+template <int K, bool KD = false, int NT = 256>
+__global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                 const double* __restrict__ dampen, double inv_avg,
                                                 int64_t n_up, int64_t g_begin, int64_t g_end,
                                                 const int32_t* __restrict__ hdr_block,
@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
   const uint8_t* rowp[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    g[k] = g_begin + ((int64_t)blockIdx.x * K + k) * 256 + threadIdx.x;
+    g[k] = g_begin + ((int64_t)blockIdx.x * K + k) * NT + threadIdx.x;
     live[k] = g[k] < g_end;
     rowp[k] = uploads + 16 * (live[k] ? g[k] : g_begin);
   }
@@ -287,8 +287,8 @@ __global__ void __launch_bounds__(256) k_update(const uint8_t* __restrict__ uplo
 #pragma unroll
   for (int k = 0; k < K; ++k) nxt[k] = *reinterpret_cast<const uint4*>(rowp[k]);
   // tables copied while the first client's groups are in flight
-  b64_tables_init(&tab);
-  if constexpr (!KD) d16_table_init(&dtab);
+  b64_tables_init<NT>(&tab);
+  if constexpr (!KD) d16_table_init<NT>(&dtab);
   __syncthreads();
   for (int c = 0; c < M; ++c) {
     uint4 cur[K];
@@ -1397,7 +1397,18 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
   } else {
     if (p.k == 4) FLEET_LAUNCH(k_update<4>, 256 * 4);
     else if (p.k == 2) FLEET_LAUNCH(k_update<2>, 256 * 2);
-    else FLEET_LAUNCH(k_update<1>, 256);
+    else {
+      const char* nt = getenv("FLEET_UPDATE_NT");  // experiments: block size of the stream kernel
+      const int v = nt ? atoi(nt) : 256;
+#define FLEET_LAUNCH_NT(N)                                                                                      \
+  hipLaunchKernelGGL((k_update<1, false, N>), dim3((unsigned)((groups + (N)-1) / (N))), dim3(N), 0, s, uploads, \
+                     pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
+      if (v == 64) FLEET_LAUNCH_NT(64);
+      else if (v == 128) FLEET_LAUNCH_NT(128);
+      else if (v == 512) FLEET_LAUNCH_NT(512);
+      else FLEET_LAUNCH_NT(256);
+#undef FLEET_LAUNCH_NT
+    }
   }
 #undef FLEET_LAUNCH
   return hipGetLastError();
