@@ -159,6 +159,35 @@ __device__ __forceinline__ void q_stage_d16(float (&out)[S], const float (&x)[S]
   for (int i = 0; i < S; ++i) out[i] = q_d16(x[i], e[i], &dt->st);
 }
 
+// q_stage_d16 with the exact in-stage fallback (the general codec per lane for
+// values outside the q_gen domain): a drop-in for q_stage where every stage
+// output is used (Kardam's side outputs).
+template <int S>
+__device__ __forceinline__ void q_stage_d16x(float (&out)[S], const float (&x)[S], const D16Table* dt,
+                                             const VarEntry* vt) {
+  uint32_t e[S], emax = 0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    e[i] = dt->d16[f2u(x[i]) >> 19];
+    emax = max(emax, e[i]);
+  }
+  if (__ballot(emax >= kD16Out) != 0) {
+    emax = 0;
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      if (e[i] == kD16Cmp) e[i] = d16_fix(x[i], vt);
+      emax = max(emax, e[i]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) out[i] = q_d16(x[i], e[i], &dt->st);
+  if (__ballot(emax >= kD16Out) != 0) {
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      if (e[i] >= kD16Out) out[i] = q(x[i]);
+  }
+}
+
 // out[i] = int2float(codes[i]) (Base64.cpp:116-139): fixed 9-step chains when
 // every code of the wave ends in 0 (|value| < 1), else step multipliers from
 // the last digit. Total: no fallback needed.
@@ -265,7 +294,7 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
   float acc[S];
   int32_t codes[S];
   uint32_t bad[K], need[K];
-  uint32_t dmax = 0;  // largest digit count seen (> 9: left the q_gen domain)
+  uint32_t dmax = 0;  // largest digit-table offset seen (>= kD16Out: left the q_gen domain)
 #pragma unroll
   for (int k = 0; k < K; ++k) need[k] = needed_chars_mask((int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g[k])));
   // layout consistency (every upload carries the last one's header codes) is
@@ -288,7 +317,7 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
   for (int k = 0; k < K; ++k) nxt[k] = *reinterpret_cast<const uint4*>(rowp[k]);
   // tables copied while the first client's groups are in flight
   b64_tables_init<NT>(&tab);
-  if constexpr (!KD) d16_table_init<NT>(&dtab);
+  d16_table_init<NT>(&dtab);
   __syncthreads();
   for (int c = 0; c < M; ++c) {
     uint4 cur[K];
@@ -320,7 +349,7 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
     // stage A: y = Q(int2float(code))
     float y0[S], y[S];
     dec_stage<S>(y0, codes, &tab);
-    if constexpr (KD) q_stage<S>(y, y0, &tab);
+    if constexpr (KD) q_stage_d16x<S>(y, y0, &dtab, tab.var);
     else q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
 
     // stage B: p = Q((float)((double)y * d))
@@ -328,7 +357,7 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
     float r[S], p[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) r[i] = (float)((double)y[i] * d);
-    if constexpr (KD) q_stage<S>(p, r, &tab);
+    if constexpr (KD) q_stage_d16x<S>(p, r, &dtab, tab.var);
     else q_stage_d16<S>(p, r, &dtab, tab.var, dmax);
 
     if constexpr (KD) {
@@ -337,7 +366,7 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
       float rg[S], G[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) rg[i] = (float)((double)p[i] * kd.lr);
-      q_stage<S>(G, rg, &tab);
+      q_stage_d16x<S>(G, rg, &dtab, tab.var);
       const bool hp = kd.prev && kd.has_prev[c];
       double sg = 0.0, sd = 0.0;
 #pragma unroll
@@ -376,14 +405,13 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
       float sm[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) sm[i] = acc[i] + p[i];
-      if constexpr (KD) q_stage_off<S>(acc, sm, &tab, dmax);
-      else q_stage_d16<S>(acc, sm, &dtab, tab.var, dmax);
+      q_stage_d16<S>(acc, sm, &dtab, tab.var, dmax);
     }
   }
   // a value left the q_gen domain somewhere in this lane's chains (|x| >= 1e8,
   // inf, NaN -- never for gradients): recompute the lane's values exactly.
-  // dmax holds digit counts (KD: q_stage_off) or their table offsets (q_stage_d16).
-  const bool out_of_domain = KD ? dmax > 9u : dmax >= kD16Out;
+  // dmax holds the largest table offset (q_stage_d16) of the serial accumulation.
+  const bool out_of_domain = dmax >= kD16Out;
   if (__ballot(out_of_domain) != 0) {
     if (out_of_domain) {
 #pragma unroll
@@ -1345,7 +1373,7 @@ const char* update_kernel_name(int64_t groups) {
   static thread_local char buf[48];
   const UpdatePlan p = plan_update(groups);
   if (p.kind == 0)
-    snprintf(buf, sizeof buf, "k_update<%d, false>", p.k);  // as rocprofv3 names it
+    snprintf(buf, sizeof buf, "k_update<%d, false, 256>", p.k);  // as rocprofv3 names it
   else if (p.kind == 2)
     snprintf(buf, sizeof buf, "k_update_pipe<%d, %d, %d, %d>", p.tg, p.ipt, p.nw, p.wp);
   else

@@ -8,7 +8,7 @@ R=$PWD
 export TMPDIR=/tmp
 B="--extras= --no-cpu-baseline --no-e2e --no-strong-block"
 for W in $WL; do
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$W -o run -- python3 $R/bench.py --workload $W $B --steps 20 --warmup 3 > $O/trace_$W.log 2>&1 &&
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_$W -o run -- python3 $R/bench.py --workload $W $B --steps 100 --warmup 3 > $O/trace_$W.log 2>&1 &&
   timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/fetch_$W -o run -- python3 $R/bench.py --workload $W $B --steps 5 --warmup 1 > $O/fetch_$W.log 2>&1 &&
   timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/write_$W -o run -- python3 $R/bench.py --workload $W $B --steps 5 --warmup 1 > $O/write_$W.log 2>&1 &&
   timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CU_CYCLES SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d $O/sq_$W -o run -- python3 $R/bench.py --workload $W $B --steps 5 --warmup 1 > $O/sq_$W.log 2>&1 || exit 1
