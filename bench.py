@@ -29,6 +29,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import sys
 import time
 
@@ -356,13 +357,28 @@ def newest_profile(name: str):
     return sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)), reverse=True)
 
 
+def kernel_key(kern: dict, kernel: str):
+    """The entry of `kernel` in a profile summary: the exact rocprofv3 name, else the
+    same kernel with default template arguments spelled differently (k_update<1> /
+    k_update<1, false> / k_update<1, false, 256>)."""
+    if kernel in kern:
+        return kernel
+    def canon(n):
+        return re.sub(r"(,false)?(,256)?>$", ">", re.sub(r"\s+", "", n))
+    for k in kern:
+        if canon(k) == canon(kernel):
+            return k
+    return None
+
+
 def sq_valu(workload: str, kernel: str):
     """VALU lane-instructions per (client, value) of the profiled kernel from the
     newest committed SQ_INSTS_VALU pass (profiles/rNN/sq.json), None when absent."""
     for path in newest_profile("sq.json"):
         try:
             with open(path) as f:
-                v = json.load(f)["workloads"][workload][kernel]["valu_lane_instr_per_element_client"]
+                kern = json.load(f)["workloads"][workload]
+            v = kern[kernel_key(kern, kernel)]["valu_lane_instr_per_element_client"]
             return float(v), os.path.relpath(path, ROOT)
         except (OSError, KeyError, ValueError):
             continue
@@ -381,8 +397,9 @@ def pmc_traffic(workload: str, kernel: str = ""):
         except (OSError, ValueError, KeyError):
             continue
         # only a profile of the same kernel variant counts
-        if kernel in kern and "hbm_bytes" in kern[kernel]:
-            return kern[kernel]["hbm_bytes"], kernel, os.path.relpath(path, ROOT)
+        k = kernel_key(kern, kernel)
+        if k and "hbm_bytes" in kern[k]:
+            return kern[k]["hbm_bytes"], k, os.path.relpath(path, ROOT)
     return None
 
 
