@@ -188,6 +188,22 @@ __device__ __forceinline__ void q_stage_d16x(float (&out)[S], const float (&x)[S
   }
 }
 
+// scalarMultiply(getDampen) (cppNN_backend.cpp:753-777): (float)((double)y * d).
+// When d is a binary32 value (1, 1/2, ... -- staleness 0 gives 1 under every
+// getDampen policy) the double product of two binary32 values is exact and one
+// binary32 multiply rounds it identically; d is uniform, so the branch is too.
+template <int S>
+__device__ __forceinline__ void dampen_stage(float (&r)[S], double d) {
+  const float df = (float)d;
+  if (__builtin_amdgcn_readfirstlane((double)df == d ? 1 : 0)) {  // uniform: a scalar branch
+#pragma unroll
+    for (int i = 0; i < S; ++i) r[i] = r[i] * df;
+  } else {
+#pragma unroll
+    for (int i = 0; i < S; ++i) r[i] = (float)((double)r[i] * d);
+  }
+}
+
 // out[i] = int2float(codes[i]) (Base64.cpp:116-139): fixed 9-step chains when
 // every code of the wave ends in 0 (|value| < 1), else step multipliers from
 // the last digit. Total: no fallback needed.
@@ -356,7 +372,8 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
     const double d = dampen[c];
     float r[S], p[S];
 #pragma unroll
-    for (int i = 0; i < S; ++i) r[i] = (float)((double)y[i] * d);
+    for (int i = 0; i < S; ++i) r[i] = y[i];
+    dampen_stage<S>(r, d);
     if constexpr (KD) q_stage_d16x<S>(p, r, &dtab, tab.var);
     else q_stage_d16<S>(p, r, &dtab, tab.var, dmax);
 
