@@ -551,6 +551,14 @@ FLEET_HDC StepTables make_step_tables() {
   }
   return t;
 }
+// int2float(c) given r16 = 16 * (|c| % 10): the /10 chain's multipliers at r16
+FLEET_HD float dec_d16(int32_t c, uint32_t r16, const StepTables* st) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const char* base = reinterpret_cast<const char*>(st);
+  const f4 h = *static_cast<const f4*>(__builtin_assume_aligned(base + sizeof(st->m) + r16, 16));
+  const MulEntry me{{1.0f, 1.0f, 1.0f, 1.0f}, {h.x, h.y, h.z, h.w}};
+  return div10_mt((float)c, me);
+}
 // the marker lanes' digit offset (the compare of var_digits_ab)
 FLEET_HD uint32_t d16_fix(float x, const VarEntry* vt) {
   return var_digits_ab(f2u(x), f2u(x) & 0x7fffffffu, vt) << 4;

@@ -159,6 +159,18 @@ __device__ __forceinline__ void q_stage_d16(float (&out)[S], const float (&x)[S]
   for (int i = 0; i < S; ++i) out[i] = q_d16(x[i], e[i], &dt->st);
 }
 
+// int2float for the stream kernel: the step multipliers from the stride-16 tables
+// by the code's last digit (total, no fast-path test: the table chain costs what
+// the fixed one does).
+template <int S>
+__device__ __forceinline__ void dec_stage_d16(float (&out)[S], const int32_t (&codes)[S], const D16Table* dt) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const uint32_t a = codes[i] < 0 ? 0u - (uint32_t)codes[i] : (uint32_t)codes[i];
+    out[i] = dec_d16(codes[i], last_digit_u(a) << 4, &dt->st);
+  }
+}
+
 // q_stage_d16 with the exact in-stage fallback (the general codec per lane for
 // values outside the q_gen domain): a drop-in for q_stage where every stage
 // output is used (Kardam's side outputs).
@@ -364,7 +376,7 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
     // with the general codec at the end (|x| >= 1e8: never for gradients).
     // stage A: y = Q(int2float(code))
     float y0[S], y[S];
-    dec_stage<S>(y0, codes, &tab);
+    dec_stage_d16<S>(y0, codes, &dtab);
     if constexpr (KD) q_stage_d16x<S>(y, y0, &dtab, tab.var);
     else q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
 
@@ -1614,11 +1626,13 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
   __shared__ DigitEntry dig[32];
   __shared__ B64Tables tab;
   __shared__ XlTable xl;
+  __shared__ D16Table dtab;
   {
     constexpr DigitEntry init[32] = FLEET_DIGIT_TABLE;
     if (threadIdx.x < 32) dig[threadIdx.x] = init[threadIdx.x];
     b64_tables_init(&tab);
     xl_table_init(&xl);
+    d16_table_init(&dtab);
     __syncthreads();
   }
   const VarEntry* var = tab.var;
@@ -1667,6 +1681,11 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
       case 17: { const float x = u2f(u);                              // one-lookup Q on |x| < 1e8 (as fn 6)
                use = q_gen_ok(x);
                o = use ? f2u(__builtin_fabsf(x) < 1e8f ? q_xl(x, xl.x) : q_lat(x)) : 0u; break; }
+      case 19: { const float x = u2f(u);                              // byte-table Q of k_update (as fn 6)
+               use = q_gen_ok(x);
+               uint32_t e = dtab.d16[u >> 19];
+               if (e == kD16Cmp) e = d16_fix(x, var);
+               o = use ? (e < kD16Out ? f2u(q_d16(x, e, &dtab.st)) : 0xdeadbeefu) : 0u; break; }
       case 18: { const float e = glibc_expf(u2f(u));                 // the teacher's expf (libm's)
                o = e != e ? 0x7fc00000u : f2u(e); break; }
       default: o = 0; use = false;

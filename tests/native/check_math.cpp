@@ -20,6 +20,7 @@ extern "C" {
 
 using namespace fleet;
 static std::atomic<long> g_bad{0};
+static const StepTables g_st = make_step_tables();
 
 template <typename F>
 void par_for(uint64_t begin, uint64_t end, uint64_t stride, F f) {
@@ -104,6 +105,11 @@ int main(int argc, char** argv) {
       }
       if (e != 16u * (uint32_t)fo_num_digits(fo_cvtt(x))) g_bad++;
       if (!same(q_d16(x, e, &st), fo_int2float(fo_float2int(x)))) g_bad++;
+    });
+    par_for(0, 1ull << 32, 1, [](uint64_t i) {  // int2float from the same tables, every code
+      const int32_t c = (int32_t)(uint32_t)i;
+      const uint32_t a = c < 0 ? 0u - (uint32_t)c : (uint32_t)c;
+      if (!same(dec_d16(c, last_digit_u(a) << 4, &g_st), fo_int2float(c))) g_bad++;
     });
     long cmp_slices = 0;
     for (uint32_t i = 0; i < 8192; ++i) cmp_slices += dt[i] == kD16Cmp;
@@ -247,8 +253,9 @@ int main(int argc, char** argv) {
     const uint32_t a = c < 0 ? 0u - (uint32_t)c : (uint32_t)c;
     if (last_digit_u(a) != a % 10u) g_bad++;
     if (!same(dec_mt_r(c, last_digit_u(a), mt), fo_int2float(c))) g_bad++;
+    if (!same(dec_d16(c, last_digit_u(a) << 4, &g_st), fo_int2float(c))) g_bad++;
   });
-  report("dec_mt/last_digit_u", b0);
+  report("dec_mt/dec_d16/last_digit_u", b0);
 
   b0 = g_bad;  // dec_gen (+ packed) vs int2float, every code
   par_for(0, 1ull << 32, s, [](uint64_t i) {
