@@ -471,6 +471,127 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
   }
 }
 
+// One lane's share of the fused update (the non-Kardam stream path): the values
+// [e0, e0 + S) of group g, S = 3 (the whole group) or S = 1 (one value; three
+// lanes of a wave share a group). Returns the lane's merged codes in out[S] and
+// its Base64 / layout error bits; tables already in LDS.
+template <int S>
+__device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table& dtab,
+                                            const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                            const double* __restrict__ dampen, double inv_avg, int64_t n_up,
+                                            int64_t g, int e0, bool live, int64_t g_safe,
+                                            const int32_t* __restrict__ hdr_block, int32_t (&out)[S],
+                                            uint32_t& bad, uint32_t& layout_bad) {
+  const int n_hdr = hdr_block[1];
+  const int64_t walk_end = hdr_block[2];
+  const int32_t* hdr = hdr_block + 4;
+  const uint8_t* rowp = uploads + 16 * (live ? g : g_safe);
+  const uint32_t need = needed_chars_mask((int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g)));
+  const uint32_t hbits = live ? (header_bits(hdr, n_hdr, 3 * g) >> e0) & ((1u << S) - 1u) : 0u;
+  const bool wave_hdr = __ballot(hbits != 0) != 0;
+  int32_t hfirst[S], codes[S];
+  float acc[S];
+  uint32_t dmax = 0;
+  uint4 nxt = *reinterpret_cast<const uint4*>(rowp);
+  for (int c = 0; c < M; ++c) {
+    const uint4 cur = nxt;
+    if (c + 1 < M) nxt = *reinterpret_cast<const uint4*>(rowp + (size_t)(c + 1) * pitch);
+    int32_t c3[3];
+    if (need == 0xffffu) bad |= b64_decode_group_full(cur, &tab, c3);
+    else bad |= b64_decode_group(cur, &tab, c3) & need;
+#pragma unroll
+    for (int i = 0; i < S; ++i) codes[i] = S == 3 ? c3[i] : c3[0] * (e0 == 0) + c3[1] * (e0 == 1) + c3[2] * (e0 == 2);
+    if (wave_hdr) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) {
+        if (c == 0) hfirst[i] = codes[i];
+        layout_bad |= (((hbits >> i) & 1u) & (uint32_t)(codes[i] != hfirst[i])) << i;
+      }
+    }
+    float y0[S], y[S], p[S];
+    dec_stage_d16<S>(y0, codes, &dtab);
+    q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
+    dampen_stage<S>(y, dampen[c]);
+    q_stage_d16<S>(p, y, &dtab, tab.var, dmax);
+    if (c == 0) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) acc[i] = p[i];
+    } else {
+      float sm[S];
+#pragma unroll
+      for (int i = 0; i < S; ++i) sm[i] = acc[i] + p[i];
+      q_stage_d16<S>(acc, sm, &dtab, tab.var, dmax);
+    }
+  }
+  if (__ballot(dmax >= kD16Out) != 0) {  // left the q_gen domain: recompute exactly (never for gradients)
+    if (dmax >= kD16Out && live) {
+#pragma unroll
+      for (int i = 0; i < S; ++i) acc[i] = chain_general(uploads, pitch, M, dampen, g, e0 + i, &tab);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    const int64_t pos = 3 * g + e0 + i;
+    const bool keep_last = ((hbits >> i) & 1u) || pos >= walk_end;
+    out[i] = (live && pos < n_up) ? merged_code(acc[i], inv_avg, codes[i], keep_last, &tab) : 0;
+  }
+}
+
+// The stream update with balanced SIMDs. The plain stream grid has
+// ceil(groups/64) waves, which leaves some SIMDs one wave more than others for
+// the whole kernel (synth1m_256: 5,462 waves on 1,024 SIMDs -> 5 or 6 each). Here
+// blocks [0, nA) run whole rounds of group-per-lane waves, and the remaining
+// groups go to blocks of one value per lane (21 groups = 63 lanes per wave):
+// three times the waves at a third of the work each, spread over every SIMD
+// instead of a sixth full wave on some. Bit-identical to k_update<1>.
+template <int NT>
+__global__ void __launch_bounds__(NT) k_update_mixed(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                     const double* __restrict__ dampen, double inv_avg,
+                                                     int64_t n_up, int64_t g_begin, int64_t g_end,
+                                                     const int32_t* __restrict__ hdr_block,
+                                                     uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                     int* __restrict__ err, int nA) {
+  __shared__ B64Tables tab;
+  __shared__ D16Table dtab;
+  b64_tables_init<NT>(&tab);
+  d16_table_init<NT>(&dtab);
+  __syncthreads();
+  uint32_t bad = 0, layout_bad = 0;
+  if ((int)blockIdx.x < nA) {  // block-uniform: one group per lane
+    const int64_t g = g_begin + (int64_t)blockIdx.x * NT + threadIdx.x;
+    const bool live = g < g_end;
+    int32_t out[3];
+    update_lane<3>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out, bad,
+                   layout_bad);
+    if (!live) return;
+    if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
+    if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+    const int r = (int)min<int64_t>(3, n_up - 3 * g);
+    *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &tab), r);
+    if (merged_f32)
+      for (int e = 0; e < r; ++e) merged_f32[3 * g + e] = dec_mt(out[e], tab.mt);
+  } else {  // one value per lane, 21 groups per wave
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t g = g_begin + (int64_t)nA * NT + ((int64_t)(blockIdx.x - nA) * (NT / 64) + wave) * 21 + lane / 3;
+    const int e = lane % 3;
+    const bool live = lane < 63 && g < g_end;
+    int32_t out[1];
+    update_lane<1>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, e, live, g_begin, hdr_block, out, bad,
+                   layout_bad);
+    const int base = lane - e;  // the group's three lanes (lane 63 reads its own)
+    const int32_t o0 = __shfl(out[0], base), o1 = __shfl(out[0], base + 1), o2 = __shfl(out[0], base + 2);
+    if (!live) return;
+    if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
+    if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+    const int r = (int)min<int64_t>(3, n_up - 3 * g);
+    if (e == 0) {
+      const int32_t o3[3] = {o0, r > 1 ? o1 : 0, r > 2 ? o2 : 0};
+      *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(o3, &tab), r);
+    }
+    if (merged_f32 && e < r) merged_f32[3 * g + e] = dec_mt(out[0], tab.mt);
+  }
+}
+
 // Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
 // of NW waves.
 template <int TG, int NW = 4>
@@ -1347,6 +1468,23 @@ hipError_t launch_descent(float* weights, float* fc_bias, const float* grad, con
 // ---------------------------------------------------------------- launchers
 
 static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+// k_update_mixed's split: the blocks of whole rounds of one-group-per-lane waves
+// (a multiple of one wave per SIMD of the current device), or -1 when the grid is
+// under one round (the plain stream grid then).
+static int stream_full_rounds_blocks(int64_t groups) {
+  static int simds = 0;
+  if (!simds) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    simds = 4 * cus;
+  }
+  const int64_t waves = (groups + 63) / 64;
+  if (waves < simds) return -1;
+  const int64_t full = waves / simds * simds;  // waves in whole rounds
+  return (int)(full * 64 / 256);
+}
 
 // groups per lane of the stream kernel: 1 at every size measured -- 1M floats
 // x 256: 1.64 / 1.85 / 2.63 ms for K = 1 / 2 / 4 (before the multiplier-table
@@ -1401,7 +1539,11 @@ static UpdatePlan plan_update(int64_t groups) {
 const char* update_kernel_name(int64_t groups) {
   static thread_local char buf[48];
   const UpdatePlan p = plan_update(groups);
-  if (p.kind == 0)
+  const char* mx = getenv("FLEET_UPDATE_MIXED");
+  if (p.kind == 0 && p.k == 1 && !getenv("FLEET_UPDATE_NT") && !(mx && atoi(mx) == 0) &&
+      stream_full_rounds_blocks(groups) >= 0)
+    snprintf(buf, sizeof buf, "k_update_mixed<256>");
+  else if (p.kind == 0)
     snprintf(buf, sizeof buf, "k_update<%d, false, 256>", p.k);  // as rocprofv3 names it
   else if (p.kind == 2)
     snprintf(buf, sizeof buf, "k_update_pipe<%d, %d, %d, %d>", p.tg, p.ipt, p.nw, p.wp);
@@ -1460,10 +1602,19 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
 #define FLEET_LAUNCH_NT(N)                                                                                      \
   hipLaunchKernelGGL((k_update<1, false, N>), dim3((unsigned)((groups + (N)-1) / (N))), dim3(N), 0, s, uploads, \
                      pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
-      if (v == 64) FLEET_LAUNCH_NT(64);
-      else if (v == 128) FLEET_LAUNCH_NT(128);
-      else if (v == 512) FLEET_LAUNCH_NT(512);
-      else FLEET_LAUNCH_NT(256);
+      const char* mx = getenv("FLEET_UPDATE_MIXED");  // experiments: 0 = the plain stream grid
+      const int nA = stream_full_rounds_blocks(groups);
+      if (nt || (mx && atoi(mx) == 0) || nA < 0) {
+        if (v == 64) FLEET_LAUNCH_NT(64);
+        else if (v == 128) FLEET_LAUNCH_NT(128);
+        else if (v == 512) FLEET_LAUNCH_NT(512);
+        else FLEET_LAUNCH_NT(256);
+      } else {
+        const int64_t rem = groups - (int64_t)nA * 256;
+        const int64_t nB = (rem + 83) / 84;
+        hipLaunchKernelGGL((k_update_mixed<256>), dim3((unsigned)(nA + nB)), dim3(256), 0, s, uploads, pitch, M,
+                           d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, nA);
+      }
 #undef FLEET_LAUNCH_NT
     }
   }

@@ -603,3 +603,35 @@ def test_model_version_matches_reference_fixture(codec):
     w, b = codec.model_version(f["w"], dims, f["b"])
     assert np.array_equal(w.view(np.uint32), f["w_out"].view(np.uint32))
     assert np.array_equal(b.view(np.uint32), f["b_out"].view(np.uint32))
+
+
+@pytest.mark.parametrize("mixed", ["1", "0"])
+def test_stream_update_mixed_grid(codec, oracle, monkeypatch, mixed):
+    """The stream kernel's SIMD-balanced grid (k_update_mixed: whole rounds of
+    group-per-lane waves, the remaining groups one value per lane) against the
+    oracle and against the plain grid: a ragged size whose remainder groups and
+    last partial group fall in the value-per-lane blocks, with values outside the
+    q_gen domain (1e9, -1e8, inf, NaN, 3e38) and power-of-ten boundaries
+    planted in both parts, under the two dampening kinds (binary32-exact and not)."""
+    monkeypatch.setenv("FLEET_UPDATE_MODE", "stream")
+    monkeypatch.setenv("FLEET_UPDATE_MIXED", mixed)
+    lay = synthetic(3 * 70000 + 2)  # 70,001 groups: one round of 65,536 + 4,465 in value-per-lane blocks
+    M = 4
+    n = lay.n_up
+    hpos = set(lay.header_positions())
+    rng = np.random.default_rng(5)
+    special = np.array([1e9, -1e8, np.inf, -np.inf, np.nan, 3e38, 1e8, 9.999999e7, 10.0, -10.0, 1e-45], np.float32)
+    ups = []
+    for c in range(M):
+        v = oracle.synth_upload(70 + c, c, list(lay.w_sizes), list(lay.b_sizes)).copy()
+        for region in ((0, 3 * 65536), (3 * 65536, n)):
+            pos = [p for p in rng.integers(region[0], region[1], 40) if p not in hpos]
+            v[pos] = rng.choice(special, len(pos))
+        ups.append(oracle.encode_floats(v))
+    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+    for pol in ("inverse", "exp"):
+        d = policy(pol, M)
+        got, f32 = codec.update(ups, d, want_f32=True)
+        exp = oracle.update_fused(ups, d, hm)
+        assert got == exp, pol
+        assert np.array_equal(f32.view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
