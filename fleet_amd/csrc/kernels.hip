@@ -492,10 +492,8 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   int32_t hfirst[S], codes[S];
   float acc[S];
   uint32_t dmax = 0;
-  uint4 nxt = *reinterpret_cast<const uint4*>(rowp);
-  for (int c = 0; c < M; ++c) {
-    const uint4 cur = nxt;
-    if (c + 1 < M) nxt = *reinterpret_cast<const uint4*>(rowp + (size_t)(c + 1) * pitch);
+  // one client's step on its group `cur`
+  auto client = [&](int c, const uint4& cur) {
     int32_t c3[3];
     if (need == 0xffffu) bad |= b64_decode_group_full(cur, &tab, c3);
     else bad |= b64_decode_group(cur, &tab, c3) & need;
@@ -522,7 +520,19 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       for (int i = 0; i < S; ++i) sm[i] = acc[i] + p[i];
       q_stage_d16<S>(acc, sm, &dtab, tab.var, dmax);
     }
+  };
+  auto group_of = [&](int c) { return *reinterpret_cast<const uint4*>(rowp + (size_t)c * pitch); };
+  // two clients per trip, the next client's group always in flight, in alternating
+  // registers (no copies between trips)
+  uint4 b0 = group_of(0), b1;
+  int c = 0;
+  for (; c + 1 < M; c += 2) {
+    b1 = group_of(c + 1);
+    client(c, b0);
+    if (c + 2 < M) b0 = group_of(c + 2);
+    client(c + 1, b1);
   }
+  if (c < M) client(c, b0);
   if (__ballot(dmax >= kD16Out) != 0) {  // left the q_gen domain: recompute exactly (never for gradients)
     if (dmax >= kD16Out && live) {
 #pragma unroll
