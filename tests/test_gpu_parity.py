@@ -635,3 +635,32 @@ def test_stream_update_mixed_grid(codec, oracle, monkeypatch, mixed):
         exp = oracle.update_fused(ups, d, hm)
         assert got == exp, pol
         assert np.array_equal(f32.view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
+
+
+def test_window_update_on_mixed_grid(codec, oracle, monkeypatch):
+    """Element windows (the N-GPU shards of fleet_update_multi / torch.distributed)
+    through the SIMD-balanced stream grid: each window's merged slice equals the
+    same bytes of the whole update."""
+    torch = pytest.importorskip("torch")
+    from fleet_amd.shard import byte_range, group_range
+    monkeypatch.setenv("FLEET_UPDATE_MODE", "stream")
+    lay = synthetic(3 * 150001 + 1)
+    M = 3
+    ups = uploads_for(oracle, lay, M, seed=41)
+    L = len(ups[0])
+    d = policy("exp", M)
+    hp = lay.header_positions()
+    groups = (F.b64_count(L) + 2) // 3
+    whole = codec.update(ups, d)
+    for world in (1, 2, 3):
+        for r in range(world):
+            gb, ge = group_range(groups, world, r)
+            b_0, b_1 = byte_range(L, gb, ge)
+            win = np.zeros((M, 16 * (ge - gb)), np.uint8)
+            for c, u in enumerate(ups):
+                win[c, : b_1 - b_0] = np.frombuffer(u, np.uint8)[b_0:b_1]
+            out = torch.zeros(16 * (ge - gb), dtype=torch.uint8, device="cuda")
+            codec.update_device(torch.from_numpy(win).cuda(), L, d, hp, out, None, gb, ge, window=True)
+            torch.cuda.synchronize()
+            codec.check()
+            assert out.cpu().numpy()[: b_1 - b_0].tobytes() == whole[b_0:b_1], (world, r)
