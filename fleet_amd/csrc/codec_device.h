@@ -165,6 +165,47 @@ __device__ __forceinline__ uint32_t b64_decode_group_full(uint4 w, const B64Tabl
   return anyf & 0x40u;
 }
 
+// One code of a group from the two 4-char quads that hold its bytes: value e of
+// the group is bytes 4e..4e+3, i.e. quads e and e+1 (w0, w1 = chars 4e..4e+7);
+// `sel` = b64_pair_selector(e). For lanes that own one value of a group.
+__device__ __forceinline__ uint32_t b64_pair_selector(int e) {
+  return e == 0 ? 0x06000102u : e == 1 ? 0x05060001u : 0x04050600u;  // the perms of b64_decode_group
+}
+// all 8 chars carry data: nonzero if any is outside the alphabet
+__device__ __forceinline__ uint32_t b64_decode_pair_full(uint32_t w0, uint32_t w1, uint32_t sel, const B64Tables* t,
+                                                         int32_t& code) {
+  const uint32_t words[2] = {w0, w1};
+  uint32_t V[2], anyf = 0;
+#pragma unroll
+  for (int qd = 0; qd < 2; ++qd) {
+    const uint32_t s0 = t->fromf[words[qd] & 0xff];
+    const uint32_t s1 = t->fromf[(words[qd] >> 8) & 0xff];
+    const uint32_t s2 = t->fromf[(words[qd] >> 16) & 0xff];
+    const uint32_t s3 = t->fromf[words[qd] >> 24];
+    anyf |= s0 | s1 | s2 | s3;
+    V[qd] = (((((s0 << 6) | s1) << 6) | s2) << 6) | s3;
+  }
+  code = (int32_t)__builtin_amdgcn_perm(V[1], V[0], sel);
+  return anyf & 0x40u;
+}
+// per-char mask of chars outside the alphabet (bit i = char 4e + i)
+__device__ __forceinline__ uint32_t b64_decode_pair(uint32_t w0, uint32_t w1, uint32_t sel, const B64Tables* t,
+                                                    int32_t& code) {
+  const uint32_t words[2] = {w0, w1};
+  uint32_t V[2], bad = 0;
+#pragma unroll
+  for (int qd = 0; qd < 2; ++qd) {
+    const uint32_t s0 = t->from[words[qd] & 0xff];
+    const uint32_t s1 = t->from[(words[qd] >> 8) & 0xff];
+    const uint32_t s2 = t->from[(words[qd] >> 16) & 0xff];
+    const uint32_t s3 = t->from[words[qd] >> 24];
+    bad |= ((s0 >> 7) | ((s1 >> 7) << 1) | ((s2 >> 7) << 2) | ((s3 >> 7) << 3)) << (4 * qd);
+    V[qd] = ((s0 & 63) << 18) | ((s1 & 63) << 12) | ((s2 & 63) << 6) | (s3 & 63);
+  }
+  code = (int32_t)__builtin_amdgcn_perm(V[1], V[0], sel);
+  return bad;
+}
+
 // 3 codes -> 12 bytes -> 16 chars (Base64.cpp:176-195).
 __device__ __forceinline__ uint4 b64_encode_group(const int32_t codes[3], const B64Tables* t) {
   const uint32_t c0 = (uint32_t)codes[0], c1 = (uint32_t)codes[1], c2 = (uint32_t)codes[2];

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "codec_device.h"
 #include "teacher_math.h"
@@ -203,14 +204,23 @@ __device__ __forceinline__ void q_stage_d16x(float (&out)[S], const float (&x)[S
 // scalarMultiply(getDampen) (cppNN_backend.cpp:753-777): (float)((double)y * d).
 // When d is a binary32 value (1, 1/2, ... -- staleness 0 gives 1 under every
 // getDampen policy) the double product of two binary32 values is exact and one
-// binary32 multiply rounds it identically; d is uniform, so the branch is too.
+// binary32 multiply rounds it identically. d is uniform (one client per step of
+// every lane), and the test and the binary32 bits are integer work on its two
+// words -- scalar instructions, no VALU; the volatile asm keeps the f64 side a
+// branch (the compiler would otherwise compute both sides and select).
 template <int S>
 __device__ __forceinline__ void dampen_stage(float (&r)[S], double d) {
-  const float df = (float)d;
-  if (__builtin_amdgcn_readfirstlane((double)df == d ? 1 : 0)) {  // uniform: a scalar branch
+  const uint64_t b = __builtin_bit_cast(uint64_t, d);
+  const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+  const uint32_t ex = (hi >> 20) & 0x7ffu;
+  // a binary32 normal value: f64 biased exponent 897..1150, no mantissa bits below
+  // binary32's (+-0 and the rest take the f64 side, exact for every d)
+  if ((lo & 0x1fffffffu) == 0 && ex - 897u < 254u) {
+    const float df = u2f((hi & 0x80000000u) | ((ex - 896u) << 23) | ((hi & 0xfffffu) << 3) | (lo >> 29));
 #pragma unroll
     for (int i = 0; i < S; ++i) r[i] = r[i] * df;
   } else {
+    asm volatile("");
 #pragma unroll
     for (int i = 0; i < S; ++i) r[i] = (float)((double)r[i] * d);
   }
@@ -493,12 +503,18 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   float acc[S];
   uint32_t dmax = 0;
   // one client's step on its group `cur`
-  auto client = [&](int c, const uint4& cur) {
-    int32_t c3[3];
-    if (need == 0xffffu) bad |= b64_decode_group_full(cur, &tab, c3);
-    else bad |= b64_decode_group(cur, &tab, c3) & need;
-#pragma unroll
-    for (int i = 0; i < S; ++i) codes[i] = S == 3 ? c3[i] : c3[0] * (e0 == 0) + c3[1] * (e0 == 1) + c3[2] * (e0 == 2);
+  // S = 1: the lane reads and decodes only the two quads that hold its value's
+  // bytes (chars 4e..4e+7); the group's three lanes together cover all 16 chars
+  const uint32_t sel = b64_pair_selector(e0), need_pair = (need >> (4 * e0)) & 0xffu;
+  using Row = typename std::conditional<S == 3, uint4, uint2>::type;
+  auto client = [&](int c, const Row& cur) {
+    if constexpr (S == 3) {
+      if (need == 0xffffu) bad |= b64_decode_group_full(cur, &tab, codes);
+      else bad |= b64_decode_group(cur, &tab, codes) & need;
+    } else {
+      if (need == 0xffffu) bad |= b64_decode_pair_full(cur.x, cur.y, sel, &tab, codes[0]);
+      else bad |= b64_decode_pair(cur.x, cur.y, sel, &tab, codes[0]) & need_pair;
+    }
     if (wave_hdr) {
 #pragma unroll
       for (int i = 0; i < S; ++i) {
@@ -521,10 +537,17 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       q_stage_d16<S>(acc, sm, &dtab, tab.var, dmax);
     }
   };
-  auto group_of = [&](int c) { return *reinterpret_cast<const uint4*>(rowp + (size_t)c * pitch); };
+  auto group_of = [&](int c) {
+    if constexpr (S == 3) {
+      return *reinterpret_cast<const uint4*>(rowp + (size_t)c * pitch);
+    } else {  // two dwords at 4e (4-byte aligned only)
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(rowp + (size_t)c * pitch + 4 * e0);
+      return make_uint2(w[0], w[1]);
+    }
+  };
   // two clients per trip, the next client's group always in flight, in alternating
   // registers (no copies between trips)
-  uint4 b0 = group_of(0), b1;
+  Row b0 = group_of(0), b1;
   int c = 0;
   for (; c + 1 < M; c += 2) {
     b1 = group_of(c + 1);
@@ -1495,6 +1518,15 @@ static int stream_full_rounds_blocks(int64_t groups) {
   const int64_t full = waves / simds * simds;  // waves in whole rounds
   return (int)(full * 64 / 256);
 }
+// the split in use: FLEET_UPDATE_MIXED=0 the plain stream grid (-1), =2 every group
+// one value per lane (0; experiments)
+static int mixed_split(int64_t groups) {
+  if (const char* mx = getenv("FLEET_UPDATE_MIXED")) {
+    if (atoi(mx) == 0) return -1;
+    if (atoi(mx) == 2) return 0;
+  }
+  return stream_full_rounds_blocks(groups);
+}
 
 // groups per lane of the stream kernel: 1 at every size measured -- 1M floats
 // x 256: 1.64 / 1.85 / 2.63 ms for K = 1 / 2 / 4 (before the multiplier-table
@@ -1549,9 +1581,7 @@ static UpdatePlan plan_update(int64_t groups) {
 const char* update_kernel_name(int64_t groups) {
   static thread_local char buf[48];
   const UpdatePlan p = plan_update(groups);
-  const char* mx = getenv("FLEET_UPDATE_MIXED");
-  if (p.kind == 0 && p.k == 1 && !getenv("FLEET_UPDATE_NT") && !(mx && atoi(mx) == 0) &&
-      stream_full_rounds_blocks(groups) >= 0)
+  if (p.kind == 0 && p.k == 1 && !getenv("FLEET_UPDATE_NT") && mixed_split(groups) >= 0)
     snprintf(buf, sizeof buf, "k_update_mixed<256>");
   else if (p.kind == 0)
     snprintf(buf, sizeof buf, "k_update<%d, false, 256>", p.k);  // as rocprofv3 names it
@@ -1612,9 +1642,8 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
 #define FLEET_LAUNCH_NT(N)                                                                                      \
   hipLaunchKernelGGL((k_update<1, false, N>), dim3((unsigned)((groups + (N)-1) / (N))), dim3(N), 0, s, uploads, \
                      pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
-      const char* mx = getenv("FLEET_UPDATE_MIXED");  // experiments: 0 = the plain stream grid
-      const int nA = stream_full_rounds_blocks(groups);
-      if (nt || (mx && atoi(mx) == 0) || nA < 0) {
+      const int nA = mixed_split(groups);
+      if (nt || nA < 0) {
         if (v == 64) FLEET_LAUNCH_NT(64);
         else if (v == 128) FLEET_LAUNCH_NT(128);
         else if (v == 512) FLEET_LAUNCH_NT(512);

@@ -605,7 +605,7 @@ def test_model_version_matches_reference_fixture(codec):
     assert np.array_equal(b.view(np.uint32), f["b_out"].view(np.uint32))
 
 
-@pytest.mark.parametrize("mixed", ["1", "0"])
+@pytest.mark.parametrize("mixed", ["1", "0", "2"])
 def test_stream_update_mixed_grid(codec, oracle, monkeypatch, mixed):
     """The stream kernel's SIMD-balanced grid (k_update_mixed: whole rounds of
     group-per-lane waves, the remaining groups one value per lane) against the
@@ -635,6 +635,55 @@ def test_stream_update_mixed_grid(codec, oracle, monkeypatch, mixed):
         exp = oracle.update_fused(ups, d, hm)
         assert got == exp, pol
         assert np.array_equal(f32.view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
+
+
+@pytest.mark.parametrize("mixed", ["1", "0"])
+def test_stream_update_dampen_kinds(codec, oracle, monkeypatch, mixed):
+    """The stream kernels' dampen step takes one binary32 multiply when d is a
+    binary32 normal value (tested on d's bits with scalar instructions) and the
+    reference's f64 product otherwise: both kinds and their edges (+-0, binary32
+    subnormal and extreme binary32 values, values just off binary32, products
+    that overflow) against the oracle, in both parts of the balanced grid."""
+    monkeypatch.setenv("FLEET_UPDATE_MODE", "stream")
+    monkeypatch.setenv("FLEET_UPDATE_MIXED", mixed)
+    f32 = lambda x: float(np.float32(x))  # noqa: E731
+    d = [1.0, 0.0, -0.0, -0.5, 2.0 ** -126, 2.0 ** -149, 2.0 ** 127, f32(3.4028235e38), 1 / 3, 1e-300, 0.1,
+         f32(0.1), 3.0, -7.25, f32(0.1) * (1 + 2.0 ** -40), 2.0 ** -127]
+    lay = synthetic(3 * 70000 + 2)
+    ups = uploads_for(oracle, lay, len(d), seed=61)
+    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
+
+
+def test_value_per_lane_decode_checks_every_char(codec, oracle, monkeypatch):
+    """Lanes that own one value of a group decode only the two quads holding its
+    bytes (FLEET_UPDATE_MIXED=2: every group one value per lane): a char outside
+    the alphabet at any of a full group's 16 positions, or at a needed position
+    of the last partial group, is still reported; the partial group's '='
+    padding is not."""
+    monkeypatch.setenv("FLEET_UPDATE_MODE", "stream")
+    monkeypatch.setenv("FLEET_UPDATE_MIXED", "2")
+    lay = synthetic(3 * 200 + 2)
+    M = 3
+    ups = uploads_for(oracle, lay, M, seed=23)
+    d = policy("inverse", M)
+    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
+    hpos = set(lay.header_positions())
+    g = next(g for g in range(100, 200) if not {3 * g, 3 * g + 1, 3 * g + 2} & hpos)
+    for ch in range(16):
+        bad = bytearray(ups[1])
+        bad[16 * g + ch] = ord("*")
+        with pytest.raises(F.Base64Error):
+            codec.update([ups[0], bytes(bad), ups[2]], d)
+    last = 16 * (len(ups[0]) // 16 - 1) if len(ups[0]) % 16 == 0 else 16 * (len(ups[0]) // 16)
+    assert ups[0][last + 11:last + 12] == b"=" and len(ups[0]) - last in (12, 16)
+    for ch in (0, 5, 6, 10):
+        bad = bytearray(ups[2])
+        bad[last + ch] = ord("*")
+        with pytest.raises(F.Base64Error):
+            codec.update([ups[0], ups[1], bytes(bad)], d)
+    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
 def test_window_update_on_mixed_grid(codec, oracle, monkeypatch):
