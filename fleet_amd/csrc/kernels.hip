@@ -726,9 +726,19 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileI
   float r[S], p[S];
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
-    const double d = dampen[it.c_base + it.cc[h]];
+    if constexpr (TG % 64 == 0) {
+      // a wave's 64 items are 64 groups of one client (items are client-major and
+      // every wave starts at a multiple of 64): d is wave-uniform, so the scalar
+      // test of dampen_stage applies (a dead lane 0 means a dead wave)
+      float t[3] = {y[3 * h], y[3 * h + 1], y[3 * h + 2]};
+      dampen_stage<3>(t, dampen[__builtin_amdgcn_readfirstlane(it.c_base + it.cc[h])]);
 #pragma unroll
-    for (int e = 0; e < 3; ++e) r[3 * h + e] = (float)((double)y[3 * h + e] * d);
+      for (int e = 0; e < 3; ++e) r[3 * h + e] = t[e];
+    } else {
+      const double d = dampen[it.c_base + it.cc[h]];
+#pragma unroll
+      for (int e = 0; e < 3; ++e) r[3 * h + e] = (float)((double)y[3 * h + e] * d);
+    }
   }
   q_stage<S>(p, r, &sh.tab);
 #pragma unroll

@@ -637,15 +637,17 @@ def test_stream_update_mixed_grid(codec, oracle, monkeypatch, mixed):
         assert np.array_equal(f32.view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
 
 
-@pytest.mark.parametrize("mixed", ["1", "0"])
-def test_stream_update_dampen_kinds(codec, oracle, monkeypatch, mixed):
-    """The stream kernels' dampen step takes one binary32 multiply when d is a
-    binary32 normal value (tested on d's bits with scalar instructions) and the
-    reference's f64 product otherwise: both kinds and their edges (+-0, binary32
-    subnormal and extreme binary32 values, values just off binary32, products
-    that overflow) against the oracle, in both parts of the balanced grid."""
-    monkeypatch.setenv("FLEET_UPDATE_MODE", "stream")
+@pytest.mark.parametrize("mode,mixed", [("stream", "1"), ("stream", "0"), ("tiled", "1")])
+def test_update_dampen_kinds(codec, oracle, monkeypatch, mode, mixed):
+    """The dampen step takes one binary32 multiply when d is a binary32 normal
+    value (tested on d's bits with scalar instructions where d is wave-uniform:
+    the stream kernels, 64-group tiles) and the reference's f64 product
+    otherwise: both kinds and their edges (+-0, binary32 subnormal and extreme
+    binary32 values, values just off binary32, products that overflow) against
+    the oracle, in both parts of the balanced grid and in the tiled kernel."""
+    monkeypatch.setenv("FLEET_UPDATE_MODE", mode)
     monkeypatch.setenv("FLEET_UPDATE_MIXED", mixed)
+    monkeypatch.setenv("FLEET_TILE_G", "64")
     f32 = lambda x: float(np.float32(x))  # noqa: E731
     d = [1.0, 0.0, -0.0, -0.5, 2.0 ** -126, 2.0 ** -149, 2.0 ** 127, f32(3.4028235e38), 1 / 3, 1e-300, 0.1,
          f32(0.1), 3.0, -7.25, f32(0.1) * (1 + 2.0 ** -40), 2.0 ** -127]
