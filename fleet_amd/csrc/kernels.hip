@@ -345,6 +345,17 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
   const bool wave_hdr = __ballot(hbits != 0) != 0;
   int32_t hfirst[S];
   uint32_t layout_bad = 0;
+  // Kardam: value slots of the flat gradient (neither header slots nor past the walk)
+  uint32_t flatbits = 0;
+  if constexpr (KD) {
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        const int64_t pos = 3 * g[k] + e;
+        if (live[k] && pos < n_up && pos < walk_end && !((hbits >> (3 * k + e)) & 1u)) flatbits |= 1u << (3 * k + e);
+      }
+  }
 #pragma unroll
   for (int i = 0; i < S; ++i) acc[i] = 0.f;
 #pragma unroll
@@ -404,24 +415,35 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
       // g.subtract(prev).getNorm() (getNorm: float products summed in double)
       float rg[S], G[S];
 #pragma unroll
-      for (int i = 0; i < S; ++i) rg[i] = (float)((double)p[i] * kd.lr);
+      for (int i = 0; i < S; ++i) rg[i] = p[i];
+      dampen_stage<S>(rg, kd.lr);  // (float)((double)p * lr); lr is uniform
       q_stage_d16x<S>(G, rg, &dtab, tab.var);
-      const bool hp = kd.prev && kd.has_prev[c];
       double sg = 0.0, sd = 0.0;
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
+      for (int i = 0; i < S; ++i)
+        if ((flatbits >> i) & 1u) sg += (double)(G[i] * G[i]);
+      if (kd.prev && kd.has_prev[c]) {  // uniform
+        float dv[S], D[S];
 #pragma unroll
-        for (int e = 0; e < 3; ++e) {
-          const int64_t pos = 3 * g[k] + e;
-          const bool flat = live[k] && pos < n_up && pos < walk_end && !((hbits >> (3 * k + e)) & 1u);
-          const float Gv = G[3 * k + e];
-          if (flat) sg += (double)(Gv * Gv);
-          if (hp && flat) {
-            const float Dv = q(Gv - kd.prev[(size_t)c * kd.vpitch + pos]);
-            sd += (double)(Dv * Dv);
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+          for (int e = 0; e < 3; ++e) {
+            const int i = 3 * k + e;
+            dv[i] = ((flatbits >> i) & 1u) ? G[i] - kd.prev[(size_t)c * kd.vpitch + 3 * g[k] + e] : 0.0f;
           }
-          if (kd.g_out && live[k] && pos < n_up) kd.g_out[(size_t)c * kd.vpitch + pos] = flat ? Gv : 0.0f;
-        }
+        q_stage_d16x<S>(D, dv, &dtab, tab.var);
+#pragma unroll
+        for (int i = 0; i < S; ++i)
+          if ((flatbits >> i) & 1u) sd += (double)(D[i] * D[i]);
+      }
+      if (kd.g_out) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+          for (int e = 0; e < 3; ++e) {
+            const int64_t pos = 3 * g[k] + e;
+            if (live[k] && pos < n_up) kd.g_out[(size_t)c * kd.vpitch + pos] = ((flatbits >> (3 * k + e)) & 1u) ? G[3 * k + e] : 0.0f;
+          }
       }
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
