@@ -200,7 +200,56 @@ def all_gather_fn(torch, dist, world, src, out):
     return f
 
 
-def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=True):
+def time_pipelined(torch, dist, codec, sh, steps, warmup, world):
+    """The same steps software-pipelined over two upload buffers: step i
+    aggregates batch i (buffer i % 2) and encodes batch i+1 into the other buffer
+    in one launch (fleet_update_encode_device; k_update_encode = the stream
+    update's blocks + the client encode's blocks). Per step: one aggregation and
+    one client encode, as in the sequential step; batch 0 is encoded before the
+    clock starts. Graph-replayed like the sequential step (an even number of
+    steps per graph, so every replay starts on buffer 0)."""
+    import fleet_amd as F
+    if not sh.n_local or sh.strong:
+        return None
+    bufs = [sh.text, torch.zeros_like(sh.text)]
+    state = {"i": 0}
+
+    def step():
+        a, b = bufs[state["i"] % 2], bufs[(state["i"] + 1) % 2]
+        state["i"] += 1
+        codec.update_encode_device(a, sh.L, sh.dampen, sh.hpos_global, sh.merged, sh.merged_f32, sh.values, b)
+
+    sh.encode()
+    for _ in range(max(2, warmup)):
+        step()
+    torch.cuda.synchronize()
+    codec.check()
+    # an even number of steps per graph (every replay starts on buffer 0); an odd
+    # step count ends with a one-step graph (buffer 0 -> 1)
+    E = steps - steps % 2
+    G = max(d for d in range(2, min(10, E) + 1, 2) if E % d == 0) if E else 0
+    state["i"] = 0
+    g = graph_of(torch, step, G) if G else None
+    state["i"] = 0
+    g1 = graph_of(torch, step, 1) if steps % 2 else None
+    if g:
+        g.replay()
+    if g1:
+        g1.replay()
+    seq = ([g.replay] * (E // G) if G else []) + ([g1.replay] if g1 else [])
+    it = iter(seq)
+    elapsed = run_timed(torch, dist, world, lambda: next(it)(), len(seq))
+    codec.check()
+    del g, g1
+    fused_ms = kernel_ms(torch, lambda: (step(), step()), reps=5) / 2  # a buffer-0/1 pair per graph entry
+    codec.check()
+    del bufs[1]
+    return {"ms_per_step": elapsed / steps * 1e3,
+            "gib_s": world * sh.M * sh.n_local * 4 / (elapsed / steps) / 2**30,
+            "steps_per_graph": G, "kernel": F.update_encode_kernel(sh.L), "kernel_ms": fused_ms}
+
+
+def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=True, pipelined_step=True):
     """Weak-scaling measurement of `name`: times `steps` steps. graph=True: a
     step (encode + aggregation) is captured once into a HIP graph of G steps
     and replayed steps/G times; graph=False: eager launches. N>1: the
@@ -241,6 +290,7 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
         elapsed = run_timed(torch, dist, world, g.replay, steps // G)
         codec.check()
         del g
+    pipelined = time_pipelined(torch, dist, codec, sh, steps, warmup, world) if (graph and pipelined_step) else None
     exchange_ms = None
     if world > 1:
         exchange = all_gather_fn(torch, dist, world, sh.merged, gathered)
@@ -260,6 +310,7 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
         "update_bytes": upd_b, "encode_bytes": enc_b,
         "update_gbs": upd_b / (upd_ms * 1e-3) / 1e9, "encode_gbs": enc_b / (enc_ms * 1e-3) / 1e9,
         "element_clients_per_s": world * M * sh.n_local / (elapsed / steps),
+        "pipelined": pipelined,
     }
     del sh
     torch.cuda.empty_cache()
@@ -576,6 +627,8 @@ def main():
     ap.add_argument("--strong", action="store_true",
                     help="value = strong scaling of configs[4] (one fixed problem split over the ranks, "
                          "all_gather of the merged slices inside every step)")
+    ap.add_argument("--sequential", action="store_true",
+                    help="value = the sequential step (encode, then aggregate) instead of the pipelined one")
     ap.add_argument("--no-strong-block", action="store_true", help="skip the strong-scaling block")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=1,
@@ -618,7 +671,7 @@ def main():
     extras = {}
     if world == 1 and args.extras:
         for w in [x for x in args.extras.split(",") if x and x != args.workload]:
-            extras[w] = time_workload(torch, dist, codec, w, max(3, args.steps // 4), 2, rank, world, args.graph)
+            extras[w] = time_workload(torch, dist, codec, w, max(4, args.steps // 8 * 2), 2, rank, world, args.graph)
 
     strong = None
     if args.strong or not args.no_strong_block:
@@ -636,13 +689,41 @@ def main():
     if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(args.workload, args.cpu_budget)
     r = main_res
-    achieved = r["update_gbs"]
+    upd_roof = {"kernel": r["update_kernel"], "achieved": r["update_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": r["update_gbs"] / HBM_PEAK_GBS, "frac_of_copy_ceiling": r["update_gbs"] / HBM_COPY_GBS,
+                "limiter": LIMITER.get(r["update_kernel"].split("<")[0], "VALU issue"),
+                "bytes_per_launch": r["update_bytes"], "kernel_ms": r["update_kernel_ms"]}
     traffic = pmc_traffic(args.workload, r["update_kernel"]) if world == 1 else None
     sq = sq_valu(args.workload, r["update_kernel"])
+    upd_roof.update({"valu_lane_instr_per_element_client": sq[0] if sq else None, "valu_source": sq[1] if sq else None,
+                     "traffic": traffic[0] if traffic else None,
+                     "traffic_source": f"{traffic[2]} ({traffic[1]})" if traffic else None})
+    pipe = r.get("pipelined") if isinstance(r.get("pipelined"), dict) and "gib_s" in r["pipelined"] else None
     value, ms, scaling = r["gib_s"], r["ms_per_step"], "weak"
+    step_form = "sequential: k_encode_f32 then the aggregation kernel, per step"
+    roofline = dict(upd_roof, bound="hbm", workload=args.workload)
+    if pipe and not args.sequential:
+        value, ms = pipe["gib_s"], pipe["ms_per_step"]
+        step_form = ("pipelined: step i aggregates batch i and encodes batch i+1 into the other upload buffer, "
+                     f"one {pipe['kernel']} launch (fleet_update_encode_device); batch 0 encoded before the clock")
+        if pipe["kernel"].startswith("k_update_encode"):
+            fb = r["update_bytes"] + r["encode_bytes"]
+            fgbs = fb / (pipe["kernel_ms"] * 1e-3) / 1e9
+            ftr = pmc_traffic(args.workload, pipe["kernel"]) if world == 1 else None
+            fsq = sq_valu(args.workload, pipe["kernel"])
+            roofline = {"bound": "hbm", "kernel": pipe["kernel"], "achieved": fgbs, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": fgbs / HBM_PEAK_GBS, "frac_of_copy_ceiling": fgbs / HBM_COPY_GBS,
+                        "limiter": "VALU issue (the aggregation's exact chain; the encode fills HBM time)",
+                        "bytes_per_launch": fb, "bytes_update": r["update_bytes"], "bytes_encode": r["encode_bytes"],
+                        "kernel_ms": pipe["kernel_ms"],
+                        "valu_lane_instr_per_element_client": fsq[0] if fsq else None,
+                        "valu_source": fsq[1] if fsq else None,
+                        "traffic": ftr[0] if ftr else None,
+                        "traffic_source": f"{ftr[2]} ({ftr[1]})" if ftr else None,
+                        "workload": args.workload, "aggregation_alone": upd_roof}
     config = {"workload": args.workload, "layout": r["layout"], "clients": r["clients"],
               "n_up_per_rank": r["n_up_per_rank"], "parallelism": f"element-shard x{world}",
-              "dampening": "policy 1 inverse, tau = c mod 3"}
+              "dampening": "policy 1 inverse, tau = c mod 3", "step": step_form}
     if args.strong:
         sd = strong["device"]
         value, ms, scaling = sd["gather_inside"]["gib_s"], sd["gather_inside"]["ms_per_step"], "strong"
@@ -663,16 +744,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic (Philox4x32-10 value mix, SURVEY.md §8d), device-resident",
         "config": config,
-        "roofline": {"bound": "hbm", "kernel": r["update_kernel"], "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                     "frac_of_copy_ceiling": achieved / HBM_COPY_GBS,
-                     "limiter": LIMITER.get(r["update_kernel"].split("<")[0], "VALU issue"),
-                     "valu_lane_instr_per_element_client": sq[0] if sq else None,
-                     "valu_source": sq[1] if sq else None,
-                     "traffic": traffic[0] if traffic else None,
-                     "traffic_source": f"{traffic[2]} ({traffic[1]})" if traffic else None,
-                     "bytes_per_launch": r["update_bytes"], "kernel_ms": r["update_kernel_ms"],
-                     "workload": args.workload},
+        "roofline": roofline,
         "cpu_baseline": cpu,
         "timing": {"graph": bool(r["graph"]), "steps_per_graph": r["steps_per_graph"],
                    "eager_ms_per_step": r["eager_ms_per_step"],
@@ -683,7 +755,8 @@ def main():
                    "kernel_ms": "HIP events around graph replays of 10 back-to-back launches"},
         "kernels": {"k_update_ms": r["update_kernel_ms"], "k_encode_f32_ms": r["encode_kernel_ms"],
                     "k_encode_gbs": r["encode_gbs"], "element_clients_per_s": r["element_clients_per_s"]},
-        "weak": {"gib_s": r["gib_s"], "ms_per_step": r["ms_per_step"]},
+        "sequential": {"gib_s": r["gib_s"], "ms_per_step": r["ms_per_step"]},
+        "pipelined": r["pipelined"],
         "strong": strong,
         "extra": extras,
         "end_to_end_host_buffers": e2e,

@@ -102,6 +102,7 @@ def lib() -> C.CDLL:
         "fleet_host_register": (i32, [vp, vp, sz]),
         "fleet_host_unregister": (i32, [vp, vp]),
         "fleet_update_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, sz, sz, vp, vp, vp]),
+        "fleet_update_encode_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, vp, vp, vp, sz, vp, vp]),
         "fleet_update_kardam_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, C.c_double, vp, vp, vp, sz, vp, vp,
                                              vp, vp, vp]),
         "fleet_update_kernel": (C.c_char_p, [sz]),
@@ -171,6 +172,15 @@ def b64_count(length: int) -> int:
 def update_kernel(length: int) -> str:
     """Aggregation kernel the library launches for uploads of `length` bytes."""
     return lib().fleet_update_kernel(length).decode()
+
+
+def update_encode_kernel(length: int) -> str:
+    """What fleet_update_encode_device launches: the fused k_update_encode on the
+    stream grid, else the update kernel and k_encode_f32 back to back."""
+    k = update_kernel(length)
+    if k == "k_update_mixed<256>" and not os.environ.get("FLEET_FUSED_STEP_OFF"):
+        return "k_update_encode<256>"
+    return k + " + k_encode_f32"
 
 
 def layout_from_sizes(w_sizes: Sequence[int], b_sizes: Sequence[int]):
@@ -389,6 +399,23 @@ class Codec:
                                          hp.ctypes.data, len(hp), group_begin, ge, merged_u8.data_ptr() - shift_b,
                                          merged_f32.data_ptr() - shift_f if merged_f32 is not None else None,
                                          _stream(stream))
+        self._check(rc)
+
+    def update_encode_device(self, uploads_u8, length: int, dampen: Sequence[float], header_pos, merged_u8,
+                             merged_f32, values_f32, next_uploads_u8, stream=None):
+        """One pipelined step (fleet_update_encode_device): update_device over the whole
+        uploads_u8 [M, pitch] and encode_device of values_f32 [M, vpitch] into
+        next_uploads_u8 [M, pitch] (a different buffer), in one launch."""
+        M, pitch = uploads_u8.shape
+        if tuple(next_uploads_u8.shape) != (M, pitch) or values_f32.shape[0] != M:
+            raise ValueError("next_uploads / values must have the uploads' rows and pitch")
+        hp = np.ascontiguousarray(header_pos, dtype=np.int32)
+        d = np.ascontiguousarray(dampen, dtype=np.float64)
+        rc = self._L.fleet_update_encode_device(self._h, uploads_u8.data_ptr(), pitch, length, M, d.ctypes.data,
+                                                hp.ctypes.data, len(hp), merged_u8.data_ptr(),
+                                                merged_f32.data_ptr() if merged_f32 is not None else None,
+                                                values_f32.data_ptr(), values_f32.shape[1],
+                                                next_uploads_u8.data_ptr(), _stream(stream))
         self._check(rc)
 
     def update_kardam_device(self, uploads_u8, length: int, dampen: Sequence[float], header_pos, lr: float,

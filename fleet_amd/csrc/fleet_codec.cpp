@@ -941,6 +941,32 @@ int fleet_update_device(fleet_ctx* c, const void* d_uploads, size_t pitch, size_
   return FLEET_OK;
 }
 
+int fleet_update_encode_device(fleet_ctx* c, const void* d_uploads, size_t pitch, size_t len, int M,
+                               const double* dampen, const int32_t* header_pos, int n_headers, void* d_merged,
+                               void* d_merged_f32, const void* d_values, size_t vpitch, void* d_next_uploads,
+                               void* stream) {
+  if (!c || !d_uploads || !dampen || M <= 0 || !d_merged || !d_values || !d_next_uploads || n_headers < 0 ||
+      n_headers > FLEET_MAX_HEADERS || (n_headers && !header_pos))
+    return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  HIP_TRY(c, hipSetDevice(c->device));
+  size_t gb = 0, ge = SIZE_MAX;
+  int rc = check_device_update(c, pitch, len, &gb, &ge);
+  if (rc) return rc;
+  const size_t n = fleet_b64_count(len);
+  if (vpitch < n) return fail(c, FLEET_ERR_ARG, "vpitch %zu < %zu values", vpitch, n);
+  // the encode writes rows [0, M) of d_next_uploads while the update reads d_uploads
+  const uintptr_t u0 = (uintptr_t)d_uploads, u1 = u0 + pitch * (size_t)M;
+  const uintptr_t e0 = (uintptr_t)d_next_uploads, e1 = e0 + pitch * (size_t)M;
+  if (u0 < e1 && e0 < u1) return fail(c, FLEET_ERR_ARG, "d_next_uploads overlaps d_uploads");
+  hipStream_t s = pick(c, stream);
+  if ((rc = dev_params(c, s, n, M, dampen, header_pos, n_headers))) return rc;
+  HIP_TRY(c, fleet::launch_update_encode((const uint8_t*)d_uploads, pitch, M, c->d_dev_dampen, (double)1 / M,
+                                         (int64_t)n, c->d_dev_hdr, (uint8_t*)d_merged, (float*)d_merged_f32,
+                                         c->d_dev_err, (const float*)d_values, vpitch, (uint8_t*)d_next_uploads, s));
+  return FLEET_OK;
+}
+
 int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch, size_t len, int M,
                                const double* dampen, const int32_t* header_pos, int n_headers, double lr,
                                const void* d_prev, const uint8_t* has_prev, void* d_g_out, size_t vpitch,

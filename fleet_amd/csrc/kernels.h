@@ -42,6 +42,9 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
                                 double* norms, hipStream_t s);
 // name of the aggregation kernel launch_update picks for `groups` groups
 const char* update_kernel_name(int64_t groups);
+hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
+                                int64_t n_up, const int32_t* d_hdr_block, uint8_t* merged, float* merged_f32,
+                                int* d_err, const float* values, size_t vpitch, uint8_t* enc_out, hipStream_t s);
 hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int rows, uint8_t* out, size_t pitch,
                              hipStream_t s);
 hipError_t launch_encode_minibatch(const float* images, int64_t n_images, int F, const int32_t* labels,

@@ -600,6 +600,50 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   }
 }
 
+// Block `bid` of the SIMD-balanced stream grid (tables already in LDS).
+template <int NT>
+__device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D16Table& dtab, int64_t bid,
+                                                   const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                   const double* __restrict__ dampen, double inv_avg, int64_t n_up,
+                                                   int64_t g_begin, int64_t g_end,
+                                                   const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
+                                                   float* __restrict__ merged_f32, int* __restrict__ err, int nA) {
+  uint32_t bad = 0, layout_bad = 0;
+  if (bid < nA) {  // block-uniform: one group per lane
+    const int64_t g = g_begin + bid * NT + threadIdx.x;
+    const bool live = g < g_end;
+    int32_t out[3];
+    update_lane<3>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out, bad,
+                   layout_bad);
+    if (!live) return;
+    if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
+    if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+    const int r = (int)min<int64_t>(3, n_up - 3 * g);
+    *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &tab), r);
+    if (merged_f32)
+      for (int e = 0; e < r; ++e) merged_f32[3 * g + e] = dec_mt(out[e], tab.mt);
+  } else {  // one value per lane, 21 groups per wave
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t g = g_begin + (int64_t)nA * NT + ((bid - nA) * (NT / 64) + wave) * 21 + lane / 3;
+    const int e = lane % 3;
+    const bool live = lane < 63 && g < g_end;
+    int32_t out[1];
+    update_lane<1>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, e, live, g_begin, hdr_block, out, bad,
+                   layout_bad);
+    const int base = lane - e;  // the group's three lanes (lane 63 reads its own)
+    const int32_t o0 = __shfl(out[0], base), o1 = __shfl(out[0], base + 1), o2 = __shfl(out[0], base + 2);
+    if (!live) return;
+    if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
+    if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+    const int r = (int)min<int64_t>(3, n_up - 3 * g);
+    if (e == 0) {
+      const int32_t o3[3] = {o0, r > 1 ? o1 : 0, r > 2 ? o2 : 0};
+      *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(o3, &tab), r);
+    }
+    if (merged_f32 && e < r) merged_f32[3 * g + e] = dec_mt(out[0], tab.mt);
+  }
+}
+
 // The stream update with balanced SIMDs. The plain stream grid has
 // ceil(groups/64) waves, which leaves some SIMDs one wave more than others for
 // the whole kernel (synth1m_256: 5,462 waves on 1,024 SIMDs -> 5 or 6 each). Here
@@ -619,40 +663,8 @@ __global__ void __launch_bounds__(NT) k_update_mixed(const uint8_t* __restrict__
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
   __syncthreads();
-  uint32_t bad = 0, layout_bad = 0;
-  if ((int)blockIdx.x < nA) {  // block-uniform: one group per lane
-    const int64_t g = g_begin + (int64_t)blockIdx.x * NT + threadIdx.x;
-    const bool live = g < g_end;
-    int32_t out[3];
-    update_lane<3>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out, bad,
-                   layout_bad);
-    if (!live) return;
-    if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
-    if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
-    const int r = (int)min<int64_t>(3, n_up - 3 * g);
-    *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &tab), r);
-    if (merged_f32)
-      for (int e = 0; e < r; ++e) merged_f32[3 * g + e] = dec_mt(out[e], tab.mt);
-  } else {  // one value per lane, 21 groups per wave
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t g = g_begin + (int64_t)nA * NT + ((int64_t)(blockIdx.x - nA) * (NT / 64) + wave) * 21 + lane / 3;
-    const int e = lane % 3;
-    const bool live = lane < 63 && g < g_end;
-    int32_t out[1];
-    update_lane<1>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, e, live, g_begin, hdr_block, out, bad,
-                   layout_bad);
-    const int base = lane - e;  // the group's three lanes (lane 63 reads its own)
-    const int32_t o0 = __shfl(out[0], base), o1 = __shfl(out[0], base + 1), o2 = __shfl(out[0], base + 2);
-    if (!live) return;
-    if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
-    if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
-    const int r = (int)min<int64_t>(3, n_up - 3 * g);
-    if (e == 0) {
-      const int32_t o3[3] = {o0, r > 1 ? o1 : 0, r > 2 ? o2 : 0};
-      *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(o3, &tab), r);
-    }
-    if (merged_f32 && e < r) merged_f32[3 * g + e] = dec_mt(out[0], tab.mt);
-  }
+  update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block,
+                         merged, merged_f32, err, nA);
 }
 
 // Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
@@ -1091,15 +1103,12 @@ __device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const 
 // Block (bx, by) encodes groups [256*bx, 256*bx+256) of rows [rpb*by, rpb*by+rpb):
 // a lane walks its group down rpb rows (next row's floats loaded while the
 // current one is encoded), so the LDS table copy is paid once per rpb rows.
-__global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ values, int64_t n, size_t vpitch,
-                                                    uint8_t* __restrict__ out, size_t pitch, int64_t groups,
-                                                    int rows, int rpb) {
-  __shared__ B64Tables tab;
-  b64_tables_init(&tab);
-  __syncthreads();
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void encode_rows(const float* __restrict__ values, int64_t n, size_t vpitch,
+                                            uint8_t* __restrict__ out, size_t pitch, int64_t groups, int rows,
+                                            int rpb, int64_t bx, int by, const B64Tables* tab) {
+  const int64_t g = bx * 256 + threadIdx.x;
   if (g >= groups) return;
-  const int row0 = blockIdx.y * rpb, row1 = min(rows, row0 + rpb);
+  const int row0 = by * rpb, row1 = min(rows, row0 + rpb);
   const int r = (int)min<int64_t>(3, n - 3 * g);
   const float* v = values + (size_t)row0 * vpitch + 3 * g;
   // one 12-byte load per full group (a wave instruction spans 768 contiguous
@@ -1119,7 +1128,57 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
       v += vpitch;
       n2 = load(v + vpitch);
     }
-    store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, &tab));
+    store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab));
+  }
+}
+
+__global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ values, int64_t n, size_t vpitch,
+                                                    uint8_t* __restrict__ out, size_t pitch, int64_t groups,
+                                                    int rows, int rpb) {
+  __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  encode_rows(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab);
+}
+
+// One launch, two independent jobs on disjoint buffers: the aggregation of the
+// uploads already in HBM (blocks [0, nU): k_update_mixed's grid) and the client
+// encode of the NEXT batch's rows into another upload buffer (blocks [nU, ...):
+// k_encode_f32's grid, flattened x-fastest). The aggregation is VALU-bound and
+// leaves HBM mostly idle, the encode is HBM-bound; the dispatcher places the
+// aggregation's blocks first (they fit the chip in one round) and streams the
+// encode's blocks through the wave slots and issue cycles they leave. Each
+// block's results are those of the separate kernels.
+struct EncodeJob {
+  const float* values;
+  int64_t n;
+  size_t vpitch;
+  uint8_t* out;
+  size_t pitch;
+  int64_t groups, gx;
+  int rows, rpb;
+};
+template <int NT>
+__global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                      const double* __restrict__ dampen, double inv_avg,
+                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
+                                                      const int32_t* __restrict__ hdr_block,
+                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                      int* __restrict__ err, int nA, int nU, EncodeJob ej) {
+  static_assert(NT == 256, "the encode blocks are 256 lanes");
+  __shared__ B64Tables tab;
+  __shared__ D16Table dtab;
+  b64_tables_init<NT>(&tab);
+  if ((int)blockIdx.x < nU) {  // block-uniform
+    d16_table_init<NT>(&dtab);
+    __syncthreads();
+    update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+                           hdr_block, merged, merged_f32, err, nA);
+  } else {
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x - nU;
+    encode_rows(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                (int)(e / ej.gx), &tab);
   }
 }
 
@@ -1742,6 +1801,14 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   return hipGetLastError();
 }
 
+// rows per block of the client encode: about 65,536 blocks in all (a lane walks its
+// group down rpb rows, so the LDS table copy is paid once per rpb rows)
+static int encode_rows_per_block(int64_t gx, int rows) {
+  int rpb = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 65535) / 65536));
+  if (const char* e = getenv("FLEET_ENCODE_RPB")) rpb = std::max(1, std::min(rows, atoi(e)));  // experiments
+  return rpb;
+}
+
 hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int rows, uint8_t* out, size_t pitch,
                              hipStream_t s) {
   int64_t groups = (n + 2) / 3;
@@ -1753,10 +1820,35 @@ hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int 
   // synth1m_256 encodes in 478-480 us at 4-8 rows per block, 483 at 16, 501 at
   // 2 and 32, 595 at 1; the same access pattern without the codec arithmetic
   // (scripts/ubench_stream.hip, 12 B in / 16 B out per lane) runs 452-486 us.
-  int rpb = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 65535) / 65536));
-  if (const char* e = getenv("FLEET_ENCODE_RPB")) rpb = std::max(1, std::min(rows, atoi(e)));  // experiments
+  const int rpb = encode_rows_per_block(gx, rows);
   hipLaunchKernelGGL(k_encode_f32, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s, values, n,
                      vpitch, out, pitch, groups, rows, rpb);
+  return hipGetLastError();
+}
+
+// The aggregation of `uploads` and the client encode of `values` into `enc_out`
+// (another buffer) in one k_update_encode launch when the update runs on the
+// SIMD-balanced stream grid; otherwise the two kernels back to back.
+hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
+                                int64_t n_up, const int32_t* d_hdr_block, uint8_t* merged, float* merged_f32,
+                                int* d_err, const float* values, size_t vpitch, uint8_t* enc_out, hipStream_t s) {
+  const int64_t groups = (n_up + 2) / 3;
+  const UpdatePlan p = plan_update(groups);
+  const int nA = mixed_split(groups);
+  if (groups == 0 || p.kind != 0 || p.k != 1 || nA < 0 || getenv("FLEET_UPDATE_NT") || getenv("FLEET_FUSED_STEP_OFF")) {
+    hipError_t e = launch_update(uploads, pitch, M, d_dampen, inv_avg, n_up, 0, groups, d_hdr_block, merged, merged_f32,
+                                 d_err, s);
+    if (e != hipSuccess) return e;
+    return launch_encode_f32(values, n_up, vpitch, M, enc_out, pitch, s);
+  }
+  const int64_t nB = (groups - (int64_t)nA * 256 + 83) / 84;
+  const int64_t gx = blocks_for(groups, 256);
+  const int rpb = encode_rows_per_block(gx, M);
+  const int64_t nE = gx * ((M + rpb - 1) / rpb);
+  const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+  hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nA + nB + nE)), dim3(256), 0, s, uploads, pitch, M,
+                     d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nA,
+                     (int)(nA + nB), ej);
   return hipGetLastError();
 }
 

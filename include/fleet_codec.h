@@ -157,6 +157,18 @@ int fleet_host_unregister(fleet_ctx* ctx, void* ptr);
 int fleet_update_device(fleet_ctx* ctx, const void* d_uploads, size_t pitch, size_t len, int M,
                         const double* dampen, const int32_t* header_pos, int n_headers, size_t group_begin,
                         size_t group_end, void* d_merged, void* d_merged_f32, void* stream);
+/* A pipelined step of the device-resident path: fleet_update_device over the
+ * whole uploads in d_uploads AND fleet_encode_device of the next batch's M rows
+ * of fp32 (d_values, n values, vpitch floats per row) into d_next_uploads (same
+ * pitch; must not overlap d_uploads), in ONE launch when the update runs on the
+ * stream grid (the aggregation is VALU-bound, the client encode HBM-bound: they
+ * share the CUs), else the two kernels back to back. Results equal the two
+ * calls' results. Replaces nothing in the reference (its clients encode on
+ * their own devices); the bench's steady-state step. */
+int fleet_update_encode_device(fleet_ctx* ctx, const void* d_uploads, size_t pitch, size_t len, int M,
+                               const double* dampen, const int32_t* header_pos, int n_headers, void* d_merged,
+                               void* d_merged_f32, const void* d_values, size_t vpitch, void* d_next_uploads,
+                               void* stream);
 /* fleet_update_device plus Kardam's bookkeeping of the same picked uploads
  * (CppNNUpdater.java:463-481, Kardam.java:48-106) as side
  * outputs of the one pass over the uploads (no second read of them):
