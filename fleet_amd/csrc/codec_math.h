@@ -575,6 +575,20 @@ FLEET_HD float q_d16(float x, uint32_t e, const StepTables* st) {
   return div10_mt(code_float_mt(mul10_mt(__builtin_fabsf(x), me), d, x), me);
 }
 
+// float2int(x) given e = 16 * numDigits((int)x) <= 144 (the client encode's form
+// of q_d16): the x10 chain's multipliers and d itself at the byte offset e; the
+// sign by two integer ops on x's sign mask ((c ^ s) - s), not a compare and select.
+FLEET_HD int32_t enc_d16(float x, uint32_t e, const StepTables* st) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const char* base = reinterpret_cast<const char*>(st);
+  const f4 m = *static_cast<const f4*>(__builtin_assume_aligned(base + e, 16));
+  const uint32_t d = *static_cast<const uint32_t*>(__builtin_assume_aligned(base + sizeof(st->m) + sizeof(st->h) + e, 16));
+  const MulEntry me{{m.x, m.y, m.z, m.w}, {1.0f, 1.0f, 1.0f, 1.0f}};
+  const uint32_t c = div10_u30((uint32_t)mul10_mt(__builtin_fabsf(x), me)) * 10u + d;
+  const uint32_t sm = (uint32_t)((int32_t)f2u(x) >> 31);
+  return (int32_t)((c ^ sm) - sm);
+}
+
 // ------------------------------------------- one-lookup latency Q (serial chain)
 // The serial accumulation A = Q(A + p) runs on ONE wave per tile: it is bound by
 // that wave's instruction issue, so the step count matters more than a table

@@ -1620,7 +1620,7 @@ const char* fleet_update_kernel(size_t len) {
 }
 
 int fleet_selftest_digest(fleet_ctx* c, int fn, uint64_t* out) {
-  if (!c || !out || fn < 0 || fn > 19) return FLEET_ERR_ARG;
+  if (!c || !out || fn < 0 || fn > 20) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   HIP_TRY(c, hipSetDevice(c->device));
   unsigned long long* d = nullptr;

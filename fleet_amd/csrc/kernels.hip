@@ -1082,6 +1082,47 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
 // One group (3 values) of one row: float2int (fixed chains when the wave is
 // in |x| < 1, multiplier-table chains otherwise, the general codec for values
 // outside the q_gen domain) and the 16 Base64 chars.
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab,
+                                              const D16Table* dt) {
+  int32_t codes[3];
+  // |x| < 1 for the whole wave iff the largest |x| bit pattern is (integer max,
+  // not three 6-cycle e64 compares)
+  uint32_t amax = 0;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) amax = max(amax, f2u(x[e]) & 0x7fffffffu);
+  if (__ballot(amax >= 0x3f800000u) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+    // byte-table digit counts (codec_math.h d16_entry): one byte load per value;
+    // the power-of-ten slices take the compare, values outside the q_gen
+    // domain (|x| >= 1e8/1e9, inf, NaN) the general codec -- both rare, per lane
+    uint32_t ofs[3], omax = 0;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      ofs[e] = dt->d16[f2u(x[e]) >> 19];
+      omax = max(omax, ofs[e]);
+    }
+    if (__ballot(omax >= kD16Out) != 0) {
+      omax = 0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        if (ofs[e] == kD16Cmp) ofs[e] = d16_fix(x[e], tab->var);
+        omax = max(omax, ofs[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
+    if (__ballot(omax >= kD16Out) != 0) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if (ofs[e] >= kD16Out) codes[e] = enc(x[e]);
+    }
+  }
+  return pad_group(b64_encode_group(codes, tab), r);
+}
+
+// The same with the VarEntry digit counts (kernels that keep only B64Tables in LDS)
 __device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
   int32_t codes[3];
   const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
@@ -1105,7 +1146,8 @@ __device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const 
 // current one is encoded), so the LDS table copy is paid once per rpb rows.
 __device__ __forceinline__ void encode_rows(const float* __restrict__ values, int64_t n, size_t vpitch,
                                             uint8_t* __restrict__ out, size_t pitch, int64_t groups, int rows,
-                                            int rpb, int64_t bx, int by, const B64Tables* tab) {
+                                            int rpb, int64_t bx, int by, const B64Tables* tab,
+                                            const D16Table* dt) {
   const int64_t g = bx * 256 + threadIdx.x;
   if (g >= groups) return;
   const int row0 = by * rpb, row1 = min(rows, row0 + rpb);
@@ -1128,7 +1170,7 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
       v += vpitch;
       n2 = load(v + vpitch);
     }
-    store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab));
+    store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab, dt));
   }
 }
 
@@ -1136,9 +1178,11 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
                                                     uint8_t* __restrict__ out, size_t pitch, int64_t groups,
                                                     int rows, int rpb) {
   __shared__ B64Tables tab;
+  __shared__ D16Table dtab;
   b64_tables_init(&tab);
+  d16_table_init(&dtab);
   __syncthreads();
-  encode_rows(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab);
+  encode_rows(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab, &dtab);
 }
 
 // One launch, two independent jobs on disjoint buffers: the aggregation of the
@@ -1169,16 +1213,15 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   __shared__ B64Tables tab;
   __shared__ D16Table dtab;
   b64_tables_init<NT>(&tab);
+  d16_table_init<NT>(&dtab);
+  __syncthreads();
   if ((int)blockIdx.x < nU) {  // block-uniform
-    d16_table_init<NT>(&dtab);
-    __syncthreads();
     update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                            hdr_block, merged, merged_f32, err, nA);
   } else {
-    __syncthreads();
     const int64_t e = (int64_t)blockIdx.x - nU;
     encode_rows(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
-                (int)(e / ej.gx), &tab);
+                (int)(e / ej.gx), &tab, &dtab);
   }
 }
 
@@ -2008,6 +2051,11 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
                uint32_t e = dtab.d16[u >> 19];
                if (e == kD16Cmp) e = d16_fix(x, var);
                o = use ? (e < kD16Out ? f2u(q_d16(x, e, &dtab.st)) : 0xdeadbeefu) : 0u; break; }
+      case 20: { const float x = u2f(u);                              // byte-table float2int of the client encode (as fn 10)
+               use = q_gen_ok(x);
+               uint32_t e = dtab.d16[u >> 19];
+               if (e == kD16Cmp) e = d16_fix(x, var);
+               o = use ? (e < kD16Out ? (uint32_t)enc_d16(x, e, &dtab.st) : 0xdeadbeefu) : 0u; break; }
       case 18: { const float e = glibc_expf(u2f(u));                 // the teacher's expf (libm's)
                o = e != e ? 0x7fc00000u : f2u(e); break; }
       default: o = 0; use = false;

@@ -223,6 +223,7 @@ int fleet_check(fleet_ctx* ctx, void* stream);
  *   fn 18: the teacher forward's expf (glibc 2.35 restated) over all 2^32 inputs,
  *          NaN results as 0x7fc00000 (the libm expf digest of tests/native/digest_ref.cpp)
  *   fn 19: byte-table Q of the stream kernel (q_d16 + compare fix-up; as fn 6)
+ *   fn 20: byte-table float2int of the client encode (enc_d16; as fn 10)
  * computed on the GPU; compare with the oracle's digests. */
 int fleet_selftest_digest(fleet_ctx* ctx, int fn, uint64_t* out);
 

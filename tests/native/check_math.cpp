@@ -105,6 +105,7 @@ int main(int argc, char** argv) {
       }
       if (e != 16u * (uint32_t)fo_num_digits(fo_cvtt(x))) g_bad++;
       if (!same(q_d16(x, e, &st), fo_int2float(fo_float2int(x)))) g_bad++;
+      if (enc_d16(x, e, &st) != fo_float2int(x)) g_bad++;  // the client encode's form
     });
     par_for(0, 1ull << 32, 1, [](uint64_t i) {  // int2float from the same tables, every code
       const int32_t c = (int32_t)(uint32_t)i;
@@ -114,7 +115,7 @@ int main(int argc, char** argv) {
     long cmp_slices = 0;
     for (uint32_t i = 0; i < 8192; ++i) cmp_slices += dt[i] == kD16Cmp;
     printf("d16 table: %ld compare slices of 8192\n", cmp_slices);
-    report("d16 / q_d16 (exhaustive)", b);
+    report("d16 / q_d16 / enc_d16 (exhaustive)", b);
     return g_bad ? 1 : 0;
   }
   const uint64_t s = exhaustive ? 1 : 97;  // sampling stride (odd, walks every residue class)
@@ -220,6 +221,7 @@ int main(int argc, char** argv) {
       }
       if (e != 16u * (uint32_t)fo_num_digits(fo_cvtt(x))) g_bad++;
       if (!same(q_d16(x, e, &st), fo_int2float(fo_float2int(x)))) g_bad++;
+      if (enc_d16(x, e, &st) != fo_float2int(x)) g_bad++;
     });
     // every power-of-ten slice, densely (where the compare decides)
     for (uint32_t sl = 0; sl < 8192; ++sl)
@@ -231,11 +233,12 @@ int main(int argc, char** argv) {
             if (e < kD16Out) g_bad++;
             return;
           }
-          if (e != 16u * (uint32_t)fo_num_digits(fo_cvtt(x)) || !same(q_d16(x, e, &st), fo_int2float(fo_float2int(x))))
+          if (e != 16u * (uint32_t)fo_num_digits(fo_cvtt(x)) || !same(q_d16(x, e, &st), fo_int2float(fo_float2int(x))) ||
+              enc_d16(x, e, &st) != fo_float2int(x))
             g_bad++;
         });
   }
-  report("d16/q_d16", b0);
+  report("d16/q_d16/enc_d16", b0);
   b0 = g_bad;
   {
     static XlEntry xt[2 * kXlSpan];
