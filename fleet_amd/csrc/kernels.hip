@@ -1144,6 +1144,7 @@ __device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const 
 // Block (bx, by) encodes groups [256*bx, 256*bx+256) of rows [rpb*by, rpb*by+rpb):
 // a lane walks its group down rpb rows (next row's floats loaded while the
 // current one is encoded), so the LDS table copy is paid once per rpb rows.
+template <bool D16>
 __device__ __forceinline__ void encode_rows(const float* __restrict__ values, int64_t n, size_t vpitch,
                                             uint8_t* __restrict__ out, size_t pitch, int64_t groups, int rows,
                                             int rpb, int64_t bx, int by, const B64Tables* tab,
@@ -1170,7 +1171,8 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
       v += vpitch;
       n2 = load(v + vpitch);
     }
-    store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab, dt));
+    if constexpr (D16) store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab, dt));
+    else store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab));
   }
 }
 
@@ -1178,11 +1180,20 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
                                                     uint8_t* __restrict__ out, size_t pitch, int64_t groups,
                                                     int rows, int rpb) {
   __shared__ B64Tables tab;
+  b64_tables_init(&tab);
+  __syncthreads();
+  encode_rows<false>(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab, nullptr);
+}
+// the same on the byte-table digit counts (experiments: FLEET_ENCODE_D16=1)
+__global__ void __launch_bounds__(256) k_encode_f32_d16(const float* __restrict__ values, int64_t n, size_t vpitch,
+                                                        uint8_t* __restrict__ out, size_t pitch, int64_t groups,
+                                                        int rows, int rpb) {
+  __shared__ B64Tables tab;
   __shared__ D16Table dtab;
   b64_tables_init(&tab);
   d16_table_init(&dtab);
   __syncthreads();
-  encode_rows(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab, &dtab);
+  encode_rows<true>(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab, &dtab);
 }
 
 // One launch, two independent jobs on disjoint buffers: the aggregation of the
@@ -1220,8 +1231,8 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
                            hdr_block, merged, merged_f32, err, nA);
   } else {
     const int64_t e = (int64_t)blockIdx.x - nU;
-    encode_rows(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
-                (int)(e / ej.gx), &tab, &dtab);
+    encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                     (int)(e / ej.gx), &tab, &dtab);
   }
 }
 
@@ -1844,6 +1855,16 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   return hipGetLastError();
 }
 
+// The standalone client encode's digit counts: the VarEntry compare (enc_mt) by
+// default, the byte table (enc_d16; FLEET_ENCODE_D16=1) for experiments. The
+// encode is HBM-bound on its own, and the byte table's 9 KB copy per block costs
+// more than its VALU saving (same-box A/B on synth1m_256: 460 vs 476 us at 6 rows
+// per block, 468 vs 470 at 12); k_update_encode, where the VALU is the limit,
+// uses the byte table.
+static bool encode_d16() {
+  const char* e = getenv("FLEET_ENCODE_D16");
+  return e && atoi(e) != 0;
+}
 // rows per block of the client encode: about 65,536 blocks in all (a lane walks its
 // group down rpb rows, so the LDS table copy is paid once per rpb rows)
 static int encode_rows_per_block(int64_t gx, int rows) {
@@ -1864,8 +1885,12 @@ hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int 
   // 2 and 32, 595 at 1; the same access pattern without the codec arithmetic
   // (scripts/ubench_stream.hip, 12 B in / 16 B out per lane) runs 452-486 us.
   const int rpb = encode_rows_per_block(gx, rows);
-  hipLaunchKernelGGL(k_encode_f32, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s, values, n,
-                     vpitch, out, pitch, groups, rows, rpb);
+  if (encode_d16())
+    hipLaunchKernelGGL(k_encode_f32_d16, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s,
+                       values, n, vpitch, out, pitch, groups, rows, rpb);
+  else
+    hipLaunchKernelGGL(k_encode_f32, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s,
+                       values, n, vpitch, out, pitch, groups, rows, rpb);
   return hipGetLastError();
 }
 
@@ -1886,7 +1911,10 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   }
   const int64_t nB = (groups - (int64_t)nA * 256 + 83) / 84;
   const int64_t gx = blocks_for(groups, 256);
-  const int rpb = encode_rows_per_block(gx, M);
+  // twice the standalone encode's rows per block: its blocks also copy the 9 KB
+  // byte table (same-box A/B on synth1m_256: 1188 / 1177 us at 6 / 12 rows per
+  // block with enc_mt, 1179 / 1170 with enc_d16)
+  const int rpb = std::min(M, 2 * encode_rows_per_block(gx, M));
   const int64_t nE = gx * ((M + rpb - 1) / rpb);
   const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
   hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nA + nB + nE)), dim3(256), 0, s, uploads, pitch, M,
