@@ -844,27 +844,29 @@ __device__ __forceinline__ void tile_epilogue(TileShared<TG, NW>& sh, const floa
 //              by chain_general.
 // Layout consistency (all uploads carry the last one's header codes) is
 // checked in phase 1 with per-slot LDS min/max of the header codes.
-template <int TG>
-__global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict__ uploads, size_t pitch, int M,
-                                                      const double* __restrict__ dampen, double inv_avg,
-                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
-                                                      const int32_t* __restrict__ hdr_block,
-                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                      int* __restrict__ err) {
-  constexpr int E = 3 * TG;
-  static_assert(E <= 256, "phase 2 is one thread per value");
 #ifndef FLEET_TILED_PT
 #define FLEET_TILED_PT 3072
 #endif
-  // p floats per chunk: 12 KiB (CM = 16 clients at TG = 64, so a chunk is two full
-  // 512-item passes); with the tables the block fits 7 per CU (measured: 24 KiB
-  // chunks 0.40 ms, 12 KiB 0.37, 8 KiB 0.50, 16 KiB 0.43 on cifar10_256)
-  constexpr int CM = FLEET_TILED_PT / E;
+// p floats per chunk: 12 KiB (CM = 16 clients at TG = 64, so a chunk is two full
+// 512-item passes); with the tables the block fits 7 per CU (measured: 24 KiB
+// chunks 0.40 ms, 12 KiB 0.37, 8 KiB 0.50, 16 KiB 0.43 on cifar10_256)
+template <int TG>
+constexpr int tiled_chunk_clients() { return FLEET_TILED_PT / (3 * TG); }
+
+// Tile `bid` of k_update_tiled (LDS state in sh / ptile)
+template <int TG>
+__device__ __forceinline__ void update_tiled_block(TileShared<TG>& sh, float* ptile, int64_t bid,
+                                                   const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                   const double* __restrict__ dampen, double inv_avg, int64_t n_up,
+                                                   int64_t g_begin, int64_t g_end,
+                                                   const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
+                                                   float* __restrict__ merged_f32, int* __restrict__ err) {
+  constexpr int E = 3 * TG;
+  static_assert(E <= 256, "phase 2 is one thread per value");
+  constexpr int CM = tiled_chunk_clients<TG>();
   FLEET_TSTAMP(0);
-  __shared__ TileShared<TG> sh;
-  __shared__ float ptile[CM * E];
   const int tid = threadIdx.x;
-  const int64_t g0 = g_begin + (int64_t)blockIdx.x * TG;
+  const int64_t g0 = g_begin + bid * TG;
   const int ng = (int)min<int64_t>(TG, g_end - g0);
   tile_init(sh, hdr_block + 4, hdr_block[1], g0, ng);
   FLEET_TSTAMP(1);
@@ -919,6 +921,19 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
   __syncthreads();
   tile_epilogue(sh, ptile, inv_avg, n_up, hdr_block[2], g0, ng, merged, merged_f32, err);
   FLEET_TSTAMP(5);
+}
+
+template <int TG>
+__global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                      const double* __restrict__ dampen, double inv_avg,
+                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
+                                                      const int32_t* __restrict__ hdr_block,
+                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                      int* __restrict__ err) {
+  __shared__ TileShared<TG> sh;
+  __shared__ float ptile[tiled_chunk_clients<TG>() * 3 * TG];
+  update_tiled_block<TG>(sh, ptile, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block,
+                         merged, merged_f32, err);
 }
 
 // Pipelined tile variant (E = 3*TG <= 64): producer waves compute p for passes
@@ -1233,6 +1248,32 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
     const int64_t e = (int64_t)blockIdx.x - nU;
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                      (int)(e / ej.gx), &tab, &dtab);
+  }
+}
+
+// The same pairing for the tiled sizes (CIFAR buckets): blocks [0, nU) are
+// k_update_tiled<TG>'s tiles (under two waves per SIMD at these sizes, so most
+// wave slots are free), the rest the client encode's blocks on the tile's B64Tables
+// (VarEntry digit counts: the tile state leaves no room for the byte table).
+template <int TG>
+__global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                             const double* __restrict__ dampen, double inv_avg,
+                                                             int64_t n_up, int64_t g_begin, int64_t g_end,
+                                                             const int32_t* __restrict__ hdr_block,
+                                                             uint8_t* __restrict__ merged,
+                                                             float* __restrict__ merged_f32, int* __restrict__ err,
+                                                             int nU, EncodeJob ej) {
+  __shared__ TileShared<TG> sh;
+  __shared__ float ptile[tiled_chunk_clients<TG>() * 3 * TG];
+  if ((int)blockIdx.x < nU) {  // block-uniform
+    update_tiled_block<TG>(sh, ptile, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block,
+                           merged, merged_f32, err);
+  } else {
+    b64_tables_init(&sh.tab);
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x - nU;
+    encode_rows<false>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                       (int)(e / ej.gx), &sh.tab, nullptr);
   }
 }
 
@@ -1903,6 +1944,20 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   const int64_t groups = (n_up + 2) / 3;
   const UpdatePlan p = plan_update(groups);
   const int nA = mixed_split(groups);
+  const int64_t gx = blocks_for(groups, 256);
+  if (groups > 0 && p.kind == 1 && (p.tg == 32 || p.tg == 64) && !getenv("FLEET_FUSED_STEP_OFF")) {
+    const int rpb = encode_rows_per_block(gx, M);
+    const int64_t nU = (groups + p.tg - 1) / p.tg, nE = gx * ((M + rpb - 1) / rpb);
+    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+#define FLEET_LAUNCH_TE(TG)                                                                                        \
+  hipLaunchKernelGGL((k_update_tiled_encode<TG>), dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, M,   \
+                     d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)nU, \
+                     ej)
+    if (p.tg == 64) FLEET_LAUNCH_TE(64);
+    else FLEET_LAUNCH_TE(32);
+#undef FLEET_LAUNCH_TE
+    return hipGetLastError();
+  }
   if (groups == 0 || p.kind != 0 || p.k != 1 || nA < 0 || getenv("FLEET_UPDATE_NT") || getenv("FLEET_FUSED_STEP_OFF")) {
     hipError_t e = launch_update(uploads, pitch, M, d_dampen, inv_avg, n_up, 0, groups, d_hdr_block, merged, merged_f32,
                                  d_err, s);
@@ -1910,7 +1965,6 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     return launch_encode_f32(values, n_up, vpitch, M, enc_out, pitch, s);
   }
   const int64_t nB = (groups - (int64_t)nA * 256 + 83) / 84;
-  const int64_t gx = blocks_for(groups, 256);
   // twice the standalone encode's rows per block: its blocks also copy the 9 KB
   // byte table (same-box A/B on synth1m_256: 1188 / 1177 us at 6 / 12 rows per
   // block with enc_mt, 1179 / 1170 with enc_d16)

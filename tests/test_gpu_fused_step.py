@@ -2,7 +2,8 @@
 batch and the client encode of the next in one launch must give exactly what
 fleet_update_device and fleet_encode_device give as two calls -- the merged text,
 merged_f32 and the next batch's uploads, byte for byte -- on the stream grid (the
-fused kernel k_update_encode) and on the tiled sizes (two launches). The two
+fused kernel k_update_encode), on the wide tiles (k_update_tiled_encode) and on
+the pipelined tiles (two launches). The two
 separate calls are themselves checked against the oracle elsewhere
 (test_gpu_parity.py, test_gpu_full_size.py)."""
 import numpy as np
@@ -26,7 +27,8 @@ def _batch(codec, torch, lay, M, seed, n_values=None):
 
 
 @pytest.mark.parametrize("lay_name,M,n_values", [("synth1m", 6, None), ("synth1m", 1, None),
-                                                  ("cifar10", 5, None), ("synth1m", 3, 1_000_003)])
+                                                  ("cifar10", 5, None), ("cifar100", 4, None), ("mnist", 3, None),
+                                                  ("synth1m", 3, 1_000_003), ("synth1m", 2, 150_001)])
 def test_update_encode_equals_two_calls(codec, lay_name, M, n_values):
     torch = pytest.importorskip("torch")
     lay = LAYOUTS[lay_name]
@@ -56,6 +58,7 @@ def test_update_encode_equals_two_calls(codec, lay_name, M, n_values):
     assert torch.equal(f32_a.view(torch.int32), f32_b.view(torch.int32))
     assert torch.equal(next_a, next_b)
     assert not torch.equal(next_b, text)  # a different batch really was encoded
+    print(lay_name, M, F.update_encode_kernel(L))
 
 
 def test_update_encode_rejects_overlap_and_bad_text(codec):
