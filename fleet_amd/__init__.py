@@ -176,14 +176,16 @@ def update_kernel(length: int) -> str:
 
 def update_encode_kernel(length: int) -> str:
     """What fleet_update_encode_device launches: the fused k_update_encode on the
-    stream grid, k_update_tiled_encode on the wide tiles, else the update kernel
-    and k_encode_f32 back to back."""
+    stream grid, k_update_tiled_encode on the wide tiles, k_update_pipe with the
+    encode's blocks appended on the pipelined tiles."""
     k = update_kernel(length)
     if not os.environ.get("FLEET_FUSED_STEP_OFF"):
         if k == "k_update_mixed<256>":
             return "k_update_encode<256>"
         if k in ("k_update_tiled<64>", "k_update_tiled<32>"):
             return k.replace("k_update_tiled", "k_update_tiled_encode")
+        if k.startswith("k_update_pipe"):
+            return k + " (with the encode's blocks)"
     return k + " + k_encode_f32"
 
 

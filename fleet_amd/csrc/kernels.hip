@@ -936,6 +936,116 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
                          merged, merged_f32, err);
 }
 
+// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
+// One group (3 values) of one row: float2int (fixed chains when the wave is
+// in |x| < 1, multiplier-table chains otherwise, the general codec for values
+// outside the q_gen domain) and the 16 Base64 chars.
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab,
+                                              const D16Table* dt) {
+  int32_t codes[3];
+  // |x| < 1 for the whole wave iff the largest |x| bit pattern is (integer max,
+  // not three 6-cycle e64 compares)
+  uint32_t amax = 0;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) amax = max(amax, f2u(x[e]) & 0x7fffffffu);
+  if (__ballot(amax >= 0x3f800000u) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+    // byte-table digit counts (codec_math.h d16_entry): one byte load per value;
+    // the power-of-ten slices take the compare, values outside the q_gen
+    // domain (|x| >= 1e8/1e9, inf, NaN) the general codec -- both rare, per lane
+    uint32_t ofs[3], omax = 0;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      ofs[e] = dt->d16[f2u(x[e]) >> 19];
+      omax = max(omax, ofs[e]);
+    }
+    if (__ballot(omax >= kD16Out) != 0) {
+      omax = 0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        if (ofs[e] == kD16Cmp) ofs[e] = d16_fix(x[e], tab->var);
+        omax = max(omax, ofs[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
+    if (__ballot(omax >= kD16Out) != 0) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if (ofs[e] >= kD16Out) codes[e] = enc(x[e]);
+    }
+  }
+  return pad_group(b64_encode_group(codes, tab), r);
+}
+
+// The same with the VarEntry digit counts (kernels that keep only B64Tables in LDS)
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
+  int32_t codes[3];
+  const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
+  if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab->var, tab->mt);
+    if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
+#pragma unroll
+      for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
+    }
+  }
+  return pad_group(b64_encode_group(codes, tab), r);
+}
+
+// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
+// Block (bx, by) encodes groups [NT*bx, NT*bx+NT) of rows [rpb*by, rpb*by+rpb):
+// a lane walks its group down rpb rows (next row's floats loaded while the
+// current one is encoded), so the LDS table copy is paid once per rpb rows.
+template <bool D16, int NT = 256>
+__device__ __forceinline__ void encode_rows(const float* __restrict__ values, int64_t n, size_t vpitch,
+                                            uint8_t* __restrict__ out, size_t pitch, int64_t groups, int rows,
+                                            int rpb, int64_t bx, int by, const B64Tables* tab,
+                                            const D16Table* dt) {
+  const int64_t g = bx * NT + threadIdx.x;
+  if (g >= groups) return;
+  const int row0 = by * rpb, row1 = min(rows, row0 + rpb);
+  const int r = (int)min<int64_t>(3, n - 3 * g);
+  const float* v = values + (size_t)row0 * vpitch + 3 * g;
+  // one 12-byte load per full group (a wave instruction spans 768 contiguous
+  // bytes once, instead of three dword loads over the same lines); two rows in
+  // flight ahead of the one being encoded
+  typedef float f3 __attribute__((ext_vector_type(3)));
+  auto load = [&](const float* p) -> f3 {
+    if (r == 3) return *reinterpret_cast<const f3*>(p);
+    return f3{p[0], r > 1 ? p[1] : 0.0f, 0.0f};
+  };
+  f3 n1 = load(v), n2 = f3{0.0f, 0.0f, 0.0f};
+  if (row0 + 1 < row1) n2 = load(v + vpitch);
+  for (int row = row0; row < row1; ++row) {
+    const float x[3] = {n1.x, n1.y, n1.z};
+    n1 = n2;
+    if (row + 2 < row1) {
+      v += vpitch;
+      n2 = load(v + vpitch);
+    }
+    if constexpr (D16) store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab, dt));
+    else store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab));
+  }
+}
+
+// A client-encode job riding in an aggregation launch (k_update_encode,
+// k_update_tiled_encode, k_update_pipe): k_encode_f32's grid, flattened x-fastest.
+struct EncodeJob {
+  const float* values;
+  int64_t n;
+  size_t vpitch;
+  uint8_t* out;
+  size_t pitch;
+  int64_t groups, gx;
+  int rows, rpb;
+};
+
 // Pipelined tile variant (E = 3*TG <= 64): producer waves compute p for passes
 // of clients into an LDS ring while wave 0 consumes them in client order (the
 // serial A = Q(A + p_c)), so the client-independent work and the serial
@@ -956,7 +1066,7 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
                                                      const int32_t* __restrict__ hdr_block,
                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                     int* __restrict__ err) {
+                                                     int* __restrict__ err, int nU, EncodeJob ej) {
   constexpr int E = 3 * TG;
   static_assert(E <= 64, "one consumer wave");
   constexpr int NPW = NW - 1;                                // producer waves
@@ -972,6 +1082,14 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   // wave index made wave-uniform (readfirstlane), so the producer/consumer
   // split below is a scalar branch and the consumer's s_setprio is its own
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  if ((int)blockIdx.x >= nU) {  // block-uniform: the next batch's client encode (fleet_update_encode_device)
+    b64_tables_init<64 * NW>(&sh.tab);
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x - nU;
+    encode_rows<false, 64 * NW>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                                (int)(e / ej.gx), &sh.tab, nullptr);
+    return;
+  }
   const int64_t g0 = g_begin + (int64_t)blockIdx.x * TG;
   const int ng = (int)min<int64_t>(TG, g_end - g0);
   if (tid < NPW) prog[tid] = 0;
@@ -1093,104 +1211,6 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
 }
 
 // ----------------------------------------------------------------------------
-// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
-// One group (3 values) of one row: float2int (fixed chains when the wave is
-// in |x| < 1, multiplier-table chains otherwise, the general codec for values
-// outside the q_gen domain) and the 16 Base64 chars.
-__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab,
-                                              const D16Table* dt) {
-  int32_t codes[3];
-  // |x| < 1 for the whole wave iff the largest |x| bit pattern is (integer max,
-  // not three 6-cycle e64 compares)
-  uint32_t amax = 0;
-#pragma unroll
-  for (int e = 0; e < 3; ++e) amax = max(amax, f2u(x[e]) & 0x7fffffffu);
-  if (__ballot(amax >= 0x3f800000u) == 0) {  // wave-uniform: gradients, |x| < 1
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
-  } else {
-    // byte-table digit counts (codec_math.h d16_entry): one byte load per value;
-    // the power-of-ten slices take the compare, values outside the q_gen
-    // domain (|x| >= 1e8/1e9, inf, NaN) the general codec -- both rare, per lane
-    uint32_t ofs[3], omax = 0;
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      ofs[e] = dt->d16[f2u(x[e]) >> 19];
-      omax = max(omax, ofs[e]);
-    }
-    if (__ballot(omax >= kD16Out) != 0) {
-      omax = 0;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        if (ofs[e] == kD16Cmp) ofs[e] = d16_fix(x[e], tab->var);
-        omax = max(omax, ofs[e]);
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
-    if (__ballot(omax >= kD16Out) != 0) {
-#pragma unroll
-      for (int e = 0; e < 3; ++e)
-        if (ofs[e] >= kD16Out) codes[e] = enc(x[e]);
-    }
-  }
-  return pad_group(b64_encode_group(codes, tab), r);
-}
-
-// The same with the VarEntry digit counts (kernels that keep only B64Tables in LDS)
-__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
-  int32_t codes[3];
-  const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
-  if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab->var, tab->mt);
-    if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
-#pragma unroll
-      for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
-    }
-  }
-  return pad_group(b64_encode_group(codes, tab), r);
-}
-
-// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
-// Block (bx, by) encodes groups [256*bx, 256*bx+256) of rows [rpb*by, rpb*by+rpb):
-// a lane walks its group down rpb rows (next row's floats loaded while the
-// current one is encoded), so the LDS table copy is paid once per rpb rows.
-template <bool D16>
-__device__ __forceinline__ void encode_rows(const float* __restrict__ values, int64_t n, size_t vpitch,
-                                            uint8_t* __restrict__ out, size_t pitch, int64_t groups, int rows,
-                                            int rpb, int64_t bx, int by, const B64Tables* tab,
-                                            const D16Table* dt) {
-  const int64_t g = bx * 256 + threadIdx.x;
-  if (g >= groups) return;
-  const int row0 = by * rpb, row1 = min(rows, row0 + rpb);
-  const int r = (int)min<int64_t>(3, n - 3 * g);
-  const float* v = values + (size_t)row0 * vpitch + 3 * g;
-  // one 12-byte load per full group (a wave instruction spans 768 contiguous
-  // bytes once, instead of three dword loads over the same lines); two rows in
-  // flight ahead of the one being encoded
-  typedef float f3 __attribute__((ext_vector_type(3)));
-  auto load = [&](const float* p) -> f3 {
-    if (r == 3) return *reinterpret_cast<const f3*>(p);
-    return f3{p[0], r > 1 ? p[1] : 0.0f, 0.0f};
-  };
-  f3 n1 = load(v), n2 = f3{0.0f, 0.0f, 0.0f};
-  if (row0 + 1 < row1) n2 = load(v + vpitch);
-  for (int row = row0; row < row1; ++row) {
-    const float x[3] = {n1.x, n1.y, n1.z};
-    n1 = n2;
-    if (row + 2 < row1) {
-      v += vpitch;
-      n2 = load(v + vpitch);
-    }
-    if constexpr (D16) store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab, dt));
-    else store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab));
-  }
-}
-
 __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ values, int64_t n, size_t vpitch,
                                                     uint8_t* __restrict__ out, size_t pitch, int64_t groups,
                                                     int rows, int rpb) {
@@ -1219,15 +1239,6 @@ __global__ void __launch_bounds__(256) k_encode_f32_d16(const float* __restrict_
 // aggregation's blocks first (they fit the chip in one round) and streams the
 // encode's blocks through the wave slots and issue cycles they leave. Each
 // block's results are those of the separate kernels.
-struct EncodeJob {
-  const float* values;
-  int64_t n;
-  size_t vpitch;
-  uint8_t* out;
-  size_t pitch;
-  int64_t groups, gx;
-  int rows, rpb;
-};
 template <int NT>
 __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                       const double* __restrict__ dampen, double inv_avg,
@@ -1786,20 +1797,18 @@ const char* update_kernel_name(int64_t groups) {
   return buf;
 }
 
-hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
-                         int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
-                         uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
-  if (g_end <= g_begin) return hipSuccess;
+// k_update_pipe in the variant the plan picked, with `nE` client-encode blocks
+// after its tiles (nE = 0: none)
+static void launch_pipe(const UpdatePlan& p, const uint8_t* uploads, size_t pitch, int M, const double* d_dampen,
+                        double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
+                        uint8_t* merged, float* merged_f32, int* d_err, int64_t nE, const EncodeJob& ej,
+                        hipStream_t s) {
   const int64_t groups = g_end - g_begin;
-  const UpdatePlan p = plan_update(groups);
-#define FLEET_LAUNCH(KERNEL, PER_BLOCK)                                                                         \
-  hipLaunchKernelGGL(KERNEL, dim3((unsigned)((groups + (PER_BLOCK)-1) / (PER_BLOCK))), dim3(256), 0, s, uploads, \
-                     pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
-  if (p.kind == 2) {
+  const int64_t nU = (groups + p.tg - 1) / p.tg;
 #define FLEET_LAUNCH_PIPE(TG, IPT, NW, WP)                                                                       \
-  hipLaunchKernelGGL((k_update_pipe<TG, IPT, NW, WP>), dim3((unsigned)((groups + TG - 1) / TG)), dim3(64 * NW), 0, \
-                     s, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged,           \
-                     merged_f32, d_err)
+  hipLaunchKernelGGL((k_update_pipe<TG, IPT, NW, WP>), dim3((unsigned)(nU + nE)), dim3(64 * NW), 0, s, uploads,    \
+                     pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err,       \
+                     nE ? (int)nU : INT32_MAX, ej)
     if (p.wp) {
       if (p.nw == 8) {
         if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 8, 1);
@@ -1822,6 +1831,20 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
       else FLEET_LAUNCH_PIPE(16, 1, 4, 0);
     }
 #undef FLEET_LAUNCH_PIPE
+}
+
+hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
+                         int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
+                         uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
+  if (g_end <= g_begin) return hipSuccess;
+  const int64_t groups = g_end - g_begin;
+  const UpdatePlan p = plan_update(groups);
+#define FLEET_LAUNCH(KERNEL, PER_BLOCK)                                                                         \
+  hipLaunchKernelGGL(KERNEL, dim3((unsigned)((groups + (PER_BLOCK)-1) / (PER_BLOCK))), dim3(256), 0, s, uploads, \
+                     pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
+  if (p.kind == 2) {
+    launch_pipe(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, 0,
+                EncodeJob{}, s);
   } else if (p.kind == 1) {
     if (p.tg == 8) FLEET_LAUNCH(k_update_tiled<8>, 8);
     else if (p.tg == 16) FLEET_LAUNCH(k_update_tiled<16>, 16);
@@ -1956,6 +1979,15 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     if (p.tg == 64) FLEET_LAUNCH_TE(64);
     else FLEET_LAUNCH_TE(32);
 #undef FLEET_LAUNCH_TE
+    return hipGetLastError();
+  }
+  if (groups > 0 && p.kind == 2 && !getenv("FLEET_FUSED_STEP_OFF")) {  // small buckets: the pipelined tiles
+    const int nt = 64 * p.nw;
+    const int64_t gxp = (groups + nt - 1) / nt;
+    const int rpb = encode_rows_per_block(gxp, M);
+    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gxp, M, rpb};
+    launch_pipe(p, uploads, pitch, M, d_dampen, inv_avg, n_up, 0, groups, d_hdr_block, merged, merged_f32, d_err,
+                gxp * ((M + rpb - 1) / rpb), ej, s);
     return hipGetLastError();
   }
   if (groups == 0 || p.kind != 0 || p.k != 1 || nA < 0 || getenv("FLEET_UPDATE_NT") || getenv("FLEET_FUSED_STEP_OFF")) {

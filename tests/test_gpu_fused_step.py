@@ -3,7 +3,7 @@ batch and the client encode of the next in one launch must give exactly what
 fleet_update_device and fleet_encode_device give as two calls -- the merged text,
 merged_f32 and the next batch's uploads, byte for byte -- on the stream grid (the
 fused kernel k_update_encode), on the wide tiles (k_update_tiled_encode) and on
-the pipelined tiles (two launches). The two
+the pipelined tiles (k_update_pipe with the encode's blocks appended). The two
 separate calls are themselves checked against the oracle elsewhere
 (test_gpu_parity.py, test_gpu_full_size.py)."""
 import numpy as np
@@ -28,7 +28,8 @@ def _batch(codec, torch, lay, M, seed, n_values=None):
 
 @pytest.mark.parametrize("lay_name,M,n_values", [("synth1m", 6, None), ("synth1m", 1, None),
                                                   ("cifar10", 5, None), ("cifar100", 4, None), ("mnist", 3, None),
-                                                  ("synth1m", 3, 1_000_003), ("synth1m", 2, 150_001)])
+                                                  ("mnist", 64, None), ("synth1m", 3, 1_000_003), ("synth1m", 2, 150_001),
+                                                  ("synth1m", 2, 100)])
 def test_update_encode_equals_two_calls(codec, lay_name, M, n_values):
     torch = pytest.importorskip("torch")
     lay = LAYOUTS[lay_name]
