@@ -1996,16 +1996,26 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     if (e != hipSuccess) return e;
     return launch_encode_f32(values, n_up, vpitch, M, enc_out, pitch, s);
   }
-  const int64_t nB = (groups - (int64_t)nA * 256 + 83) / 84;
+  // the plain stream grid (every update block group-per-lane): the encode's blocks
+  // fill the SIMDs the last round of update waves leaves idle, so the value-per-lane
+  // balancing of k_update_mixed only adds instructions here (same-box A/B on
+  // synth1m_256: 1172.7 vs 1181.3 us, scripts/gpu_fused_ab.sh); FLEET_FUSED_PLAIN=0
+  // restores the balanced grid
+  int nAf = (int)((groups + 255) / 256);
+  int64_t nB = 0;
+  if (const char* e = getenv("FLEET_FUSED_PLAIN"); e && !atoi(e)) {
+    nAf = nA;
+    nB = (groups - (int64_t)nA * 256 + 83) / 84;
+  }
   // twice the standalone encode's rows per block: its blocks also copy the 9 KB
   // byte table (same-box A/B on synth1m_256: 1188 / 1177 us at 6 / 12 rows per
   // block with enc_mt, 1179 / 1170 with enc_d16)
   const int rpb = std::min(M, 2 * encode_rows_per_block(gx, M));
   const int64_t nE = gx * ((M + rpb - 1) / rpb);
   const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
-  hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nA + nB + nE)), dim3(256), 0, s, uploads, pitch, M,
-                     d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nA,
-                     (int)(nA + nB), ej);
+  hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nAf + nB + nE)), dim3(256), 0, s, uploads, pitch, M,
+                     d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf,
+                     (int)(nAf + nB), ej);
   return hipGetLastError();
 }
 
