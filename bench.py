@@ -3,9 +3,15 @@
 
 One step = the hot path over one batch of M synthetic client gradient buckets
 already resident in HBM:
-  1. client-side encode  (Base64::encode(vector<float>) of every bucket; k_encode_f32)
+  1. client-side encode  (Base64::encode(vector<float>) of every bucket)
   2. server aggregation  (CppNNUpdater.update's decode/dampen/sum/average/merge
-                          chain, bit-exact; k_update*) -> merged Base64 + fp32
+                          chain, bit-exact) -> merged Base64 + fp32
+`value` times the steps software-pipelined over two upload buffers: step i
+aggregates batch i and encodes batch i+1 in ONE launch (k_update_encode /
+k_update_tiled_encode / k_update_pipe with encode blocks;
+fleet_update_encode_device), batch 0 encoded before the clock. The sequential
+form (k_encode_f32, then k_update*) is reported beside it (`sequential`;
+--sequential makes it the value).
 
 Headline (N=1): synth1m_256, the north-star configuration (1 M-float buckets,
 C = 256 clients, 1.43 GB of Base64 >> the 256 MiB Infinity Cache).
