@@ -1709,7 +1709,7 @@ static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t -
 // k_update_mixed's split: the blocks of whole rounds of one-group-per-lane waves
 // (a multiple of one wave per SIMD of the current device), or -1 when the grid is
 // under one round (the plain stream grid then).
-static int stream_full_rounds_blocks(int64_t groups) {
+static int device_simds() {
   static int simds = 0;
   if (!simds) {
     int dev = 0, cus = 0;
@@ -1718,6 +1718,10 @@ static int stream_full_rounds_blocks(int64_t groups) {
       cus = 256;
     simds = 4 * cus;
   }
+  return simds;
+}
+static int stream_full_rounds_blocks(int64_t groups) {
+  const int simds = device_simds();
   const int64_t waves = (groups + 63) / 64;
   if (waves < simds) return -1;
   const int64_t full = waves / simds * simds;  // waves in whole rounds
@@ -2007,10 +2011,15 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     nAf = nA;
     nB = (groups - (int64_t)nA * 256 + 83) / 84;
   }
-  // twice the standalone encode's rows per block: its blocks also copy the 9 KB
-  // byte table (same-box A/B on synth1m_256: 1188 / 1177 us at 6 / 12 rows per
-  // block with enc_mt, 1179 / 1170 with enc_d16)
-  const int rpb = std::min(M, 2 * encode_rows_per_block(gx, M));
+  // 12 rows per encode block: short blocks that fill the slots the update's waves
+  // leave (a lane walks its group down the rows with two loads in flight, so a
+  // block of hundreds of rows -- the standalone rule at configs[4] -- is a
+  // latency-bound straggler); same-box A/B on synth1m_256: 1188 / 1177 us at 6 /
+  // 12 rows per block with enc_mt, 1179 / 1170 with enc_d16 (the blocks also copy
+  // the 9 KB byte table); synth4m_4096 79.1 ms at 12, 64 or 684. FLEET_FUSED_RPB
+  // overrides.
+  int rpb = std::min(M, 12);
+  if (const char* e = getenv("FLEET_FUSED_RPB")) rpb = std::max(1, std::min(M, atoi(e)));
   const int64_t nE = gx * ((M + rpb - 1) / rpb);
   const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
   hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nAf + nB + nE)), dim3(256), 0, s, uploads, pitch, M,
