@@ -58,3 +58,6 @@ def test_null_context_rejected():
     n = C.c_size_t(0)
     assert L.fleet_encode_f32(None, None, 0, None, 0, C.byref(n)) == F.FLEET_ERR_ARG
     assert L.fleet_update(None, None, None, 0, None, None, 0, None, None) == F.FLEET_ERR_ARG
+    assert L.fleet_update_device(None, None, 0, 0, 0, None, None, 0, 0, 0, None, None, None) == F.FLEET_ERR_ARG
+    assert L.fleet_update_encode_device(None, None, 0, 0, 0, None, None, 0, None, None, None, 0, None,
+                                        None) == F.FLEET_ERR_ARG
