@@ -7,7 +7,7 @@ one() { # $1 = label, $2 = workload, rest = env
   env "$@" timeout -k 10 300 python bench.py --workload $w --extras= --no-cpu-baseline --no-e2e --no-strong-block --steps ${STEPS:-20} --warmup 3 > gpurun_out/abw.json 2>/dev/null || exit 1
   python3 -c "
 import json; r=json.loads(open('gpurun_out/abw.json').read().strip().splitlines()[-1])
-print('$lab', '$w', 'update', round(r['kernels']['k_update_ms']*1e3,1), 'us  encode', round(r['kernels']['k_encode_f32_ms']*1e3,1), 'us  step', round(r['ms_per_step']*1e3,1), 'us')"
+print('$lab', '$w', 'update', round(r['kernels']['k_update_ms']*1e3,1), 'us  encode', round(r['kernels']['k_encode_f32_ms']*1e3,1), 'us  step', round(r['ms_per_step']*1e3,1), 'us  fused', round(r['roofline']['kernel_ms']*1e3,1), 'us  sequential', round(r['sequential']['ms_per_step']*1e3,1))"
 }
 for rep in 1 2; do
   for w in $WL; do
