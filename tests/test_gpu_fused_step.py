@@ -30,7 +30,7 @@ def _batch(codec, torch, lay, M, seed, n_values=None):
                                                   ("cifar10", 5, None), ("cifar100", 4, None), ("mnist", 3, None),
                                                   ("mnist", 64, None), ("synth1m", 3, 1_000_003), ("synth1m", 2, 150_001),
                                                   ("synth1m", 2, 100)])
-def test_update_encode_equals_two_calls(codec, lay_name, M, n_values):
+def test_update_encode_equals_two_calls(codec, lay_name, M, n_values, pad=0):
     torch = pytest.importorskip("torch")
     lay = LAYOUTS[lay_name]
     n, groups, hp, values = _batch(codec, torch, lay, M, 7 + M, n_values)
@@ -38,7 +38,7 @@ def test_update_encode_equals_two_calls(codec, lay_name, M, n_values):
     L = F.b64_len(n)
     dev = values.device
     dampen = [1.0 / (c % 3 + 1) for c in range(M)]
-    text = torch.zeros((M, 16 * groups), dtype=torch.uint8, device=dev)
+    text = torch.zeros((M, 16 * groups + pad), dtype=torch.uint8, device=dev)
     codec.encode_device(values, n, text)
 
     # reference: the two separate calls
@@ -60,6 +60,12 @@ def test_update_encode_equals_two_calls(codec, lay_name, M, n_values):
     assert torch.equal(next_a, next_b)
     assert not torch.equal(next_b, text)  # a different batch really was encoded
     print(lay_name, M, F.update_encode_kernel(L))
+
+
+@pytest.mark.parametrize("lay_name,M", [("synth1m", 3), ("cifar10", 3), ("mnist", 5)])
+def test_update_encode_padded_rows(codec, lay_name, M):
+    """Upload rows wider than the text (pitch = 16 * groups + 48): both jobs honour the pitch."""
+    test_update_encode_equals_two_calls(codec, lay_name, M, None, pad=48)
 
 
 def test_update_encode_rejects_overlap_and_bad_text(codec):
