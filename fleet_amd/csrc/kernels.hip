@@ -1002,7 +1002,11 @@ __device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const 
 // Block (bx, by) encodes groups [NT*bx, NT*bx+NT) of rows [rpb*by, rpb*by+rpb):
 // a lane walks its group down rpb rows (next row's floats loaded while the
 // current one is encoded), so the LDS table copy is paid once per rpb rows.
-template <bool D16, int NT = 256>
+// ROT = true: the rows in flight rotate through registers with a row loop
+// unrolled by two (no copies between rows) -- the standalone encode, 467 -> 448 us
+// on synth1m_256 (same-box A/B); ROT = false: one register pair copied forward per
+// row -- the form the fused step keeps (the rotating loop made it 1 % slower there).
+template <bool D16, int NT = 256, bool ROT = false>
 __device__ __forceinline__ void encode_rows(const float* __restrict__ values, int64_t n, size_t vpitch,
                                             uint8_t* __restrict__ out, size_t pitch, int64_t groups, int rows,
                                             int rpb, int64_t bx, int by, const B64Tables* tab,
@@ -1016,21 +1020,39 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
   // bytes once, instead of three dword loads over the same lines); two rows in
   // flight ahead of the one being encoded
   typedef float f3 __attribute__((ext_vector_type(3)));
-  auto load = [&](const float* p) -> f3 {
+  auto load = [&](int rr) -> f3 {
+    const float* p = v + (size_t)(rr - row0) * vpitch;
     if (r == 3) return *reinterpret_cast<const f3*>(p);
     return f3{p[0], r > 1 ? p[1] : 0.0f, 0.0f};
   };
-  f3 n1 = load(v), n2 = f3{0.0f, 0.0f, 0.0f};
-  if (row0 + 1 < row1) n2 = load(v + vpitch);
-  for (int row = row0; row < row1; ++row) {
-    const float x[3] = {n1.x, n1.y, n1.z};
-    n1 = n2;
-    if (row + 2 < row1) {
-      v += vpitch;
-      n2 = load(v + vpitch);
+  auto emit = [&](int rr, const float (&x)[3]) {
+    if constexpr (D16) store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab, dt));
+    else store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab));
+  };
+  if constexpr (ROT) {
+    f3 buf[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) buf[k] = row0 + k < row1 ? load(row0 + k) : f3{0.0f, 0.0f, 0.0f};
+    for (int row = row0; row < row1; row += 2) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int rr = row + k;
+        if (rr < row1) {  // block-uniform
+          const float x[3] = {buf[k].x, buf[k].y, buf[k].z};
+          if (rr + 2 < row1) buf[k] = load(rr + 2);
+          emit(rr, x);
+        }
+      }
     }
-    if constexpr (D16) store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab, dt));
-    else store_stream16(out + (size_t)row * pitch + 16 * g, encode_group(x, r, tab));
+  } else {
+    f3 n1 = load(row0), n2 = f3{0.0f, 0.0f, 0.0f};
+    if (row0 + 1 < row1) n2 = load(row0 + 1);
+    for (int row = row0; row < row1; ++row) {
+      const float x[3] = {n1.x, n1.y, n1.z};
+      n1 = n2;
+      if (row + 2 < row1) n2 = load(row + 2);
+      emit(row, x);
+    }
   }
 }
 
@@ -1217,7 +1239,7 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
   __shared__ B64Tables tab;
   b64_tables_init(&tab);
   __syncthreads();
-  encode_rows<false>(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab, nullptr);
+  encode_rows<false, 256, true>(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab, nullptr);
 }
 // the same on the byte-table digit counts (experiments: FLEET_ENCODE_D16=1)
 __global__ void __launch_bounds__(256) k_encode_f32_d16(const float* __restrict__ values, int64_t n, size_t vpitch,
@@ -1228,7 +1250,7 @@ __global__ void __launch_bounds__(256) k_encode_f32_d16(const float* __restrict_
   b64_tables_init(&tab);
   d16_table_init(&dtab);
   __syncthreads();
-  encode_rows<true>(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab, &dtab);
+  encode_rows<true, 256, true>(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab, &dtab);
 }
 
 // One launch, two independent jobs on disjoint buffers: the aggregation of the
