@@ -153,6 +153,30 @@ int fail(fleet_ctx* c, int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return fail((ctx), FLEET_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
   } while (0)
 
+// Every entry point runs on its context's device and leaves the calling
+// thread's current device as it found it (a JVM request thread or a torch
+// process keeps its own notion of the current GPU): hipGetDevice on entry,
+// hipSetDevice back on every return path.
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int device) {
+    if (hipGetDevice(&prev) != hipSuccess) {
+      (void)hipGetLastError();
+      prev = -1;
+    }
+    ok = prev == device || hipSetDevice(device) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (ok && prev >= 0) (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+#define DEVICE_SCOPE(ctx)                                                                       \
+  DeviceGuard device_guard_((ctx)->device);                                                     \
+  if (!device_guard_.ok) return fail((ctx), FLEET_ERR_HIP, "hipSetDevice(%d) failed", (ctx)->device)
+
 template <typename T>
 int grow_dev(fleet_ctx* c, T** p, size_t* cap, size_t need_elems) {
   if (need_elems <= *cap) return FLEET_OK;
@@ -418,7 +442,8 @@ int fleet_create(int device, fleet_ctx** out) {
     fleet_destroy(c);
     return code;
   };
-  if (hipSetDevice(device) != hipSuccess) return bail(FLEET_ERR_HIP);
+  DeviceGuard dg(device);
+  if (!dg.ok) return bail(FLEET_ERR_HIP);
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) return bail(FLEET_ERR_HIP);
   if (hipMalloc((void**)&c->d_hdr, kHdrWords * sizeof(int32_t)) != hipSuccess) return bail(FLEET_ERR_NOMEM);
   if (hipMalloc((void**)&c->d_err, 64) != hipSuccess) return bail(FLEET_ERR_NOMEM);
@@ -459,7 +484,7 @@ int fleet_sync(fleet_ctx* c, void* stream) {
 int fleet_check(fleet_ctx* c, void* stream) {
   if (!c) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   return read_err(c, pick(c, stream), c->d_dev_err);
 }
 
@@ -493,7 +518,7 @@ int fleet_layout_parse(fleet_ctx* c, const char* upload, size_t len, int32_t* he
                        size_t* n_up) {
   if (!c || (!upload && len)) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   int rc = check_text_len(c, len);
   if (rc) return rc;
   size_t n = fleet_b64_count(len);
@@ -512,7 +537,7 @@ int fleet_layout_parse(fleet_ctx* c, const char* upload, size_t len, int32_t* he
 int fleet_encode_f32(fleet_ctx* c, const float* values, size_t n, char* out, size_t cap, size_t* out_len) {
   if (!c || (!values && n)) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   int rc;
   if ((rc = grow_dev(c, &c->d_f32, &c->d_f32_cap, n + 3))) return rc;
   if ((rc = grow_dev(c, &c->d_out, &c->d_out_cap, 16 * groups_of(n) + 16))) return rc;
@@ -524,7 +549,7 @@ int fleet_encode_f32(fleet_ctx* c, const float* values, size_t n, char* out, siz
 int fleet_encode_i32(fleet_ctx* c, const int32_t* codes, size_t n, char* out, size_t cap, size_t* out_len) {
   if (!c || (!codes && n)) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   int rc;
   if ((rc = grow_dev(c, &c->d_a, &c->d_a_cap, 4 * n + 16))) return rc;
   if ((rc = grow_dev(c, &c->d_out, &c->d_out_cap, 16 * groups_of(n) + 16))) return rc;
@@ -537,7 +562,7 @@ static int decode_common(fleet_ctx* c, const char* text, size_t len, void* out, 
                          int as_codes) {
   if (!c || (!text && len)) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   int rc = check_text_len(c, len);
   if (rc) return rc;
   size_t n = fleet_b64_count(len);
@@ -562,7 +587,7 @@ int fleet_decode_i32(fleet_ctx* c, const char* text, size_t len, int32_t* out, s
 int fleet_flat_gradient(fleet_ctx* c, const char* g, size_t len, char* out, size_t cap, size_t* out_len) {
   if (!c || (!g && len)) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   int rc = check_text_len(c, len);
   if (rc) return rc;
   size_t n = fleet_b64_count(len);
@@ -581,7 +606,7 @@ int fleet_merge_flat_gradient(fleet_ctx* c, const char* g, size_t glen, const ch
                               size_t cap, size_t* out_len) {
   if (!c || (!g && glen) || (!flat && flen)) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   int rc = check_text_len(c, glen);
   if (rc || (rc = check_text_len(c, flen))) return rc;
   size_t n = fleet_b64_count(glen), nf = fleet_b64_count(flen);
@@ -602,7 +627,7 @@ static int elementwise(fleet_ctx* c, const char* a, size_t alen, const char* b, 
                        char* out, size_t cap, size_t* out_len) {
   if (!c || (!a && alen) || (op && !b && blen)) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   int rc = check_text_len(c, alen);
   if (rc) return rc;
   size_t n = fleet_b64_count(alen);
@@ -633,7 +658,7 @@ int fleet_subtract(fleet_ctx* c, const char* a, size_t alen, const char* b, size
 int fleet_norm(fleet_ctx* c, const char* v, size_t len, double* out) {
   if (!c || (!v && len) || !out) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   int rc = check_text_len(c, len);
   if (rc) return rc;
   size_t n = fleet_b64_count(len);
@@ -738,7 +763,7 @@ int fleet_update(fleet_ctx* c, const char* const* uploads, const size_t* lens, i
                  char* merged, size_t cap, size_t* out_len, float* merged_f32) {
   if (!c || !uploads || !lens || !dampen || !merged || M <= 0) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   size_t len = 0;
   int rc = check_update_args(c, uploads, lens, M, cap, out_len, &len);
   if (rc) return rc;
@@ -784,7 +809,7 @@ int update_multi_impl(fleet_ctx* const* ctxs, int n_ctx, const char* const* uplo
   // a malformed header: the single-device flow reports the same error as a full device run
   if (hw[0] != 0) {
     std::lock_guard<std::mutex> lk(c0->mu);
-    HIP_TRY(c0, hipSetDevice(c0->device));
+    DEVICE_SCOPE(c0);
     return update_host_fallback(c0, uploads, len, M, dampen, merged, merged_f32);
   }
   const int threads = std::max(1, stage_threads(round16(len) * (size_t)M) / n_ctx);
@@ -795,7 +820,8 @@ int update_multi_impl(fleet_ctx* const* ctxs, int n_ctx, const char* const* uplo
     const size_t gb = (size_t)k * base + std::min((size_t)k, rem), ge = gb + base + ((size_t)k < rem ? 1 : 0);
     fleet_ctx* c = ctxs[k];
     std::lock_guard<std::mutex> lk(c->mu);
-    if (hipSetDevice(c->device) != hipSuccess) {
+    DeviceGuard dg(c->device);
+    if (!dg.ok) {
       rcs[(size_t)k] = fail(c, FLEET_ERR_HIP, "hipSetDevice(%d) failed", c->device);
       return;
     }
@@ -860,7 +886,7 @@ int fleet_update_rows_multi(fleet_ctx* const* ctxs, int n_ctx, const char* rows,
 int fleet_host_register(fleet_ctx* c, void* ptr, size_t bytes) {
   if (!c || !ptr || !bytes) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   HIP_TRY(c, hipHostRegister(ptr, bytes, hipHostRegisterPortable));
   return FLEET_OK;
 }
@@ -868,7 +894,7 @@ int fleet_host_register(fleet_ctx* c, void* ptr, size_t bytes) {
 int fleet_host_unregister(fleet_ctx* c, void* ptr) {
   if (!c || !ptr) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   HIP_TRY(c, hipHostUnregister(ptr));
   return FLEET_OK;
 }
@@ -929,7 +955,7 @@ int fleet_update_device(fleet_ctx* c, const void* d_uploads, size_t pitch, size_
       (n_headers && !header_pos))
     return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   int rc = check_device_update(c, pitch, len, &group_begin, &group_end);
   if (rc) return rc;
   const size_t n = fleet_b64_count(len);
@@ -949,7 +975,7 @@ int fleet_update_encode_device(fleet_ctx* c, const void* d_uploads, size_t pitch
       n_headers > FLEET_MAX_HEADERS || (n_headers && !header_pos))
     return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   size_t gb = 0, ge = SIZE_MAX;
   int rc = check_device_update(c, pitch, len, &gb, &ge);
   if (rc) return rc;
@@ -975,7 +1001,7 @@ int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch
       n_headers > FLEET_MAX_HEADERS || (n_headers && !header_pos) || (d_prev && !has_prev))
     return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   size_t gb = 0, ge = SIZE_MAX;
   int rc = check_device_update(c, pitch, len, &gb, &ge);
   if (rc) return rc;
@@ -1012,7 +1038,7 @@ int fleet_encode_device(fleet_ctx* c, const void* d_values, size_t n, size_t vpi
   if (!c || !d_values || !d_out || M <= 0) return FLEET_ERR_ARG;
   if (pitch % 16 != 0 || pitch < 16 * groups_of(n)) return fail(c, FLEET_ERR_ARG, "bad pitch");
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   HIP_TRY(c, fleet::launch_encode_f32((const float*)d_values, (int64_t)n, vpitch, M, (uint8_t*)d_out, pitch,
                                       pick(c, stream)));
   return FLEET_OK;
@@ -1022,7 +1048,7 @@ int fleet_decode_device(fleet_ctx* c, const void* d_text, size_t len, size_t pit
                         size_t vpitch, void* stream) {
   if (!c || !d_text || !d_values || M <= 0) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   int rc = check_text_len(c, len);
   if (rc) return rc;
   HIP_TRY(c, fleet::launch_decode((const uint8_t*)d_text, (int64_t)fleet_b64_count(len), pitch, M, d_values,
@@ -1036,7 +1062,7 @@ int fleet_synth_device(fleet_ctx* c, uint64_t seed, int M, int client0, const in
   if (!c || !d_values || M <= 0 || n_headers < 0 || n_headers > FLEET_MAX_HEADERS || vpitch < n_up)
     return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   hipStream_t s = pick(c, stream);
   int32_t* d_pos = nullptr;
   float* d_val = nullptr;
@@ -1104,7 +1130,7 @@ int fleet_model_quantize_index(fleet_ctx* c, const float* weights, const int32_t
                                float* quantized, float* dict, int* n_dict, int32_t* index) {
   if (!c) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   size_t n = 0;
   int rc = model_total(c, dims, n_mats, &n);
   if (rc) return rc;
@@ -1125,7 +1151,7 @@ int fleet_model_weights_text(fleet_ctx* c, const float* weights, const int32_t* 
                              size_t cap, size_t* out_len) {
   if (!c) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   size_t n = 0;
   int rc = model_total(c, dims, n_mats, &n);
   if (rc) return rc;
@@ -1158,7 +1184,7 @@ int fleet_model_read_weights(fleet_ctx* c, const char* text, size_t len, const i
                              float* weights_out) {
   if (!c || (!text && len)) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   size_t n = 0;
   int rc = model_total(c, dims, n_mats, &n);
   if (rc) return rc;
@@ -1218,7 +1244,7 @@ int fleet_model_params_device(fleet_ctx* c, const float* d_weights, size_t n_wei
   if (!c || !d_out || graph_edges < 0 || (n_weights && !d_weights) || (n_biases && graph_edges && !d_biases))
     return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   HIP_TRY(c, fleet::launch_encode_model_params(d_weights, (int64_t)n_weights, d_biases, (int64_t)n_biases,
                                                n_biases ? (int64_t)graph_edges : 0, (uint8_t*)d_out,
                                                pick(c, stream)));
@@ -1230,7 +1256,7 @@ int fleet_kardam_grads(fleet_ctx* c, const char* const* uploads, const size_t* l
                        double* norm_g, double* norm_diff) {
   if (!c || !uploads || !lens || !dampen || M <= 0 || !norm_g || !norm_diff) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   const size_t len = lens[0];
   int rc = check_text_len(c, len);
   if (rc) return rc;
@@ -1307,7 +1333,7 @@ int fleet_minibatch_device(fleet_ctx* c, const void* d_images, size_t n_images, 
       (d_teacher && num_labels == 0))
     return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   HIP_TRY(c, fleet::launch_encode_minibatch((const float*)d_images, (int64_t)n_images, F, (const int32_t*)d_labels,
                                             (const int32_t*)d_idx, B, (const float*)d_teacher, num_labels, header,
                                             (uint8_t*)d_out, c->d_dev_err, pick(c, stream)));
@@ -1327,7 +1353,7 @@ int fleet_minibatch(fleet_ctx* c, const float* images, size_t n_images, int F, c
     if (idx[b] < 0 || (size_t)idx[b] >= n_images)
       return fail(c, FLEET_ERR_ARG, "sample %d: index %d outside the %zu images", b, idx[b], n_images);
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   // staging: [B x F features | B labels | 0..B-1 | B x NL teacher]; the device gathers nothing
   const size_t nl = teacher ? (size_t)num_labels : 0;
   const size_t o_lab = round16(sizeof(float) * (size_t)B * (size_t)F), o_idx = o_lab + round16(4 * (size_t)B);
@@ -1362,7 +1388,7 @@ int fleet_teacher_forward_device(fleet_ctx* c, const void* d_w, const void* d_b,
                                  int F, const void* d_idx, int B, float temperature, void* d_probs, void* stream) {
   if (!c || B < 0 || (B && (!d_w || !d_b || !d_images || !d_probs)) || F < 28 * 28) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   HIP_TRY(c, fleet::launch_teacher_forward((const float*)d_w, (const float*)d_b, (const float*)d_images,
                                            (int64_t)n_images, F, (const int32_t*)d_idx, B, temperature,
                                            (float*)d_probs, c->d_dev_err, pick(c, stream)));
@@ -1380,7 +1406,7 @@ int fleet_teacher_forward(fleet_ctx* c, const float* w, size_t n_w, const float*
       return fail(c, FLEET_ERR_ARG, "sample %d: index %d outside the %zu images", i, idx[i], n_images);
   if (B == 0) return FLEET_OK;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   // staging: [w | b | B gathered rows | B x 10 probs]
   const size_t o_b = round16(sizeof(float) * n_w), o_x = o_b + round16(sizeof(float) * n_b);
   const size_t o_p = o_x + round16(sizeof(float) * (size_t)B * (size_t)F);
@@ -1414,7 +1440,7 @@ int fleet_model_params(fleet_ctx* c, const float* weights, size_t n_weights, con
   DevMem dw, db, dt;
   {
     std::lock_guard<std::mutex> lk(c->mu);
-    HIP_TRY(c, hipSetDevice(c->device));
+    DEVICE_SCOPE(c);
     if (n_weights) HIP_TRY(c, hipMalloc(&dw.p, n_weights * sizeof(float)));
     if (n_biases) HIP_TRY(c, hipMalloc(&db.p, n_biases * sizeof(float)));
     HIP_TRY(c, hipMalloc(&dt.p, 16 * groups_of(n) + 16));
@@ -1491,7 +1517,7 @@ int fleet_descent_device(fleet_ctx* c, float* d_weights, float* d_fc_bias, const
                          const uint8_t* fc_layer, int n_b, float lr, void* stream) {
   if (!c || !d_grad) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   size_t n_up = 0, nw = 0, nf = 0;
   std::vector<fleet::DescentSegs> segs;
   int rc = descent_segments(c, w_sizes, w_present, n_w, b_sizes, fc_layer, n_b, &n_up, &nw, &nf, &segs);
@@ -1508,7 +1534,7 @@ int fleet_descent_window_device(fleet_ctx* c, float* d_weights, float* d_fc_bias
                                 int n_b, float lr, void* stream) {
   if (!c || !d_grad_window || value_end < value_begin) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   size_t n_up = 0, nw = 0, nf = 0;
   std::vector<fleet::DescentSegs> segs;
   int rc = descent_segments(c, w_sizes, w_present, n_w, b_sizes, fc_layer, n_b, &n_up, &nw, &nf, &segs, value_begin,
@@ -1551,7 +1577,7 @@ int fleet_descent(fleet_ctx* c, float* weights, size_t n_weights, float* fc_bias
   DevMem dw, db, dg;
   {
     std::lock_guard<std::mutex> lk(c->mu);
-    HIP_TRY(c, hipSetDevice(c->device));
+    DEVICE_SCOPE(c);
     if (nw) HIP_TRY(c, hipMalloc(&dw.p, nw * sizeof(float)));
     if (nf) HIP_TRY(c, hipMalloc(&db.p, nf * sizeof(float)));
     HIP_TRY(c, hipMalloc(&dg.p, n_grad * sizeof(float)));
@@ -1578,7 +1604,7 @@ int fleet_model_version(fleet_ctx* c, const float* weights, const int32_t* dims,
                         size_t n_biases, float* weights_out, float* biases_out) {
   if (!c || (n_biases && (!biases || !biases_out))) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   size_t n = 0;
   int rc = model_total(c, dims, n_mats, &n);
   if (rc) return rc;
@@ -1622,7 +1648,7 @@ const char* fleet_update_kernel(size_t len) {
 int fleet_selftest_digest(fleet_ctx* c, int fn, uint64_t* out) {
   if (!c || !out || fn < 0 || fn > 20) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
-  HIP_TRY(c, hipSetDevice(c->device));
+  DEVICE_SCOPE(c);
   unsigned long long* d = nullptr;
   HIP_TRY(c, hipMalloc((void**)&d, sizeof(unsigned long long)));
   HIP_TRY(c, hipMemsetAsync(d, 0, sizeof(unsigned long long), c->stream));

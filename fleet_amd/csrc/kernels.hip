@@ -8,6 +8,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1020,9 +1021,11 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
   // bytes once, instead of three dword loads over the same lines); two rows in
   // flight ahead of the one being encoded
   typedef float f3 __attribute__((ext_vector_type(3)));
+  // 12*g is only 4-byte aligned: the load's type promises no more than that
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
   auto load = [&](int rr) -> f3 {
     const float* p = v + (size_t)(rr - row0) * vpitch;
-    if (r == 3) return *reinterpret_cast<const f3*>(p);
+    if (r == 3) return *reinterpret_cast<const f3u*>(p);
     return f3{p[0], r > 1 ? p[1] : 0.0f, 0.0f};
   };
   auto emit = [&](int rr, const float (&x)[3]) {
@@ -1732,15 +1735,25 @@ static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t -
 // (a multiple of one wave per SIMD of the current device), or -1 when the grid is
 // under one round (the plain stream grid then).
 static int device_simds() {
-  static int simds = 0;
-  if (!simds) {
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-    simds = 4 * cus;
+  // per device (a process may drive several GPUs, one launching thread each), set
+  // once per device with an atomic store: concurrent first calls compute the same value
+  static std::atomic<int> simds[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    (void)hipGetLastError();
+    return 4 * 256;
   }
-  return simds;
+  int v = simds[dev].load(std::memory_order_relaxed);
+  if (!v) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
+      (void)hipGetLastError();
+      cus = 256;
+    }
+    v = 4 * cus;
+    simds[dev].store(v, std::memory_order_relaxed);
+  }
+  return v;
 }
 static int stream_full_rounds_blocks(int64_t groups) {
   const int simds = device_simds();

@@ -8,7 +8,16 @@ fo_update_fused, parity status in oracle/fleet_oracle.h) run on
 the uploads cut down to those groups. The full-size uploads are generated and
 encoded on the GPU (k_synth, k_encode_f32), aggregated by the kernel the launch
 plan picks at that size, and ~1,500 random groups plus the (padded) last group
-are checked byte for byte, with merged_f32 at the same positions bitwise."""
+are checked byte for byte, with merged_f32 at the same positions bitwise.
+
+The same uploads then go through the pipelined step the bench times
+(fleet_update_encode_device: k_update_encode<256> on the stream sizes,
+k_update_tiled_encode at CIFAR sizes) at the full client count, with a second
+synthetic batch as the next round's values: its merged text and merged_f32 are
+checked against the same oracle result, and the next batch's uploads it writes
+against the oracle's client encode (fo_encode_floats, Base64.cpp:140-205) of the
+sampled values -- Base64 groups are independent, so the cut-down text of the
+sampled groups is the encode of the sampled values."""
 import numpy as np
 import pytest
 
@@ -60,12 +69,33 @@ def test_full_size_sampled_groups(codec, oracle, name):
     cols = (16 * sel[:, None] + np.arange(16)[None, :]).reshape(-1)
     cols = cols[: cols.size - (16 - tail)]
     cols_t = torch.from_numpy(cols).to(dev)
-    sub = text.index_select(1, cols_t).cpu().numpy()
-    got = merged.index_select(0, cols_t).cpu().numpy().tobytes()
     pos = (3 * sel[:, None] + np.arange(3)[None, :]).reshape(-1)
     pos = pos[pos < n]
-    got_f32 = merged_f32.index_select(0, torch.from_numpy(pos).to(dev)).cpu().numpy()
-    del text
+    pos_t = torch.from_numpy(pos).to(dev)
+    sub = text.index_select(1, cols_t).cpu().numpy()
+    got = merged.index_select(0, cols_t).cpu().numpy().tobytes()
+    got_f32 = merged_f32.index_select(0, pos_t).cpu().numpy()
+    del merged, merged_f32
+
+    # the pipelined step at full M: this batch's aggregation + the next batch's encode
+    # (peak: the uploads, the next batch's values and its uploads)
+    free, _ = torch.cuda.mem_get_info()
+    need = M * 16 * groups + M * 12 * groups + 4 * 2**30
+    assert free > need, f"{name}: {free / 2**30:.1f} GiB free, the fused step needs {need / 2**30:.1f}"
+    values_next = torch.empty((M, 3 * groups), dtype=torch.float32, device=dev)
+    codec.synth_device(20261018, values_next, n, hp, lay.header_values())
+    text_next = torch.empty_like(text)
+    fmerged = torch.zeros(16 * groups, dtype=torch.uint8, device=dev)
+    fmerged_f32 = torch.zeros(3 * groups, dtype=torch.float32, device=dev)
+    codec.update_encode_device(text, L, dampen, hp, fmerged, fmerged_f32, values_next, text_next)
+    torch.cuda.synchronize()
+    codec.check()
+    kernel = F.update_encode_kernel(L)
+    fgot = fmerged.index_select(0, cols_t).cpu().numpy().tobytes()
+    fgot_f32 = fmerged_f32.index_select(0, pos_t).cpu().numpy()
+    nsub = text_next.index_select(1, cols_t).cpu().numpy()
+    nvals = values_next.index_select(1, pos_t).cpu().numpy()
+    del text, text_next, values_next, fmerged, fmerged_f32
     torch.cuda.empty_cache()
 
     hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))[pos]
@@ -74,6 +104,12 @@ def test_full_size_sampled_groups(codec, oracle, name):
     assert len(got) == 16 * (sel.size - 1) + tail and len(ups) == M
     assert got == exp, name
     assert np.array_equal(got_f32.view(np.uint32), exp_f32.view(np.uint32)), name
+    # the timed kernel (k_update_encode / k_update_tiled_encode) at the full client count
+    assert fgot == exp, (name, kernel)
+    assert np.array_equal(fgot_f32.view(np.uint32), exp_f32.view(np.uint32)), (name, kernel)
+    for c in range(M):
+        assert nsub[c].tobytes() == oracle.encode_floats(nvals[c]), (name, kernel, c)
+    print(name, M, kernel)
 
 
 def test_full_size_host_ingress_paths(oracle):
