@@ -142,6 +142,21 @@ def lib() -> C.CDLL:
         "fleet_model_get_lrate": (C.c_double, [vp]),
         "fleet_model_shape": (i32, [vp, szp, szp, C.POINTER(i32), C.POINTER(i32)]),
         "fleet_model_export": (i32, [vp, i32, vp, sz, vp, sz]),
+        "fleet_sampler_create": (i32, [vp, C.c_char_p, i32, i32, i32, i32, i32, C.POINTER(vp)]),
+        "fleet_sampler_create_from": (i32, [vp, vp, vp, sz, i32, i32, i32, i32, i32, i32, i32, C.POINTER(vp)]),
+        "fleet_sampler_destroy": (None, [vp]),
+        "fleet_sampler_last_error": (C.c_char_p, [vp]),
+        "fleet_updater_reseed": (None, [i32]),
+        "fleet_sampler_set_hyper": (i32, [vp, i32, C.c_double, C.c_double]),
+        "fleet_sampler_set_teacher": (i32, [vp, vp, sz, vp, sz]),
+        "fleet_sampler_minibatch": (i32, [vp, i32, C.c_float, vp, sz, szp]),
+        "fleet_sampler_minibatch_len": (sz, [vp, i32]),
+        "fleet_sampler_num_labels": (i32, [vp]),
+        "fleet_sampler_has_outlier": (i32, [vp]),
+        "fleet_sampler_num_samples": (sz, [vp]),
+        "fleet_sampler_bucket": (i32, [vp, i32, vp, sz, szp]),
+        "fleet_sampler_sorted_index": (i32, [vp, vp, sz, szp]),
+        "fleet_sampler_last_indices": (i32, [vp, vp, sz, szp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

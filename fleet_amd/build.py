@@ -27,7 +27,8 @@ ARCH = os.environ.get("FLEET_OFFLOAD_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", f"-I{INCLUDE}", f"-I{CSRC}"]
 
-SOURCES = [("kernels.hip", True), ("model_codec.hip", True), ("fleet_codec.cpp", True), ("model_state.cpp", True), ("teacher.hip", True)]
+SOURCES = [("kernels.hip", True), ("model_codec.hip", True), ("fleet_codec.cpp", True), ("model_state.cpp", True), ("teacher.hip", True),
+           ("sampler_state.cpp", True)]
 
 
 def _newer(target: str, deps) -> bool:

@@ -778,14 +778,19 @@ int fleet_update(fleet_ctx* c, const char* const* uploads, const size_t* lens, i
 
 namespace {
 
-// true when [p, p + bytes) is page-locked host memory the GPUs can DMA from
-bool is_pinned(const void* p) {
-  hipPointerAttribute_t a;
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return a.type == hipMemoryTypeHost;
+// Ranges page-locked by fleet_host_register (process-wide: every context's
+// device DMAs from them). The copy-free row path requires the WHOLE row range
+// to lie inside ONE live registration -- not just its two end bytes, which a
+// freed and reallocated buffer could still satisfy.
+std::mutex g_reg_mu;
+std::vector<std::pair<uintptr_t, size_t>> g_registered;  // (base, bytes)
+
+bool in_one_registration(const void* p, size_t bytes) {
+  const uintptr_t a = (uintptr_t)p;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (const auto& r : g_registered)
+    if (a >= r.first && bytes <= r.second && a - r.first <= r.second - bytes) return true;
+  return false;
 }
 
 int update_multi_impl(fleet_ctx* const* ctxs, int n_ctx, const char* const* uploads, const size_t* lens, int M,
@@ -857,7 +862,7 @@ int update_rows_impl(fleet_ctx* const* ctxs, int n_ctx, const char* rows, size_t
   std::vector<const char*> ptrs((size_t)M);
   std::vector<size_t> lens((size_t)M, len);
   for (int i = 0; i < M; ++i) ptrs[(size_t)i] = rows + (size_t)i * row_pitch;
-  const bool pinned = is_pinned(rows) && is_pinned(rows + (size_t)(M - 1) * row_pitch + (len ? len - 1 : 0));
+  const bool pinned = in_one_registration(rows, (size_t)(M - 1) * row_pitch + len);
   return update_multi_impl(ctxs, n_ctx, ptrs.data(), lens.data(), M, dampen, merged, cap, out_len, merged_f32,
                            pinned ? rows : nullptr, row_pitch);
 }
@@ -887,7 +892,23 @@ int fleet_host_register(fleet_ctx* c, void* ptr, size_t bytes) {
   if (!c || !ptr || !bytes) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DEVICE_SCOPE(c);
+  const uintptr_t a = (uintptr_t)ptr;
+  {
+    // a live registration overlapping the new range belongs to memory that was
+    // freed and reused (a collected direct buffer): it is released first
+    std::lock_guard<std::mutex> rk(g_reg_mu);
+    for (size_t i = g_registered.size(); i-- > 0;) {
+      const auto r = g_registered[i];
+      if (r.first < a + bytes && a < r.first + r.second) {
+        (void)hipHostUnregister((void*)r.first);
+        (void)hipGetLastError();
+        g_registered.erase(g_registered.begin() + (long)i);
+      }
+    }
+  }
   HIP_TRY(c, hipHostRegister(ptr, bytes, hipHostRegisterPortable));
+  std::lock_guard<std::mutex> rk(g_reg_mu);
+  g_registered.emplace_back(a, bytes);
   return FLEET_OK;
 }
 
@@ -895,6 +916,11 @@ int fleet_host_unregister(fleet_ctx* c, void* ptr) {
   if (!c || !ptr) return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
   DEVICE_SCOPE(c);
+  {
+    std::lock_guard<std::mutex> rk(g_reg_mu);
+    for (size_t i = g_registered.size(); i-- > 0;)
+      if (g_registered[i].first == (uintptr_t)ptr) g_registered.erase(g_registered.begin() + (long)i);
+  }
   HIP_TRY(c, hipHostUnregister(ptr));
   return FLEET_OK;
 }
@@ -917,6 +943,15 @@ int dev_params(fleet_ctx* c, hipStream_t s, size_t n, int M, const double* dampe
   if (!c->dev_params_valid || c->dev_hdr != hdr_words || c->dev_dampen.size() != (size_t)M ||
       std::memcmp(c->dev_dampen.data(), dampen, sizeof(double) * (size_t)M) != 0) {
     int rc;
+    // new parameters are uploaded synchronously, which a stream under capture
+    // cannot do (it would invalidate the capture): the caller makes one eager
+    // call with them first (fleet_codec.h, device-resident entry points)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) == hipSuccess && cap != hipStreamCaptureStatusNone)
+      return fail(c, FLEET_ERR_ARG,
+                  "dampen / header positions changed while the stream is being captured: make one eager call "
+                  "with them before capturing");
+    (void)hipGetLastError();
     HIP_TRY(c, hipStreamSynchronize(s));
     if ((size_t)M > c->d_dev_dampen_cap) {  // grow; the old buffer may sit in a captured graph: retire it
       if (c->d_dev_dampen) c->retired.push_back(c->d_dev_dampen);

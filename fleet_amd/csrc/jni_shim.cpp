@@ -19,17 +19,29 @@
 //     Java_apps_cppNN_CppNNUpdater_getParametersNative :244-280
 //     Java_apps_cppNN_CppNNUpdater_getModelParametersNative :227-242
 //     ..._modelsSize, _getPriority/_setPriority, _getCurrEpoch/_setCurrEpoch, _getLrate :129-159,324-327
+//     ..._getNumLabels, _hasOutlier                    :129-137
+//     ..._printParamsNative                            :304-322
+//   the offline sampler (fleet_sampler; dataset, buckets, client rotation, E/sigma/C)
+//     Java_apps_cppNN_CppNNOfflineSampler_initSampler  :385-551
+//     Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch :677-699
+// so no native of libnative.so is reached any more: every global the
+// reference's natives share (the model, E/sigma/C, the libc rand() stream that
+// initSampler and initUpdater reseed) lives behind this one library;
 // and the batched natives of an updater that makes one call per update:
 //   byte[] apps.cppNN.FleetUpdater.aggregateNative(byte[][] uploads, double[] dampen)
 //   byte[] apps.cppNN.FleetUpdater.aggregateDirectNative(ByteBuffer rows, int M, int len, int rowPitch,
 //                                                          double[] dampen)
 //   boolean apps.cppNN.FleetUpdater.registerDirectNative(ByteBuffer rows)
-// The sampler's natives (initSampler / getMiniBatch, dataset loading) stay in
-// the reference's libnative.so (load order, learning-rate note).
+//   void apps.cppNN.FleetUpdater.unregisterDirectNative(ByteBuffer rows)
 //
 // Environment: FLEET_GPUS = devices the batched natives spread one update over
 // (element sharding, fleet_update_multi; default 1, "all" = every visible GPU);
-// FLEET_DISTILLATION_MODE = the reference's compile-time DISTILLATION_MODE (default 1).
+// FLEET_DISTILLATION_MODE = the reference's compile-time DISTILLATION_MODE (default 1);
+// FLEET_SAMPLER_IID / FLEET_SAMPLER_OUTLIER / FLEET_SAMPLER_CLIENTS = the
+// reference's source-edited sampler globals iid / outlier / numClients
+// (cppNN_backend.cpp:59-61; defaults 0, 0, 10). DISTILLATION_MODE=1 with iid
+// sampling is refused at initSampler: its mini-batches carry the outputs of a
+// teacher network initSampler trains (:480-546), which is not rebuilt.
 //
 // Same argument meaning and results as the reference; failures return null / 0
 // (Java sees a NullPointerException at the caller) and print the C-ABI error
@@ -53,7 +65,15 @@ namespace {
 std::mutex g_mu;
 std::vector<fleet_ctx*> g_ctxs;  // [0]: per-op natives, the model; all: the batched update
 bool g_init = false;
+// the updater's model and the sampler, each used only under its lock (a fetch
+// replaces the model while another request thread may be reading it)
+std::mutex g_model_mu;
 fleet_model* g_model = nullptr;
+std::mutex g_sampler_mu;
+fleet_sampler* g_sampler = nullptr;
+int g_E = 0;  // initUpdater's globals (cppNN_backend.cpp:47-50; zero until it runs)
+double g_sigma = 0.0, g_C = 0.0;
+constexpr int kSeed = 1;  // cppNN_backend.cpp:71
 std::mutex g_rows_mu;
 std::vector<char> g_rows;  // row staging of aggregateNative when the JVM cannot grant M local refs
 
@@ -85,6 +105,11 @@ std::vector<fleet_ctx*> all_ctx() {
 int distillation_mode() {
   const char* e = std::getenv("FLEET_DISTILLATION_MODE");
   return e ? (std::atoi(e) != 0) : 1;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
 }
 
 // JVM byte[] -> host bytes (no NUL terminator needed: lengths are explicit)
@@ -314,6 +339,19 @@ JNIEXPORT jboolean JNICALL Java_apps_cppNN_FleetUpdater_registerDirectNative(JNI
   return rc == FLEET_OK ? JNI_TRUE : JNI_FALSE;
 }
 
+// Releases the page lock before the buffer is dropped (its Cleaner frees the
+// memory). A registration left behind is released anyway when a later
+// registerDirectNative covers the same memory (fleet_host_register), and rows
+// are only DMA'd copy-free from inside one live registration.
+JNIEXPORT void JNICALL Java_apps_cppNN_FleetUpdater_unregisterDirectNative(JNIEnv* env, jobject, jobject buf) {
+  fleet_ctx* c = ctx();
+  if (!c || !buf) return;
+  void* p = env->GetDirectBufferAddress(buf);
+  if (!p) return;
+  const int rc = fleet_host_unregister(c, p);
+  if (rc != FLEET_OK) fail(c, "unregisterDirectNative", rc);
+}
+
 // ------------------------------------------------------------------- model
 
 JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_fetchParamsNative(JNIEnv* env, jobject, jbyteArray input) {
@@ -327,14 +365,25 @@ JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_fetchParamsNative(JNIEnv* en
     fail(c, "fetchParamsNative", rc);
     return;
   }
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> lk(g_model_mu);
   if (g_model) fleet_model_destroy(g_model);
   g_model = m;
 }
 
+// initUpdater (:161-225): srand(seed) and the two rand() draws of its
+// cnn.train_class (fleet_updater_reseed), E / sigma / C for the sampler's
+// mini-batch headers, and the model part (lrates, the first version).
 JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_initUpdater(JNIEnv* env, jobject, jdoubleArray lrates, jint E,
                                                                 jdouble sigma, jdouble C) {
-  (void)E, (void)sigma, (void)C;  // the sampler's mini-batch header values (libnative.so keeps them)
+  {
+    std::lock_guard<std::mutex> lk(g_sampler_mu);
+    fleet_updater_reseed(kSeed);
+    g_E = E;
+    g_sigma = sigma;
+    g_C = C;
+    if (g_sampler) fleet_sampler_set_hyper(g_sampler, E, sigma, C);
+  }
+  std::lock_guard<std::mutex> lk(g_model_mu);
   if (!g_model || !lrates) return;
   const jsize n = env->GetArrayLength(lrates);
   std::vector<double> lr((size_t)std::max<jsize>(n, 0));
@@ -345,14 +394,17 @@ JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_initUpdater(JNIEnv* env, job
 
 JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_descentNative(JNIEnv* env, jobject, jbyteArray input,
                                                                   jint clientBatchSize, jint staleSize) {
-  if (!g_model || !input) return;
+  if (!input) return;
   Bytes in(env, input);
   if (!in.ok()) return;
+  std::lock_guard<std::mutex> lk(g_model_mu);
+  if (!g_model) return;
   const int rc = fleet_model_descent(g_model, in.data(), (size_t)in.n, clientBatchSize, staleSize);
   if (rc != FLEET_OK) mfail("descentNative", rc);
 }
 
 static jbyteArray model_text(JNIEnv* env, jint p, bool params) {
+  std::lock_guard<std::mutex> lk(g_model_mu);
   if (!g_model) return nullptr;
   auto fn = params ? fleet_model_get_params : fleet_model_get_model_params;
   size_t need = 0;
@@ -373,22 +425,118 @@ JNIEXPORT jbyteArray JNICALL Java_apps_cppNN_CppNNUpdater_getModelParametersNati
 }
 
 JNIEXPORT jint JNICALL Java_apps_cppNN_CppNNUpdater_modelsSize(JNIEnv*, jobject) {
+  std::lock_guard<std::mutex> lk(g_model_mu);
   return g_model ? fleet_model_count(g_model) : 0;
 }
 JNIEXPORT jint JNICALL Java_apps_cppNN_CppNNUpdater_getPriority(JNIEnv*, jobject) {
+  std::lock_guard<std::mutex> lk(g_model_mu);
   return g_model ? fleet_model_get_priority(g_model) : 0;
 }
 JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_setPriority(JNIEnv*, jobject, jint p) {
+  std::lock_guard<std::mutex> lk(g_model_mu);
   if (g_model) fleet_model_set_priority(g_model, p);
 }
 JNIEXPORT jint JNICALL Java_apps_cppNN_CppNNUpdater_getCurrEpoch(JNIEnv*, jobject) {
+  std::lock_guard<std::mutex> lk(g_model_mu);
   return g_model ? fleet_model_get_epoch(g_model) : 0;
 }
 JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_setCurrEpoch(JNIEnv*, jobject, jint e) {
+  std::lock_guard<std::mutex> lk(g_model_mu);
   if (g_model) fleet_model_set_epoch(g_model, e);
 }
 JNIEXPORT jdouble JNICALL Java_apps_cppNN_CppNNUpdater_getLrate(JNIEnv*, jobject) {
+  std::lock_guard<std::mutex> lk(g_model_mu);
   return g_model ? fleet_model_get_lrate(g_model) : 0.0;
+}
+
+// getNumLabels / hasOutlier (:129-137): the sampler's globals (0 / the
+// configured outlier flag before initSampler, like the zero-initialised globals)
+JNIEXPORT jint JNICALL Java_apps_cppNN_CppNNUpdater_getNumLabels(JNIEnv*, jobject) {
+  std::lock_guard<std::mutex> lk(g_sampler_mu);
+  return g_sampler ? fleet_sampler_num_labels(g_sampler) : 0;
+}
+JNIEXPORT jboolean JNICALL Java_apps_cppNN_CppNNUpdater_hasOutlier(JNIEnv*, jobject) {
+  return env_int("FLEET_SAMPLER_OUTLIER", 0) != 0 ? JNI_TRUE : JNI_FALSE;
+}
+
+// printParamsNative (:304-322): the upload's int32 codes on stdout
+JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_printParamsNative(JNIEnv* env, jobject, jbyteArray input) {
+  fleet_ctx* c = ctx();
+  if (!c || !input) return;
+  Bytes in(env, input);
+  if (!in.ok()) return;
+  std::vector<int32_t> codes(fleet_b64_count((size_t)in.n) + 3);
+  size_t n = 0;
+  const int rc = fleet_decode_i32(c, in.data(), (size_t)in.n, codes.data(), codes.size(), &n);
+  if (rc != FLEET_OK) {
+    fail(c, "printParamsNative", rc);
+    return;
+  }
+  std::string line = "Got Numbers: ";
+  char buf[16];
+  for (size_t i = 0; i < n; ++i) {
+    std::snprintf(buf, sizeof buf, "%d ", codes[i]);
+    line += buf;
+  }
+  std::printf("%s\n", line.c_str());
+  std::fflush(stdout);
+}
+
+// ----------------------------------------------------------------- sampler
+
+// initSampler (:385-551) with the reference's source-edited globals taken from
+// the environment (FLEET_SAMPLER_*); the dataset stays in this library.
+JNIEXPORT void JNICALL Java_apps_cppNN_CppNNOfflineSampler_initSampler(JNIEnv* env, jobject, jstring prefix) {
+  fleet_ctx* c = ctx();
+  if (!c || !prefix) return;
+  const int iid = env_int("FLEET_SAMPLER_IID", 0) != 0, outlier = env_int("FLEET_SAMPLER_OUTLIER", 0) != 0;
+  const int clients = env_int("FLEET_SAMPLER_CLIENTS", 10), mode = distillation_mode();
+  std::printf("IID: %d\nOutlier: %d\n", iid, outlier);
+  std::fflush(stdout);
+  if (iid && mode) {
+    std::fprintf(stderr,
+                 "[fleet] initSampler: DISTILLATION_MODE=1 with iid sampling is not supported (its mini-batches "
+                 "carry the outputs of the teacher initSampler trains, cppNN_backend.cpp:480-546, not rebuilt)\n");
+    return;
+  }
+  const char* path = env->GetStringUTFChars(prefix, nullptr);
+  if (!path) return;
+  const std::string data_path(path);
+  env->ReleaseStringUTFChars(prefix, path);
+  fleet_sampler* s = nullptr;
+  const int rc = fleet_sampler_create(c, data_path.c_str(), iid, outlier, clients, mode, kSeed, &s);
+  if (rc != FLEET_OK) return;  // fleet_sampler_create printed the reason
+  std::lock_guard<std::mutex> lk(g_sampler_mu);
+  fleet_sampler_set_hyper(s, g_E, g_sigma, g_C);
+  if (g_sampler) fleet_sampler_destroy(g_sampler);
+  g_sampler = s;
+  std::printf("Train data size: %zu\n", fleet_sampler_num_samples(s));
+  std::fflush(stdout);
+}
+
+// getMiniBatch (:677-699): batch_size * E samples of the current client, the
+// header's learning rate from the updater's model (cnn.get_learning_rate(),
+// moved along lrates by descentNative).
+JNIEXPORT jbyteArray JNICALL Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch(JNIEnv* env, jobject, jint batch_size) {
+  float lr = 0.0f;
+  {
+    std::lock_guard<std::mutex> lk(g_model_mu);
+    if (g_model) lr = (float)fleet_model_get_lrate(g_model);
+  }
+  std::lock_guard<std::mutex> lk(g_sampler_mu);
+  if (!g_sampler) {
+    std::fprintf(stderr, "[fleet] getMiniBatch: no sampler (initSampler failed or was not called)\n");
+    return nullptr;
+  }
+  const size_t len = fleet_sampler_minibatch_len(g_sampler, batch_size);
+  std::vector<char> out(len + 16);
+  size_t n = 0;
+  const int rc = fleet_sampler_minibatch(g_sampler, batch_size, lr, out.data(), out.size(), &n);
+  if (rc != FLEET_OK) {
+    std::fprintf(stderr, "[fleet] getMiniBatch failed (%d): %s\n", rc, fleet_sampler_last_error(g_sampler));
+    return nullptr;
+  }
+  return to_java(env, out.data(), n);
 }
 
 }  // extern "C"

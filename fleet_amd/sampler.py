@@ -13,9 +13,13 @@ forward pass (uniformSample's teacher.forward, :603) runs on the GPU too
 training in initSampler (:480-546: 300 rand()-drawn MNIST samples) is dataset
 plumbing and stays with the caller, who hands over the trained weights.
 
-Bucket construction (initSampler :409-470: label sort, 2-shard buckets,
-``std::random_shuffle``) is dataset plumbing outside the hot path; buckets are
-given.
+``NativeSampler`` is the whole sampler state of the reference's backend in the
+C-ABI (fleet_amd/csrc/sampler_state.cpp, the fleet_sampler_* entry points the
+JNI shim's initSampler / getMiniBatch use): the MNIST set loaded by
+initSampler's parser, the non-IID buckets it builds (:409-479: label sort,
+2-shard buckets, ``std::random_shuffle`` over libc ``rand()``), the client
+rotation and initUpdater's E / sigma / C. ``OfflineSampler`` below takes the
+buckets as given (any dataset).
 """
 from __future__ import annotations
 
@@ -138,3 +142,94 @@ class Teacher:
 
     def __call__(self, idx) -> np.ndarray:
         return self.codec.teacher_forward(self.w, self.b, self.images, idx, self.TEMPERATURE)
+
+
+class NativeSampler:
+    """fleet_sampler (include/fleet_codec.h): CppNNOfflineSampler's native state.
+
+    ``NativeSampler(codec, data_path=...)`` is initSampler on an MNIST directory;
+    ``NativeSampler(codec, images=..., labels=...)`` the same over a dataset in
+    memory. ``codec`` may be None for the host state alone (buckets)."""
+
+    def __init__(self, codec, data_path: Optional[str] = None, images=None, labels=None, num_labels: int = 10,
+                 iid: bool = False, outlier: bool = False, num_clients: int = 10, distillation_mode: int = 1,
+                 seed: int = 1):
+        from . import lib, FleetError
+        self._L = L = lib()
+        self.codec = codec
+        h = ctypes.c_void_p()
+        cp = codec._h if codec is not None else None
+        if data_path is not None:
+            rc = L.fleet_sampler_create(cp, data_path.encode(), int(iid), int(outlier), num_clients,
+                                        distillation_mode, seed, ctypes.byref(h))
+        else:
+            self._images = np.ascontiguousarray(images, dtype=np.float32)
+            self._labels = np.ascontiguousarray(labels, dtype=np.int32)
+            rc = L.fleet_sampler_create_from(cp, self._images.ctypes.data, self._labels.ctypes.data,
+                                             len(self._labels), self._images.shape[1], num_labels, int(iid),
+                                             int(outlier), num_clients, distillation_mode, seed, ctypes.byref(h))
+        if rc != 0:
+            raise FleetError(rc, "fleet_sampler_create failed (see stderr)")
+        self._h = h.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.fleet_sampler_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        if rc != 0:
+            from . import FleetError
+            raise FleetError(rc, self._L.fleet_sampler_last_error(self._h).decode())
+
+    @staticmethod
+    def reseed_updater(seed: int = 1) -> None:
+        """initUpdater's srand(seed) and its train_class's two rand() draws."""
+        from . import lib
+        lib().fleet_updater_reseed(seed)
+
+    def set_hyper(self, E: int, sigma: float, C: float) -> None:
+        self._check(self._L.fleet_sampler_set_hyper(self._h, int(E), float(sigma), float(C)))
+
+    def set_teacher(self, w, b) -> None:
+        self._tw = np.ascontiguousarray(w, dtype=np.float32).reshape(-1)
+        self._tb = np.ascontiguousarray(b, dtype=np.float32).reshape(-1)
+        self._check(self._L.fleet_sampler_set_teacher(self._h, self._tw.ctypes.data, len(self._tw),
+                                                      self._tb.ctypes.data, len(self._tb)))
+
+    def getMiniBatch(self, batch_size: int, lr: float) -> bytes:  # noqa: N802  (cppNN_backend.cpp:677)
+        n = self._L.fleet_sampler_minibatch_len(self._h, int(batch_size))
+        out = ctypes.create_string_buffer(max(n, 1))
+        got = ctypes.c_size_t(0)
+        self._check(self._L.fleet_sampler_minibatch(self._h, int(batch_size), float(np.float32(lr)), out, n,
+                                                    ctypes.byref(got)))
+        return out.raw[:got.value]
+
+    def _ints(self, fn, *args) -> np.ndarray:
+        n = ctypes.c_size_t(0)
+        fn(self._h, *args, None, 0, ctypes.byref(n))
+        a = np.zeros(max(n.value, 1), np.int32)
+        self._check(fn(self._h, *args, a.ctypes.data, a.size, ctypes.byref(n)))
+        return a[:n.value]
+
+    def bucket(self, client: int) -> np.ndarray:
+        """Positions (in the label-sorted order) of the client's bucket."""
+        return self._ints(self._L.fleet_sampler_bucket, int(client))
+
+    def sorted_index(self) -> np.ndarray:
+        return self._ints(self._L.fleet_sampler_sorted_index)
+
+    def last_indices(self) -> np.ndarray:
+        """Image indices (loaded order) of the last mini-batch."""
+        return self._ints(self._L.fleet_sampler_last_indices)
+
+    @property
+    def num_labels(self) -> int:
+        return self._L.fleet_sampler_num_labels(self._h)
+
+    @property
+    def num_samples(self) -> int:
+        return self._L.fleet_sampler_num_samples(self._h)

@@ -130,15 +130,19 @@ int fleet_update_multi(fleet_ctx* const* ctxs, int n_ctx, const char* const* upl
 /* fleet_update / fleet_update_multi over uploads stored as M rows `row_pitch`
  * bytes apart (row i = upload i, `len` Base64 chars): the ingress of a caller
  * that deserialises the uploads into one buffer (a Java direct ByteBuffer,
- * INTEGRATION.md). When that buffer is page-locked (fleet_host_register, or
- * allocated pinned) every context DMAs its column window straight from it --
- * no host copy at all; otherwise the rows are staged as in fleet_update. */
+ * INTEGRATION.md). When the whole row range lies inside ONE live
+ * fleet_host_register registration every context DMAs its column window
+ * straight from it -- no host copy at all; otherwise the rows are staged as
+ * in fleet_update. */
 int fleet_update_rows(fleet_ctx* ctx, const char* rows, size_t row_pitch, size_t len, int M, const double* dampen,
                       char* merged, size_t cap, size_t* out_len, float* merged_f32);
 int fleet_update_rows_multi(fleet_ctx* const* ctxs, int n_ctx, const char* rows, size_t row_pitch, size_t len, int M,
                             const double* dampen, char* merged, size_t cap, size_t* out_len, float* merged_f32);
 /* Page-lock (hipHostRegister, portable to every device) / release a long-lived
- * host buffer, e.g. the upload rows of fleet_update_rows. */
+ * host buffer, e.g. the upload rows of fleet_update_rows. The registrations
+ * are tracked process-wide: registering a range that overlaps a live
+ * registration releases the old one first (its memory was freed and reused,
+ * e.g. a collected Java direct buffer). */
 int fleet_host_register(fleet_ctx* ctx, void* ptr, size_t bytes);
 int fleet_host_unregister(fleet_ctx* ctx, void* ptr);
 
@@ -153,7 +157,13 @@ int fleet_host_unregister(fleet_ctx* ctx, void* ptr);
  * values [3*group_begin, 3*group_end) of d_merged_f32) are dereferenced, so a
  * rank holding just its window of every upload passes the window's address
  * minus 16*group_begin (3*group_begin floats for merged_f32) and pitch >=
- * 16*(group_end - group_begin): fleet_amd/shard.py does exactly that. */
+ * 16*(group_end - group_begin): fleet_amd/shard.py does exactly that.
+ * Graph capture: the dampen and header words live in ONE device buffer per
+ * context, re-uploaded (synchronously) whenever a call passes different ones.
+ * Every graph captured on the context therefore replays with the parameters of
+ * the context's latest call, and a capture cannot introduce new parameters
+ * (FLEET_ERR_ARG): make one eager call with them first, and do not change them
+ * while captured graphs that must keep the old ones are still replayed. */
 int fleet_update_device(fleet_ctx* ctx, const void* d_uploads, size_t pitch, size_t len, int M,
                         const double* dampen, const int32_t* header_pos, int n_headers, size_t group_begin,
                         size_t group_end, void* d_merged, void* d_merged_f32, void* stream);
@@ -408,6 +418,55 @@ double fleet_model_get_lrate(fleet_model* m);
 int fleet_model_shape(fleet_model* m, size_t* n_weights, size_t* n_biases, int* graph_edges, int* n_layers);
 /* weights / biases of models[version] (version -1: the current `cnn`) */
 int fleet_model_export(fleet_model* m, int version, float* weights, size_t n_weights, float* biases, size_t n_biases);
+
+/* The offline sampler's state (the CppNNOfflineSampler natives
+ * of Server/src/main/c++/cppNN_backend.cpp and the globals they keep). Random
+ * draws come from libc rand(), the process-wide generator the reference uses.
+ * Errors: fleet_sampler_last_error. */
+typedef struct fleet_sampler fleet_sampler;
+/* initSampler (:385-479): srand(seed) (the reference's seed is 1, :71), the
+ * MNIST training set under data_path (commonLib/cppNN/mnist_parser.h:
+ * train-images.idx3-ubyte or train-images-idx3-ubyte and the labels file,
+ * pixels (b / 255) * 2 - 1), numLabels = 10, and with iid == 0 the non-IID
+ * buckets (:411-479): sort_indexes of the labels (std::sort), with outlier != 0
+ * a first bucket of the label-0 samples, then 2*(num_clients - outliers) shards
+ * shuffled and dealt two per client, every bucket shuffled (std::random_shuffle
+ * over rand() % i). iid, outlier and num_clients are the reference's
+ * compile-time globals (:59-61; defaults 0, 0, 10). The teacher's training in
+ * DISTILLATION_MODE=1 (:480-546) is not rebuilt: fleet_sampler_set_teacher.
+ * ctx may be NULL (host state only; fleet_sampler_minibatch then fails). */
+int fleet_sampler_create(fleet_ctx* ctx, const char* data_path, int iid, int outlier, int num_clients,
+                         int distillation_mode, int seed, fleet_sampler** out);
+/* the same over a dataset in memory: images n x F floats, labels n */
+int fleet_sampler_create_from(fleet_ctx* ctx, const float* images, const int32_t* labels, size_t n, int F,
+                              int num_labels, int iid, int outlier, int num_clients, int distillation_mode, int seed,
+                              fleet_sampler** out);
+void fleet_sampler_destroy(fleet_sampler* s);
+const char* fleet_sampler_last_error(const fleet_sampler* s);
+/* initUpdater's generator side effects (:163, :216/:222): srand(seed), then the
+ * two rand() draws of cnn.train_class's random shift (network.h:1840). */
+void fleet_updater_reseed(int seed);
+/* initUpdater's E, sigma, C (:169-171), read by every later mini-batch header */
+int fleet_sampler_set_hyper(fleet_sampler* s, int E, double sigma, double C);
+/* DISTILLATION_MODE=1 with iid sampling: the trained teacher's weights
+ * (fleet_teacher_forward's layout); uniformSample then appends its outputs */
+int fleet_sampler_set_teacher(fleet_sampler* s, const float* w, size_t n_w, const float* b, size_t n_b);
+/* getMiniBatch (:677-699): B = batch_size * E samples -- uniformSample's
+ * rand() % N draws, or nonIIDSample's cursor over the current client's bucket
+ * -- the client rotation advanced, header {E, sigma, C, lr, B, F, numLabels}
+ * (lr = the updater's cnn.get_learning_rate()), encoded on the GPU
+ * (fleet_minibatch). B <= 0 (E = 0 before initUpdater) is FLEET_ERR_ARG: the
+ * reference reads sample 0 of an empty batch there. */
+int fleet_sampler_minibatch(fleet_sampler* s, int batch_size, float lr, char* out, size_t cap, size_t* out_len);
+size_t fleet_sampler_minibatch_len(fleet_sampler* s, int batch_size);
+int fleet_sampler_num_labels(const fleet_sampler* s);   /* getNumLabels (:129-132) */
+int fleet_sampler_has_outlier(const fleet_sampler* s);  /* hasOutlier (:134-137) */
+size_t fleet_sampler_num_samples(const fleet_sampler* s);
+/* introspection (tests): bucket `client` (positions in the label-sorted order),
+ * the label-sorted order itself, and the last request's image indices */
+int fleet_sampler_bucket(fleet_sampler* s, int client, int32_t* out, size_t cap, size_t* n);
+int fleet_sampler_sorted_index(fleet_sampler* s, int32_t* out, size_t cap, size_t* n);
+int fleet_sampler_last_indices(fleet_sampler* s, int32_t* out, size_t cap, size_t* n);
 
 /* Name of the aggregation kernel fleet_update / fleet_update_device launch for
  * an upload of `len` Base64 bytes (or a group window of that many bytes):

@@ -23,14 +23,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "liboracle.so")
 ORACLE_O0_SO = os.path.join(HERE, "liboracle_O0.so")  # same source at -O0 (bench.py's faithful CPU leg)
 REF_MODEL_SO = os.path.join(HERE, "_ref", "libfleetref_model.so")
+SAMPLER_SO = os.path.join(HERE, "libsampler_oracle.so")  # initSampler's buckets (sampler_oracle.cpp)
 
 _c_char_pp = C.POINTER(C.c_char_p)
 
 
 def build(force: bool = False) -> None:
     """Compile liboracle.so (and the reference build when /root/reference exists)."""
-    if force or not os.path.exists(ORACLE_SO) or not os.path.exists(ORACLE_O0_SO):
-        subprocess.check_call(["make", "-s", "liboracle.so", "liboracle_O0.so"], cwd=HERE)
+    if force or not all(os.path.exists(p) for p in (ORACLE_SO, ORACLE_O0_SO, SAMPLER_SO)):
+        subprocess.check_call(["make", "-s", "liboracle.so", "liboracle_O0.so", "libsampler_oracle.so"], cwd=HERE)
     if os.path.isdir("/root/reference/Server") and (force or not os.path.exists(REF_MODEL_SO)):
         subprocess.check_call(["make", "-s", "ref"], cwd=HERE)
 
@@ -461,3 +462,27 @@ class ReferenceModel:
         wo, bo = np.empty_like(w), np.empty_like(b)
         self.lib.ref_mnist_version_copy(w.ctypes.data, b.ctypes.data, wo.ctypes.data, bo.ctypes.data)
         return wo, bo
+
+
+def sampler_buckets(labels, num_clients: int = 10, outlier: bool = False, seed: int = 1):
+    """initSampler's non-IID buckets (sampler_oracle.cpp: the C++ library's own
+    std::sort / std::random_shuffle over libc rand() after srand(seed)).
+    Returns (sorted_index[n], [bucket positions into the sorted order, per client])."""
+    L = C.CDLL(SAMPLER_SO)
+    L.fo_sampler_buckets.restype = C.c_int
+    L.fo_sampler_buckets.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                     C.c_long, C.c_void_p]
+    lab = np.ascontiguousarray(labels, dtype=np.int32)
+    n = len(lab)
+    srt = np.zeros(n, np.int32)
+    flat = np.zeros(n + 1, np.int32)
+    lens = np.zeros(num_clients, np.int32)
+    k = L.fo_sampler_buckets(lab.ctypes.data, n, num_clients, int(outlier), seed, srt.ctypes.data, flat.ctypes.data,
+                             n, lens.ctypes.data)
+    if k < 0:
+        raise ValueError("dataset too small for the clients")
+    out, o = [], 0
+    for i in range(k):
+        out.append(flat[o:o + lens[i]].copy())
+        o += lens[i]
+    return srt, out

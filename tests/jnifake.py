@@ -38,6 +38,8 @@ def fakejvm():
     L.fakejvm_new_object_array.argtypes = [vp, C.c_int]
     L.fakejvm_new_direct.restype = vp
     L.fakejvm_new_direct.argtypes = [vp, C.c_long]
+    L.fakejvm_new_string.restype = vp
+    L.fakejvm_new_string.argtypes = [C.c_char_p]
     L.fakejvm_array_len.restype = C.c_int
     L.fakejvm_array_len.argtypes = [vp]
     L.fakejvm_array_data.restype = vp
@@ -74,6 +76,10 @@ def new_object_array(ptrs) -> int:
 
 def new_direct(buf: np.ndarray) -> int:
     return fakejvm().fakejvm_new_direct(buf.ctypes.data, buf.nbytes)
+
+
+def new_string(text: str) -> int:
+    return fakejvm().fakejvm_new_string(text.encode())
 
 
 def read_bytes(p: int) -> bytes:

@@ -328,6 +328,14 @@ __attribute__((visibility("default"))) void* fakejvm_new_direct(void* p, long ca
   return o;
 }
 
+// a java.lang.String (modified UTF-8 = the bytes given, NUL-terminated)
+__attribute__((visibility("default"))) void* fakejvm_new_string(const char* utf) {
+  const jsize n = (jsize)std::strlen(utf);
+  Obj* o = make(STRING, n, 1);
+  std::memcpy(o->data.data(), utf, (size_t)n);
+  return o;
+}
+
 __attribute__((visibility("default"))) int fakejvm_array_len(const void* a) { return a ? O(a)->len : -1; }
 __attribute__((visibility("default"))) const void* fakejvm_array_data(const void* a) {
   return a ? O(a)->data.data() : nullptr;

@@ -21,10 +21,14 @@ BYTES_OUT = {
     "Java_apps_cppNN_FleetUpdater_aggregateNative": 2, UPDATER + "getParametersNative": None,
     UPDATER + "getModelParametersNative": None, "Java_apps_cppNN_FleetUpdater_aggregateDirectNative": None,
 }
+SAMPLER = "Java_apps_cppNN_CppNNOfflineSampler_"
 SYMBOLS = list(BYTES_OUT) + ["Java_utils_ByteVec_getNorm", UPDATER + "fetchParamsNative", UPDATER + "initUpdater",
                              UPDATER + "descentNative", UPDATER + "modelsSize", UPDATER + "getPriority",
                              UPDATER + "setPriority", UPDATER + "getCurrEpoch", UPDATER + "setCurrEpoch",
-                             UPDATER + "getLrate", "Java_apps_cppNN_FleetUpdater_registerDirectNative"]
+                             UPDATER + "getLrate", UPDATER + "getNumLabels", UPDATER + "hasOutlier",
+                             UPDATER + "printParamsNative", SAMPLER + "initSampler", SAMPLER + "getMiniBatch",
+                             "Java_apps_cppNN_FleetUpdater_registerDirectNative",
+                             "Java_apps_cppNN_FleetUpdater_unregisterDirectNative"]
 
 
 def load():
@@ -47,13 +51,20 @@ def load():
         UPDATER + "getModelParametersNative": [vp, vp, i32], UPDATER + "modelsSize": [vp, vp],
         UPDATER + "getCurrEpoch": [vp, vp], UPDATER + "setCurrEpoch": [vp, vp, i32],
         UPDATER + "getPriority": [vp, vp], UPDATER + "setPriority": [vp, vp, i32], UPDATER + "getLrate": [vp, vp],
+        UPDATER + "getNumLabels": [vp, vp], UPDATER + "hasOutlier": [vp, vp], UPDATER + "printParamsNative": [vp, vp, vp],
+        SAMPLER + "initSampler": [vp, vp, vp], SAMPLER + "getMiniBatch": [vp, vp, i32],
+        "Java_apps_cppNN_FleetUpdater_unregisterDirectNative": [vp, vp, vp],
     }
     for s, a in sig.items():
         getattr(L, s).argtypes = a
     L.Java_utils_ByteVec_getNorm.restype = f64
     L.Java_apps_cppNN_CppNNUpdater_getLrate.restype = f64
     L.Java_apps_cppNN_FleetUpdater_registerDirectNative.restype = C.c_uint8
-    for s in ("modelsSize", "getCurrEpoch", "getPriority"):
+    L.Java_apps_cppNN_CppNNUpdater_hasOutlier.restype = C.c_uint8
+    L.Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch.restype = vp
+    L.Java_apps_cppNN_FleetUpdater_unregisterDirectNative.restype = None
+    L.Java_apps_cppNN_CppNNUpdater_printParamsNative.restype = None
+    for s in ("modelsSize", "getCurrEpoch", "getPriority", "getNumLabels"):
         getattr(L, UPDATER + s).restype = i32
     return L
 
@@ -61,6 +72,21 @@ def load():
 def test_shim_exports_reference_symbols():
     L = load()
     for s in SYMBOLS:
+        assert hasattr(L, s), s
+
+
+def test_shim_exports_every_reference_native():
+    """Every Java_* native of the reference's server backend (cppNN_backend.cpp: 22
+    symbols) is served by the shim, so the JVM never binds one of them
+    to libnative.so."""
+    ref = ["getNumLabels", "hasOutlier", "setCurrEpoch", "getCurrEpoch", "setPriority", "getPriority", "getLrate",
+           "initUpdater", "getModelParametersNative", "getParametersNative", "fetchParamsNative",
+           "printParamsNative", "modelsSize", "descentNative", "getFlatGradient", "mergeFlatGradient"]
+    names = [UPDATER + r for r in ref] + [SAMPLER + "initSampler", SAMPLER + "getMiniBatch"] + [
+        "Java_utils_ByteVec_" + r for r in ("scalarMulNative", "getNorm", "addNative", "subtractNative")]
+    assert len(names) == 22
+    L = load()
+    for s in names:
         assert hasattr(L, s), s
 
 
@@ -191,4 +217,45 @@ def test_shim_model_natives_match_reference_session(oracle):
             oracle.encode_floats(s[f"oldest_params{step}"])
     assert L.Java_apps_cppNN_CppNNUpdater_getCurrEpoch(env, None) == 3
     assert L.Java_apps_cppNN_CppNNUpdater_getLrate(env, None) == float(np.float32(s["lrates"][2]))
+    check_rules(J)
+
+
+@pytest.mark.gpu
+def test_shim_print_params(oracle, capfd):
+    """printParamsNative (:304-322): the upload's int32 codes on stdout."""
+    import jnifake as J
+    L = load()
+    codes = np.array([100000001, -10000002, 7, 0, 123456789], np.int32)
+    J.begin()
+    L.Java_apps_cppNN_CppNNUpdater_printParamsNative(J.env(), None, J.new_bytes(oracle.encode_ints(codes)))
+    check_rules(J)
+    assert "Got Numbers: 100000001 -10000002 7 0 123456789 \n" in capfd.readouterr().out
+
+
+@pytest.mark.gpu
+def test_shim_direct_buffer_reregistration(oracle):
+    """A registration outlives nothing: unregisterDirectNative releases it, and a new
+    buffer over the same memory re-registers cleanly (the stale one is released)."""
+    import jnifake as J
+    L = load()
+    env = J.env()
+    M = 3
+    ups = [oracle.encode_floats(oracle.synth_upload(9, c, list(MNIST.w_sizes), list(MNIST.b_sizes)))
+           for c in range(M)]
+    Lb = len(ups[0])
+    rows = np.zeros(M * Lb, np.uint8)
+    for i, u in enumerate(ups):
+        rows[i * Lb:(i + 1) * Lb] = np.frombuffer(u, np.uint8)
+    d = [1.0, 0.5, 0.25]
+    J.begin()
+    buf = J.new_direct(rows)
+    assert L.Java_apps_cppNN_FleetUpdater_registerDirectNative(env, None, buf) == 1
+    assert L.Java_apps_cppNN_FleetUpdater_registerDirectNative(env, None, J.new_direct(rows[: 2 * Lb])) == 1
+    out = J.read_bytes(L.Java_apps_cppNN_FleetUpdater_aggregateDirectNative(env, None, buf, M, Lb, Lb,
+                                                                             J.new_doubles(d)))
+    assert out == oracle.update_faithful(ups, d)  # rows now outside the (smaller) registration: staged
+    L.Java_apps_cppNN_FleetUpdater_unregisterDirectNative(env, None, buf)
+    out = J.read_bytes(L.Java_apps_cppNN_FleetUpdater_aggregateDirectNative(env, None, buf, M, Lb, Lb,
+                                                                             J.new_doubles(d)))
+    assert out == oracle.update_faithful(ups, d)
     check_rules(J)
