@@ -17,15 +17,23 @@ Headline (N=1): synth1m_256, the north-star configuration (1 M-float buckets,
 C = 256 clients, 1.43 GB of Base64 >> the 256 MiB Infinity Cache).
 
 Multi-GPU (element-range sharding):
-  * `value` at N>1 is weak scaling -- every rank owns a full-size slice of a
-    model N times larger; no collective in the timed steps (each rank's merged
-    slice stays resident, as the whole merged vector does at N=1).
-  * the `strong` block (every N, including 1) splits ONE fixed problem over the
-    N ranks: configs[4] (synthetic 4 M floats x 4096 clients) device-resident,
-    timed with the all_gather of the merged slices inside the step and without
-    it; and configs[3] (CIFAR-100 x 1024) host-staged: pinned-host H2D of the
-    rank's column window + aggregation + D2H of its merged slice (+ the gather).
+  * `value` is strong scaling of ONE fixed problem, the headline's: synth1m_256
+    split over the N ranks by 3-value group ranges; each rank's step is the same
+    pipelined launch on its column window (aggregation of batch i + encode of
+    batch i+1) followed by the all_gather of the merged slices (RCCL over xGMI)
+    inside the timed step, so every rank ends the step holding the whole merged
+    text. At N=1 this is exactly the headline step (no gather).
+  * `weak` beside it: every rank a full-size synth1m_256 slice of a model N times
+    larger, no collective in the timed steps (all_gather timed separately).
+  * the `strong` block splits the larger configs over the N ranks: configs[4]
+    (synthetic 4 M floats x 4096 clients) device-resident, timed with the
+    all_gather of the merged slices inside the step and without it; and
+    configs[3] (CIFAR-100 x 1024) host-staged: pinned-host H2D of the rank's
+    column window + aggregation + D2H of its merged slice (+ the gather).
   * --strong makes the strong configs[4] gather-inside line the `value`.
+  * `python bench.py --gpus N` without a launcher starts its N ranks itself
+    (torch.distributed.run as a child process, before anything touches a GPU);
+    under a launcher, --gpus must equal WORLD_SIZE.
 
 Output: ONE JSON line on rank 0 (see DESIGN.md §6 for every field).
 """
@@ -253,6 +261,67 @@ def time_pipelined(torch, dist, codec, sh, steps, warmup, world):
     return {"ms_per_step": elapsed / steps * 1e3,
             "gib_s": world * sh.M * sh.n_local * 4 / (elapsed / steps) / 2**30,
             "steps_per_graph": G, "kernel": F.update_encode_kernel(sh.L), "kernel_ms": fused_ms}
+
+
+def strong_pipelined(torch, dist, codec, name, steps, warmup, rank, world):
+    """`value`: strong scaling of ONE fixed problem. The rank's column window of
+    every upload is a bucket of its own (n_local values, the header slots that
+    fall inside it): the pipelined step (fleet_update_encode_device on the window,
+    the same launch as the N=1 headline step) writes the rank's merged slice,
+    which is copied into the padded all_gather source; the all_gather of every
+    rank's slice (RCCL) runs inside the timed step. Graph replays of the local
+    launch (one graph per buffer parity), the gather eager after each."""
+    import fleet_amd as F
+    from fleet_amd.layouts import LAYOUTS
+    lay_name, M, note = WORKLOADS[name]
+    layout = LAYOUTS[lay_name]
+    sh = Shard(codec, torch, layout, M, rank, world, strong=True)
+    G = (layout.n_up + 2) // 3
+    wmax = max(b - a for a, b in (group_range(G, world, r) for r in range(world)))
+    dev = sh.merged.device
+    src = torch.zeros(16 * wmax, dtype=torch.uint8, device=dev)
+    out = torch.empty(world * 16 * wmax, dtype=torch.uint8, device=dev)
+    gather = all_gather_fn(torch, dist, world, src, out)
+    v0 = 3 * sh.gb
+    hloc = sh.hpos_global[(sh.hpos_global >= v0) & (sh.hpos_global < v0 + sh.n_local)] - v0
+    L_loc = F.b64_len(sh.n_local)
+    bufs = [sh.text, torch.zeros_like(sh.text)]
+    nb = 16 * sh.groups
+
+    def local(i):
+        codec.update_encode_device(bufs[i % 2], L_loc, sh.dampen, hloc, sh.merged, sh.merged_f32, sh.values,
+                                   bufs[(i + 1) % 2])
+        src[:nb].copy_(sh.merged[:nb])
+
+    sh.encode()
+    for i in range(max(2, warmup)):
+        local(i)
+        gather()
+    torch.cuda.synchronize()
+    codec.check()
+    graphs = [graph_of(torch, lambda: local(0), 1), graph_of(torch, lambda: local(1), 1)]
+    graphs[0].replay()
+    graphs[1].replay()
+    state = {"i": 0}
+
+    def step():
+        graphs[state["i"] % 2].replay()
+        state["i"] += 1
+        gather()
+
+    elapsed = run_timed(torch, dist, world, step, steps)
+    codec.check()
+    if world > 1 and not torch.equal(out[rank * 16 * wmax: rank * 16 * wmax + nb], src[:nb]):
+        raise RuntimeError("all_gather returned a different merged slice")
+    kern_ms = kernel_ms(torch, lambda: (local(0), local(1)), reps=5) / 2
+    res = {"workload": name, "note": note, "clients": M, "n_up_total": layout.n_up, "n_up_per_rank": sh.n_local,
+           "groups_per_rank_max": wmax, "ms_per_step": elapsed / steps * 1e3,
+           "gib_s": M * layout.n_up * 4 / (elapsed / steps) / 2**30,
+           "kernel": F.update_encode_kernel(L_loc), "kernel_ms_rank0": kern_ms,
+           "step": "pipelined launch on the rank's column window + all_gather of the merged slices (inside)"}
+    del graphs, bufs, sh, src, out
+    torch.cuda.empty_cache()
+    return res
 
 
 def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=True, pipelined_step=True):
@@ -645,6 +714,21 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     args = ap.parse_args()
 
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: start the N ranks as a child torch.distributed.run (this process has
+        # touched no GPU) and exit with its status
+        import socket
+        import subprocess
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+        sys.exit(subprocess.call(cmd))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (one rank per GPU)")
+
     import torch
     import torch.distributed as dist
 
@@ -667,6 +751,9 @@ def main():
     codec = F.Codec(local)
 
     main_res = time_workload(torch, dist, codec, args.workload, args.steps, args.warmup, rank, world, args.graph)
+    strong_value = None
+    if world > 1 and args.graph:
+        strong_value = strong_pipelined(torch, dist, codec, args.workload, args.steps, args.warmup, rank, world)
     # the host-buffer paths before the extras: after the 150 GiB synth4m_4096 extra the
     # process's small pinned-host copies run 2-3x slower (measured on MNIST-64: 0.81 vs
     # 0.30 ms), an allocator-state effect that is not the path's
@@ -730,6 +817,17 @@ def main():
     config = {"workload": args.workload, "layout": r["layout"], "clients": r["clients"],
               "n_up_per_rank": r["n_up_per_rank"], "parallelism": f"element-shard x{world}",
               "dampening": "policy 1 inverse, tau = c mod 3", "step": step_form}
+    weak = None
+    if strong_value is not None:  # N>1: value = the fixed headline problem split over the ranks
+        weak = {"gib_s": value, "ms_per_step": ms, "step": step_form,
+                "what": "every rank a full-size slice of a model N times larger; no collective in the timed steps"}
+        value, ms, scaling = strong_value["gib_s"], strong_value["ms_per_step"], "strong"
+        config = {"workload": args.workload, "layout": r["layout"], "clients": r["clients"],
+                  "n_up_total": strong_value["n_up_total"], "n_up_per_rank": strong_value["n_up_per_rank"],
+                  "parallelism": f"element-shard x{world}, all_gather of the merged slices inside the step",
+                  "dampening": "policy 1 inverse, tau = c mod 3", "step": strong_value["step"]}
+    elif world == 1:
+        scaling = "strong"  # the N=1 point of the strong curve: the same fixed problem on one GPU
     if args.strong:
         sd = strong["device"]
         value, ms, scaling = sd["gather_inside"]["gib_s"], sd["gather_inside"]["ms_per_step"], "strong"
@@ -764,6 +862,8 @@ def main():
         "sequential": {"gib_s": r["gib_s"], "ms_per_step": r["ms_per_step"]},
         "pipelined": r["pipelined"],
         "strong": strong,
+        "weak": weak,
+        "strong_value": strong_value,
         "extra": extras,
         "end_to_end_host_buffers": e2e,
     }

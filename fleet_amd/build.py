@@ -46,27 +46,29 @@ def _run(cmd):
     return r
 
 
-def build_codec(force: bool = False) -> str:
+def build_codec(force: bool = False, out: str = LIB, defines=()) -> str:
+    """Build libfleetcodec.so; `out` / `defines` (-D flags) build an experiment
+    variant elsewhere (e.g. ab/ for scripts/gpu_ab_workloads.sh) from the same sources."""
     srcs = [os.path.join(CSRC, s) for s, _ in SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in ("codec_device.h", "codec_math.h", "kernels.h", "model_codec.h", "teacher_math.h")] + [
         os.path.join(INCLUDE, "fleet_codec.h")]
-    if not force and not _newer(LIB, deps):
-        return LIB
-    objdir = os.path.join(PKG, "build")
+    if not force and not defines and not _newer(out, deps):
+        return out
+    objdir = os.path.join(PKG, "build") if out == LIB else out + ".objs"
     os.makedirs(objdir, exist_ok=True)
 
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         lang = ["-x", "hip", f"--offload-arch={ARCH}"]
-        _run([HIPCC, *lang, *COMMON, "-c", src, "-o", obj])
+        _run([HIPCC, *lang, *COMMON, *[f"-D{d}" for d in defines], "-c", src, "-o", obj])
         return obj
 
     with ThreadPoolExecutor(max_workers=len(srcs)) as ex:
         objs = list(ex.map(compile_one, srcs))
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp])
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 def build_jni(force: bool = False) -> str:
@@ -95,5 +97,10 @@ def build_all(force: bool = False) -> None:
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv)
-    print(LIB)
+    # python -m fleet_amd.build [--force] | --variant OUT.so NAME=VALUE ...
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        print(build_codec(True, os.path.abspath(sys.argv[i + 1]), tuple(sys.argv[i + 2:])))
+    else:
+        build_all(force="--force" in sys.argv)
+        print(LIB)

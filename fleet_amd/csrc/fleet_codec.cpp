@@ -1632,9 +1632,10 @@ int fleet_descent(fleet_ctx* c, float* weights, size_t n_weights, float* fc_bias
 // cnnNew->read(cnn.getParams()) of the unquantised model. getParams prints the
 // biases and the first-occurrence dictionary values with `ostream << float`
 // (precision 6 = %g) and read() parses them back (strtof); every weight takes
-// its dictionary entry's value. Dictionary on the device (sort-based, no
-// O(n*U) scans); the U dictionary values and the biases are formatted and
-// parsed on the host (the same libc as the reference).
+// its dictionary entry's value. All on the device: the dictionary (sort-based,
+// no O(n*U) scans), the %g / strtof round trip of the U values and the biases
+// (decimal6.h: exact integer arithmetic, checked against libc on every finite
+// binary32, digest fn 22) and the gather; no host round trip of the values.
 int fleet_model_version(fleet_ctx* c, const float* weights, const int32_t* dims, int n_mats, const float* biases,
                         size_t n_biases, float* weights_out, float* biases_out) {
   if (!c || (n_biases && (!biases || !biases_out))) return FLEET_ERR_ARG;
@@ -1644,35 +1645,40 @@ int fleet_model_version(fleet_ctx* c, const float* weights, const int32_t* dims,
   int rc = model_total(c, dims, n_mats, &n);
   if (rc) return rc;
   if (n && (!weights || !weights_out)) return FLEET_ERR_ARG;
-  auto g6 = [](float v) {
-    char buf[48];
-    snprintf(buf, sizeof buf, "%g", (double)v);
-    return strtof(buf, nullptr);
-  };
-  for (size_t k = 0; k < n_biases; ++k) {
-    if (!std::isfinite(biases[k])) return fail(c, FLEET_ERR_ARG, "non-finite bias: the reference's text read fails");
-    biases_out[k] = g6(biases[k]);
+  DevMem dw, dd, di, db;
+  // the biases' text round trip on the device as well (getParams prints them with `<<` too)
+  if (n_biases) {
+    HIP_TRY(c, hipMalloc(&db.p, n_biases * sizeof(float)));
+    HIP_TRY(c, hipMemcpyAsync(db.p, biases, n_biases * sizeof(float), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(c, hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+    HIP_TRY(c, fleet::model_g6_inplace((float*)db.p, (int64_t)n_biases, c->d_err, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(biases_out, db.p, n_biases * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipMemcpyAsync(c->h_err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+    if (*c->h_err) {
+      HIP_TRY(c, hipMemset(c->d_err, 0, sizeof(int)));
+      return fail(c, FLEET_ERR_ARG, "non-finite bias: the reference's text read fails");
+    }
   }
   if (!n) return FLEET_OK;
-  DevMem dw, dd, di, dv;
   HIP_TRY(c, hipMalloc(&dw.p, n * sizeof(float)));
-  HIP_TRY(c, hipMalloc(&dd.p, n * sizeof(float)));
+  HIP_TRY(c, hipMalloc(&dd.p, (n + 1) * sizeof(float)));
   HIP_TRY(c, hipMalloc(&di.p, n * sizeof(int32_t)));
   HIP_TRY(c, hipMemcpyAsync(dw.p, weights, n * sizeof(float), hipMemcpyHostToDevice, c->stream));
   int32_t U = 0;
   HIP_TRY(c, fleet::model_quantize_index((const float*)dw.p, dims, n_mats, nullptr, (float*)dd.p, (int32_t*)di.p,
                                          &U, c->stream, false));
-  std::vector<float> dict((size_t)U);
-  if (U) HIP_TRY(c, hipMemcpy(dict.data(), dd.p, (size_t)U * sizeof(float), hipMemcpyDeviceToHost));
-  for (float& v : dict) {
-    if (!std::isfinite(v)) return fail(c, FLEET_ERR_ARG, "non-finite weight: the reference's text read fails");
-    v = g6(v);
-  }
-  HIP_TRY(c, hipMalloc(&dv.p, ((size_t)U + 1) * sizeof(float)));
-  if (U) HIP_TRY(c, hipMemcpyAsync(dv.p, dict.data(), (size_t)U * sizeof(float), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(c, fleet::model_dict_gather((const int32_t*)di.p, (int64_t)n, (const float*)dv.p, (float*)dw.p, c->stream));
+  // the U dictionary values through `<<` / `>>` (decimal6.h), in place, then the gather
+  HIP_TRY(c, hipMemsetAsync(c->d_err, 0, sizeof(int), c->stream));
+  HIP_TRY(c, fleet::model_g6_inplace((float*)dd.p, (int64_t)U, c->d_err, c->stream));
+  HIP_TRY(c, fleet::model_dict_gather((const int32_t*)di.p, (int64_t)n, (const float*)dd.p, (float*)dw.p, c->stream));
   HIP_TRY(c, hipMemcpyAsync(weights_out, dw.p, n * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipMemcpyAsync(c->h_err, c->d_err, sizeof(int), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (*c->h_err) {
+    HIP_TRY(c, hipMemset(c->d_err, 0, sizeof(int)));
+    return fail(c, FLEET_ERR_ARG, "non-finite weight: the reference's text read fails");
+  }
   return FLEET_OK;
 }
 

@@ -15,6 +15,7 @@
 #include <type_traits>
 
 #include "codec_device.h"
+#include "decimal6.h"
 #include "teacher_math.h"
 
 namespace fleet {
@@ -165,6 +166,22 @@ __device__ __forceinline__ void q_stage_d16(float (&out)[S], const float (&x)[S]
     }
   }
   dmax = max(dmax, emax);
+#pragma unroll
+  for (int i = 0; i < S; ++i) out[i] = q_d16(x[i], e[i], &dt->st);
+}
+
+// q_stage_d16 with the digit offsets from the VarEntry compare (var_d16): branch-
+// free, for the serial accumulation A = Q(A + p) whose sums hit the byte table's
+// compare slices in most waves.
+template <int S>
+__device__ __forceinline__ void q_stage_v16(float (&out)[S], const float (&x)[S], const D16Table* dt,
+                                            const VarEntry* vt, uint32_t& dmax) {
+  uint32_t e[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    e[i] = var_d16(f2u(x[i]), vt);
+    dmax = max(dmax, e[i]);
+  }
 #pragma unroll
   for (int i = 0; i < S; ++i) out[i] = q_d16(x[i], e[i], &dt->st);
 }
@@ -512,6 +529,11 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
   }
 }
 
+#ifndef FLEET_STAGEC_VAR
+#define FLEET_STAGEC_VAR 1
+#endif
+constexpr bool kStageCVar = FLEET_STAGEC_VAR != 0;
+
 // One lane's share of the fused update (the non-Kardam stream path): the values
 // [e0, e0 + S) of group g, S = 3 (the whole group) or S = 1 (one value; three
 // lanes of a wave share a group). Returns the lane's merged codes in out[S] and
@@ -565,7 +587,8 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       float sm[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) sm[i] = acc[i] + p[i];
-      q_stage_d16<S>(acc, sm, &dtab, tab.var, dmax);
+      if (kStageCVar) q_stage_v16<S>(acc, sm, &dtab, tab.var, dmax);
+      else q_stage_d16<S>(acc, sm, &dtab, tab.var, dmax);
     }
   };
   auto group_of = [&](int c) {
@@ -2224,6 +2247,13 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
                uint32_t e = dtab.d16[u >> 19];
                if (e == kD16Cmp) e = d16_fix(x, var);
                o = use ? (e < kD16Out ? (uint32_t)enc_d16(x, e, &dtab.st) : 0xdeadbeefu) : 0u; break; }
+      case 21: { const float x = u2f(u);                              // stage C's VarEntry-offset Q (as fn 6)
+               use = q_gen_ok(x);
+               const uint32_t e = var_d16(u, var);
+               o = use ? (e < kD16Out ? f2u(q_d16(x, e, &dtab.st)) : 0xdeadbeefu) : 0u; break; }
+      case 22: { const float x = u2f(u);                              // strtof("%.6g") of the model-version copy
+               use = (u & 0x7f800000u) != 0x7f800000u;
+               o = use ? f2u(g6_roundtrip(x)) : 0u; break; }
       case 18: { const float e = glibc_expf(u2f(u));                 // the teacher's expf (libm's)
                o = e != e ? 0x7fc00000u : f2u(e); break; }
       default: o = 0; use = false;

@@ -15,6 +15,9 @@ hipError_t model_quantize_index(const float* d_w, const int32_t* h_dims, int n_m
                                 int32_t* d_index, int32_t* h_U, hipStream_t s, bool quantize = true);
 // w[i] = vals[index[i]] (0.0f for index -1)
 hipError_t model_dict_gather(const int32_t* d_index, int64_t n, const float* d_vals, float* d_w, hipStream_t s);
+// v[i] = strtof(sprintf("%.6g", v[i])) in place (decimal6.h: getParams' `<<` and
+// read's `>>` of a value); *d_bad |= 1 for a non-finite value
+hipError_t model_g6_inplace(float* d_v, int64_t n, int* d_bad, hipStream_t s);
 // the index lines of getParams' mode-1 section, formatted on the device
 hipError_t model_index_text(const int32_t* d_index, const int32_t* h_dims, int n_mats, std::vector<char>* out,
                             hipStream_t s);

@@ -35,6 +35,7 @@
 #include <vector>
 
 #include "model_codec.h"
+#include "decimal6.h"
 
 namespace fleet {
 namespace {
@@ -423,6 +424,23 @@ __global__ void __launch_bounds__(256) k_dict_gather(const int32_t* __restrict__
   if (i >= n) return;
   const int32_t k = index[i];
   w[i] = k >= 0 ? vals[k] : 0.0f;
+}
+
+__global__ void __launch_bounds__(256) k_g6_inplace(float* __restrict__ v, int64_t n, int* __restrict__ bad) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float x = v[i];
+  if ((f2u(x) & 0x7f800000u) == 0x7f800000u) {  // inf / NaN: the reference's text read fails
+    atomicOr(bad, 1);
+    return;
+  }
+  v[i] = g6_roundtrip(x);
+}
+
+hipError_t model_g6_inplace(float* d_v, int64_t n, int* d_bad, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_g6_inplace, dim3(nb(n)), dim3(256), 0, s, d_v, n, d_bad);
+  return hipGetLastError();
 }
 
 hipError_t model_dict_gather(const int32_t* d_index, int64_t n, const float* d_vals, float* d_w, hipStream_t s) {

@@ -266,7 +266,9 @@ int fleet_model_read_weights(fleet_ctx* ctx, const char* text, size_t len, const
  * model, network.h:611-706 + 956-997): every weight becomes the %g/strtof
  * round trip of its first-occurrence dictionary entry (|a-b| < 1e-8f), every
  * bias the round trip of itself. The O(n*U) dictionary scans of the reference
- * become a device sort. Non-finite weights or biases: FLEET_ERR_ARG (the
+ * become a device sort, and the decimal round trips run on the device too
+ * (exact integer arithmetic, checked against libc's snprintf/strtof on every
+ * finite binary32). Non-finite weights or biases: FLEET_ERR_ARG (the
  * reference's text parse fails on "nan"/"inf"). */
 int fleet_model_version(fleet_ctx* ctx, const float* weights, const int32_t* dims, int n_mats, const float* biases,
                         size_t n_biases, float* weights_out, float* biases_out);

@@ -3,17 +3,21 @@
 //
 //   check_math sample      ~1e8 sampled inputs per function (CPU test suite)
 //   check_math exhaustive  every input in each fast path's domain (dev check; ~1 min on 8 cores)
+//   check_math g6          the model-version copy's %g / strtof round trip (decimal6.h) against
+//                          libc's snprintf / strtof on every finite binary32 (~8 min on 8 cores)
 //
 // Exit status 0 = all bit-identical.
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
 #include <vector>
 
 #include "../../fleet_amd/csrc/codec_math.h"
+#include "../../fleet_amd/csrc/decimal6.h"
 extern "C" {
 #include "../../oracle/fleet_oracle.h"
 }
@@ -100,10 +104,11 @@ int main(int argc, char** argv) {
       uint32_t e = dt[(uint32_t)i >> 19];
       if (e == kD16Cmp) e = d16_fix(x, vt);
       if (!q_gen_ok(x)) {
-        if (e < kD16Out) g_bad++;
+        if (e < kD16Out || var_d16((uint32_t)i, vt) < kD16Out) g_bad++;
         return;
       }
       if (e != 16u * (uint32_t)fo_num_digits(fo_cvtt(x))) g_bad++;
+      if (var_d16((uint32_t)i, vt) != e) g_bad++;  // stage C's compare form
       if (!same(q_d16(x, e, &st), fo_int2float(fo_float2int(x)))) g_bad++;
       if (enc_d16(x, e, &st) != fo_float2int(x)) g_bad++;  // the client encode's form
     });
@@ -116,6 +121,18 @@ int main(int argc, char** argv) {
     for (uint32_t i = 0; i < 8192; ++i) cmp_slices += dt[i] == kD16Cmp;
     printf("d16 table: %ld compare slices of 8192\n", cmp_slices);
     report("d16 / q_d16 / enc_d16 (exhaustive)", b);
+    return g_bad ? 1 : 0;
+  }
+  if (argc > 1 && std::string(argv[1]) == "g6") {  // %g / strtof round trip, every finite input
+    long b = g_bad;
+    par_for(0, 1ull << 32, 1, [](uint64_t i) {
+      const uint32_t u = (uint32_t)i;
+      if ((u & 0x7f800000u) == 0x7f800000u) return;
+      char buf[64];
+      snprintf(buf, sizeof buf, "%g", (double)u2f(u));
+      if (!same(g6_roundtrip(u2f(u)), strtof(buf, nullptr))) g_bad++;
+    });
+    report("g6_roundtrip (exhaustive)", b);
     return g_bad ? 1 : 0;
   }
   const uint64_t s = exhaustive ? 1 : 97;  // sampling stride (odd, walks every residue class)
@@ -216,10 +233,11 @@ int main(int argc, char** argv) {
       uint32_t e = dt[(uint32_t)i >> 19];
       if (e == kD16Cmp) e = d16_fix(x, vt);
       if (!q_gen_ok(x)) {
-        if (e < kD16Out) g_bad++;
+        if (e < kD16Out || var_d16((uint32_t)i, vt) < kD16Out) g_bad++;
         return;
       }
       if (e != 16u * (uint32_t)fo_num_digits(fo_cvtt(x))) g_bad++;
+      if (var_d16((uint32_t)i, vt) != e) g_bad++;  // stage C's compare form
       if (!same(q_d16(x, e, &st), fo_int2float(fo_float2int(x)))) g_bad++;
       if (enc_d16(x, e, &st) != fo_float2int(x)) g_bad++;
     });
@@ -283,6 +301,32 @@ int main(int argc, char** argv) {
     if (enc(x) != fo_float2int(x)) g_bad++;
   });
   report("enc (general)", b0);
+
+  b0 = g_bad;  // stage C's VarEntry digit offsets against the byte table's, sampled
+  {
+    static VarEntry vt2[512];
+    static uint8_t dt2[8192];
+    for (uint32_t i = 0; i < 512; ++i) vt2[i] = var_entry(i);
+    for (uint32_t i = 0; i < 8192; ++i) dt2[i] = d16_entry(i);
+    par_for(0, 1ull << 32, s, [](uint64_t i) {
+      const float x = u2f((uint32_t)i);
+      uint32_t e = dt2[(uint32_t)i >> 19];
+      if (e == kD16Cmp) e = d16_fix(x, vt2);
+      const uint32_t v = var_d16((uint32_t)i, vt2);
+      if (q_gen_ok(x) ? v != e : v < kD16Out) g_bad++;
+    });
+  }
+  report("var_d16", b0);
+
+  b0 = g_bad;  // %g / strtof round trip against libc, sampled
+  par_for(0, 1ull << 32, exhaustive ? 1 : 1009, [](uint64_t i) {
+    const uint32_t u = (uint32_t)i;
+    if ((u & 0x7f800000u) == 0x7f800000u) return;
+    char buf[64];
+    snprintf(buf, sizeof buf, "%g", (double)u2f(u));
+    if (!same(g6_roundtrip(u2f(u)), strtof(buf, nullptr))) g_bad++;
+  });
+  report("g6_roundtrip", b0);
 
   printf("%s\n", g_bad ? "FAILED" : "ALL OK");
   return g_bad ? 1 : 0;

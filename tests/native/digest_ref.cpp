@@ -5,6 +5,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -50,6 +51,15 @@ static uint64_t digest(int fn) {
           case 11: use = (u & 0x7fffffffu) < 0x3f800000u; if (use) o = (uint32_t)fo_float2int(u2f(u)); break;
           case 12: { float x = u2f(u); use = x < 1e9f && x > -1e8f; if (use) o = f2u(Q(x)); break; }
           case 18: { float e = expf(u2f(u)); o = e != e ? 0x7fc00000u : f2u(e); break; }  // libm expf
+          case 22: {  // libc's %g / strtof round trip (ostream << float, istream >> float)
+            use = (u & 0x7f800000u) != 0x7f800000u;
+            if (use) {
+              char b[64];
+              snprintf(b, sizeof b, "%g", (double)u2f(u));
+              o = f2u(strtof(b, nullptr));
+            }
+            break;
+          }
         }
         if (use) sum += splitmix64(((uint64_t)u << 32) | o);
       }
@@ -65,8 +75,12 @@ int main(int argc, char** argv) {
   const char* path = argc > 1 ? argv[1] : "tests/golden/digests.json";
   FILE* f = fopen(path, "w");
   fprintf(f, "{\n  \"generator\": \"tests/native/digest_ref.cpp over oracle/fleet_oracle.c\",\n");
-  const int fns[] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 18};
-  const int nf = (int)(sizeof fns / sizeof fns[0]);
+  std::vector<int> fns = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 18, 22};
+  if (argc > 2) {  // argv[2..]: print only these functions' digests (no file written)
+    for (int a = 2; a < argc; ++a) printf("fn%d %016llx\n", atoi(argv[a]), (unsigned long long)digest(atoi(argv[a])));
+    return 0;
+  }
+  const int nf = (int)fns.size();
   for (int j = 0; j < nf; ++j) {
     const int fn = fns[j];
     uint64_t d = digest(fn);

@@ -109,3 +109,26 @@ def test_update_rows(contexts, oracle, N, pad, pinned):
     expected = oracle.update_faithful(ups, d)
     assert merged == expected
     assert np.array_equal(f32.view(np.uint32), oracle.decode_floats(expected).view(np.uint32))
+
+
+def test_entry_points_keep_the_callers_device(contexts, oracle):
+    """Every C-ABI entry restores the calling thread's current device (fleet_codec.cpp
+    DeviceGuard): creating a context on the last visible GPU, a multi-context update,
+    device-resident and host-buffer calls leave torch's current device as it was."""
+    torch = pytest.importorskip("torch")
+    n = torch.cuda.device_count()
+    before = torch.cuda.current_device()
+    last = F.Codec(n - 1)
+    try:
+        assert torch.cuda.current_device() == before
+        ups = uploads_for(oracle, MNIST, 3, seed=5)
+        d = [1.0, 0.5, 0.25]
+        assert F.update_multi([contexts[0], last] if n > 1 else contexts[:2], ups, d) == oracle.update_faithful(ups, d)
+        assert torch.cuda.current_device() == before
+        assert last.update(ups, d) == oracle.update_faithful(ups, d)
+        assert torch.cuda.current_device() == before
+        last.check()
+        assert torch.cuda.current_device() == before
+    finally:
+        last.close()
+    assert torch.cuda.current_device() == before
