@@ -1044,8 +1044,13 @@ int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch
   if ((d_prev || d_g_out) && vpitch < n) return fail(c, FLEET_ERR_ARG, "vpitch %zu < %zu values", vpitch, n);
   hipStream_t s = pick(c, stream);
   if ((rc = dev_params(c, s, n, M, dampen, header_pos, n_headers))) return rc;
-  const size_t n_waves = 4 * ((ge + 255) / 256);
-  // scratch: [partials M x waves x 2 | norms M x 2 | has_prev M]; synchronous call (host outputs)
+  int nw_sz = 0;  // partial slots per client of the launch plan (sizing call)
+  fleet::KardamOut kd0{lr, nullptr, nullptr, 0, nullptr, nullptr};
+  (void)fleet::launch_update_kardam(nullptr, pitch, M, nullptr, 0.0, (int64_t)n, 0, (int64_t)ge, nullptr, nullptr,
+                                    nullptr, nullptr, kd0, &nw_sz, nullptr, s);
+  (void)hipGetLastError();
+  const size_t n_waves = (size_t)std::max(nw_sz, 1);
+  // scratch: [partials M x slots x 2 | norms M x 2 | has_prev M]; synchronous call (host outputs)
   const size_t o_norm = sizeof(double) * 2 * (size_t)M * n_waves, o_has = o_norm + sizeof(double) * 2 * (size_t)M;
   if ((rc = grow_dev(c, &c->d_b, &c->d_b_cap, o_has + (size_t)M + 64))) return rc;
   HIP_TRY(c, hipStreamSynchronize(s));
@@ -1687,7 +1692,8 @@ const char* fleet_update_kernel(size_t len) {
 }
 
 int fleet_selftest_digest(fleet_ctx* c, int fn, uint64_t* out) {
-  if (!c || !out || fn < 0 || fn > 20) return FLEET_ERR_ARG;
+  if (!c || !out) return FLEET_ERR_ARG;
+  if (fn < 0 || fn > 22) return fail(c, FLEET_ERR_ARG, "no self-test function %d", fn);
   std::lock_guard<std::mutex> lk(c->mu);
   DEVICE_SCOPE(c);
   unsigned long long* d = nullptr;

@@ -756,10 +756,71 @@ __device__ __forceinline__ void tile_load(TileItems<TG, IPT>& it, const uint8_t*
   }
 }
 
+// Kardam's side outputs in a tile producer (CppNNUpdater.java:463-481,
+// Kardam.java:48-106): the tile's index among the grid's tiles (partials slot) and
+// the end of network::flatGrad's walk (slots past it are not gradient values).
+struct TileKd {
+  KardamOut kd;
+  int64_t tile, ntiles, walk_end;
+};
+
+// Per item (one client, one group): the text Kardam.setGrad stores, G =
+// Q(f32(f64(p) * lr)), written to g_out; ||G||^2 and, with the worker's previous
+// G, ||Q(G - prev)||^2 over the flat gradient's slots (getNorm: float products
+// summed in double). A client's TG groups of the tile are TG consecutive lanes of
+// one wave (items are client-major and waves start at multiples of 64), so the
+// lane group's sum is the (client, tile) partial: one write, no atomics, a fixed
+// order (k_kardam_reduce then sums the tiles in order).
 template <int TG, int IPT, int NW>
+__device__ __forceinline__ void tile_kardam(TileShared<TG, NW>& sh, const TileItems<TG, IPT>& it,
+                                            const float (&p)[3 * IPT], int64_t n_up, int64_t g0, const TileKd& tk) {
+  static_assert(64 % TG == 0, "a client's groups in one lane group");
+  constexpr int S = 3 * IPT;
+  const KardamOut& kd = tk.kd;
+  float rg[S], G[S];
+#pragma unroll
+  for (int i = 0; i < S; ++i) rg[i] = p[i];
+  dampen_stage<S>(rg, kd.lr);  // (float)((double)p * lr), lr uniform
+  q_stage<S>(G, rg, &sh.tab);  // exact (in-stage fallback)
+#pragma unroll
+  for (int h = 0; h < IPT; ++h) {
+    const int c = it.c_base + it.cc[h];
+    const int64_t gp = 3 * (g0 + it.gl[h]);
+    const uint32_t hm = it.live[h] ? sh.hmask[it.gl[h]] : 7u;
+    const bool hasp = kd.prev && it.live[h] && kd.has_prev[c];
+    double sg = 0.0, sd = 0.0;
+    float dv[3], D[3];
+    bool flat[3];
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      const int64_t pos = gp + e;
+      flat[e] = it.live[h] && !((hm >> e) & 1u) && pos < n_up && pos < tk.walk_end;
+      const float g = G[3 * h + e];
+      if (flat[e]) sg += (double)(g * g);
+      dv[e] = (flat[e] && hasp) ? g - kd.prev[(size_t)c * kd.vpitch + pos] : 0.0f;
+      if (kd.g_out && it.live[h] && pos < n_up) kd.g_out[(size_t)c * kd.vpitch + pos] = flat[e] ? g : 0.0f;
+    }
+    q_stage<3>(D, dv, &sh.tab);
+#pragma unroll
+    for (int e = 0; e < 3; ++e)
+      if (flat[e] && hasp) sd += (double)(D[e] * D[e]);
+#pragma unroll
+    for (int o = TG / 2; o > 0; o >>= 1) {
+      sg += __shfl_xor(sg, o);
+      sd += __shfl_xor(sd, o);
+    }
+    if (it.live[h] && it.gl[h] == 0) {  // the lane group's head: its item is the client's first group
+      kd.partials[((size_t)c * tk.ntiles + tk.tile) * 2] = sg;
+      kd.partials[((size_t)c * tk.ntiles + tk.tile) * 2 + 1] = sd;
+    }
+  }
+}
+
+template <int TG, int IPT, int NW, bool KD = false>
 __device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileItems<TG, IPT>& it, int M,
                                              const double* __restrict__ dampen, int64_t n_up, int64_t g0,
-                                             float* __restrict__ pdst, uint32_t& badacc) {
+                                             float* __restrict__ pdst, uint32_t& badacc,
+                                             const TileKd& tk = TileKd{}) {
   constexpr int E = 3 * TG, S = 3 * IPT;
   int32_t codes[S];
 #pragma unroll
@@ -812,16 +873,17 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileI
     if (it.live[h])
 #pragma unroll
       for (int e = 0; e < 3; ++e) pdst[it.cc[h] * E + 3 * it.gl[h] + e] = p[3 * h + e];
+  if constexpr (KD) tile_kardam<TG, IPT, NW>(sh, it, p, n_up, g0, tk);
 }
 
-template <int TG, int IPT, int NW>
+template <int TG, int IPT, int NW, bool KD = false>
 __device__ __forceinline__ void tile_produce(TileShared<TG, NW>& sh, const uint8_t* __restrict__ uploads, size_t pitch,
                                              int M, const double* __restrict__ dampen, int64_t n_up, int64_t g0,
                                              int ng, int c_base, int nitems, int it0, int stride,
-                                             float* __restrict__ pdst, uint32_t& badacc) {
+                                             float* __restrict__ pdst, uint32_t& badacc, const TileKd& tk) {
   TileItems<TG, IPT> it;
   tile_load<TG, IPT>(it, uploads, pitch, g0, ng, c_base, nitems, it0, stride);
-  tile_compute<TG, IPT, NW>(sh, it, M, dampen, n_up, g0, pdst, badacc);
+  tile_compute<TG, IPT, NW, KD>(sh, it, M, dampen, n_up, g0, pdst, badacc, tk);
 }
 
 // Final values of the tile (vals[0..E)) -> merged Base64 (+ fp32), layout
@@ -878,13 +940,14 @@ template <int TG>
 constexpr int tiled_chunk_clients() { return FLEET_TILED_PT / (3 * TG); }
 
 // Tile `bid` of k_update_tiled (LDS state in sh / ptile)
-template <int TG>
+template <int TG, bool KD = false>
 __device__ __forceinline__ void update_tiled_block(TileShared<TG>& sh, float* ptile, int64_t bid,
                                                    const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                    const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                                    int64_t g_begin, int64_t g_end,
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
-                                                   float* __restrict__ merged_f32, int* __restrict__ err) {
+                                                   float* __restrict__ merged_f32, int* __restrict__ err,
+                                                   const TileKd& tk = TileKd{}) {
   constexpr int E = 3 * TG;
   static_assert(E <= 256, "phase 2 is one thread per value");
   constexpr int CM = tiled_chunk_clients<TG>();
@@ -903,7 +966,8 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG>& sh, float* pt
     const int cm = min(CM, M - c0);
     const int nitems = cm * TG;
     for (int base = 0; base < nitems; base += 512) {
-      tile_produce<TG, 2>(sh, uploads, pitch, M, dampen, n_up, g0, ng, c0, nitems, base + tid, 256, ptile, badacc);
+      tile_produce<TG, 2, 4, KD>(sh, uploads, pitch, M, dampen, n_up, g0, ng, c0, nitems, base + tid, 256, ptile,
+                                 badacc, tk);
       if (base == 0) FLEET_TSTAMP(2);
     }
     __syncthreads();
@@ -947,17 +1011,19 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG>& sh, float* pt
   FLEET_TSTAMP(5);
 }
 
-template <int TG>
+// KD = true: Kardam's side outputs from the tile producers (tile_kardam).
+template <int TG, bool KD = false>
 __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                       const double* __restrict__ dampen, double inv_avg,
                                                       int64_t n_up, int64_t g_begin, int64_t g_end,
                                                       const int32_t* __restrict__ hdr_block,
                                                       uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                      int* __restrict__ err) {
+                                                      int* __restrict__ err, KardamOut kd = KardamOut{}) {
   __shared__ TileShared<TG> sh;
   __shared__ float ptile[tiled_chunk_clients<TG>() * 3 * TG];
-  update_tiled_block<TG>(sh, ptile, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block,
-                         merged, merged_f32, err);
+  update_tiled_block<TG, KD>(sh, ptile, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+                             hdr_block, merged, merged_f32, err,
+                             TileKd{kd, (int64_t)blockIdx.x, (int64_t)gridDim.x, (int64_t)hdr_block[2]});
 }
 
 // Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
@@ -1108,13 +1174,14 @@ struct EncodeJob {
 // reading a pass, and publishes "passes consumed" so producers never overwrite
 // a ring slot still being read. Every wait has a partner that always makes
 // progress, so the grid drains.
-template <int TG, int IPT, int NW, int WP = 0>
+template <int TG, int IPT, int NW, int WP = 0, bool KD = false>
 __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                      const double* __restrict__ dampen, double inv_avg,
                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
                                                      const int32_t* __restrict__ hdr_block,
                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                     int* __restrict__ err, int nU, EncodeJob ej) {
+                                                     int* __restrict__ err, int nU, EncodeJob ej,
+                                                     KardamOut kd = KardamOut{}) {
   constexpr int E = 3 * TG;
   static_assert(E <= 64, "one consumer wave");
   constexpr int NPW = NW - 1;                                // producer waves
@@ -1166,7 +1233,8 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
         while (__hip_atomic_load(&consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < pass - RING + 1)
           __builtin_amdgcn_s_sleep(1);
       }
-      tile_compute<TG, IPT, NW>(sh, cur, M, dampen, n_up, g0, ptile + (pass % RING) * CPP * E, badacc);
+      tile_compute<TG, IPT, NW, KD>(sh, cur, M, dampen, n_up, g0, ptile + (pass % RING) * CPP * E, badacc,
+                                    TileKd{kd, (int64_t)blockIdx.x, (int64_t)gridDim.x, (int64_t)hdr_block[2]});
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       ++done;
       if (lane == 0) __hip_atomic_store(&prog[w], done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1971,12 +2039,38 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
                                 double* norms, hipStream_t s) {
   const int64_t groups = g_end - g_begin;
-  const unsigned blocks = (unsigned)((groups + 255) / 256);
-  *n_waves = (int)blocks * 4;
+  // the update's own launch plan (plan_update): the stream kernel, the wide tiles or the
+  // pipelined tiles, each with the side outputs; partial slots per client = waves of the
+  // stream grid or the tiles. Launch variants the plan takes only under experiment
+  // overrides fall back to the stream kernel.
+  const UpdatePlan p = plan_update(groups);
+  const bool pipe = p.kind == 2 && p.ipt == 1 && p.nw == 5 && !p.wp && (p.tg == 8 || p.tg == 16);
+  const bool tiled = p.kind == 1 && (p.tg == 16 || p.tg == 32 || p.tg == 64);
+  const int64_t per = pipe || tiled ? p.tg : 256;
+  const unsigned blocks = (unsigned)((groups + per - 1) / per);
+  *n_waves = pipe || tiled ? (int)blocks : (int)blocks * 4;
   if (groups <= 0) return hipSuccess;
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
-  hipLaunchKernelGGL((k_update<1, true>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
-                     g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd);
+  if (pipe) {
+    if (p.tg == 8)
+      hipLaunchKernelGGL((k_update_pipe<8, 1, 5, 0, true>), dim3(blocks), dim3(64 * 5), 0, s, uploads, pitch, M, d_dampen,
+                         inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX, EncodeJob{}, kd);
+    else
+      hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0, true>), dim3(blocks), dim3(64 * 5), 0, s, uploads, pitch, M,
+                         d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
+                         EncodeJob{}, kd);
+  } else if (tiled) {
+#define FLEET_LAUNCH_TK(TG)                                                                                       \
+  hipLaunchKernelGGL((k_update_tiled<TG, true>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, \
+                     n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd)
+    if (p.tg == 16) FLEET_LAUNCH_TK(16);
+    else if (p.tg == 32) FLEET_LAUNCH_TK(32);
+    else FLEET_LAUNCH_TK(64);
+#undef FLEET_LAUNCH_TK
+  } else {
+    hipLaunchKernelGGL((k_update<1, true>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
+                       g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd);
+  }
   hipLaunchKernelGGL(k_kardam_reduce, dim3((unsigned)M), dim3(256), 0, s, kd.partials, (int64_t)*n_waves, norms);
   return hipGetLastError();
 }

@@ -234,6 +234,9 @@ int fleet_check(fleet_ctx* ctx, void* stream);
  *          NaN results as 0x7fc00000 (the libm expf digest of tests/native/digest_ref.cpp)
  *   fn 19: byte-table Q of the stream kernel (q_d16 + compare fix-up; as fn 6)
  *   fn 20: byte-table float2int of the client encode (enc_d16; as fn 10)
+ *   fn 21: the serial accumulation's Q with VarEntry digit offsets (var_d16; as fn 6)
+ *   fn 22: the model-version copy's strtof("%.6g") round trip over every finite
+ *          binary32 (decimal6.h; against libc's snprintf/strtof)
  * computed on the GPU; compare with the oracle's digests. */
 int fleet_selftest_digest(fleet_ctx* ctx, int fn, uint64_t* out);
 

@@ -9,7 +9,7 @@ import pytest
 import torch
 
 import fleet_amd as F
-from fleet_amd.layouts import MNIST, synthetic
+from fleet_amd.layouts import CIFAR10, MNIST, synthetic
 
 pytestmark = pytest.mark.gpu
 
@@ -23,7 +23,11 @@ def scatter_flat(flat, layout):
     return out
 
 
-@pytest.mark.parametrize("layout,M", [(MNIST, 6), (synthetic(3001), 4)])
+# every launch plan of the update carries the side outputs: the pipelined tiles
+# (MNIST, small buckets), the wide tiles at TG = 32 and 64 (CIFAR-10 sizes) and
+# the stream kernel (1 M floats)
+@pytest.mark.parametrize("layout,M", [(MNIST, 6), (synthetic(3001), 4), (CIFAR10, 5), (synthetic(120_001), 3),
+                                      (synthetic(1_048_576), 2)])
 def test_kardam_side_outputs(codec, oracle, layout, M):
     dev = torch.device("cuda", 0)
     lr = 0.05
@@ -44,6 +48,7 @@ def test_kardam_side_outputs(codec, oracle, layout, M):
         g_out = torch.zeros((M, vpitch), dtype=torch.float32, device=dev)
         ng, nd = codec.update_kardam_device(t, L, d, hpos, lr, merged, None, prev_dev, has, g_out)
         codec.check()
+        print(layout.n_up, M, F.update_kernel(L))
         torch.cuda.synchronize()
         assert merged.cpu().numpy()[:L].tobytes() == codec.update(ups, d)
         prev_arg = None if prev_texts is None else [p if h else None for p, h in zip(prev_texts, has)]
