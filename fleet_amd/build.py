@@ -27,8 +27,8 @@ ARCH = os.environ.get("FLEET_OFFLOAD_ARCH", "gfx950")
 HIPCC = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-fno-slp-vectorize", f"-I{INCLUDE}", f"-I{CSRC}"]
 
-SOURCES = [("kernels.hip", True), ("model_codec.hip", True), ("fleet_codec.cpp", True), ("model_state.cpp", True), ("teacher.hip", True),
-           ("sampler_state.cpp", True)]
+SOURCES = [("kernels.hip", True), ("stream_kernels.hip", True), ("model_codec.hip", True), ("fleet_codec.cpp", True),
+           ("model_state.cpp", True), ("teacher.hip", True), ("sampler_state.cpp", True)]
 
 
 def _newer(target: str, deps) -> bool:
@@ -50,7 +50,8 @@ def build_codec(force: bool = False, out: str = LIB, defines=()) -> str:
     """Build libfleetcodec.so; `out` / `defines` (-D flags) build an experiment
     variant elsewhere (e.g. ab/ for scripts/gpu_ab_workloads.sh) from the same sources."""
     srcs = [os.path.join(CSRC, s) for s, _ in SOURCES]
-    deps = srcs + [os.path.join(CSRC, h) for h in ("codec_device.h", "codec_math.h", "kernels.h", "model_codec.h", "teacher_math.h")] + [
+    deps = srcs + [os.path.join(CSRC, h) for h in ("codec_device.h", "codec_math.h", "decimal6.h", "kernels.h", "model_codec.h",
+                                                   "teacher_math.h")] + [
         os.path.join(INCLUDE, "fleet_codec.h")]
     if not force and not defines and not _newer(out, deps):
         return out
@@ -60,7 +61,13 @@ def build_codec(force: bool = False, out: str = LIB, defines=()) -> str:
     def compile_one(src):
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         lang = ["-x", "hip", f"--offload-arch={ARCH}"]
-        _run([HIPCC, *lang, *COMMON, *[f"-D{d}" for d in defines], "-c", src, "-o", obj])
+        # the stream kernels are VALU-issue bound at 5-6 waves per SIMD: the ILP-first
+        # machine scheduler beats the default there and loses on the tiles, hence their
+        # own unit (FLEET_STREAM_SCHED=default builds it with the default scheduler)
+        sched = os.environ.get("FLEET_STREAM_SCHED", "max-ilp")
+        extra = ["-mllvm", f"-amdgpu-sched-strategy={sched}"] if (
+            src.endswith("stream_kernels.hip") and sched != "default") else []
+        _run([HIPCC, *lang, *COMMON, *extra, *[f"-D{d}" for d in defines], "-c", src, "-o", obj])
         return obj
 
     with ThreadPoolExecutor(max_workers=len(srcs)) as ex:

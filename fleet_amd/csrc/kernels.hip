@@ -740,6 +740,8 @@ struct TileItems {
   uint4 w[IPT];
   int cc[IPT], gl[IPT], c_base;
   bool live[IPT];
+  int cl[IPT];       // the item's client in the pass, also for dead groups past the tile's last
+  bool cvalid[IPT];  // the item's client exists (item < nitems)
 };
 
 template <int TG, int IPT>
@@ -749,6 +751,8 @@ __device__ __forceinline__ void tile_load(TileItems<TG, IPT>& it, const uint8_t*
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
     const int item = it0 + h * stride;
+    it.cvalid[h] = item < nitems;
+    it.cl[h] = item / TG;
     it.live[h] = item < nitems && (item % TG) < ng;
     it.cc[h] = it.live[h] ? item / TG : 0;
     it.gl[h] = it.live[h] ? item % TG : 0;
@@ -764,6 +768,30 @@ struct TileKd {
   int64_t tile, ntiles, walk_end;
 };
 
+// Sum of v over each aligned group of TG lanes (16, 32 or 64), valid in the
+// group's last lane, by DPP lane moves inside the VALU (no LDS crossbar):
+// row_half_mirror + two quad_perms + row_mirror give every lane its 16-lane row's
+// sum, row_bcast15 / row_bcast31 then fold rows 0+1, 2+3 and 0..3. Call with
+// every lane of the wave active.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_move_f64(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int TG>
+__device__ __forceinline__ double group_sum_f64(double v) {
+  static_assert(TG == 16 || TG == 32 || TG == 64, "DPP group sums over rows of 16 lanes");
+  v += dpp_move_f64<0x141, 0xf>(v);  // row_half_mirror
+  v += dpp_move_f64<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+  v += dpp_move_f64<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v += dpp_move_f64<0x140, 0xf>(v);  // row_mirror: every lane holds its row's sum
+  if constexpr (TG >= 32) v += dpp_move_f64<0x142, 0xa>(v);  // row_bcast15 into rows 1, 3
+  if constexpr (TG == 64) v += dpp_move_f64<0x143, 0x8>(v);  // row_bcast31 into row 3
+  return v;
+}
+
 // Per item (one client, one group): the text Kardam.setGrad stores, G =
 // Q(f32(f64(p) * lr)), written to g_out; ||G||^2 and, with the worker's previous
 // G, ||Q(G - prev)||^2 over the flat gradient's slots (getNorm: float products
@@ -774,7 +802,7 @@ struct TileKd {
 template <int TG, int IPT, int NW>
 __device__ __forceinline__ void tile_kardam(TileShared<TG, NW>& sh, const TileItems<TG, IPT>& it,
                                             const float (&p)[3 * IPT], int64_t n_up, int64_t g0, const TileKd& tk) {
-  static_assert(64 % TG == 0, "a client's groups in one lane group");
+  static_assert(64 % TG == 0 && TG >= 16, "a client's groups in one lane group of 16, 32 or 64");
   constexpr int S = 3 * IPT;
   const KardamOut& kd = tk.kd;
   float rg[S], G[S];
@@ -804,14 +832,12 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW>& sh, const TileIt
 #pragma unroll
     for (int e = 0; e < 3; ++e)
       if (flat[e] && hasp) sd += (double)(D[e] * D[e]);
-#pragma unroll
-    for (int o = TG / 2; o > 0; o >>= 1) {
-      sg += __shfl_xor(sg, o);
-      sd += __shfl_xor(sd, o);
-    }
-    if (it.live[h] && it.gl[h] == 0) {  // the lane group's head: its item is the client's first group
-      kd.partials[((size_t)c * tk.ntiles + tk.tile) * 2] = sg;
-      kd.partials[((size_t)c * tk.ntiles + tk.tile) * 2 + 1] = sd;
+    sg = group_sum_f64<TG>(sg);
+    sd = group_sum_f64<TG>(sd);
+    if (it.cvalid[h] && (threadIdx.x & (TG - 1)) == TG - 1) {  // the group's last lane: its client's tile sum
+      const size_t slot = ((size_t)(it.c_base + it.cl[h]) * tk.ntiles + tk.tile) * 2;
+      kd.partials[slot] = sg;
+      kd.partials[slot + 1] = sd;
     }
   }
 }
@@ -1327,6 +1353,7 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
 }
 
 // ----------------------------------------------------------------------------
+#ifndef FLEET_STREAM_TU  // (the stream unit needs only the two stream kernels)
 __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ values, int64_t n, size_t vpitch,
                                                     uint8_t* __restrict__ out, size_t pitch, int64_t groups,
                                                     int rows, int rpb) {
@@ -1346,6 +1373,7 @@ __global__ void __launch_bounds__(256) k_encode_f32_d16(const float* __restrict_
   __syncthreads();
   encode_rows<true, 256, true>(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab, &dtab);
 }
+#endif
 
 // One launch, two independent jobs on disjoint buffers: the aggregation of the
 // uploads already in HBM (blocks [0, nU): k_update_mixed's grid) and the client
@@ -1377,6 +1405,32 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
                      (int)(e / ej.gx), &tab, &dtab);
   }
 }
+
+// The stream kernels are compiled in their own translation unit
+// (stream_kernels.hip: this file under FLEET_STREAM_TU) with the ILP-first
+// machine scheduler, which helps them (VALU-issue bound at 5-6 waves per SIMD)
+// and hurts the tiled and pipelined kernels; the main unit only
+// declares their instantiations.
+#ifdef FLEET_STREAM_TU
+template __global__ void k_update_mixed<256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
+                                             double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
+                                             uint8_t* __restrict__, float* __restrict__, int* __restrict__, int);
+template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
+                                              double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
+                                              uint8_t* __restrict__, float* __restrict__, int* __restrict__, int, int,
+                                              EncodeJob);
+#else
+extern template __global__ void k_update_mixed<256>(const uint8_t* __restrict__, size_t, int,
+                                                    const double* __restrict__, double, int64_t, int64_t, int64_t,
+                                                    const int32_t* __restrict__, uint8_t* __restrict__,
+                                                    float* __restrict__, int* __restrict__, int);
+extern template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_t, int,
+                                                     const double* __restrict__, double, int64_t, int64_t, int64_t,
+                                                     const int32_t* __restrict__, uint8_t* __restrict__,
+                                                     float* __restrict__, int* __restrict__, int, int, EncodeJob);
+#endif
+
+#ifndef FLEET_STREAM_TU
 
 // The same pairing for the tiled sizes (CIFAR buckets): blocks [0, nU) are
 // k_update_tiled<TG>'s tiles (under two waves per SIMD at these sizes, so most
@@ -2044,7 +2098,11 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   // stream grid or the tiles. Launch variants the plan takes only under experiment
   // overrides fall back to the stream kernel.
   const UpdatePlan p = plan_update(groups);
-  const bool pipe = p.kind == 2 && p.ipt == 1 && p.nw == 5 && !p.wp && (p.tg == 8 || p.tg == 16);
+  const bool pipe = p.kind == 2 && p.ipt == 1 && p.nw == 5 && !p.wp && p.tg == 16;
+  // the side outputs double the producers' work: more producer waves per tile
+  // (FLEET_KARDAM_PIPE_NW = 5 keeps the plain update's four)
+  const char* knw = getenv("FLEET_KARDAM_PIPE_NW");
+  const int pnw = knw && atoi(knw) == 5 ? 5 : 8;
   const bool tiled = p.kind == 1 && (p.tg == 16 || p.tg == 32 || p.tg == 64);
   const int64_t per = pipe || tiled ? p.tg : 256;
   const unsigned blocks = (unsigned)((groups + per - 1) / per);
@@ -2052,9 +2110,10 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   if (groups <= 0) return hipSuccess;
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
   if (pipe) {
-    if (p.tg == 8)
-      hipLaunchKernelGGL((k_update_pipe<8, 1, 5, 0, true>), dim3(blocks), dim3(64 * 5), 0, s, uploads, pitch, M, d_dampen,
-                         inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX, EncodeJob{}, kd);
+    if (pnw == 8)
+      hipLaunchKernelGGL((k_update_pipe<16, 1, 8, 0, true>), dim3(blocks), dim3(64 * 8), 0, s, uploads, pitch, M,
+                         d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
+                         EncodeJob{}, kd);
     else
       hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0, true>), dim3(blocks), dim3(64 * 5), 0, s, uploads, pitch, M,
                          d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
@@ -2363,4 +2422,5 @@ hipError_t launch_digest(int fn, unsigned long long* out, hipStream_t s) {
   return hipGetLastError();
 }
 
+#endif  // FLEET_STREAM_TU
 }  // namespace fleet
