@@ -529,6 +529,11 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
   }
 }
 
+#ifndef FLEET_TILE_XCD
+#define FLEET_TILE_XCD 1
+#endif
+constexpr bool kTileXcd = FLEET_TILE_XCD != 0;
+
 #ifndef FLEET_STAGEC_VAR
 #define FLEET_STAGEC_VAR 1
 #endif
@@ -1037,6 +1042,18 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG>& sh, float* pt
   FLEET_TSTAMP(5);
 }
 
+// XCD-aware tile order: the dispatcher deals workgroups to the 8 XCDs round robin
+// (b % 8; placement is unspecified, so this is for speed only, never correctness).
+// Tiles of neighbouring column ranges share the 128-byte lines their 1 KiB row
+// segments straddle (rows are only 16-byte aligned); dealt round robin, those
+// lines were fetched once per XCD's L2 (PMC traffic 1.11x the algorithmic bytes
+// on cifar10_256). Here XCD x runs one contiguous run of tiles instead.
+__device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb) {
+  if (nb < 16) return b;
+  const int64_t q = nb / 8, r = nb % 8, x = b % 8, i = b / 8;
+  return x * q + (x < r ? x : r) + i;
+}
+
 // KD = true: Kardam's side outputs from the tile producers (tile_kardam).
 template <int TG, bool KD = false>
 __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict__ uploads, size_t pitch, int M,
@@ -1047,7 +1064,8 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
                                                       int* __restrict__ err, KardamOut kd = KardamOut{}) {
   __shared__ TileShared<TG> sh;
   __shared__ float ptile[tiled_chunk_clients<TG>() * 3 * TG];
-  update_tiled_block<TG, KD>(sh, ptile, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+  update_tiled_block<TG, KD>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x, uploads, pitch, M,
+                             dampen, inv_avg, n_up, g_begin, g_end,
                              hdr_block, merged, merged_f32, err,
                              TileKd{kd, (int64_t)blockIdx.x, (int64_t)gridDim.x, (int64_t)hdr_block[2]});
 }
@@ -1447,7 +1465,8 @@ __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __re
   __shared__ TileShared<TG> sh;
   __shared__ float ptile[tiled_chunk_clients<TG>() * 3 * TG];
   if ((int)blockIdx.x < nU) {  // block-uniform
-    update_tiled_block<TG>(sh, ptile, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block,
+    update_tiled_block<TG>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nU) : blockIdx.x, uploads, pitch, M, dampen,
+                           inv_avg, n_up, g_begin, g_end, hdr_block,
                            merged, merged_f32, err);
   } else {
     b64_tables_init(&sh.tab);
