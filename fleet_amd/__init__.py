@@ -197,8 +197,8 @@ def update_encode_kernel(length: int) -> str:
     if not os.environ.get("FLEET_FUSED_STEP_OFF"):
         if k == "k_update_mixed<256>":
             return "k_update_encode<256>"
-        if k in ("k_update_tiled<64>", "k_update_tiled<32>"):
-            return k.replace("k_update_tiled", "k_update_tiled_encode")
+        if k.startswith(("k_update_tiled<64", "k_update_tiled<32")):
+            return "k_update_tiled_encode<%s>" % k[len("k_update_tiled<"):].split(",")[0].rstrip(">")
         if k.startswith("k_update_pipe"):
             return k + " (with the encode's blocks)"
     return k + " + k_encode_f32"

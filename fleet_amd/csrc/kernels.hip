@@ -1055,20 +1055,42 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb) {
 }
 
 // KD = true: Kardam's side outputs from the tile producers (tile_kardam).
-template <int TG, bool KD = false>
+//
+// TG2 > 0: a two-width grid. Every tile of a launch is resident at once at CIFAR
+// sizes (cifar10_256: 1,635 tiles of 64 groups for 1,792 block slots), so the
+// kernel takes as long as its most loaded CU: 7 tiles where the average is 6.4.
+// Blocks [0, nW) are whole rounds of TG-wide tiles (nW a multiple of the CU
+// count: the same number on every CU), the groups after them go to TG2-wide
+// tiles (a quarter or half of a wide tile's work) spread over the CUs, so the
+// last partial round costs its share of the work instead of a whole tile.
+template <int TG, bool KD = false, int TG2 = 0>
 __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                       const double* __restrict__ dampen, double inv_avg,
                                                       int64_t n_up, int64_t g_begin, int64_t g_end,
                                                       const int32_t* __restrict__ hdr_block,
                                                       uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                      int* __restrict__ err, KardamOut kd = KardamOut{}) {
+                                                      int* __restrict__ err, KardamOut kd = KardamOut{},
+                                                      int nW = INT32_MAX) {
+  static_assert(TG2 == 0 || (TG2 < TG && sizeof(TileShared<TG2>) <= sizeof(TileShared<TG>) &&
+                             tiled_chunk_clients<TG2>() * 3 * TG2 <= tiled_chunk_clients<TG>() * 3 * TG),
+                "the narrow tiles' state fits the wide tiles' LDS");
   __shared__ TileShared<TG> sh;
   __shared__ float ptile[tiled_chunk_clients<TG>() * 3 * TG];
-  update_tiled_block<TG, KD>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x, uploads, pitch, M,
-                             dampen, inv_avg, n_up, g_begin, g_end,
-                             hdr_block, merged, merged_f32, err,
-                             TileKd{kd, (int64_t)blockIdx.x, (int64_t)gridDim.x, (int64_t)hdr_block[2]});
+  const TileKd tk{kd, (int64_t)blockIdx.x, (int64_t)gridDim.x, (int64_t)hdr_block[2]};
+  if constexpr (TG2 > 0) {
+    if ((int)blockIdx.x >= nW) {  // block-uniform: a narrow tile after the wide rounds
+      const int64_t nN = (int64_t)gridDim.x - nW, b = (int64_t)blockIdx.x - nW;
+      update_tiled_block<TG2, KD>(reinterpret_cast<TileShared<TG2>&>(sh), ptile, kTileXcd ? xcd_tile(b, nN) : b,
+                                  uploads, pitch, M, dampen, inv_avg, n_up, g_begin + (int64_t)nW * TG, g_end,
+                                  hdr_block, merged, merged_f32, err, tk);
+      return;
+    }
+  }
+  const int64_t nw = TG2 > 0 ? (int64_t)nW : (int64_t)gridDim.x;
+  update_tiled_block<TG, KD>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nw) : blockIdx.x, uploads, pitch, M,
+                             dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged, merged_f32, err, tk);
 }
+
 
 // Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
 // One group (3 values) of one row: float2int (fixed chains when the wave is
@@ -1926,6 +1948,29 @@ static int stream_full_rounds_blocks(int64_t groups) {
   const int64_t full = waves / simds * simds;  // waves in whole rounds
   return (int)(full * 64 / 256);
 }
+// The two-width split of k_update_tiled's TG-wide grid over `groups` groups: nW
+// wide tiles (whole rounds over the CUs: the same count on every CU) and nN tiles
+// of TG2 groups for the rest; nW = -1 (the one-width grid) when there is no whole
+// round or no partial one. FLEET_TILE_MIX = 0 turns it off, 16 / 32 pick TG2
+// (default 16 for TG = 64; experiments).
+struct TileSplit {
+  int nW, tg2;
+  int64_t nN;
+};
+static TileSplit tile_split(int64_t groups, int tg) {
+  TileSplit t{-1, 0, 0};
+  int tg2 = tg == 64 ? 16 : 0;
+  if (const char* e = getenv("FLEET_TILE_MIX")) tg2 = atoi(e);
+  if (tg != 64 || (tg2 != 16 && tg2 != 32)) return t;
+  const int cus = device_simds() / 4;
+  const int64_t tiles = (groups + tg - 1) / tg, rounds = tiles / cus;
+  if (rounds < 1 || tiles % cus == 0) return t;
+  t.nW = (int)(rounds * cus);
+  t.tg2 = tg2;
+  t.nN = (groups - (int64_t)t.nW * tg + tg2 - 1) / tg2;
+  return t;
+}
+
 // the split in use: FLEET_UPDATE_MIXED=0 the plain stream grid (-1), =2 every group
 // one value per lane (0; experiments)
 static int mixed_split(int64_t groups) {
@@ -1995,6 +2040,8 @@ const char* update_kernel_name(int64_t groups) {
     snprintf(buf, sizeof buf, "k_update<%d, false, 256>", p.k);  // as rocprofv3 names it
   else if (p.kind == 2)
     snprintf(buf, sizeof buf, "k_update_pipe<%d, %d, %d, %d>", p.tg, p.ipt, p.nw, p.wp);
+  else if (const TileSplit t = tile_split(groups, p.tg); t.nW >= 0)
+    snprintf(buf, sizeof buf, "k_update_tiled<%d, false, %d>", p.tg, t.tg2);
   else
     snprintf(buf, sizeof buf, "k_update_tiled<%d>", p.tg);
   return buf;
@@ -2052,7 +2099,15 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
     if (p.tg == 8) FLEET_LAUNCH(k_update_tiled<8>, 8);
     else if (p.tg == 16) FLEET_LAUNCH(k_update_tiled<16>, 16);
     else if (p.tg == 32) FLEET_LAUNCH(k_update_tiled<32>, 32);
-    else FLEET_LAUNCH(k_update_tiled<64>, 64);
+    else if (const TileSplit t = tile_split(groups, 64); t.nW >= 0) {
+      const dim3 grid((unsigned)(t.nW + t.nN));
+      if (t.tg2 == 32)
+        hipLaunchKernelGGL((k_update_tiled<64, false, 32>), grid, dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg,
+                           n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, KardamOut{}, t.nW);
+      else
+        hipLaunchKernelGGL((k_update_tiled<64, false, 16>), grid, dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg,
+                           n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, KardamOut{}, t.nW);
+    } else FLEET_LAUNCH(k_update_tiled<64>, 64);
   } else {
     if (p.k == 4) FLEET_LAUNCH(k_update<4>, 256 * 4);
     else if (p.k == 2) FLEET_LAUNCH(k_update<2>, 256 * 2);
@@ -2081,29 +2136,56 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
   return hipGetLastError();
 }
 
-// per client: the wave partials of k_update<1, true> summed in a fixed order
-__global__ void __launch_bounds__(256) k_kardam_reduce(const double* __restrict__ partials, int64_t n_waves,
-                                                       double* __restrict__ norms) {
-  __shared__ double red[2][256];
+// per client: the (client, wave or tile) partials of the update summed in a fixed
+// order. A lane sums a strided run of partial pairs (8 independent 16-byte loads in
+// flight), the wave folds its lanes by butterfly shuffles, the block's waves meet
+// in LDS. One wave per client for the tiles' few hundred partials (no barrier on
+// the path: the reduce is latency, 6 us with a 256-thread LDS tree on MNIST-64),
+// four for the stream grid's thousands.
+template <int NT>
+__global__ void __launch_bounds__(NT) k_kardam_reduce(const double* __restrict__ partials, int64_t n_waves,
+                                                      double* __restrict__ norms) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
   const int c = blockIdx.x;
-  double a = 0.0, b = 0.0;
-  for (int64_t w = threadIdx.x; w < n_waves; w += blockDim.x) {
-    a += partials[((size_t)c * n_waves + w) * 2];
-    b += partials[((size_t)c * n_waves + w) * 2 + 1];
+  const d2* p = reinterpret_cast<const d2*>(partials) + (size_t)c * n_waves;
+  d2 acc[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = d2{0.0, 0.0};
+  int64_t w = threadIdx.x;
+  for (; w + 7 * NT < n_waves; w += 8 * NT)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += p[w + u * NT];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (w + u * NT < n_waves) acc[u] += p[w + u * NT];
+  double a = ((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x)) + ((acc[4].x + acc[5].x) + (acc[6].x + acc[7].x));
+  double b = ((acc[0].y + acc[1].y) + (acc[2].y + acc[3].y)) + ((acc[4].y + acc[5].y) + (acc[6].y + acc[7].y));
+#pragma unroll
+  for (int s = 32; s > 0; s >>= 1) {
+    a += __shfl_xor(a, s);
+    b += __shfl_xor(b, s);
   }
-  red[0][threadIdx.x] = a;
-  red[1][threadIdx.x] = b;
-  __syncthreads();
-  for (int s = blockDim.x / 2; s > 0; s >>= 1) {
-    if ((int)threadIdx.x < s) {
-      red[0][threadIdx.x] += red[0][threadIdx.x + s];
-      red[1][threadIdx.x] += red[1][threadIdx.x + s];
+  if constexpr (NT == 64) {
+    if (threadIdx.x == 0) {
+      norms[2 * c] = a;
+      norms[2 * c + 1] = b;
+    }
+  } else {
+    __shared__ double red[2][NT / 64];
+    if ((threadIdx.x & 63) == 0) {
+      red[0][threadIdx.x / 64] = a;
+      red[1][threadIdx.x / 64] = b;
     }
     __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    norms[2 * c] = red[0][0];
-    norms[2 * c + 1] = red[1][0];
+    if (threadIdx.x == 0) {
+      double sa = 0.0, sb = 0.0;
+      for (int i = 0; i < NT / 64; ++i) {
+        sa += red[0][i];
+        sb += red[1][i];
+      }
+      norms[2 * c] = sa;
+      norms[2 * c + 1] = sb;
+    }
   }
 }
 
@@ -2124,7 +2206,8 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   const int pnw = knw && atoi(knw) == 5 ? 5 : 8;
   const bool tiled = p.kind == 1 && (p.tg == 16 || p.tg == 32 || p.tg == 64);
   const int64_t per = pipe || tiled ? p.tg : 256;
-  const unsigned blocks = (unsigned)((groups + per - 1) / per);
+  const TileSplit ts = tiled ? tile_split(groups, p.tg) : TileSplit{-1, 0, 0};
+  const unsigned blocks = ts.nW >= 0 ? (unsigned)(ts.nW + ts.nN) : (unsigned)((groups + per - 1) / per);
   *n_waves = pipe || tiled ? (int)blocks : (int)blocks * 4;
   if (groups <= 0) return hipSuccess;
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
@@ -2143,13 +2226,24 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
                      n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd)
     if (p.tg == 16) FLEET_LAUNCH_TK(16);
     else if (p.tg == 32) FLEET_LAUNCH_TK(32);
-    else FLEET_LAUNCH_TK(64);
+    else if (ts.nW >= 0) {
+      if (ts.tg2 == 32)
+        hipLaunchKernelGGL((k_update_tiled<64, true, 32>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
+                           inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd, ts.nW);
+      else
+        hipLaunchKernelGGL((k_update_tiled<64, true, 16>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
+                           inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd, ts.nW);
+    } else FLEET_LAUNCH_TK(64);
 #undef FLEET_LAUNCH_TK
   } else {
     hipLaunchKernelGGL((k_update<1, true>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
                        g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd);
   }
-  hipLaunchKernelGGL(k_kardam_reduce, dim3((unsigned)M), dim3(256), 0, s, kd.partials, (int64_t)*n_waves, norms);
+  if (*n_waves <= 2048)
+    hipLaunchKernelGGL(k_kardam_reduce<64>, dim3((unsigned)M), dim3(64), 0, s, kd.partials, (int64_t)*n_waves, norms);
+  else
+    hipLaunchKernelGGL(k_kardam_reduce<256>, dim3((unsigned)M), dim3(256), 0, s, kd.partials, (int64_t)*n_waves,
+                       norms);
   return hipGetLastError();
 }
 

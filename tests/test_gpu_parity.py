@@ -361,6 +361,33 @@ def test_update_large_magnitudes_slow_path(codec, oracle, monkeypatch, env):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm) == oracle.update_faithful(ups, d)
 
 
+@pytest.mark.parametrize("mix", ["16", "32", "0"])
+def test_update_two_width_tiles(codec, oracle, monkeypatch, mix):
+    """k_update_tiled's two-width grid (whole rounds of 64-group tiles, the rest in
+    16- or 32-group tiles; FLEET_TILE_MIX=0 the one-width grid): 16,668 groups =
+    one round of 256 wide tiles + 284 groups, the last narrow tile ragged; large
+    magnitudes force the in-stage fallbacks and the general-chain recompute in
+    both tile widths."""
+    monkeypatch.setenv("FLEET_UPDATE_MODE", "tiled")
+    monkeypatch.setenv("FLEET_TILE_G", "64")
+    monkeypatch.setenv("FLEET_TILE_MIX", mix)
+    lay = synthetic(50_003)
+    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+    rng = np.random.default_rng(11)
+    M = 6
+    ups = []
+    for c in range(M):
+        v = oracle.synth_upload(5, c, list(lay.w_sizes), list(lay.b_sizes))
+        big = (rng.random(len(v)) < 0.05) & (hm == 0)  # header slots keep the layout
+        v[big] = (np.exp(rng.uniform(0, 21, big.sum())) * rng.choice([-1, 1], big.sum())).astype(np.float32)
+        v[-5:-1] = [9.99e8, -9.99e8, 2.1e9, 0.999999]
+        ups.append(oracle.encode_floats(v))
+    d = [1.0, 7.5, 0.25, 10.0, 1 / 3, 1.0]
+    want = "k_update_tiled<64>" if mix == "0" else "k_update_tiled<64, false, %s>" % mix
+    assert F.update_kernel(len(ups[0])) == want
+    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
+
+
 @pytest.mark.parametrize("mode", ["tiled", "tiled-nopipe", "tiled-wide", "tiled-ipt2", "tiled-8waves",
                                   "tiled-4waves", "tiled-wavepass", "stream"])
 def test_update_modes(codec, oracle, monkeypatch, mode):
