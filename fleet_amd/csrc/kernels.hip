@@ -1476,18 +1476,30 @@ extern template __global__ void k_update_encode<256>(const uint8_t* __restrict__
 // k_update_tiled<TG>'s tiles (under two waves per SIMD at these sizes, so most
 // wave slots are free), the rest the client encode's blocks on the tile's B64Tables
 // (VarEntry digit counts: the tile state leaves no room for the byte table).
-template <int TG>
+// TG2 > 0: the update's tiles on k_update_tiled's two-width grid (blocks [0, nW)
+// wide, [nW, nU) TG2-wide).
+template <int TG, int TG2 = 0>
 __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                              const double* __restrict__ dampen, double inv_avg,
                                                              int64_t n_up, int64_t g_begin, int64_t g_end,
                                                              const int32_t* __restrict__ hdr_block,
                                                              uint8_t* __restrict__ merged,
                                                              float* __restrict__ merged_f32, int* __restrict__ err,
-                                                             int nU, EncodeJob ej) {
+                                                             int nU, EncodeJob ej, int nW = INT32_MAX) {
   __shared__ TileShared<TG> sh;
   __shared__ float ptile[tiled_chunk_clients<TG>() * 3 * TG];
   if ((int)blockIdx.x < nU) {  // block-uniform
-    update_tiled_block<TG>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nU) : blockIdx.x, uploads, pitch, M, dampen,
+    if constexpr (TG2 > 0) {
+      if ((int)blockIdx.x >= nW) {
+        const int64_t nN = (int64_t)nU - nW, b = (int64_t)blockIdx.x - nW;
+        update_tiled_block<TG2>(reinterpret_cast<TileShared<TG2>&>(sh), ptile, kTileXcd ? xcd_tile(b, nN) : b,
+                                uploads, pitch, M, dampen, inv_avg, n_up, g_begin + (int64_t)nW * TG, g_end,
+                                hdr_block, merged, merged_f32, err);
+        return;
+      }
+    }
+    const int64_t nw = TG2 > 0 ? (int64_t)nW : (int64_t)nU;
+    update_tiled_block<TG>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nw) : blockIdx.x, uploads, pitch, M, dampen,
                            inv_avg, n_up, g_begin, g_end, hdr_block,
                            merged, merged_f32, err);
   } else {
@@ -2298,14 +2310,24 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   const int64_t gx = blocks_for(groups, 256);
   if (groups > 0 && p.kind == 1 && (p.tg == 32 || p.tg == 64) && !getenv("FLEET_FUSED_STEP_OFF")) {
     const int rpb = encode_rows_per_block(gx, M);
-    const int64_t nU = (groups + p.tg - 1) / p.tg, nE = gx * ((M + rpb - 1) / rpb);
+    int64_t nU = (groups + p.tg - 1) / p.tg;
+    const int64_t nE = gx * ((M + rpb - 1) / rpb);
     const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
-#define FLEET_LAUNCH_TE(TG)                                                                                        \
-  hipLaunchKernelGGL((k_update_tiled_encode<TG>), dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, M,   \
-                     d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)nU, \
-                     ej)
-    if (p.tg == 64) FLEET_LAUNCH_TE(64);
-    else FLEET_LAUNCH_TE(32);
+    // one-width tiles here: the encode's blocks already fill the CUs the last partial
+    // round of tiles leaves idle, and the narrow tiles' extra work then costs step time
+    // (two-width grid, FLEET_FUSED_TILE_MIX=1: cifar10_256 415 -> 441 us, cifar100_1024
+    // 1623 -> 1734 us per step, same box)
+    const char* fm = getenv("FLEET_FUSED_TILE_MIX");
+    const TileSplit t = (fm && atoi(fm) == 1) ? tile_split(groups, p.tg) : TileSplit{-1, 0, 0};
+    if (t.nW >= 0) nU = t.nW + t.nN;
+#define FLEET_LAUNCH_TE(TG, TG2)                                                                                    \
+  hipLaunchKernelGGL((k_update_tiled_encode<TG, TG2>), dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, \
+                     M, d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err,        \
+                     (int)nU, ej, t.nW)
+    if (p.tg == 64 && t.nW >= 0 && t.tg2 == 32) FLEET_LAUNCH_TE(64, 32);
+    else if (p.tg == 64 && t.nW >= 0) FLEET_LAUNCH_TE(64, 16);
+    else if (p.tg == 64) FLEET_LAUNCH_TE(64, 0);
+    else FLEET_LAUNCH_TE(32, 0);
 #undef FLEET_LAUNCH_TE
     return hipGetLastError();
   }
