@@ -12,7 +12,7 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PROF = os.path.join(ROOT, "profiles", "r02")
+PROF = os.path.join(ROOT, "profiles", "r03")
 
 
 def _kernel_avg_ns(stats_csv, kernel):
@@ -27,7 +27,7 @@ def _kernel_avg_ns(stats_csv, kernel):
     raise KeyError(kernel)
 
 
-@pytest.mark.parametrize("line", ["bench_default.json", "bench_recheck_rebuilt_tree.json"])
+@pytest.mark.parametrize("line", ["bench_default.json"])
 def test_headline_roofline_matches_profile(line):
     path = os.path.join(PROF, line)
     d = json.loads(open(path).read().strip().splitlines()[-1])
