@@ -5,8 +5,14 @@ serial across clients but independent across elements, so rank r of N owns a
 contiguous range of 16-char / 3-value Base64 groups of EVERY upload, runs the
 exact chain there (fleet_update_device on just that window), and the merged
 slices are all-gathered -- RCCL over xGMI with the "nccl" backend, gloo on CPU.
-No reduction crosses ranks, so the result is byte-identical to one GPU's; a
-client-sharded sum would reorder the re-quantised adds and is not offered.
+No reduction crosses ranks, so the result is byte-identical to one GPU's.
+
+ClientShardedUpdater is the opt-in APPROXIMATE alternative (SURVEY.md §8e's
+"approx" mode, the literal "RCCL reduce producing the final model delta"): rank r
+aggregates its block of clients with the exact chain, and one all_reduce sums the
+ranks' partial averages. That reorders the re-quantised adds of
+CppNNUpdater.java:490-493, so its text is NOT the reference's; `deviation`
+reports how far it lands from the exact result.
 
 One process per GPU (torch.distributed); every rank receives the full merged
 Base64 (the reference returns it to the Java updater on the server host).
@@ -129,3 +135,97 @@ class ShardedUpdater:
         sizes = [byte_range(L, *group_range(groups, self.world, r)) for r in range(self.world)]
         full = gather_slices(local, [s1 - s0 for s0, s1 in sizes], self.group)
         return full.cpu().numpy().tobytes()
+
+
+class ClientShardedUpdater(ShardedUpdater):
+    """Opt-in approximate aggregation sharded over CLIENTS ("approx").
+
+    Rank r takes the contiguous block of picked uploads [cb, ce) (group_range over
+    clients) and runs the exact chain of CppNNUpdater.update on them alone
+    (fleet_update_device: decode, dampen, serial re-quantised sum, average by its
+    own M_r), giving merged_f32_r = dec(merged_r). One all_reduce(SUM) in float64
+    (RCCL over xGMI) of (M_r / M) * merged_f32_r gives the average over all M
+    clients; header slots (and slots past the layout walk) carry the LAST upload's
+    decoded codes, contributed with weight 1 by the rank holding client M-1. The
+    sum is encoded (Base64::encode(vector<float>)) on every rank.
+
+    Not bit-exact: the reference adds the M dampened uploads one by one,
+    re-quantising after every add (CppNNUpdater.java:490-493); here each rank's
+    block is summed that way and the blocks are added in float64 at the end, then
+    quantised once. Use `deviation(approx, exact)` to report the difference; the
+    exact, byte-identical default is ShardedUpdater (element sharding)."""
+
+    def local_partial(self, uploads: Sequence[bytes], dampen: Sequence[float], header_pos):
+        """This rank's block of uploads through the exact chain: (merged_f32 as a
+        float64 tensor of n values, the merged Base64 as bytes)."""
+        import torch
+        M, L = len(uploads), len(uploads[0])
+        groups = (b64_count(L) + 2) // 3
+        host = np.zeros((M, 16 * groups), np.uint8)
+        for c, u in enumerate(uploads):
+            host[c, :L] = np.frombuffer(u, np.uint8)
+        dev = torch.from_numpy(host).pin_memory().to(self.device, non_blocking=True)
+        merged = torch.empty(16 * groups, dtype=torch.uint8, device=self.device)
+        f32 = torch.empty(3 * groups, dtype=torch.float32, device=self.device)
+        self.codec.update_device(dev, L, dampen, header_pos, merged, f32)
+        self.codec.check()
+        return f32[: b64_count(L)].double(), merged[:L].cpu().numpy().tobytes()
+
+    def encode(self, values) -> bytes:
+        """Base64 text of the summed average (float32)."""
+        return self.codec.encode_floats(values.float().cpu().numpy())
+
+    def update(self, uploads: Sequence[bytes], dampen: Sequence[float]) -> bytes:
+        import torch
+        import torch.distributed as dist
+        M = len(uploads)
+        if M == 0 or len(dampen) != M:
+            raise ValueError("need one dampening factor per upload")
+        L = len(uploads[0])
+        if any(len(u) != L for u in uploads):
+            raise ValueError("uploads differ in length (one layout per update)")
+        n = b64_count(L)
+        cb, ce = group_range(M, self.world, self.rank)
+        last_owner = next(r for r in range(self.world) if group_range(M, self.world, r)[1] == M)
+        acc = torch.zeros(n, dtype=torch.float64, device=self.device)
+        status = 0
+        err: Optional[BaseException] = None
+        try:
+            hpos = self.layout(uploads[-1])
+            if ce > cb:
+                part, text = self.local_partial(uploads[cb:ce], list(dampen[cb:ce]), hpos)
+                if self.world == 1:
+                    return text  # one rank holds every client: the exact chain
+                keep = torch.zeros(n, dtype=torch.bool, device=self.device)
+                if hpos:
+                    keep[torch.as_tensor(hpos, dtype=torch.long, device=self.device)] = True
+                acc = torch.where(keep, part if self.rank == last_owner else torch.zeros_like(part),
+                                  part * ((ce - cb) / M))
+        except Exception as e:  # every rank raises together below
+            err, status = e, 1
+        if self.world > 1:
+            flag = torch.tensor([status], dtype=torch.int32, device=self.device)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+            status = int(flag.item())
+        if status:
+            if err is not None:
+                raise err
+            raise RuntimeError("fleet update failed on another rank")
+        if self.world > 1:
+            dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=self.group)
+        return self.encode(acc)
+
+
+def deviation(approx: np.ndarray, exact: np.ndarray) -> dict:
+    """How far an approximate merged gradient (decoded float32) lands from the exact
+    one: the fraction of values that differ, the largest absolute difference and
+    the largest difference relative to max(|exact|, 1e-30)."""
+    a = np.asarray(approx, np.float32).astype(np.float64)
+    e = np.asarray(exact, np.float32).astype(np.float64)
+    if a.shape != e.shape:
+        raise ValueError("different lengths")
+    if a.size == 0:
+        return {"n": 0, "frac_differ": 0.0, "max_abs": 0.0, "max_rel": 0.0}
+    d = np.abs(a - e)
+    return {"n": int(a.size), "frac_differ": float(np.mean(a != e)), "max_abs": float(d.max()),
+            "max_rel": float((d / np.maximum(np.abs(e), 1e-30)).max())}

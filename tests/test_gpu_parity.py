@@ -449,6 +449,28 @@ def test_device_window_update(codec, oracle):
     assert ShardedUpdater(codec).update(ups, d) == exp
 
 
+def test_client_sharded_partials_on_device(codec, oracle):
+    """The approximate client-sharded mode's per-rank HIP step (fleet_amd.shard.
+    ClientShardedUpdater.local_partial): a block of clients through the exact
+    chain on the GPU equals the oracle on that block (bytes and decoded floats);
+    with one rank the mode IS the exact chain. Its N-rank combination runs under
+    gloo in tests/test_shard_gloo.py."""
+    from fleet_amd.shard import ClientShardedUpdater
+    lay = MNIST
+    M = 7
+    ups = uploads_for(oracle, lay, M, seed=23)
+    d = policy("inverse", M)
+    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+    cs = ClientShardedUpdater(codec)
+    hp = cs.layout(ups[-1])
+    for cb, ce in ((0, 3), (3, 7)):
+        part, text = cs.local_partial(ups[cb:ce], d[cb:ce], hp)
+        want = oracle.update_fused(ups[cb:ce], d[cb:ce], hm)
+        assert text == want
+        assert np.array_equal(part.float().cpu().numpy().view(np.uint32), oracle.decode_floats(want).view(np.uint32))
+    assert cs.update(ups, d) == oracle.update_fused(ups, d, hm)
+
+
 # ---- DISTILLATION_MODE=1 model codec (SURVEY.md §8 a15-a19) ---------------------------------
 
 def _model_fixture(name):

@@ -106,3 +106,64 @@ def test_sharded_update_gloo_matches_single_process(world, tmp_path):
     for r in range(world):
         flags = (tmp_path / f"rank{r}.txt").read_text().split()
         assert flags == ["1"] * (len(cases) + 1), f"rank {r}: {flags}"
+
+
+def _client_rank_main(rank, world, port, cases, out_dir):
+    """ClientShardedUpdater (the opt-in approximate mode) with the oracle standing in
+    for the per-rank HIP update and the encode; gloo carries the float64 all_reduce."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+
+    import pyoracle
+    from fleet_amd.shard import ClientShardedUpdater, deviation
+
+    o = pyoracle.Oracle()
+
+    class OracleClientRank(ClientShardedUpdater):
+        def __init__(self, layout):
+            super().__init__(codec=None, device="cpu")
+            self.mask = o.header_mask(list(layout.w_sizes), list(layout.b_sizes))
+
+        def layout(self, last_upload):
+            return np.nonzero(self.mask)[0].tolist()
+
+        def local_partial(self, uploads, dampen, header_pos):
+            text = o.update_fused(list(uploads), list(dampen), self.mask, threads=1)
+            return torch.from_numpy(o.decode_floats(text).astype(np.float64)), text
+
+        def encode(self, values):
+            return o.encode_floats(values.float().numpy())
+
+    lines = []
+    for name, M in cases:
+        lay = MNIST if name == "mnist" else synthetic(int(name))
+        ups = [o.encode_floats(o.synth_upload(9, c, list(lay.w_sizes), list(lay.b_sizes))) for c in range(M)]
+        d = [1.0 / ((c % 3) + 1) for c in range(M)]
+        hm = o.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+        exact = o.update_fused(ups, d, hm)
+        got = OracleClientRank(lay).update(ups, d)
+        a, e = o.decode_floats(got), o.decode_floats(exact)
+        dv = deviation(a, e)
+        ok = (len(got) == len(exact) and np.array_equal(a[hm != 0], e[hm != 0])
+              and dv["max_abs"] <= 2e-6 * max(1.0, float(np.abs(e).max())))
+        lines.append("%d %s %d %.6g %.6g" % (ok, name, M, dv["frac_differ"], dv["max_abs"]))
+    with open(os.path.join(out_dir, f"crank{rank}.txt"), "w") as f:
+        f.write("\n".join(lines))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_client_sharded_approx_gloo(world, tmp_path):
+    """The approximate client-sharded mode: header slots exact, payload within a
+    bound of the exact chain (|diff| <= 2e-6 max|exact| on the synthetic mix), the
+    same text on every rank; M < world leaves ranks without clients."""
+    import torch.multiprocessing as mp
+    cases = [("mnist", 8), ("1000", 5), ("5000", 2)]
+    mp.start_processes(_client_rank_main, args=(world, _free_port(), cases, str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    texts = [(tmp_path / f"crank{r}.txt").read_text().splitlines() for r in range(world)]
+    for r in range(world):
+        assert all(line.startswith("1 ") for line in texts[r]), texts[r]
+        assert texts[r] == texts[0]
