@@ -20,7 +20,6 @@ struct B64Tables {
   MulEntry mt[16];    // step multipliers by digit count (codec_math.h)
   VarEntry var[512];  // digit count by sign + biased exponent (codec_math.h)
   uint8_t from[256];  // Base64.cpp:56-68, 0xff = not in the alphabet
-  uint8_t fromf[256]; // same, 0x40 = not in the alphabet
   uint8_t to[64];
 };
 static_assert(sizeof(B64Tables) % 16 == 0, "copied as uint4");
@@ -34,13 +33,6 @@ FLEET_HDC uint8_t b64_from_value(int ch) {
   return 0xff;
 }
 
-// 0..63, or 0x40 for a byte outside the alphabet (one flag bit, so a group's
-// validity is the OR of its sextets)
-FLEET_HDC uint8_t b64_from_value_flag(int ch) {
-  const uint8_t v = b64_from_value(ch);
-  return v == 0xff ? 0x40 : v;
-}
-
 FLEET_HDC uint8_t b64_to_value(int s) {
   return (uint8_t)(s < 26 ? 'A' + s : s < 52 ? 'a' + s - 26 : s < 62 ? '0' + s - 52 : s == 62 ? '+' : '/');
 }
@@ -51,7 +43,6 @@ FLEET_HDC B64Tables make_b64_tables() {
   for (int i = 0; i < 512; ++i) t.var[i] = var_entry((uint32_t)i);
   for (int i = 0; i < 256; ++i) {
     t.from[i] = b64_from_value(i);
-    t.fromf[i] = b64_from_value_flag(i);
   }
   for (int i = 0; i < 64; ++i) t.to[i] = b64_to_value(i);
   return t;
@@ -60,7 +51,7 @@ FLEET_HDC B64Tables make_b64_tables() {
 static __constant__ B64Tables g_b64_tables = make_b64_tables();
 
 // Copy the tables into the block's LDS (call from every thread of an NT-thread
-// block, then __syncthreads()): 340 16-byte loads from an L2-resident image.
+// block, then __syncthreads()): 308 16-byte loads from an L2-resident image.
 template <int NT = 256>
 __device__ __forceinline__ void b64_tables_init(B64Tables* t) {
   constexpr int n16 = (int)(sizeof(B64Tables) / 16);
@@ -145,17 +136,19 @@ __device__ __forceinline__ uint32_t b64_decode_group(uint4 w, const B64Tables* t
 }
 
 // Same decode for a full group (all 16 chars carry data): returns nonzero if any
-// char is outside the alphabet. Sextets compose by shift-or; no per-char mask.
+// char is outside the alphabet. Sextets compose by shift-or; no per-char mask:
+// valid entries are 0..63 and the invalid marker 0xff has bit 6 set, so the OR of
+// the group's sextets flags it (the codes are garbage then, and the caller fails).
 __device__ __forceinline__ uint32_t b64_decode_group_full(uint4 w, const B64Tables* t, int32_t codes[3]) {
   const uint32_t words[4] = {w.x, w.y, w.z, w.w};
   uint32_t V[4];
   uint32_t anyf = 0;
 #pragma unroll
   for (int qd = 0; qd < 4; ++qd) {
-    const uint32_t s0 = t->fromf[words[qd] & 0xff];
-    const uint32_t s1 = t->fromf[(words[qd] >> 8) & 0xff];
-    const uint32_t s2 = t->fromf[(words[qd] >> 16) & 0xff];
-    const uint32_t s3 = t->fromf[words[qd] >> 24];
+    const uint32_t s0 = t->from[words[qd] & 0xff];
+    const uint32_t s1 = t->from[(words[qd] >> 8) & 0xff];
+    const uint32_t s2 = t->from[(words[qd] >> 16) & 0xff];
+    const uint32_t s3 = t->from[words[qd] >> 24];
     anyf |= s0 | s1 | s2 | s3;
     V[qd] = (((((s0 << 6) | s1) << 6) | s2) << 6) | s3;  // flag bits only land above bit 23
   }
@@ -178,10 +171,10 @@ __device__ __forceinline__ uint32_t b64_decode_pair_full(uint32_t w0, uint32_t w
   uint32_t V[2], anyf = 0;
 #pragma unroll
   for (int qd = 0; qd < 2; ++qd) {
-    const uint32_t s0 = t->fromf[words[qd] & 0xff];
-    const uint32_t s1 = t->fromf[(words[qd] >> 8) & 0xff];
-    const uint32_t s2 = t->fromf[(words[qd] >> 16) & 0xff];
-    const uint32_t s3 = t->fromf[words[qd] >> 24];
+    const uint32_t s0 = t->from[words[qd] & 0xff];
+    const uint32_t s1 = t->from[(words[qd] >> 8) & 0xff];
+    const uint32_t s2 = t->from[(words[qd] >> 16) & 0xff];
+    const uint32_t s3 = t->from[words[qd] >> 24];
     anyf |= s0 | s1 | s2 | s3;
     V[qd] = (((((s0 << 6) | s1) << 6) | s2) << 6) | s3;
   }

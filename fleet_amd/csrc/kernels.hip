@@ -698,20 +698,28 @@ __global__ void __launch_bounds__(NT) k_update_mixed(const uint8_t* __restrict__
 
 // Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
 // of NW waves.
-template <int TG, int NW = 4>
-struct TileShared {
+// D16: the tile also holds the byte-table digit counts (D16Table, 9 KB), and the
+// epilogue assembles its merged codes in the tile's p buffer instead of outcodes.
+template <bool D16>
+struct TileD16 {};
+template <>
+struct TileD16<true> {
+  D16Table dt;
+};
+template <int TG, int NW = 4, bool D16 = false>
+struct TileShared : TileD16<D16> {
   static constexpr int E = 3 * TG;
   B64Tables tab;
-  int32_t last_codes[E];        // codes of the last upload (mergeFlatGradient's g)
-  int32_t hmin[E], hmax[E];     // header-slot codes over all uploads (layout check)
-  uint32_t hmask[TG];           // bit e = slot 3*g+e is a header slot
-  int32_t outcodes[E];          // merged codes (epilogue)
+  int32_t last_codes[E];            // codes of the last upload (mergeFlatGradient's g)
+  int32_t hmin[E], hmax[E];         // header-slot codes over all uploads (layout check)
+  uint32_t hmask[TG];               // bit e = slot 3*g+e is a header slot
+  int32_t outcodes[D16 ? 1 : E];    // merged codes (epilogue)
 };
 
 // Tables, header slots of the tile (every thread checks one header position:
 // one independent load each, not a per-group binary search), min/max init.
-template <int TG, int NW>
-__device__ __forceinline__ void tile_init(TileShared<TG, NW>& sh, const int32_t* __restrict__ hdr, int n_hdr,
+template <int TG, int NW, bool D16>
+__device__ __forceinline__ void tile_init(TileShared<TG, NW, D16>& sh, const int32_t* __restrict__ hdr, int n_hdr,
                                           int64_t g0, int ng) {
   constexpr int E = 3 * TG;
   const int tid = threadIdx.x;
@@ -719,6 +727,7 @@ __device__ __forceinline__ void tile_init(TileShared<TG, NW>& sh, const int32_t*
   int32_t hp = -1;
   if (tid < n_hdr) hp = hdr[tid];
   b64_tables_init<64 * NW>(&sh.tab);
+  if constexpr (D16) d16_table_init<64 * NW>(&sh.dt);
   if (tid < TG) sh.hmask[tid] = 0u;
   if (tid < E) {
     sh.hmin[tid] = INT32_MAX;
@@ -804,8 +813,8 @@ __device__ __forceinline__ double group_sum_f64(double v) {
 // one wave (items are client-major and waves start at multiples of 64), so the
 // lane group's sum is the (client, tile) partial: one write, no atomics, a fixed
 // order (k_kardam_reduce then sums the tiles in order).
-template <int TG, int IPT, int NW>
-__device__ __forceinline__ void tile_kardam(TileShared<TG, NW>& sh, const TileItems<TG, IPT>& it,
+template <int TG, int IPT, int NW, bool D16>
+__device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const TileItems<TG, IPT>& it,
                                             const float (&p)[3 * IPT], int64_t n_up, int64_t g0, const TileKd& tk) {
   static_assert(64 % TG == 0 && TG >= 16, "a client's groups in one lane group of 16, 32 or 64");
   constexpr int S = 3 * IPT;
@@ -814,7 +823,8 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW>& sh, const TileIt
 #pragma unroll
   for (int i = 0; i < S; ++i) rg[i] = p[i];
   dampen_stage<S>(rg, kd.lr);  // (float)((double)p * lr), lr uniform
-  q_stage<S>(G, rg, &sh.tab);  // exact (in-stage fallback)
+  if constexpr (D16) q_stage_d16x<S>(G, rg, &sh.dt, sh.tab.var);  // exact (in-stage fallback)
+  else q_stage<S>(G, rg, &sh.tab);
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
     const int c = it.c_base + it.cc[h];
@@ -833,7 +843,8 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW>& sh, const TileIt
       dv[e] = (flat[e] && hasp) ? g - kd.prev[(size_t)c * kd.vpitch + pos] : 0.0f;
       if (kd.g_out && it.live[h] && pos < n_up) kd.g_out[(size_t)c * kd.vpitch + pos] = flat[e] ? g : 0.0f;
     }
-    q_stage<3>(D, dv, &sh.tab);
+    if constexpr (D16) q_stage_d16x<3>(D, dv, &sh.dt, sh.tab.var);
+    else q_stage<3>(D, dv, &sh.tab);
 #pragma unroll
     for (int e = 0; e < 3; ++e)
       if (flat[e] && hasp) sd += (double)(D[e] * D[e]);
@@ -847,8 +858,8 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW>& sh, const TileIt
   }
 }
 
-template <int TG, int IPT, int NW, bool KD = false>
-__device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileItems<TG, IPT>& it, int M,
+template <int TG, int IPT, int NW, bool KD = false, bool D16 = false>
+__device__ __forceinline__ void tile_compute(TileShared<TG, NW, D16>& sh, const TileItems<TG, IPT>& it, int M,
                                              const double* __restrict__ dampen, int64_t n_up, int64_t g0,
                                              float* __restrict__ pdst, uint32_t& badacc,
                                              const TileKd& tk = TileKd{}) {
@@ -876,10 +887,15 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileI
       }
     }
   }
-  // stage A: y = Q(int2float(code))
+  // stage A: y = Q(int2float(code)); D16: the stream kernel's byte-table stages
   float y0[S], y[S];
-  dec_stage<S>(y0, codes, &sh.tab);
-  q_stage<S>(y, y0, &sh.tab);
+  if constexpr (D16) {
+    dec_stage_d16<S>(y0, codes, &sh.dt);
+    q_stage_d16x<S>(y, y0, &sh.dt, sh.tab.var);
+  } else {
+    dec_stage<S>(y0, codes, &sh.tab);
+    q_stage<S>(y, y0, &sh.tab);
+  }
   // stage B: p = Q(f32(f64(y) * d)), per-item client
   float r[S], p[S];
 #pragma unroll
@@ -898,7 +914,8 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileI
       for (int e = 0; e < 3; ++e) r[3 * h + e] = (float)((double)y[3 * h + e] * d);
     }
   }
-  q_stage<S>(p, r, &sh.tab);
+  if constexpr (D16) q_stage_d16x<S>(p, r, &sh.dt, sh.tab.var);
+  else q_stage<S>(p, r, &sh.tab);
 #pragma unroll
   for (int h = 0; h < IPT; ++h)
     if (it.live[h])
@@ -907,8 +924,8 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW>& sh, const TileI
   if constexpr (KD) tile_kardam<TG, IPT, NW>(sh, it, p, n_up, g0, tk);
 }
 
-template <int TG, int IPT, int NW, bool KD = false>
-__device__ __forceinline__ void tile_produce(TileShared<TG, NW>& sh, const uint8_t* __restrict__ uploads, size_t pitch,
+template <int TG, int IPT, int NW, bool KD = false, bool D16 = false>
+__device__ __forceinline__ void tile_produce(TileShared<TG, NW, D16>& sh, const uint8_t* __restrict__ uploads, size_t pitch,
                                              int M, const double* __restrict__ dampen, int64_t n_up, int64_t g0,
                                              int ng, int c_base, int nitems, int it0, int stride,
                                              float* __restrict__ pdst, uint32_t& badacc, const TileKd& tk) {
@@ -921,12 +938,16 @@ __device__ __forceinline__ void tile_produce(TileShared<TG, NW>& sh, const uint8
 // check. One thread per value computes its merged code (the longest part),
 // then one thread per group assembles the 16 Base64 chars. Call from every
 // thread of the block (contains a barrier).
-template <int TG, int NW>
-__device__ __forceinline__ void tile_epilogue(TileShared<TG, NW>& sh, const float* __restrict__ vals, double inv_avg,
-                                              int64_t n_up, int64_t walk_end, int64_t g0, int ng,
+// D16: `outc` (E ints, not overlapping vals) takes the merged codes.
+template <int TG, int NW, bool D16>
+__device__ __forceinline__ void tile_epilogue(TileShared<TG, NW, D16>& sh, const float* __restrict__ vals,
+                                              double inv_avg, int64_t n_up, int64_t walk_end, int64_t g0, int ng,
                                               uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                              int* __restrict__ err) {
+                                              int* __restrict__ err, int32_t* outc = nullptr) {
   const int tid = threadIdx.x;
+  int32_t* oc;
+  if constexpr (D16) oc = outc;
+  else oc = sh.outcodes;
   if (tid < 3 * ng) {
     const int gl = tid / 3, e = tid % 3;
     const int64_t p = 3 * g0 + tid;
@@ -937,13 +958,13 @@ __device__ __forceinline__ void tile_epilogue(TileShared<TG, NW>& sh, const floa
       o = merged_code(vals[tid], inv_avg, sh.last_codes[tid], hdr || p >= walk_end, &sh.tab);
       if (merged_f32) merged_f32[p] = dec_mt(o, sh.tab.mt);
     }
-    sh.outcodes[tid] = o;
+    oc[tid] = o;
   }
   __syncthreads();
   if (tid < ng) {
     const int64_t g = g0 + tid;
     const int r = (int)min<int64_t>(3, n_up - 3 * g);
-    const int32_t out[3] = {sh.outcodes[3 * tid], sh.outcodes[3 * tid + 1], sh.outcodes[3 * tid + 2]};
+    const int32_t out[3] = {oc[3 * tid], oc[3 * tid + 1], oc[3 * tid + 2]};
     *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &sh.tab), r);
   }
 }
@@ -967,12 +988,17 @@ __device__ __forceinline__ void tile_epilogue(TileShared<TG, NW>& sh, const floa
 // p floats per chunk: 12 KiB (CM = 16 clients at TG = 64, so a chunk is two full
 // 512-item passes); with the tables the block fits 7 per CU (measured: 24 KiB
 // chunks 0.40 ms, 12 KiB 0.37, 8 KiB 0.50, 16 KiB 0.43 on cifar10_256)
-template <int TG>
-constexpr int tiled_chunk_clients() { return FLEET_TILED_PT / (3 * TG); }
+// D16 tiles: 6 KiB (CM = 8 at TG = 64: one full 512-item pass per chunk), so the
+// byte table fits with 7 blocks per CU (22.6 KB per block)
+#ifndef FLEET_TILED_PT_D16
+#define FLEET_TILED_PT_D16 1536
+#endif
+template <int TG, bool D16 = false>
+constexpr int tiled_chunk_clients() { return TG > 0 ? (D16 ? FLEET_TILED_PT_D16 : FLEET_TILED_PT) / (3 * TG) : 0; }
 
 // Tile `bid` of k_update_tiled (LDS state in sh / ptile)
-template <int TG, bool KD = false>
-__device__ __forceinline__ void update_tiled_block(TileShared<TG>& sh, float* ptile, int64_t bid,
+template <int TG, bool KD = false, bool D16 = false>
+__device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, float* ptile, int64_t bid,
                                                    const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                    const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                                    int64_t g_begin, int64_t g_end,
@@ -981,7 +1007,8 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG>& sh, float* pt
                                                    const TileKd& tk = TileKd{}) {
   constexpr int E = 3 * TG;
   static_assert(E <= 256, "phase 2 is one thread per value");
-  constexpr int CM = tiled_chunk_clients<TG>();
+  constexpr int CM = tiled_chunk_clients<TG, D16>();
+  static_assert(CM >= 2, "the epilogue's codes go after the E final values in ptile");
   FLEET_TSTAMP(0);
   const int tid = threadIdx.x;
   const int64_t g0 = g_begin + bid * TG;
@@ -1021,9 +1048,15 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG>& sh, float* pt
 #pragma unroll 2
         for (; k < cm; ++k) {
           const float s = A + ptile[k * E + tid];
-          const uint32_t d = var_digits(s, sh.tab.var);
-          off_domain |= (uint32_t)(d > 9u);
-          A = q_mt_d(s, d, sh.tab.mt);
+          if constexpr (D16) {  // the stream kernel's stage C (var_d16: branch-free)
+            const uint32_t e = var_d16(f2u(s), sh.tab.var);
+            off_domain |= (uint32_t)(e >= kD16Out);
+            A = q_d16(s, e, &sh.dt.st);
+          } else {
+            const uint32_t d = var_digits(s, sh.tab.var);
+            off_domain |= (uint32_t)(d > 9u);
+            A = q_mt_d(s, d, sh.tab.mt);
+          }
         }
       }
     }
@@ -1038,7 +1071,8 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG>& sh, float* pt
   }
   if (tid < E) ptile[tid] = A;
   __syncthreads();
-  tile_epilogue(sh, ptile, inv_avg, n_up, hdr_block[2], g0, ng, merged, merged_f32, err);
+  tile_epilogue(sh, ptile, inv_avg, n_up, hdr_block[2], g0, ng, merged, merged_f32, err,
+                D16 ? reinterpret_cast<int32_t*>(ptile + E) : nullptr);
   FLEET_TSTAMP(5);
 }
 
@@ -1063,7 +1097,8 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb) {
 // count: the same number on every CU), the groups after them go to TG2-wide
 // tiles (a quarter or half of a wide tile's work) spread over the CUs, so the
 // last partial round costs its share of the work instead of a whole tile.
-template <int TG, bool KD = false, int TG2 = 0>
+// D16: the tiles on the byte-table digit counts (TileShared<..., true>).
+template <int TG, bool KD = false, int TG2 = 0, bool D16 = false>
 __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                       const double* __restrict__ dampen, double inv_avg,
                                                       int64_t n_up, int64_t g_begin, int64_t g_end,
@@ -1071,24 +1106,24 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
                                                       uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
                                                       int* __restrict__ err, KardamOut kd = KardamOut{},
                                                       int nW = INT32_MAX) {
-  static_assert(TG2 == 0 || (TG2 < TG && sizeof(TileShared<TG2>) <= sizeof(TileShared<TG>) &&
-                             tiled_chunk_clients<TG2>() * 3 * TG2 <= tiled_chunk_clients<TG>() * 3 * TG),
+  static_assert(TG2 == 0 || (TG2 < TG && sizeof(TileShared<TG2, 4, D16>) <= sizeof(TileShared<TG, 4, D16>) &&
+                             tiled_chunk_clients<TG2, D16>() * 3 * TG2 <= tiled_chunk_clients<TG, D16>() * 3 * TG),
                 "the narrow tiles' state fits the wide tiles' LDS");
-  __shared__ TileShared<TG> sh;
-  __shared__ float ptile[tiled_chunk_clients<TG>() * 3 * TG];
+  __shared__ TileShared<TG, 4, D16> sh;
+  __shared__ float ptile[tiled_chunk_clients<TG, D16>() * 3 * TG];
   const TileKd tk{kd, (int64_t)blockIdx.x, (int64_t)gridDim.x, (int64_t)hdr_block[2]};
   if constexpr (TG2 > 0) {
     if ((int)blockIdx.x >= nW) {  // block-uniform: a narrow tile after the wide rounds
       const int64_t nN = (int64_t)gridDim.x - nW, b = (int64_t)blockIdx.x - nW;
-      update_tiled_block<TG2, KD>(reinterpret_cast<TileShared<TG2>&>(sh), ptile, kTileXcd ? xcd_tile(b, nN) : b,
-                                  uploads, pitch, M, dampen, inv_avg, n_up, g_begin + (int64_t)nW * TG, g_end,
-                                  hdr_block, merged, merged_f32, err, tk);
+      update_tiled_block<TG2, KD, D16>(reinterpret_cast<TileShared<TG2, 4, D16>&>(sh), ptile,
+                                       kTileXcd ? xcd_tile(b, nN) : b, uploads, pitch, M, dampen, inv_avg, n_up,
+                                       g_begin + (int64_t)nW * TG, g_end, hdr_block, merged, merged_f32, err, tk);
       return;
     }
   }
   const int64_t nw = TG2 > 0 ? (int64_t)nW : (int64_t)gridDim.x;
-  update_tiled_block<TG, KD>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nw) : blockIdx.x, uploads, pitch, M,
-                             dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged, merged_f32, err, tk);
+  update_tiled_block<TG, KD, D16>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nw) : blockIdx.x, uploads, pitch, M,
+                                  dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged, merged_f32, err, tk);
 }
 
 
@@ -1477,8 +1512,9 @@ extern template __global__ void k_update_encode<256>(const uint8_t* __restrict__
 // wave slots are free), the rest the client encode's blocks on the tile's B64Tables
 // (VarEntry digit counts: the tile state leaves no room for the byte table).
 // TG2 > 0: the update's tiles on k_update_tiled's two-width grid (blocks [0, nW)
-// wide, [nW, nU) TG2-wide).
-template <int TG, int TG2 = 0>
+// wide, [nW, nU) TG2-wide). D16: tiles and encode blocks on the byte-table digit
+// counts (the encode as in k_update_encode: enc_d16).
+template <int TG, int TG2 = 0, bool D16 = false>
 __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                              const double* __restrict__ dampen, double inv_avg,
                                                              int64_t n_up, int64_t g_begin, int64_t g_end,
@@ -1486,28 +1522,32 @@ __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __re
                                                              uint8_t* __restrict__ merged,
                                                              float* __restrict__ merged_f32, int* __restrict__ err,
                                                              int nU, EncodeJob ej, int nW = INT32_MAX) {
-  __shared__ TileShared<TG> sh;
-  __shared__ float ptile[tiled_chunk_clients<TG>() * 3 * TG];
+  __shared__ TileShared<TG, 4, D16> sh;
+  __shared__ float ptile[tiled_chunk_clients<TG, D16>() * 3 * TG];
   if ((int)blockIdx.x < nU) {  // block-uniform
     if constexpr (TG2 > 0) {
       if ((int)blockIdx.x >= nW) {
         const int64_t nN = (int64_t)nU - nW, b = (int64_t)blockIdx.x - nW;
-        update_tiled_block<TG2>(reinterpret_cast<TileShared<TG2>&>(sh), ptile, kTileXcd ? xcd_tile(b, nN) : b,
-                                uploads, pitch, M, dampen, inv_avg, n_up, g_begin + (int64_t)nW * TG, g_end,
-                                hdr_block, merged, merged_f32, err);
+        update_tiled_block<TG2, false, D16>(reinterpret_cast<TileShared<TG2, 4, D16>&>(sh), ptile,
+                                            kTileXcd ? xcd_tile(b, nN) : b, uploads, pitch, M, dampen, inv_avg, n_up,
+                                            g_begin + (int64_t)nW * TG, g_end, hdr_block, merged, merged_f32, err);
         return;
       }
     }
     const int64_t nw = TG2 > 0 ? (int64_t)nW : (int64_t)nU;
-    update_tiled_block<TG>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nw) : blockIdx.x, uploads, pitch, M, dampen,
-                           inv_avg, n_up, g_begin, g_end, hdr_block,
-                           merged, merged_f32, err);
+    update_tiled_block<TG, false, D16>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nw) : blockIdx.x, uploads, pitch,
+                                       M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged, merged_f32, err);
   } else {
     b64_tables_init(&sh.tab);
+    if constexpr (D16) d16_table_init(&sh.dt);
     __syncthreads();
     const int64_t e = (int64_t)blockIdx.x - nU;
-    encode_rows<false>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
-                       (int)(e / ej.gx), &sh.tab, nullptr);
+    if constexpr (D16)
+      encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                        (int)(e / ej.gx), &sh.tab, &sh.dt);
+    else
+      encode_rows<false>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                         (int)(e / ej.gx), &sh.tab, nullptr);
   }
 }
 
@@ -1983,6 +2023,53 @@ static TileSplit tile_split(int64_t groups, int tg) {
   return t;
 }
 
+// The wide tiles (TG = 32 / 64) on the byte-table digit counts (FLEET_TILE_D16=0:
+// the VarEntry compare, experiments).
+static bool tile_d16(int tg) {
+  if (tg != 32 && tg != 64) return false;
+  const char* e = getenv("FLEET_TILE_D16");
+  return !(e && atoi(e) == 0);
+}
+
+// k_update_tiled in the variant the plan picked: width tg, the two-width split
+// (tile_split), the byte-table tiles (tile_d16); KD: with Kardam's side outputs.
+// Returns the block count (= Kardam's partial slots per client).
+template <bool KD>
+static unsigned launch_tiled(int tg, int64_t groups, const uint8_t* uploads, size_t pitch, int M,
+                             const double* d_dampen, double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end,
+                             const int32_t* d_hdr_block, uint8_t* merged, float* merged_f32, int* d_err,
+                             const KardamOut& kd, hipStream_t s, bool launch = true) {
+  const TileSplit t = tile_split(groups, tg);
+  const bool d16 = tile_d16(tg);
+  const unsigned blocks = t.nW >= 0 ? (unsigned)(t.nW + t.nN) : (unsigned)((groups + tg - 1) / tg);
+  if (!launch) return blocks;
+  const int nW = t.nW >= 0 ? t.nW : INT32_MAX;
+#define FLEET_TL(TG, TG2, D)                                                                                     \
+  hipLaunchKernelGGL((k_update_tiled<TG, KD, TG2, D>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, \
+                     inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd, nW)
+  if (tg == 64) {
+    if (t.nW >= 0 && t.tg2 == 32) {
+      if (d16) FLEET_TL(64, 32, true);
+      else FLEET_TL(64, 32, false);
+    } else if (t.nW >= 0) {
+      if (d16) FLEET_TL(64, 16, true);
+      else FLEET_TL(64, 16, false);
+    } else {
+      if (d16) FLEET_TL(64, 0, true);
+      else FLEET_TL(64, 0, false);
+    }
+  } else if (tg == 32) {
+    if (d16) FLEET_TL(32, 0, true);
+    else FLEET_TL(32, 0, false);
+  } else if (tg == 16) {
+    FLEET_TL(16, 0, false);
+  } else if constexpr (!KD) {  // Kardam's tile sums need TG >= 16
+    FLEET_TL(8, 0, false);
+  }
+#undef FLEET_TL
+  return blocks;
+}
+
 // the split in use: FLEET_UPDATE_MIXED=0 the plain stream grid (-1), =2 every group
 // one value per lane (0; experiments)
 static int mixed_split(int64_t groups) {
@@ -2052,10 +2139,11 @@ const char* update_kernel_name(int64_t groups) {
     snprintf(buf, sizeof buf, "k_update<%d, false, 256>", p.k);  // as rocprofv3 names it
   else if (p.kind == 2)
     snprintf(buf, sizeof buf, "k_update_pipe<%d, %d, %d, %d>", p.tg, p.ipt, p.nw, p.wp);
-  else if (const TileSplit t = tile_split(groups, p.tg); t.nW >= 0)
-    snprintf(buf, sizeof buf, "k_update_tiled<%d, false, %d>", p.tg, t.tg2);
-  else
-    snprintf(buf, sizeof buf, "k_update_tiled<%d>", p.tg);
+  else {  // as rocprofv3 names it (every template argument)
+    const TileSplit t = tile_split(groups, p.tg);
+    snprintf(buf, sizeof buf, "k_update_tiled<%d, false, %d, %s>", p.tg, t.nW >= 0 ? t.tg2 : 0,
+             tile_d16(p.tg) ? "true" : "false");
+  }
   return buf;
 }
 
@@ -2108,18 +2196,8 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
     launch_pipe(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, 0,
                 EncodeJob{}, s);
   } else if (p.kind == 1) {
-    if (p.tg == 8) FLEET_LAUNCH(k_update_tiled<8>, 8);
-    else if (p.tg == 16) FLEET_LAUNCH(k_update_tiled<16>, 16);
-    else if (p.tg == 32) FLEET_LAUNCH(k_update_tiled<32>, 32);
-    else if (const TileSplit t = tile_split(groups, 64); t.nW >= 0) {
-      const dim3 grid((unsigned)(t.nW + t.nN));
-      if (t.tg2 == 32)
-        hipLaunchKernelGGL((k_update_tiled<64, false, 32>), grid, dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg,
-                           n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, KardamOut{}, t.nW);
-      else
-        hipLaunchKernelGGL((k_update_tiled<64, false, 16>), grid, dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg,
-                           n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, KardamOut{}, t.nW);
-    } else FLEET_LAUNCH(k_update_tiled<64>, 64);
+    (void)launch_tiled<false>(p.tg, groups, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block,
+                              merged, merged_f32, d_err, KardamOut{}, s);
   } else {
     if (p.k == 4) FLEET_LAUNCH(k_update<4>, 256 * 4);
     else if (p.k == 2) FLEET_LAUNCH(k_update<2>, 256 * 2);
@@ -2217,9 +2295,10 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   const char* knw = getenv("FLEET_KARDAM_PIPE_NW");
   const int pnw = knw && atoi(knw) == 5 ? 5 : 8;
   const bool tiled = p.kind == 1 && (p.tg == 16 || p.tg == 32 || p.tg == 64);
-  const int64_t per = pipe || tiled ? p.tg : 256;
-  const TileSplit ts = tiled ? tile_split(groups, p.tg) : TileSplit{-1, 0, 0};
-  const unsigned blocks = ts.nW >= 0 ? (unsigned)(ts.nW + ts.nN) : (unsigned)((groups + per - 1) / per);
+  const int64_t per = pipe ? p.tg : 256;
+  const unsigned blocks = tiled ? launch_tiled<true>(p.tg, groups, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin,
+                                                     g_end, d_hdr_block, merged, merged_f32, d_err, kd, s, false)
+                                : (unsigned)((groups + per - 1) / per);
   *n_waves = pipe || tiled ? (int)blocks : (int)blocks * 4;
   if (groups <= 0) return hipSuccess;
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
@@ -2233,20 +2312,8 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
                          d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
                          EncodeJob{}, kd);
   } else if (tiled) {
-#define FLEET_LAUNCH_TK(TG)                                                                                       \
-  hipLaunchKernelGGL((k_update_tiled<TG, true>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, \
-                     n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd)
-    if (p.tg == 16) FLEET_LAUNCH_TK(16);
-    else if (p.tg == 32) FLEET_LAUNCH_TK(32);
-    else if (ts.nW >= 0) {
-      if (ts.tg2 == 32)
-        hipLaunchKernelGGL((k_update_tiled<64, true, 32>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
-                           inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd, ts.nW);
-      else
-        hipLaunchKernelGGL((k_update_tiled<64, true, 16>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
-                           inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd, ts.nW);
-    } else FLEET_LAUNCH_TK(64);
-#undef FLEET_LAUNCH_TK
+    (void)launch_tiled<true>(p.tg, groups, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block,
+                             merged, merged_f32, d_err, kd, s);
   } else {
     hipLaunchKernelGGL((k_update<1, true>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
                        g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd);
@@ -2320,14 +2387,24 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     const char* fm = getenv("FLEET_FUSED_TILE_MIX");
     const TileSplit t = (fm && atoi(fm) == 1) ? tile_split(groups, p.tg) : TileSplit{-1, 0, 0};
     if (t.nW >= 0) nU = t.nW + t.nN;
-#define FLEET_LAUNCH_TE(TG, TG2)                                                                                    \
-  hipLaunchKernelGGL((k_update_tiled_encode<TG, TG2>), dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, \
-                     M, d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err,        \
+    const bool d16 = tile_d16(p.tg);
+#define FLEET_LAUNCH_TE(TG, TG2, D)                                                                                 \
+  hipLaunchKernelGGL((k_update_tiled_encode<TG, TG2, D>), dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads,     \
+                     pitch, M, d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, \
                      (int)nU, ej, t.nW)
-    if (p.tg == 64 && t.nW >= 0 && t.tg2 == 32) FLEET_LAUNCH_TE(64, 32);
-    else if (p.tg == 64 && t.nW >= 0) FLEET_LAUNCH_TE(64, 16);
-    else if (p.tg == 64) FLEET_LAUNCH_TE(64, 0);
-    else FLEET_LAUNCH_TE(32, 0);
+    if (p.tg == 64 && t.nW >= 0 && t.tg2 == 32) {
+      if (d16) FLEET_LAUNCH_TE(64, 32, true);
+      else FLEET_LAUNCH_TE(64, 32, false);
+    } else if (p.tg == 64 && t.nW >= 0) {
+      if (d16) FLEET_LAUNCH_TE(64, 16, true);
+      else FLEET_LAUNCH_TE(64, 16, false);
+    } else if (p.tg == 64) {
+      if (d16) FLEET_LAUNCH_TE(64, 0, true);
+      else FLEET_LAUNCH_TE(64, 0, false);
+    } else {
+      if (d16) FLEET_LAUNCH_TE(32, 0, true);
+      else FLEET_LAUNCH_TE(32, 0, false);
+    }
 #undef FLEET_LAUNCH_TE
     return hipGetLastError();
   }

@@ -93,5 +93,5 @@ def test_update_encode_two_width_tiles(codec, monkeypatch):
     """The fused tile step on the two-width grid (FLEET_FUSED_TILE_MIX=1, an
     experiment: wide tiles, narrow tiles, then the encode's blocks)."""
     monkeypatch.setenv("FLEET_FUSED_TILE_MIX", "1")
-    assert F.update_encode_kernel(F.b64_len(LAYOUTS["cifar10"].n_up)) == "k_update_tiled_encode<64, 16>"
+    assert F.update_encode_kernel(F.b64_len(LAYOUTS["cifar10"].n_up)) == "k_update_tiled_encode<64, 16, true>"
     test_update_encode_equals_two_calls(codec, "cifar10", 3, None)

@@ -361,8 +361,9 @@ def test_update_large_magnitudes_slow_path(codec, oracle, monkeypatch, env):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm) == oracle.update_faithful(ups, d)
 
 
+@pytest.mark.parametrize("d16", ["1", "0"])
 @pytest.mark.parametrize("mix", ["16", "32", "0"])
-def test_update_two_width_tiles(codec, oracle, monkeypatch, mix):
+def test_update_two_width_tiles(codec, oracle, monkeypatch, mix, d16):
     """k_update_tiled's two-width grid (whole rounds of 64-group tiles, the rest in
     16- or 32-group tiles; FLEET_TILE_MIX=0 the one-width grid): 16,668 groups =
     one round of 256 wide tiles + 284 groups, the last narrow tile ragged; large
@@ -371,6 +372,7 @@ def test_update_two_width_tiles(codec, oracle, monkeypatch, mix):
     monkeypatch.setenv("FLEET_UPDATE_MODE", "tiled")
     monkeypatch.setenv("FLEET_TILE_G", "64")
     monkeypatch.setenv("FLEET_TILE_MIX", mix)
+    monkeypatch.setenv("FLEET_TILE_D16", d16)
     lay = synthetic(50_003)
     hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
     rng = np.random.default_rng(11)
@@ -383,7 +385,7 @@ def test_update_two_width_tiles(codec, oracle, monkeypatch, mix):
         v[-5:-1] = [9.99e8, -9.99e8, 2.1e9, 0.999999]
         ups.append(oracle.encode_floats(v))
     d = [1.0, 7.5, 0.25, 10.0, 1 / 3, 1.0]
-    want = "k_update_tiled<64>" if mix == "0" else "k_update_tiled<64, false, %s>" % mix
+    want = "k_update_tiled<64, false, %s, %s>" % (mix, "true" if d16 == "1" else "false")
     assert F.update_kernel(len(ups[0])) == want
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
