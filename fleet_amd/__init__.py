@@ -198,10 +198,13 @@ def update_encode_kernel(length: int) -> str:
         if k == "k_update_mixed<256>":
             return "k_update_encode<256>"
         if k.startswith(("k_update_tiled<64", "k_update_tiled<32")):
-            # k_update_tiled<TG, KD, TG2, D16> -> k_update_tiled_encode<TG, TG2 (opt-in), D16>
+            # k_update_tiled<TG, KD, TG2, D16> -> k_update_tiled_encode<TG, TG2, D16, INL>: one
+            # width unless FLEET_FUSED_TILE_MIX=1; the inline encode (FLEET_FUSED_TILE_INLINE=1,
+            # byte-table tiles only) keeps the update's two-width grid
             tg, _, tg2, d16 = [a.strip() for a in k[len("k_update_tiled<"):].rstrip(">").split(",")]
-            mix = tg2 != "0" and os.environ.get("FLEET_FUSED_TILE_MIX", "") == "1"
-            return "k_update_tiled_encode<%s, %s, %s>" % (tg, tg2 if mix else "0", d16)
+            inl = d16 == "true" and os.environ.get("FLEET_FUSED_TILE_INLINE", "") == "1"
+            mix = inl or os.environ.get("FLEET_FUSED_TILE_MIX", "") == "1"
+            return "k_update_tiled_encode<%s, %s, %s, %s>" % (tg, tg2 if mix else "0", d16, "true" if inl else "false")
         if k.startswith("k_update_pipe"):
             return k + " (with the encode's blocks)"
     return k + " + k_encode_f32"

@@ -698,6 +698,90 @@ __global__ void __launch_bounds__(NT) k_update_mixed(const uint8_t* __restrict__
 
 // Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
 // of NW waves.
+// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
+// One group (3 values) of one row: float2int (fixed chains when the wave is
+// in |x| < 1, multiplier-table chains otherwise, the general codec for values
+// outside the q_gen domain) and the 16 Base64 chars.
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab,
+                                              const D16Table* dt) {
+  int32_t codes[3];
+  // |x| < 1 for the whole wave iff the largest |x| bit pattern is (integer max,
+  // not three 6-cycle e64 compares)
+  uint32_t amax = 0;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) amax = max(amax, f2u(x[e]) & 0x7fffffffu);
+  if (__ballot(amax >= 0x3f800000u) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+    // byte-table digit counts (codec_math.h d16_entry): one byte load per value;
+    // the power-of-ten slices take the compare, values outside the q_gen
+    // domain (|x| >= 1e8/1e9, inf, NaN) the general codec -- both rare, per lane
+    uint32_t ofs[3], omax = 0;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      ofs[e] = dt->d16[f2u(x[e]) >> 19];
+      omax = max(omax, ofs[e]);
+    }
+    if (__ballot(omax >= kD16Out) != 0) {
+      omax = 0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        if (ofs[e] == kD16Cmp) ofs[e] = d16_fix(x[e], tab->var);
+        omax = max(omax, ofs[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
+    if (__ballot(omax >= kD16Out) != 0) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if (ofs[e] >= kD16Out) codes[e] = enc(x[e]);
+    }
+  }
+  return pad_group(b64_encode_group(codes, tab), r);
+}
+
+// The same with the VarEntry digit counts (kernels that keep only B64Tables in LDS)
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
+  int32_t codes[3];
+  const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
+  if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab->var, tab->mt);
+    if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
+#pragma unroll
+      for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
+    }
+  }
+  return pad_group(b64_encode_group(codes, tab), r);
+}
+
+// A client-encode job riding in an aggregation launch (k_update_encode,
+// k_update_tiled_encode, k_update_pipe): k_encode_f32's grid, flattened x-fastest
+// (the tiles' inline form, k_update_tiled_encode<..., INL>, uses values / n / vpitch /
+// out / pitch only).
+struct EncodeJob {
+  const float* values;
+  int64_t n;
+  size_t vpitch;
+  uint8_t* out;
+  size_t pitch;
+  int64_t groups, gx;
+  int rows, rpb;
+  int prio = 0;  // s_setprio of the encode's waves (experiments: FLEET_FUSED_ENC_PRIO)
+};
+
+// s_setprio takes an immediate: the wave's issue priority from a uniform value
+__device__ __forceinline__ void set_wave_prio(int prio) {
+  if (prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (prio >= 3) __builtin_amdgcn_s_setprio(3);
+}
+
 // D16: the tile also holds the byte-table digit counts (D16Table, 9 KB), and the
 // epilogue assembles its merged codes in the tile's p buffer instead of outcodes.
 template <bool D16>
@@ -997,16 +1081,20 @@ template <int TG, bool D16 = false>
 constexpr int tiled_chunk_clients() { return TG > 0 ? (D16 ? FLEET_TILED_PT_D16 : FLEET_TILED_PT) / (3 * TG) : 0; }
 
 // Tile `bid` of k_update_tiled (LDS state in sh / ptile)
-template <int TG, bool KD = false, bool D16 = false>
+// ENC: the next batch's client encode of the tile's column range rides in the tile
+// (k_update_tiled_encode's inline form): each chunk's phase 1 also encodes the
+// chunk's rows of ej->values into ej->out.
+template <int TG, bool KD = false, bool D16 = false, bool ENC = false>
 __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, float* ptile, int64_t bid,
                                                    const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                    const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                                    int64_t g_begin, int64_t g_end,
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
                                                    float* __restrict__ merged_f32, int* __restrict__ err,
-                                                   const TileKd& tk = TileKd{}) {
+                                                   const TileKd& tk = TileKd{}, const EncodeJob* ej = nullptr) {
   constexpr int E = 3 * TG;
   static_assert(E <= 256, "phase 2 is one thread per value");
+  static_assert(!ENC || D16, "the inline encode uses the tile's byte table");
   constexpr int CM = tiled_chunk_clients<TG, D16>();
   static_assert(CM >= 2, "the epilogue's codes go after the E final values in ptile");
   FLEET_TSTAMP(0);
@@ -1027,6 +1115,26 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
       tile_produce<TG, 2, 4, KD>(sh, uploads, pitch, M, dampen, n_up, g0, ng, c0, nitems, base + tid, 256, ptile,
                                  badacc, tk);
       if (base == 0) FLEET_TSTAMP(2);
+    }
+    // ENC: the chunk's rows of the next batch over this tile's groups (a wave: one
+    // row's 64), at most 2 items per thread (CM * TG <= 512): the values are loaded
+    // here, encoded after phase 2, so the loads fly during the serial phase
+    constexpr int EI = ENC ? 2 : 0;
+    float ex[EI > 0 ? EI : 1][3];
+    if constexpr (ENC) {
+      static_assert(CM * TG <= 512, "two encode items per thread and chunk");
+#pragma unroll
+      for (int h = 0; h < EI; ++h) {
+        const int it = tid + 256 * h, row = c0 + it / TG, gl = it % TG;
+        const int64_t g = g0 + gl;
+        const int r = (int)min<int64_t>(3, ej->n - 3 * g);
+        if (it < nitems && gl < ng) {
+          const float* v = ej->values + (size_t)row * ej->vpitch + 3 * g;
+          ex[h][0] = v[0];
+          ex[h][1] = r > 1 ? v[1] : 0.0f;
+          ex[h][2] = r > 2 ? v[2] : 0.0f;
+        }
+      }
     }
     __syncthreads();
     FLEET_TSTAMP(3);
@@ -1058,6 +1166,16 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
             A = q_mt_d(s, d, sh.tab.mt);
           }
         }
+      }
+    }
+    if constexpr (ENC) {
+#pragma unroll
+      for (int h = 0; h < EI; ++h) {
+        const int it = tid + 256 * h, row = c0 + it / TG, gl = it % TG;
+        const int64_t g = g0 + gl;
+        const int r = (int)min<int64_t>(3, ej->n - 3 * g);
+        if (it < nitems && gl < ng)
+          store_stream16(ej->out + (size_t)row * ej->pitch + 16 * g, encode_group(ex[h], r, &sh.tab, &sh.dt));
       }
     }
     __syncthreads();
@@ -1128,68 +1246,6 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
 
 
 // Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
-// One group (3 values) of one row: float2int (fixed chains when the wave is
-// in |x| < 1, multiplier-table chains otherwise, the general codec for values
-// outside the q_gen domain) and the 16 Base64 chars.
-__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab,
-                                              const D16Table* dt) {
-  int32_t codes[3];
-  // |x| < 1 for the whole wave iff the largest |x| bit pattern is (integer max,
-  // not three 6-cycle e64 compares)
-  uint32_t amax = 0;
-#pragma unroll
-  for (int e = 0; e < 3; ++e) amax = max(amax, f2u(x[e]) & 0x7fffffffu);
-  if (__ballot(amax >= 0x3f800000u) == 0) {  // wave-uniform: gradients, |x| < 1
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
-  } else {
-    // byte-table digit counts (codec_math.h d16_entry): one byte load per value;
-    // the power-of-ten slices take the compare, values outside the q_gen
-    // domain (|x| >= 1e8/1e9, inf, NaN) the general codec -- both rare, per lane
-    uint32_t ofs[3], omax = 0;
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      ofs[e] = dt->d16[f2u(x[e]) >> 19];
-      omax = max(omax, ofs[e]);
-    }
-    if (__ballot(omax >= kD16Out) != 0) {
-      omax = 0;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        if (ofs[e] == kD16Cmp) ofs[e] = d16_fix(x[e], tab->var);
-        omax = max(omax, ofs[e]);
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
-    if (__ballot(omax >= kD16Out) != 0) {
-#pragma unroll
-      for (int e = 0; e < 3; ++e)
-        if (ofs[e] >= kD16Out) codes[e] = enc(x[e]);
-    }
-  }
-  return pad_group(b64_encode_group(codes, tab), r);
-}
-
-// The same with the VarEntry digit counts (kernels that keep only B64Tables in LDS)
-__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
-  int32_t codes[3];
-  const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
-  if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab->var, tab->mt);
-    if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
-#pragma unroll
-      for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
-    }
-  }
-  return pad_group(b64_encode_group(codes, tab), r);
-}
-
-// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
 // Block (bx, by) encodes groups [NT*bx, NT*bx+NT) of rows [rpb*by, rpb*by+rpb):
 // a lane walks its group down rpb rows (next row's floats loaded while the
 // current one is encoded), so the LDS table copy is paid once per rpb rows.
@@ -1248,18 +1304,6 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
     }
   }
 }
-
-// A client-encode job riding in an aggregation launch (k_update_encode,
-// k_update_tiled_encode, k_update_pipe): k_encode_f32's grid, flattened x-fastest.
-struct EncodeJob {
-  const float* values;
-  int64_t n;
-  size_t vpitch;
-  uint8_t* out;
-  size_t pitch;
-  int64_t groups, gx;
-  int rows, rpb;
-};
 
 // Pipelined tile variant (E = 3*TG <= 64): producer waves compute p for passes
 // of clients into an LDS ring while wave 0 consumes them in client order (the
@@ -1475,6 +1519,7 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
     update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                            hdr_block, merged, merged_f32, err, nA);
   } else {
+    set_wave_prio(ej.prio);
     const int64_t e = (int64_t)blockIdx.x - nU;
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                      (int)(e / ej.gx), &tab, &dtab);
@@ -1513,8 +1558,10 @@ extern template __global__ void k_update_encode<256>(const uint8_t* __restrict__
 // (VarEntry digit counts: the tile state leaves no room for the byte table).
 // TG2 > 0: the update's tiles on k_update_tiled's two-width grid (blocks [0, nW)
 // wide, [nW, nU) TG2-wide). D16: tiles and encode blocks on the byte-table digit
-// counts (the encode as in k_update_encode: enc_d16).
-template <int TG, int TG2 = 0, bool D16 = false>
+// counts (the encode as in k_update_encode: enc_d16). INL (with D16): no encode
+// blocks -- every tile encodes the next batch's rows of its own column range, a
+// chunk's rows in each chunk's phase 1 (nU = the tiles).
+template <int TG, int TG2 = 0, bool D16 = false, bool INL = false>
 __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                              const double* __restrict__ dampen, double inv_avg,
                                                              int64_t n_up, int64_t g_begin, int64_t g_end,
@@ -1528,19 +1575,22 @@ __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __re
     if constexpr (TG2 > 0) {
       if ((int)blockIdx.x >= nW) {
         const int64_t nN = (int64_t)nU - nW, b = (int64_t)blockIdx.x - nW;
-        update_tiled_block<TG2, false, D16>(reinterpret_cast<TileShared<TG2, 4, D16>&>(sh), ptile,
-                                            kTileXcd ? xcd_tile(b, nN) : b, uploads, pitch, M, dampen, inv_avg, n_up,
-                                            g_begin + (int64_t)nW * TG, g_end, hdr_block, merged, merged_f32, err);
+        update_tiled_block<TG2, false, D16, INL>(reinterpret_cast<TileShared<TG2, 4, D16>&>(sh), ptile,
+                                                 kTileXcd ? xcd_tile(b, nN) : b, uploads, pitch, M, dampen, inv_avg,
+                                                 n_up, g_begin + (int64_t)nW * TG, g_end, hdr_block, merged,
+                                                 merged_f32, err, TileKd{}, &ej);
         return;
       }
     }
     const int64_t nw = TG2 > 0 ? (int64_t)nW : (int64_t)nU;
-    update_tiled_block<TG, false, D16>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nw) : blockIdx.x, uploads, pitch,
-                                       M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged, merged_f32, err);
+    update_tiled_block<TG, false, D16, INL>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nw) : blockIdx.x, uploads,
+                                            pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged,
+                                            merged_f32, err, TileKd{}, &ej);
   } else {
     b64_tables_init(&sh.tab);
     if constexpr (D16) d16_table_init(&sh.dt);
     __syncthreads();
+    set_wave_prio(ej.prio);
     const int64_t e = (int64_t)blockIdx.x - nU;
     if constexpr (D16)
       encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
@@ -2379,7 +2429,8 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     const int rpb = encode_rows_per_block(gx, M);
     int64_t nU = (groups + p.tg - 1) / p.tg;
     const int64_t nE = gx * ((M + rpb - 1) / rpb);
-    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+    EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+    if (const char* e = getenv("FLEET_FUSED_ENC_PRIO")) ej.prio = atoi(e);
     // one-width tiles here: the encode's blocks already fill the CUs the last partial
     // round of tiles leaves idle, and the narrow tiles' extra work then costs step time
     // (two-width grid, FLEET_FUSED_TILE_MIX=1: cifar10_256 415 -> 441 us, cifar100_1024
@@ -2388,6 +2439,22 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     const TileSplit t = (fm && atoi(fm) == 1) ? tile_split(groups, p.tg) : TileSplit{-1, 0, 0};
     if (t.nW >= 0) nU = t.nW + t.nN;
     const bool d16 = tile_d16(p.tg);
+    // FLEET_FUSED_TILE_INLINE=1: the encode inside the tiles (experiment)
+    const char* fi = getenv("FLEET_FUSED_TILE_INLINE");
+    if (d16 && fi && atoi(fi) == 1) {
+      const TileSplit t2 = tile_split(groups, p.tg);
+      const int64_t nT = t2.nW >= 0 ? t2.nW + t2.nN : nU;
+#define FLEET_LAUNCH_TI(TG, TG2)                                                                                     \
+  hipLaunchKernelGGL((k_update_tiled_encode<TG, TG2, true, true>), dim3((unsigned)nT), dim3(256), 0, s, uploads,    \
+                     pitch, M, d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err,  \
+                     (int)nT, ej, t2.nW)
+      if (p.tg == 64 && t2.nW >= 0 && t2.tg2 == 32) FLEET_LAUNCH_TI(64, 32);
+      else if (p.tg == 64 && t2.nW >= 0) FLEET_LAUNCH_TI(64, 16);
+      else if (p.tg == 64) FLEET_LAUNCH_TI(64, 0);
+      else FLEET_LAUNCH_TI(32, 0);
+#undef FLEET_LAUNCH_TI
+      return hipGetLastError();
+    }
 #define FLEET_LAUNCH_TE(TG, TG2, D)                                                                                 \
   hipLaunchKernelGGL((k_update_tiled_encode<TG, TG2, D>), dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads,     \
                      pitch, M, d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, \
@@ -2444,7 +2511,8 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   int rpb = std::min(M, 12);
   if (const char* e = getenv("FLEET_FUSED_RPB")) rpb = std::max(1, std::min(M, atoi(e)));
   const int64_t nE = gx * ((M + rpb - 1) / rpb);
-  const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+  EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+  if (const char* e = getenv("FLEET_FUSED_ENC_PRIO")) ej.prio = atoi(e);
   hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nAf + nB + nE)), dim3(256), 0, s, uploads, pitch, M,
                      d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf,
                      (int)(nAf + nB), ej);

@@ -93,5 +93,17 @@ def test_update_encode_two_width_tiles(codec, monkeypatch):
     """The fused tile step on the two-width grid (FLEET_FUSED_TILE_MIX=1, an
     experiment: wide tiles, narrow tiles, then the encode's blocks)."""
     monkeypatch.setenv("FLEET_FUSED_TILE_MIX", "1")
-    assert F.update_encode_kernel(F.b64_len(LAYOUTS["cifar10"].n_up)) == "k_update_tiled_encode<64, 16, true>"
+    assert F.update_encode_kernel(F.b64_len(LAYOUTS["cifar10"].n_up)) == "k_update_tiled_encode<64, 16, true, false>"
     test_update_encode_equals_two_calls(codec, "cifar10", 3, None)
+
+
+@pytest.mark.parametrize("lay_name,M,n_values", [("cifar10", 5, None), ("cifar100", 3, None), ("synth1m", 4, 150_001),
+                                                  ("synth1m", 9, 250_001)])
+def test_update_encode_inline_tiles(codec, monkeypatch, lay_name, M, n_values):
+    """The encode inside the tiles (FLEET_FUSED_TILE_INLINE=1): every tile encodes
+    the next batch's rows of its own column range; ragged groups, both tile
+    widths of the two-width grid, chunks of 8 rows with M not a multiple of 8."""
+    monkeypatch.setenv("FLEET_FUSED_TILE_INLINE", "1")
+    L = F.b64_len(LAYOUTS[lay_name].n_up if n_values is None else n_values)
+    assert F.update_encode_kernel(L).endswith(", true, true>")
+    test_update_encode_equals_two_calls(codec, lay_name, M, n_values)
