@@ -326,6 +326,30 @@ __device__ __noinline__ float chain_general(const uint8_t* __restrict__ uploads,
 // 463-481, Kardam.java:48-106) as side outputs of the client loop
 // (KardamOut), so it costs no second pass over the uploads; stages A and B then
 // use the exact in-stage fallback (their values feed the side outputs).
+// Sum of v over each aligned group of TG lanes (16, 32 or 64), valid in the
+// group's last lane, by DPP lane moves inside the VALU (no LDS crossbar):
+// row_half_mirror + two quad_perms + row_mirror give every lane its 16-lane row's
+// sum, row_bcast15 / row_bcast31 then fold rows 0+1, 2+3 and 0..3. Call with
+// every lane of the wave active.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_move_f64(double v) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+template <int TG>
+__device__ __forceinline__ double group_sum_f64(double v) {
+  static_assert(TG == 16 || TG == 32 || TG == 64, "DPP group sums over rows of 16 lanes");
+  v += dpp_move_f64<0x141, 0xf>(v);  // row_half_mirror
+  v += dpp_move_f64<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+  v += dpp_move_f64<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v += dpp_move_f64<0x140, 0xf>(v);  // row_mirror: every lane holds its row's sum
+  if constexpr (TG >= 32) v += dpp_move_f64<0x142, 0xa>(v);  // row_bcast15 into rows 1, 3
+  if constexpr (TG == 64) v += dpp_move_f64<0x143, 0x8>(v);  // row_bcast31 into row 3
+  return v;
+}
+
 template <int K, bool KD = false, int NT = 256>
 __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                 const double* __restrict__ dampen, double inv_avg,
@@ -471,12 +495,11 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
             if (live[k] && pos < n_up) kd.g_out[(size_t)c * kd.vpitch + pos] = ((flatbits >> (3 * k + e)) & 1u) ? G[3 * k + e] : 0.0f;
           }
       }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        sg += __shfl_xor(sg, o);
-        sd += __shfl_xor(sd, o);
-      }
-      if (lane == 0) {
+      // the wave's sums by DPP lane moves in the VALU (the xor shuffles were
+      // ds_bpermute round trips through the LDS crossbar: 24 per client and lane)
+      sg = group_sum_f64<64>(sg);
+      sd = group_sum_f64<64>(sd);
+      if (lane == 63) {
         const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
         const size_t nw = (size_t)gridDim.x * (blockDim.x / 64);
         kd.partials[((size_t)c * nw + w) * 2] = sg;
@@ -865,30 +888,6 @@ struct TileKd {
   KardamOut kd;
   int64_t tile, ntiles, walk_end;
 };
-
-// Sum of v over each aligned group of TG lanes (16, 32 or 64), valid in the
-// group's last lane, by DPP lane moves inside the VALU (no LDS crossbar):
-// row_half_mirror + two quad_perms + row_mirror give every lane its 16-lane row's
-// sum, row_bcast15 / row_bcast31 then fold rows 0+1, 2+3 and 0..3. Call with
-// every lane of the wave active.
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ double dpp_move_f64(double v) {
-  const uint64_t b = __builtin_bit_cast(uint64_t, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROW_MASK, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, ROW_MASK, 0xf, false);
-  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-template <int TG>
-__device__ __forceinline__ double group_sum_f64(double v) {
-  static_assert(TG == 16 || TG == 32 || TG == 64, "DPP group sums over rows of 16 lanes");
-  v += dpp_move_f64<0x141, 0xf>(v);  // row_half_mirror
-  v += dpp_move_f64<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
-  v += dpp_move_f64<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
-  v += dpp_move_f64<0x140, 0xf>(v);  // row_mirror: every lane holds its row's sum
-  if constexpr (TG >= 32) v += dpp_move_f64<0x142, 0xa>(v);  // row_bcast15 into rows 1, 3
-  if constexpr (TG == 64) v += dpp_move_f64<0x143, 0x8>(v);  // row_bcast31 into row 3
-  return v;
-}
 
 // Per item (one client, one group): the text Kardam.setGrad stores, G =
 // Q(f32(f64(p) * lr)), written to g_out; ||G||^2 and, with the worker's previous
@@ -1532,6 +1531,10 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
 // and hurts the tiled and pipelined kernels; the main unit only
 // declares their instantiations.
 #ifdef FLEET_STREAM_TU
+template __global__ void k_update<1, true, 256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
+                                               double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
+                                               uint8_t* __restrict__, float* __restrict__, int* __restrict__,
+                                               KardamOut);
 template __global__ void k_update_mixed<256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
                                              double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
                                              uint8_t* __restrict__, float* __restrict__, int* __restrict__, int);
@@ -1540,6 +1543,10 @@ template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_
                                               uint8_t* __restrict__, float* __restrict__, int* __restrict__, int, int,
                                               EncodeJob);
 #else
+extern template __global__ void k_update<1, true, 256>(const uint8_t* __restrict__, size_t, int,
+                                                      const double* __restrict__, double, int64_t, int64_t, int64_t,
+                                                      const int32_t* __restrict__, uint8_t* __restrict__,
+                                                      float* __restrict__, int* __restrict__, KardamOut);
 extern template __global__ void k_update_mixed<256>(const uint8_t* __restrict__, size_t, int,
                                                     const double* __restrict__, double, int64_t, int64_t, int64_t,
                                                     const int32_t* __restrict__, uint8_t* __restrict__,
