@@ -472,15 +472,30 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
 #pragma unroll
       for (int i = 0; i < S; ++i)
         if ((flatbits >> i) & 1u) sg += (double)(G[i] * G[i]);
+      // prev / G rows: one 12-byte access per whole group (rows are 4-byte aligned)
+      typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
       if (kd.prev && kd.has_prev[c]) {  // uniform
         float dv[S], D[S];
 #pragma unroll
-        for (int k = 0; k < K; ++k)
+        for (int k = 0; k < K; ++k) {
+          const float* pr = kd.prev + (size_t)c * kd.vpitch + 3 * g[k];
+          float pv[3] = {0.0f, 0.0f, 0.0f};
+          if (live[k] && 3 * g[k] + 2 < n_up) {
+            const f3u t = *reinterpret_cast<const f3u*>(pr);
+            pv[0] = t.x;
+            pv[1] = t.y;
+            pv[2] = t.z;
+          } else {
+#pragma unroll
+            for (int e = 0; e < 3; ++e)
+              if ((flatbits >> (3 * k + e)) & 1u) pv[e] = pr[e];
+          }
 #pragma unroll
           for (int e = 0; e < 3; ++e) {
             const int i = 3 * k + e;
-            dv[i] = ((flatbits >> i) & 1u) ? G[i] - kd.prev[(size_t)c * kd.vpitch + 3 * g[k] + e] : 0.0f;
+            dv[i] = ((flatbits >> i) & 1u) ? G[i] - pv[e] : 0.0f;
           }
+        }
         q_stage_d16x<S>(D, dv, &dtab, tab.var);
 #pragma unroll
         for (int i = 0; i < S; ++i)
@@ -488,12 +503,19 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
       }
       if (kd.g_out) {
 #pragma unroll
-        for (int k = 0; k < K; ++k)
+        for (int k = 0; k < K; ++k) {
+          float* go = kd.g_out + (size_t)c * kd.vpitch + 3 * g[k];
+          float gv[3];
 #pragma unroll
-          for (int e = 0; e < 3; ++e) {
-            const int64_t pos = 3 * g[k] + e;
-            if (live[k] && pos < n_up) kd.g_out[(size_t)c * kd.vpitch + pos] = ((flatbits >> (3 * k + e)) & 1u) ? G[3 * k + e] : 0.0f;
+          for (int e = 0; e < 3; ++e) gv[e] = ((flatbits >> (3 * k + e)) & 1u) ? G[3 * k + e] : 0.0f;
+          if (live[k] && 3 * g[k] + 2 < n_up) {
+            *reinterpret_cast<f3u*>(go) = f3u{gv[0], gv[1], gv[2]};
+          } else {
+#pragma unroll
+            for (int e = 0; e < 3; ++e)
+              if (live[k] && 3 * g[k] + e < n_up) go[e] = gv[e];
           }
+        }
       }
       // the wave's sums by DPP lane moves in the VALU (the xor shuffles were
       // ds_bpermute round trips through the LDS crossbar: 24 per client and lane)
@@ -917,14 +939,36 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const T
     double sg = 0.0, sd = 0.0;
     float dv[3], D[3];
     bool flat[3];
+    // prev / G rows: one 12-byte access per whole group (rows are 4-byte aligned)
+    typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+    const bool whole = it.live[h] && gp + 2 < n_up;
+    float pv[3] = {0.0f, 0.0f, 0.0f};
+    if (hasp && whole) {
+      const f3u t = *reinterpret_cast<const f3u*>(kd.prev + (size_t)c * kd.vpitch + gp);
+      pv[0] = t.x;
+      pv[1] = t.y;
+      pv[2] = t.z;
+    }
+    float gv[3];
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
       const int64_t pos = gp + e;
       flat[e] = it.live[h] && !((hm >> e) & 1u) && pos < n_up && pos < tk.walk_end;
       const float g = G[3 * h + e];
       if (flat[e]) sg += (double)(g * g);
-      dv[e] = (flat[e] && hasp) ? g - kd.prev[(size_t)c * kd.vpitch + pos] : 0.0f;
-      if (kd.g_out && it.live[h] && pos < n_up) kd.g_out[(size_t)c * kd.vpitch + pos] = flat[e] ? g : 0.0f;
+      if (hasp && !whole && flat[e]) pv[e] = kd.prev[(size_t)c * kd.vpitch + pos];
+      dv[e] = (flat[e] && hasp) ? g - pv[e] : 0.0f;
+      gv[e] = flat[e] ? g : 0.0f;
+    }
+    if (kd.g_out) {
+      float* go = kd.g_out + (size_t)c * kd.vpitch + gp;
+      if (whole) {
+        *reinterpret_cast<f3u*>(go) = f3u{gv[0], gv[1], gv[2]};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+          if (it.live[h] && gp + e < n_up) go[e] = gv[e];
+      }
     }
     if constexpr (D16) q_stage_d16x<3>(D, dv, &sh.dt, sh.tab.var);
     else q_stage<3>(D, dv, &sh.tab);
