@@ -866,6 +866,13 @@ def main():
         "weak": weak,
         "strong_value": strong_value,
         "extra": extras,
+        # the extras in the headline's own form (the pipelined step), beside their sequential step
+        "extra_steps": {w: {"pipelined_ms": (x["pipelined"] or {}).get("ms_per_step"),
+                            "pipelined_gib_s": (x["pipelined"] or {}).get("gib_s"),
+                            "pipelined_kernel": (x["pipelined"] or {}).get("kernel"),
+                            "sequential_ms": x["ms_per_step"], "sequential_gib_s": x["gib_s"],
+                            "update_kernel": x["update_kernel"], "update_kernel_ms": x["update_kernel_ms"]}
+                        for w, x in extras.items()},
         "end_to_end_host_buffers": e2e,
     }
     if cpu:
