@@ -403,9 +403,11 @@ FLEET_HDC MulEntry mul_entry(uint32_t d) {  // d = numDigits; d > 9 (slow marker
 // sub) with no select or bit-field extract. d > 9 marks values outside the
 // q_gen domain (-1e8 < x < 1e9), NaN and inf (callers send those through the
 // general codec): base = 10 where only dhi leaves the domain (dlo = 9), 15
-// where both do.
+// where both do. The threshold is kept as bits WITH the entry's sign bit: x's
+// bits and thr's then share bit 31, so bits - thr borrows exactly when
+// |x| < thr and no |x| mask is needed.
 struct alignas(8) VarEntry {
-  float thr;
+  uint32_t thr;  // bits of the threshold | the entry's sign bit
   uint32_t base;
 };
 constexpr uint32_t kSlowDigits = 15u;
@@ -426,15 +428,17 @@ FLEET_HDC DigitPair digit_pair(uint32_t i) {
 }
 FLEET_HDC VarEntry var_entry(uint32_t i) {
   const DigitPair p = digit_pair(i);
-  return VarEntry{p.thr, p.dlo <= 9u ? p.dlo + 1u : kSlowDigits};
+  return VarEntry{__builtin_bit_cast(uint32_t, p.thr) | (((i >> 8) & 1u) << 31),
+                  p.dlo <= 9u ? p.dlo + 1u : kSlowDigits};
 }
 
-// numDigits((int)x) on the q_gen domain, a value > 9 outside it. `ab` = the
-// bits of |x|: |x| < thr compares as integers (both non-negative, below 2^31),
-// the borrow of ab - thr is the comparison.
+// numDigits((int)x) on the q_gen domain, a value > 9 outside it. bits - thr
+// borrows iff |x| < thr (both carry x's sign bit, the magnitudes are below
+// 2^31). `ab` (the bits of |x|) is unused, kept for the callers' signature.
 FLEET_HD uint32_t var_digits_ab(uint32_t bits, uint32_t ab, const VarEntry* vt) {
+  (void)ab;
   const VarEntry v = vt[bits >> 23];
-  return v.base - ((ab - f2u(v.thr)) >> 31);
+  return v.base - ((bits - v.thr) >> 31);
 }
 FLEET_HD uint32_t var_digits(float x, const VarEntry* vt) {
   return var_digits_ab(f2u(x), f2u(x) & 0x7fffffffu, vt);
@@ -570,7 +574,7 @@ FLEET_HD uint32_t d16_fix(float x, const VarEntry* vt) {
 // the byte table's divergent fix-up costs more than this compare for every value.
 FLEET_HD uint32_t var_d16(uint32_t bits, const VarEntry* vt) {
   const VarEntry v = vt[bits >> 23];
-  return (v.base - (((bits & 0x7fffffffu) - f2u(v.thr)) >> 31)) << 4;
+  return (v.base - ((bits - v.thr) >> 31)) << 4;
 }
 
 // Q(x) given e = 16 * numDigits((int)x) <= 144 (garbage, never a fault, for e >= kD16Out)

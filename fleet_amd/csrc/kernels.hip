@@ -584,17 +584,94 @@ constexpr bool kTileXcd = FLEET_TILE_XCD != 0;
 #endif
 constexpr bool kStageCVar = FLEET_STAGEC_VAR != 0;
 
+// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
+// One group (3 values) of one row: float2int (fixed chains when the wave is
+// in |x| < 1, multiplier-table chains otherwise, the general codec for values
+// outside the q_gen domain) and the 16 Base64 chars.
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab,
+                                              const D16Table* dt, const B64Pairs* pairs = nullptr) {
+  int32_t codes[3];
+  // |x| < 1 for the whole wave iff the largest |x| bit pattern is (integer max,
+  // not three 6-cycle e64 compares)
+  uint32_t amax = 0;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) amax = max(amax, f2u(x[e]) & 0x7fffffffu);
+  if (__ballot(amax >= 0x3f800000u) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+    // byte-table digit counts (codec_math.h d16_entry): one byte load per value;
+    // the power-of-ten slices take the compare, values outside the q_gen
+    // domain (|x| >= 1e8/1e9, inf, NaN) the general codec -- both rare, per lane
+    uint32_t ofs[3], omax = 0;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      ofs[e] = dt->d16[f2u(x[e]) >> 19];
+      omax = max(omax, ofs[e]);
+    }
+    if (__ballot(omax >= kD16Out) != 0) {
+      omax = 0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        if (ofs[e] == kD16Cmp) ofs[e] = d16_fix(x[e], tab->var);
+        omax = max(omax, ofs[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
+    if (__ballot(omax >= kD16Out) != 0) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if (ofs[e] >= kD16Out) codes[e] = enc(x[e]);
+    }
+  }
+  return pad_group(pairs ? b64_encode_group_pairs(codes, pairs) : b64_encode_group(codes, tab), r);
+}
+
+// The same with the VarEntry digit counts (kernels that keep only B64Tables in LDS)
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
+  int32_t codes[3];
+  const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
+  if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab->var, tab->mt);
+    if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
+#pragma unroll
+      for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
+    }
+  }
+  return pad_group(b64_encode_group(codes, tab), r);
+}
+
+// The client encode of the next batch riding inside the stream update's waves
+// (k_update_encode_inline): lane g also encodes group g of every row of `values`
+// into `out`, one row per client step, its loads issued with the next client's
+// upload group.
+struct InlineEnc {
+  const float* values;
+  int64_t n;
+  size_t vpitch;
+  uint8_t* out;
+  size_t pitch;
+};
+
 // One lane's share of the fused update (the non-Kardam stream path): the values
 // [e0, e0 + S) of group g, S = 3 (the whole group) or S = 1 (one value; three
 // lanes of a wave share a group). Returns the lane's merged codes in out[S] and
 // its Base64 / layout error bits; tables already in LDS.
-template <int S>
+//   ENC (S = 3 only): also the client encode of group g of every row of ie
+// (InlineEnc), row c encoded in client c's step.
+template <int S, bool ENC = false>
 __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table& dtab,
                                             const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                             const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                             int64_t g, int e0, bool live, int64_t g_safe,
                                             const int32_t* __restrict__ hdr_block, int32_t (&out)[S],
-                                            uint32_t& bad, uint32_t& layout_bad) {
+                                            uint32_t& bad, uint32_t& layout_bad, InlineEnc ie = InlineEnc{}) {
+  static_assert(!ENC || S == 3, "the inline encode needs whole groups");
   const int n_hdr = hdr_block[1];
   const int64_t walk_end = hdr_block[2];
   const int32_t* hdr = hdr_block + 4;
@@ -610,7 +687,23 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // bytes (chars 4e..4e+7); the group's three lanes together cover all 16 chars
   const uint32_t sel = b64_pair_selector(e0), need_pair = (need >> (4 * e0)) & 0xffu;
   using Row = typename std::conditional<S == 3, uint4, uint2>::type;
+  // the inline encode: group g's three values of row c (one 12-byte load per full group)
+  typedef float f3 __attribute__((ext_vector_type(3)));
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+  const int er = live ? (int)min<int64_t>(3, ie.n - 3 * g) : 3;
+  const float* ev = ENC ? ie.values + 3 * (live ? g : g_safe) : nullptr;
+  auto vals_of = [&](int c) -> f3 {
+    const float* q = ev + (size_t)c * ie.vpitch;
+    if (er == 3) return *reinterpret_cast<const f3u*>(q);
+    return f3{q[0], er > 1 ? q[1] : 0.0f, 0.0f};
+  };
+  f3 xv{0.0f, 0.0f, 0.0f};  // row c's values while client c's step runs
   auto client = [&](int c, const Row& cur) {
+    if constexpr (ENC) {
+      const float x[3] = {xv.x, xv.y, xv.z};
+      const uint4 t = encode_group(x, er, &tab, &dtab);
+      if (live) store_stream16(ie.out + (size_t)c * ie.pitch + 16 * g, t);
+    }
     if constexpr (S == 3) {
       if (need == 0xffffu) bad |= b64_decode_group_full(cur, &tab, codes);
       else bad |= b64_decode_group(cur, &tab, codes) & need;
@@ -650,16 +743,26 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
     }
   };
   // two clients per trip, the next client's group always in flight, in alternating
-  // registers (no copies between trips)
+  // registers (no copies between trips); with ENC the next row's values ride along
   Row b0 = group_of(0), b1;
+  f3 x0{0.0f, 0.0f, 0.0f}, x1{0.0f, 0.0f, 0.0f};
+  if constexpr (ENC) x0 = vals_of(0);
   int c = 0;
   for (; c + 1 < M; c += 2) {
     b1 = group_of(c + 1);
+    if constexpr (ENC) { x1 = vals_of(c + 1); xv = x0; }
     client(c, b0);
-    if (c + 2 < M) b0 = group_of(c + 2);
+    if (c + 2 < M) {
+      b0 = group_of(c + 2);
+      if constexpr (ENC) x0 = vals_of(c + 2);
+    }
+    if constexpr (ENC) xv = x1;
     client(c + 1, b1);
   }
-  if (c < M) client(c, b0);
+  if (c < M) {
+    if constexpr (ENC) xv = x0;
+    client(c, b0);
+  }
   if (__ballot(dmax >= kD16Out) != 0) {  // left the q_gen domain: recompute exactly (never for gradients)
     if (dmax >= kD16Out && live) {
 #pragma unroll
@@ -675,20 +778,22 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
 }
 
 // Block `bid` of the SIMD-balanced stream grid (tables already in LDS).
-template <int NT>
+// ENC: the group-per-lane blocks also encode their groups of every row of ie.
+template <int NT, bool ENC = false>
 __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D16Table& dtab, int64_t bid,
                                                    const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                    const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                                    int64_t g_begin, int64_t g_end,
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
-                                                   float* __restrict__ merged_f32, int* __restrict__ err, int nA) {
+                                                   float* __restrict__ merged_f32, int* __restrict__ err, int nA,
+                                                   InlineEnc ie = InlineEnc{}) {
   uint32_t bad = 0, layout_bad = 0;
   if (bid < nA) {  // block-uniform: one group per lane
     const int64_t g = g_begin + bid * NT + threadIdx.x;
     const bool live = g < g_end;
     int32_t out[3];
-    update_lane<3>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out, bad,
-                   layout_bad);
+    update_lane<3, ENC>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out,
+                        bad, layout_bad, ie);
     if (!live) return;
     if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
@@ -743,68 +848,6 @@ __global__ void __launch_bounds__(NT) k_update_mixed(const uint8_t* __restrict__
 
 // Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
 // of NW waves.
-// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
-// One group (3 values) of one row: float2int (fixed chains when the wave is
-// in |x| < 1, multiplier-table chains otherwise, the general codec for values
-// outside the q_gen domain) and the 16 Base64 chars.
-__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab,
-                                              const D16Table* dt) {
-  int32_t codes[3];
-  // |x| < 1 for the whole wave iff the largest |x| bit pattern is (integer max,
-  // not three 6-cycle e64 compares)
-  uint32_t amax = 0;
-#pragma unroll
-  for (int e = 0; e < 3; ++e) amax = max(amax, f2u(x[e]) & 0x7fffffffu);
-  if (__ballot(amax >= 0x3f800000u) == 0) {  // wave-uniform: gradients, |x| < 1
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
-  } else {
-    // byte-table digit counts (codec_math.h d16_entry): one byte load per value;
-    // the power-of-ten slices take the compare, values outside the q_gen
-    // domain (|x| >= 1e8/1e9, inf, NaN) the general codec -- both rare, per lane
-    uint32_t ofs[3], omax = 0;
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      ofs[e] = dt->d16[f2u(x[e]) >> 19];
-      omax = max(omax, ofs[e]);
-    }
-    if (__ballot(omax >= kD16Out) != 0) {
-      omax = 0;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        if (ofs[e] == kD16Cmp) ofs[e] = d16_fix(x[e], tab->var);
-        omax = max(omax, ofs[e]);
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
-    if (__ballot(omax >= kD16Out) != 0) {
-#pragma unroll
-      for (int e = 0; e < 3; ++e)
-        if (ofs[e] >= kD16Out) codes[e] = enc(x[e]);
-    }
-  }
-  return pad_group(b64_encode_group(codes, tab), r);
-}
-
-// The same with the VarEntry digit counts (kernels that keep only B64Tables in LDS)
-__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
-  int32_t codes[3];
-  const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
-  if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab->var, tab->mt);
-    if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
-#pragma unroll
-      for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
-    }
-  }
-  return pad_group(b64_encode_group(codes, tab), r);
-}
-
 // A client-encode job riding in an aggregation launch (k_update_encode,
 // k_update_tiled_encode, k_update_pipe): k_encode_f32's grid, flattened x-fastest
 // (the tiles' inline form, k_update_tiled_encode<..., INL>, uses values / n / vpitch /
@@ -1300,7 +1343,7 @@ template <bool D16, int NT = 256, bool ROT = false>
 __device__ __forceinline__ void encode_rows(const float* __restrict__ values, int64_t n, size_t vpitch,
                                             uint8_t* __restrict__ out, size_t pitch, int64_t groups, int rows,
                                             int rpb, int64_t bx, int by, const B64Tables* tab,
-                                            const D16Table* dt) {
+                                            const D16Table* dt, const B64Pairs* pairs = nullptr) {
   const int64_t g = bx * NT + threadIdx.x;
   if (g >= groups) return;
   const int row0 = by * rpb, row1 = min(rows, row0 + rpb);
@@ -1318,7 +1361,7 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
     return f3{p[0], r > 1 ? p[1] : 0.0f, 0.0f};
   };
   auto emit = [&](int rr, const float (&x)[3]) {
-    if constexpr (D16) store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab, dt));
+    if constexpr (D16) store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab, dt, pairs));
     else store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab));
   };
   if constexpr (ROT) {
@@ -1545,6 +1588,10 @@ __global__ void __launch_bounds__(256) k_encode_f32_d16(const float* __restrict_
 // aggregation's blocks first (they fit the chip in one round) and streams the
 // encode's blocks through the wave slots and issue cycles they leave. Each
 // block's results are those of the separate kernels.
+#ifndef FLEET_FUSED_PAIRS
+#define FLEET_FUSED_PAIRS 0
+#endif
+constexpr bool kFusedPairs = FLEET_FUSED_PAIRS != 0;
 template <int NT>
 __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                       const double* __restrict__ dampen, double inv_avg,
@@ -1555,8 +1602,10 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   static_assert(NT == 256, "the encode blocks are 256 lanes");
   __shared__ B64Tables tab;
   __shared__ D16Table dtab;
+  __shared__ B64Pairs pairs;  // the encode's Base64 by sextet pairs (kFusedPairs)
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
+  if (kFusedPairs && (int)blockIdx.x >= nU) b64_pairs_init<NT>(&pairs);
   __syncthreads();
   if ((int)blockIdx.x < nU) {  // block-uniform
     update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
@@ -1565,7 +1614,39 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
     set_wave_prio(ej.prio);
     const int64_t e = (int64_t)blockIdx.x - nU;
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
-                     (int)(e / ej.gx), &tab, &dtab);
+                     (int)(e / ej.gx), &tab, &dtab, kFusedPairs ? &pairs : nullptr);
+  }
+}
+
+// The pipelined step with the client encode INSIDE the update's waves: blocks
+// [0, nA) are k_update_mixed's group-per-lane blocks, each lane also encoding its
+// group of every row of the next batch (InlineEnc: one row per client step, the
+// values loaded with the next client's upload group), so the encode's VALU work
+// and its HBM traffic are spread over the whole aggregation instead of queueing
+// behind it; blocks [nA, nU) the value-per-lane remainder of the update, blocks
+// [nU, ...) k_encode_f32's grid over the remainder's groups (ej: values / out
+// already offset to the first of them). Each block's results are those of the
+// separate kernels.
+template <int NT>
+__global__ void __launch_bounds__(NT) k_update_encode_inline(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                             const double* __restrict__ dampen, double inv_avg,
+                                                             int64_t n_up, int64_t g_begin, int64_t g_end,
+                                                             const int32_t* __restrict__ hdr_block,
+                                                             uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                             int* __restrict__ err, int nA, int nU, InlineEnc ie,
+                                                             EncodeJob ej) {
+  __shared__ B64Tables tab;
+  __shared__ D16Table dtab;
+  b64_tables_init<NT>(&tab);
+  d16_table_init<NT>(&dtab);
+  __syncthreads();
+  if ((int)blockIdx.x < nU) {  // block-uniform
+    update_mixed_block<NT, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+                                 hdr_block, merged, merged_f32, err, nA, ie);
+  } else {
+    const int64_t e = (int64_t)blockIdx.x - nU;
+    encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                      (int)(e / ej.gx), &tab, &dtab);
   }
 }
 
@@ -1586,6 +1667,11 @@ template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_
                                               double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
                                               uint8_t* __restrict__, float* __restrict__, int* __restrict__, int, int,
                                               EncodeJob);
+template __global__ void k_update_encode_inline<256>(const uint8_t* __restrict__, size_t, int,
+                                                     const double* __restrict__, double, int64_t, int64_t, int64_t,
+                                                     const int32_t* __restrict__, uint8_t* __restrict__,
+                                                     float* __restrict__, int* __restrict__, int, int, InlineEnc,
+                                                     EncodeJob);
 #else
 extern template __global__ void k_update<1, true, 256>(const uint8_t* __restrict__, size_t, int,
                                                       const double* __restrict__, double, int64_t, int64_t, int64_t,
@@ -1599,6 +1685,11 @@ extern template __global__ void k_update_encode<256>(const uint8_t* __restrict__
                                                      const double* __restrict__, double, int64_t, int64_t, int64_t,
                                                      const int32_t* __restrict__, uint8_t* __restrict__,
                                                      float* __restrict__, int* __restrict__, int, int, EncodeJob);
+extern template __global__ void k_update_encode_inline<256>(const uint8_t* __restrict__, size_t, int,
+                                                            const double* __restrict__, double, int64_t, int64_t,
+                                                            int64_t, const int32_t* __restrict__,
+                                                            uint8_t* __restrict__, float* __restrict__,
+                                                            int* __restrict__, int, int, InlineEnc, EncodeJob);
 #endif
 
 #ifndef FLEET_STREAM_TU
@@ -2540,6 +2631,26 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
                                  d_err, s);
     if (e != hipSuccess) return e;
     return launch_encode_f32(values, n_up, vpitch, M, enc_out, pitch, s);
+  }
+  // FLEET_FUSED_INLINE=1: the encode inside the update's waves (k_update_encode_inline)
+  // on the SIMD-balanced grid -- an experiment, slower than the separate encode blocks
+  // below (synth1m_256: 1167-1177 vs 1134-1136 us per step, three same-box pairs,
+  // scripts/gpu_r03_d2.sh): 79 VGPRs (6 waves per SIMD) and the encode's VALU work
+  // on every update wave's critical path
+  const char* fin = getenv("FLEET_FUSED_INLINE");
+  if (fin && atoi(fin)) {
+    const int64_t nB = (groups - (int64_t)nA * 256 + 83) / 84;
+    const int64_t g0 = std::min<int64_t>(groups, (int64_t)nA * 256);  // first group of the remainder
+    const int64_t rg = groups - g0;
+    const int64_t gxr = blocks_for(rg, 256);
+    const int rpb = std::min(M, 12);
+    const int64_t nE = rg > 0 ? gxr * ((M + rpb - 1) / rpb) : 0;
+    const InlineEnc ie{values, n_up, vpitch, enc_out, pitch};
+    const EncodeJob ej{values + 3 * g0, n_up - 3 * g0, vpitch, enc_out + 16 * g0, pitch, rg, gxr, M, rpb};
+    hipLaunchKernelGGL((k_update_encode_inline<256>), dim3((unsigned)(nA + nB + nE)), dim3(256), 0, s, uploads, pitch,
+                       M, d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nA,
+                       (int)(nA + nB), ie, ej);
+    return hipGetLastError();
   }
   // the plain stream grid (every update block group-per-lane): the encode's blocks
   // fill the SIMDs the last round of update waves leaves idle, so the value-per-lane
