@@ -658,6 +658,27 @@ struct InlineEnc {
   size_t pitch;
 };
 
+// One launch of a client-chunked stream update (launch_update / launch_update_encode
+// for large M): clients [c0, c1) of the M picked uploads. The running sums A carry
+// over between launches in the merged output itself: `acc` = the merged text as
+// floats, a group's three sums in the first 12 of its 16 bytes (read at c0 > 0,
+// written at c1 < M, by the lanes that own the group; the last chunk reads them
+// before it writes the group's merged chars). A lane whose chain has left the q_gen
+// domain writes NaN, which keeps every later chunk out of the domain too, so the
+// last chunk recomputes it exactly over all M clients. c1 <= 0: the whole range
+// [0, M) in one launch.
+struct ClientChunk {
+  int c0 = 0, c1 = 0;
+  float* acc = nullptr;
+};
+
+// Client groups in flight ahead of the one being aggregated by a stream lane
+// (FLEET_UPDATE_PF: 1 = the next client's, 2 = the next two clients').
+#ifndef FLEET_UPDATE_PF
+#define FLEET_UPDATE_PF 1
+#endif
+constexpr int kUpdatePF = FLEET_UPDATE_PF;
+
 // One lane's share of the fused update (the non-Kardam stream path): the values
 // [e0, e0 + S) of group g, S = 3 (the whole group) or S = 1 (one value; three
 // lanes of a wave share a group). Returns the lane's merged codes in out[S] and
@@ -670,8 +691,11 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
                                             const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                             int64_t g, int e0, bool live, int64_t g_safe,
                                             const int32_t* __restrict__ hdr_block, int32_t (&out)[S],
-                                            uint32_t& bad, uint32_t& layout_bad, InlineEnc ie = InlineEnc{}) {
+                                            uint32_t& bad, uint32_t& layout_bad, InlineEnc ie = InlineEnc{},
+                                            ClientChunk ck = ClientChunk{}) {
   static_assert(!ENC || S == 3, "the inline encode needs whole groups");
+  const int c0 = ck.c1 > 0 ? ck.c0 : 0, c1 = ck.c1 > 0 ? ck.c1 : M;
+  float* acc_at = ck.c1 > 0 ? ck.acc + 4 * (live ? g : g_safe) + e0 : nullptr;  // this lane's running sums
   const int n_hdr = hdr_block[1];
   const int64_t walk_end = hdr_block[2];
   const int32_t* hdr = hdr_block + 4;
@@ -698,6 +722,16 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
     return f3{q[0], er > 1 ? q[1] : 0.0f, 0.0f};
   };
   f3 xv{0.0f, 0.0f, 0.0f};  // row c's values while client c's step runs
+  if (c0 > 0) {  // a later chunk: the running sums so far, and (header waves) client 0's header codes
+#pragma unroll
+    for (int i = 0; i < S; ++i) acc[i] = live ? acc_at[i] : 0.0f;
+    if (wave_hdr) {
+      int32_t h0[3];
+      b64_decode_group(*reinterpret_cast<const uint4*>(uploads + 16 * (live ? g : g_safe)), &tab, h0);
+#pragma unroll
+      for (int i = 0; i < S; ++i) hfirst[i] = h0[e0 + i];
+    }
+  }
   auto client = [&](int c, const Row& cur) {
     if constexpr (ENC) {
       const float x[3] = {xv.x, xv.y, xv.z};
@@ -744,24 +778,59 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   };
   // two clients per trip, the next client's group always in flight, in alternating
   // registers (no copies between trips); with ENC the next row's values ride along
-  Row b0 = group_of(0), b1;
+  Row b0 = group_of(c0), b1;
   f3 x0{0.0f, 0.0f, 0.0f}, x1{0.0f, 0.0f, 0.0f};
-  if constexpr (ENC) x0 = vals_of(0);
-  int c = 0;
-  for (; c + 1 < M; c += 2) {
+  if constexpr (ENC) x0 = vals_of(c0);
+  int c = c0;
+  if constexpr (kUpdatePF == 2 && !ENC) {
+    // three clients per trip, the next TWO clients' groups in flight (rotating registers)
+    Row b2;
+    if (c0 + 1 < c1) b1 = group_of(c0 + 1);
+    for (; c + 2 < c1; c += 3) {
+      b2 = group_of(c + 2);
+      client(c, b0);
+      if (c + 3 < c1) b0 = group_of(c + 3);
+      client(c + 1, b1);
+      if (c + 4 < c1) b1 = group_of(c + 4);
+      client(c + 2, b2);
+    }
+    if (c < c1) client(c, b0);
+    if (c + 1 < c1) client(c + 1, b1);
+    c = c1;
+  }
+  // kUpdatePF == 3 (experiment): every lane also touches one dword of its group
+  // three clients ahead, warming the translation and the DRAM page for the row
+  uint32_t touch = 0;
+  for (; c + 1 < c1; c += 2) {
     b1 = group_of(c + 1);
+    if constexpr (kUpdatePF == 3) {
+      if (c + 3 < c1) touch |= *reinterpret_cast<const uint32_t*>(rowp + (size_t)(c + 3) * pitch);
+    }
     if constexpr (ENC) { x1 = vals_of(c + 1); xv = x0; }
     client(c, b0);
-    if (c + 2 < M) {
+    if (c + 2 < c1) {
       b0 = group_of(c + 2);
       if constexpr (ENC) x0 = vals_of(c + 2);
     }
     if constexpr (ENC) xv = x1;
     client(c + 1, b1);
   }
-  if (c < M) {
+  if (c < c1) {
     if constexpr (ENC) xv = x0;
     client(c, b0);
+  }
+  if constexpr (kUpdatePF == 3) {
+    if (touch == 0x5a5a5a5au && g < 0) bad |= 1u;  // keeps the touches (never true: g >= 0)
+  }
+  if (c1 < M) {  // not the last chunk: hand the running sums on (NaN: left the domain)
+    if (live) {
+      const bool od = dmax >= kD16Out;
+#pragma unroll
+      for (int i = 0; i < S; ++i) acc_at[i] = od ? __builtin_nanf("") : acc[i];
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) out[i] = 0;
+    return;
   }
   if (__ballot(dmax >= kD16Out) != 0) {  // left the q_gen domain: recompute exactly (never for gradients)
     if (dmax >= kD16Out && live) {
@@ -786,17 +855,19 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
                                                    int64_t g_begin, int64_t g_end,
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
                                                    float* __restrict__ merged_f32, int* __restrict__ err, int nA,
-                                                   InlineEnc ie = InlineEnc{}) {
+                                                   InlineEnc ie = InlineEnc{}, ClientChunk ck = ClientChunk{}) {
   uint32_t bad = 0, layout_bad = 0;
+  const bool last = ck.c1 <= 0 || ck.c1 >= M;  // this launch ends the client loop: merged codes out
   if (bid < nA) {  // block-uniform: one group per lane
     const int64_t g = g_begin + bid * NT + threadIdx.x;
     const bool live = g < g_end;
     int32_t out[3];
     update_lane<3, ENC>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out,
-                        bad, layout_bad, ie);
+                        bad, layout_bad, ie, ck);
     if (!live) return;
     if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+    if (!last) return;
     const int r = (int)min<int64_t>(3, n_up - 3 * g);
     *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &tab), r);
     if (merged_f32)
@@ -808,12 +879,13 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
     const bool live = lane < 63 && g < g_end;
     int32_t out[1];
     update_lane<1>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, e, live, g_begin, hdr_block, out, bad,
-                   layout_bad);
+                   layout_bad, InlineEnc{}, ck);
     const int base = lane - e;  // the group's three lanes (lane 63 reads its own)
     const int32_t o0 = __shfl(out[0], base), o1 = __shfl(out[0], base + 1), o2 = __shfl(out[0], base + 2);
     if (!live) return;
     if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
+    if (!last) return;
     const int r = (int)min<int64_t>(3, n_up - 3 * g);
     if (e == 0) {
       const int32_t o3[3] = {o0, r > 1 ? o1 : 0, r > 2 ? o2 : 0};
@@ -836,14 +908,14 @@ __global__ void __launch_bounds__(NT) k_update_mixed(const uint8_t* __restrict__
                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
                                                      const int32_t* __restrict__ hdr_block,
                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                     int* __restrict__ err, int nA) {
+                                                     int* __restrict__ err, int nA, ClientChunk ck) {
   __shared__ B64Tables tab;
   __shared__ D16Table dtab;
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
   __syncthreads();
   update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block,
-                         merged, merged_f32, err, nA);
+                         merged, merged_f32, err, nA, InlineEnc{}, ck);
 }
 
 // Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
@@ -1598,7 +1670,8 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
                                                       int64_t n_up, int64_t g_begin, int64_t g_end,
                                                       const int32_t* __restrict__ hdr_block,
                                                       uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                      int* __restrict__ err, int nA, int nU, EncodeJob ej) {
+                                                      int* __restrict__ err, int nA, int nU, EncodeJob ej,
+                                                      ClientChunk ck) {
   static_assert(NT == 256, "the encode blocks are 256 lanes");
   __shared__ B64Tables tab;
   __shared__ D16Table dtab;
@@ -1609,7 +1682,7 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   __syncthreads();
   if ((int)blockIdx.x < nU) {  // block-uniform
     update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
-                           hdr_block, merged, merged_f32, err, nA);
+                           hdr_block, merged, merged_f32, err, nA, InlineEnc{}, ck);
   } else {
     set_wave_prio(ej.prio);
     const int64_t e = (int64_t)blockIdx.x - nU;
@@ -1662,11 +1735,12 @@ template __global__ void k_update<1, true, 256>(const uint8_t* __restrict__, siz
                                                KardamOut);
 template __global__ void k_update_mixed<256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
                                              double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
-                                             uint8_t* __restrict__, float* __restrict__, int* __restrict__, int);
+                                             uint8_t* __restrict__, float* __restrict__, int* __restrict__, int,
+                                             ClientChunk);
 template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
                                               double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
                                               uint8_t* __restrict__, float* __restrict__, int* __restrict__, int, int,
-                                              EncodeJob);
+                                              EncodeJob, ClientChunk);
 template __global__ void k_update_encode_inline<256>(const uint8_t* __restrict__, size_t, int,
                                                      const double* __restrict__, double, int64_t, int64_t, int64_t,
                                                      const int32_t* __restrict__, uint8_t* __restrict__,
@@ -1680,11 +1754,12 @@ extern template __global__ void k_update<1, true, 256>(const uint8_t* __restrict
 extern template __global__ void k_update_mixed<256>(const uint8_t* __restrict__, size_t, int,
                                                     const double* __restrict__, double, int64_t, int64_t, int64_t,
                                                     const int32_t* __restrict__, uint8_t* __restrict__,
-                                                    float* __restrict__, int* __restrict__, int);
+                                                    float* __restrict__, int* __restrict__, int, ClientChunk);
 extern template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_t, int,
                                                      const double* __restrict__, double, int64_t, int64_t, int64_t,
                                                      const int32_t* __restrict__, uint8_t* __restrict__,
-                                                     float* __restrict__, int* __restrict__, int, int, EncodeJob);
+                                                     float* __restrict__, int* __restrict__, int, int, EncodeJob,
+                                                     ClientChunk);
 extern template __global__ void k_update_encode_inline<256>(const uint8_t* __restrict__, size_t, int,
                                                             const double* __restrict__, double, int64_t, int64_t,
                                                             int64_t, const int32_t* __restrict__,
@@ -2375,6 +2450,23 @@ static void launch_pipe(const UpdatePlan& p, const uint8_t* uploads, size_t pitc
 #undef FLEET_LAUNCH_PIPE
 }
 
+// Client chunks of the stream update: a launch walks at most ~256 clients (the
+// chunks evenly sized), the running sums handed on through the merged output
+// (ClientChunk). A wave of
+// the stream grid walks every client of its groups; over thousands of clients the
+// waves of one round drift apart and each client step of the round touches rows
+// the others left long ago: configs[4]'s column window at N = 4 (349,526 groups,
+// one round of 5.3 waves per SIMD) took 6.4 us per client at M = 1024..4096
+// against 3.4 at M = 256 (scripts/strong_probe.py). FLEET_UPDATE_CHUNK overrides
+// (0 = one launch).
+int update_chunk_clients(int M) {
+  int ch = 0;
+  if (const char* e = getenv("FLEET_UPDATE_CHUNK")) ch = atoi(e);
+  if (ch <= 0 || M <= ch + ch / 2) return 0;
+  const int k = (M + ch - 1) / ch;
+  return (M + k - 1) / k;
+}
+
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
@@ -2408,8 +2500,12 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
       } else {
         const int64_t rem = groups - (int64_t)nA * 256;
         const int64_t nB = (rem + 83) / 84;
-        hipLaunchKernelGGL((k_update_mixed<256>), dim3((unsigned)(nA + nB)), dim3(256), 0, s, uploads, pitch, M,
-                           d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, nA);
+        const int per = update_chunk_clients(M);
+        for (int c0 = 0; c0 < M; c0 += per ? per : M) {
+          const ClientChunk ck{c0, per ? std::min(M, c0 + per) : 0, reinterpret_cast<float*>(merged)};
+          hipLaunchKernelGGL((k_update_mixed<256>), dim3((unsigned)(nA + nB)), dim3(256), 0, s, uploads, pitch, M,
+                             d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, nA, ck);
+        }
       }
 #undef FLEET_LAUNCH_NT
     }
@@ -2670,14 +2766,21 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   // 12 rows per block with enc_mt, 1179 / 1170 with enc_d16 (the blocks also copy
   // the 9 KB byte table); synth4m_4096 79.1 ms at 12, 64 or 684. FLEET_FUSED_RPB
   // overrides.
-  int rpb = std::min(M, 12);
-  if (const char* e = getenv("FLEET_FUSED_RPB")) rpb = std::max(1, std::min(M, atoi(e)));
-  const int64_t nE = gx * ((M + rpb - 1) / rpb);
-  EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
-  if (const char* e = getenv("FLEET_FUSED_ENC_PRIO")) ej.prio = atoi(e);
-  hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nAf + nB + nE)), dim3(256), 0, s, uploads, pitch, M,
-                     d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf,
-                     (int)(nAf + nB), ej);
+  // client chunks (update_chunk_clients): launch k aggregates clients [c0, c1) and
+  // encodes rows [c0, c1) of the next batch
+  const int per = update_chunk_clients(M);
+  for (int c0 = 0; c0 < M; c0 += per ? per : M) {
+    const int c1 = per ? std::min(M, c0 + per) : M, rows = c1 - c0;
+    int rpb = std::min(rows, 12);
+    if (const char* e = getenv("FLEET_FUSED_RPB")) rpb = std::max(1, std::min(rows, atoi(e)));
+    const int64_t nE = gx * ((rows + rpb - 1) / rpb);
+    EncodeJob ej{values + (size_t)c0 * vpitch, n_up, vpitch, enc_out + (size_t)c0 * pitch, pitch, groups, gx, rows, rpb};
+    if (const char* e = getenv("FLEET_FUSED_ENC_PRIO")) ej.prio = atoi(e);
+    const ClientChunk ck{c0, per ? c1 : 0, reinterpret_cast<float*>(merged)};
+    hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nAf + nB + nE)), dim3(256), 0, s, uploads, pitch, M,
+                       d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf,
+                       (int)(nAf + nB), ej, ck);
+  }
   return hipGetLastError();
 }
 
