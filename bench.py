@@ -267,9 +267,9 @@ def strong_pipelined(torch, dist, codec, name, steps, warmup, rank, world):
     """`value`: strong scaling of ONE fixed problem. The rank's column window of
     every upload is a bucket of its own (n_local values, the header slots that
     fall inside it): the pipelined step (fleet_update_encode_device on the window,
-    the same launch as the N=1 headline step) writes the rank's merged slice,
-    which is copied into the padded all_gather source; the all_gather of every
-    rank's slice (RCCL) runs inside the timed step. Graph replays of the local
+    the same launch as the N=1 headline step) writes the rank's merged slice
+    straight into the padded all_gather source; the all_gather of every rank's
+    slice (RCCL) runs inside the timed step. Graph replays of the local
     launch (one graph per buffer parity), the gather eager after each."""
     import fleet_amd as F
     from fleet_amd.layouts import LAYOUTS
@@ -288,10 +288,9 @@ def strong_pipelined(torch, dist, codec, name, steps, warmup, rank, world):
     bufs = [sh.text, torch.zeros_like(sh.text)]
     nb = 16 * sh.groups
 
-    def local(i):
-        codec.update_encode_device(bufs[i % 2], L_loc, sh.dampen, hloc, sh.merged, sh.merged_f32, sh.values,
+    def local(i):  # the rank's merged slice written straight into the all_gather source
+        codec.update_encode_device(bufs[i % 2], L_loc, sh.dampen, hloc, src, sh.merged_f32, sh.values,
                                    bufs[(i + 1) % 2])
-        src[:nb].copy_(sh.merged[:nb])
 
     sh.encode()
     for i in range(max(2, warmup)):
