@@ -270,7 +270,12 @@ def strong_pipelined(torch, dist, codec, name, steps, warmup, rank, world):
     the same launch as the N=1 headline step) writes the rank's merged slice
     straight into the padded all_gather source; the all_gather of every rank's
     slice (RCCL) runs inside the timed step. Graph replays of the local
-    launch (one graph per buffer parity), the gather eager after each."""
+    launch (one graph per buffer parity), the gather eager after each, issued
+    asynchronously: step i's all_gather (RCCL's own stream) overlaps step i+1's
+    launch, the slice buffers double-buffered by step parity, and the step that
+    reuses a slice buffer first waits for the gather that read it (every gather
+    completes inside the timed region; FLEET_BENCH_GATHER_OVERLAP=0 runs them in
+    line)."""
     import fleet_amd as F
     from fleet_amd.layouts import LAYOUTS
     lay_name, M, note = WORKLOADS[name]
@@ -279,46 +284,69 @@ def strong_pipelined(torch, dist, codec, name, steps, warmup, rank, world):
     G = (layout.n_up + 2) // 3
     wmax = max(b - a for a, b in (group_range(G, world, r) for r in range(world)))
     dev = sh.merged.device
-    src = torch.zeros(16 * wmax, dtype=torch.uint8, device=dev)
-    out = torch.empty(world * 16 * wmax, dtype=torch.uint8, device=dev)
-    gather = all_gather_fn(torch, dist, world, src, out)
+    srcs = [torch.zeros(16 * wmax, dtype=torch.uint8, device=dev) for _ in range(2)]
+    outs = [torch.empty(world * 16 * wmax, dtype=torch.uint8, device=dev) for _ in range(2)]
+    overlap = world > 1 and os.environ.get("FLEET_BENCH_GATHER_OVERLAP", "1") != "0"
     v0 = 3 * sh.gb
     hloc = sh.hpos_global[(sh.hpos_global >= v0) & (sh.hpos_global < v0 + sh.n_local)] - v0
     L_loc = F.b64_len(sh.n_local)
     bufs = [sh.text, torch.zeros_like(sh.text)]
     nb = 16 * sh.groups
 
-    def local(i):  # the rank's merged slice written straight into the all_gather source
-        codec.update_encode_device(bufs[i % 2], L_loc, sh.dampen, hloc, src, sh.merged_f32, sh.values,
+    def local(i):  # the rank's merged slice written straight into the all_gather source of its parity
+        codec.update_encode_device(bufs[i % 2], L_loc, sh.dampen, hloc, srcs[i % 2], sh.merged_f32, sh.values,
                                    bufs[(i + 1) % 2])
+
+    def gather(k, async_op=False):
+        if world == 1:
+            return None
+        if dist.get_backend() == "gloo":  # CPU-collective rehearsal (FLEET_BENCH_BACKEND=gloo)
+            return dist.all_gather(list(outs[k].chunk(world)), srcs[k], async_op=async_op)
+        return dist.all_gather_into_tensor(outs[k], srcs[k], async_op=async_op)
 
     sh.encode()
     for i in range(max(2, warmup)):
         local(i)
-        gather()
+        gather(i % 2)
     torch.cuda.synchronize()
     codec.check()
     graphs = [graph_of(torch, lambda: local(0), 1), graph_of(torch, lambda: local(1), 1)]
     graphs[0].replay()
     graphs[1].replay()
     state = {"i": 0}
+    works = [None, None]
 
     def step():
-        graphs[state["i"] % 2].replay()
+        i = state["i"]
+        k = i % 2
         state["i"] += 1
-        gather()
+        if not overlap:
+            graphs[k].replay()
+            gather(k)
+            return
+        if works[k] is not None:  # the gather of step i-2 read srcs[k]: the stream waits for it
+            works[k].wait()
+        graphs[k].replay()
+        works[k] = gather(k, async_op=True)
+        if i == steps - 1:  # the last step: both outstanding gathers complete inside the timed region
+            for j in (0, 1):
+                if works[j] is not None:
+                    works[j].wait()
+                    works[j] = None
 
     elapsed = run_timed(torch, dist, world, step, steps)
     codec.check()
-    if world > 1 and not torch.equal(out[rank * 16 * wmax: rank * 16 * wmax + nb], src[:nb]):
+    kl = (steps - 1) % 2
+    if world > 1 and not torch.equal(outs[kl][rank * 16 * wmax: rank * 16 * wmax + nb], srcs[kl][:nb]):
         raise RuntimeError("all_gather returned a different merged slice")
     kern_ms = kernel_ms(torch, lambda: (local(0), local(1)), reps=5) / 2
     res = {"workload": name, "note": note, "clients": M, "n_up_total": layout.n_up, "n_up_per_rank": sh.n_local,
            "groups_per_rank_max": wmax, "ms_per_step": elapsed / steps * 1e3,
            "gib_s": M * layout.n_up * 4 / (elapsed / steps) / 2**30,
            "kernel": F.update_encode_kernel(L_loc), "kernel_ms_rank0": kern_ms,
-           "step": "pipelined launch on the rank's column window + all_gather of the merged slices (inside)"}
-    del graphs, bufs, sh, src, out
+           "step": "pipelined launch on the rank's column window + all_gather of the merged slices (inside; "
+                   + ("issued async, overlapping the next step's launch)" if overlap else "in line)")}
+    del graphs, bufs, sh, srcs, outs
     torch.cuda.empty_cache()
     return res
 

@@ -2383,9 +2383,12 @@ static UpdatePlan plan_update(int64_t groups) {
   if (p.ipt == 2) p.nw = 4, p.wp = 0;
   if (p.wp && p.nw == 5) p.nw = 4;
   if (use_tiled(groups)) {
-    // widest tile that still gives >= 4 blocks per CU; the narrow tiles are
-    // pipelined (producer waves + one consumer wave)
-    p.tg = groups >= 64LL * 1024 ? 64 : groups >= 32LL * 1024 ? 32 : 16;
+    // 64-group tiles down to 2 per CU (32 k groups): below 4 per CU they still beat
+    // the 32-group tiles, whose phase 2 runs 1.5 waves of serial chains per tile
+    // against 3 (synth1m_256's strong-scaling windows, scripts/gpu_r03_d13.sh: update
+    // alone 221 -> 195 us at 58,255 groups, 164 -> 153 us at 43,691); the narrow
+    // tiles are pipelined (producer waves + one consumer wave)
+    p.tg = groups >= 32LL * 1024 ? 64 : 16;
     if (const char* e = getenv("FLEET_TILE_G")) p.tg = atoi(e);
     if (p.tg != 8 && p.tg != 16 && p.tg != 32 && p.tg != 64) p.tg = 16;
     const char* pe = getenv("FLEET_UPDATE_PIPE");
