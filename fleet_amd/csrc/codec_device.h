@@ -113,96 +113,6 @@ __device__ __forceinline__ void d16_table_init(D16Table* t) {
   }
 }
 
-// FLEET_DEC_I8 = 1: the decode table is read sign-extended (see b64_quad_full);
-// 0: the unsigned reads with per-char flag extraction (r02 form, A/B).
-#ifndef FLEET_DEC_I8
-#define FLEET_DEC_I8 0
-#endif
-#if FLEET_DEC_I8
-// One 16-char group -> 12 bytes -> 3 little-endian int32 codes.
-// Returns a 16-bit mask of chars that are not in the alphabet (bit i = char i).
-// The table is read sign-extended like b64_decode_group_full's (the same loads
-// then serve both forms where a kernel has both), the marker 0xff as -1.
-__device__ __forceinline__ uint32_t b64_decode_group(uint4 w, const B64Tables* t, int32_t codes[3]) {
-  const int8_t* from = reinterpret_cast<const int8_t*>(t->from);
-  const uint32_t words[4] = {w.x, w.y, w.z, w.w};
-  uint32_t V[4];
-  uint32_t bad = 0;
-#pragma unroll
-  for (int qd = 0; qd < 4; ++qd) {
-    const int32_t s0 = from[words[qd] & 0xff];
-    const int32_t s1 = from[(words[qd] >> 8) & 0xff];
-    const int32_t s2 = from[(words[qd] >> 16) & 0xff];
-    const int32_t s3 = from[words[qd] >> 24];
-    bad |= ((uint32_t)(s0 < 0) | ((uint32_t)(s1 < 0) << 1) | ((uint32_t)(s2 < 0) << 2) | ((uint32_t)(s3 < 0) << 3))
-           << (4 * qd);
-    V[qd] = ((uint32_t)(s0 & 63) << 18) | ((uint32_t)(s1 & 63) << 12) | ((uint32_t)(s2 & 63) << 6) | (uint32_t)(s3 & 63);
-  }
-  // bytes of quad q are V[q] big-endian; codes are little-endian int32
-  codes[0] = (int32_t)__builtin_amdgcn_perm(V[1], V[0], 0x06000102u);
-  codes[1] = (int32_t)__builtin_amdgcn_perm(V[2], V[1], 0x05060001u);
-  codes[2] = (int32_t)__builtin_amdgcn_perm(V[3], V[2], 0x04050600u);
-  return bad;
-}
-
-// Same decode for a full group (all 16 chars carry data): returns nonzero if any
-// char is outside the alphabet. The table is read sign-extended (ds_read_i8):
-// valid entries are 0..63, the invalid marker 0xff becomes -1, so a bad char sets
-// bit 31 of its quad's shift-or word wherever it sits in the quad (valid words stay
-// below 2^24), and one OR of the four words flags the group (the codes are garbage
-// then, and the caller fails) -- no per-char flag extraction.
-__device__ __forceinline__ uint32_t b64_quad_full(uint32_t w, const int8_t* from) {
-  const uint32_t s0 = (uint32_t)(int32_t)from[w & 0xff];
-  const uint32_t s1 = (uint32_t)(int32_t)from[(w >> 8) & 0xff];
-  const uint32_t s2 = (uint32_t)(int32_t)from[(w >> 16) & 0xff];
-  const uint32_t s3 = (uint32_t)(int32_t)from[w >> 24];
-  return (((((s0 << 6) | s1) << 6) | s2) << 6) | s3;
-}
-__device__ __forceinline__ uint32_t b64_decode_group_full(uint4 w, const B64Tables* t, int32_t codes[3]) {
-  const int8_t* from = reinterpret_cast<const int8_t*>(t->from);
-  const uint32_t V0 = b64_quad_full(w.x, from), V1 = b64_quad_full(w.y, from);
-  const uint32_t V2 = b64_quad_full(w.z, from), V3 = b64_quad_full(w.w, from);
-  codes[0] = (int32_t)__builtin_amdgcn_perm(V1, V0, 0x06000102u);
-  codes[1] = (int32_t)__builtin_amdgcn_perm(V2, V1, 0x05060001u);
-  codes[2] = (int32_t)__builtin_amdgcn_perm(V3, V2, 0x04050600u);
-  return (V0 | V1 | V2 | V3) & 0x80000000u;
-}
-
-// One code of a group from the two 4-char quads that hold its bytes: value e of
-// the group is bytes 4e..4e+3, i.e. quads e and e+1 (w0, w1 = chars 4e..4e+7);
-// `sel` = b64_pair_selector(e). For lanes that own one value of a group.
-__device__ __forceinline__ uint32_t b64_pair_selector(int e) {
-  return e == 0 ? 0x06000102u : e == 1 ? 0x05060001u : 0x04050600u;  // the perms of b64_decode_group
-}
-// all 8 chars carry data: nonzero if any is outside the alphabet (b64_quad_full)
-__device__ __forceinline__ uint32_t b64_decode_pair_full(uint32_t w0, uint32_t w1, uint32_t sel, const B64Tables* t,
-                                                         int32_t& code) {
-  const int8_t* from = reinterpret_cast<const int8_t*>(t->from);
-  const uint32_t V0 = b64_quad_full(w0, from), V1 = b64_quad_full(w1, from);
-  code = (int32_t)__builtin_amdgcn_perm(V1, V0, sel);
-  return (V0 | V1) & 0x80000000u;
-}
-// per-char mask of chars outside the alphabet (bit i = char 4e + i)
-__device__ __forceinline__ uint32_t b64_decode_pair(uint32_t w0, uint32_t w1, uint32_t sel, const B64Tables* t,
-                                                    int32_t& code) {
-  const int8_t* from = reinterpret_cast<const int8_t*>(t->from);
-  const uint32_t words[2] = {w0, w1};
-  uint32_t V[2], bad = 0;
-#pragma unroll
-  for (int qd = 0; qd < 2; ++qd) {
-    const int32_t s0 = from[words[qd] & 0xff];
-    const int32_t s1 = from[(words[qd] >> 8) & 0xff];
-    const int32_t s2 = from[(words[qd] >> 16) & 0xff];
-    const int32_t s3 = from[words[qd] >> 24];
-    bad |= ((uint32_t)(s0 < 0) | ((uint32_t)(s1 < 0) << 1) | ((uint32_t)(s2 < 0) << 2) | ((uint32_t)(s3 < 0) << 3))
-           << (4 * qd);
-    V[qd] = ((uint32_t)(s0 & 63) << 18) | ((uint32_t)(s1 & 63) << 12) | ((uint32_t)(s2 & 63) << 6) | (uint32_t)(s3 & 63);
-  }
-  code = (int32_t)__builtin_amdgcn_perm(V[1], V[0], sel);
-  return bad;
-}
-
-#else
 // One 16-char group -> 12 bytes -> 3 little-endian int32 codes.
 // Returns a 16-bit mask of chars that are not in the alphabet (bit i = char i).
 __device__ __forceinline__ uint32_t b64_decode_group(uint4 w, const B64Tables* t, int32_t codes[3]) {
@@ -289,8 +199,6 @@ __device__ __forceinline__ uint32_t b64_decode_pair(uint32_t w0, uint32_t w1, ui
   return bad;
 }
 
-#endif
-
 // 3 codes -> 12 bytes -> 16 chars (Base64.cpp:176-195).
 __device__ __forceinline__ uint4 b64_encode_group(const int32_t codes[3], const B64Tables* t) {
   const uint32_t c0 = (uint32_t)codes[0], c1 = (uint32_t)codes[1], c2 = (uint32_t)codes[2];
@@ -309,46 +217,6 @@ __device__ __forceinline__ uint4 b64_encode_group(const int32_t codes[3], const 
     uint32_t d = t->to[V[qd] & 63];
     out[qd] = a | (b << 8) | (c << 16) | (d << 24);
   }
-  return make_uint4(out[0], out[1], out[2], out[3]);
-}
-
-// Base64 encode by sextet PAIRS (the fused step's client encode): entry
-// (a << 6) | b holds the two chars to[a] | to[b] << 8, so a 4-char quad is two
-// 2-byte lookups addressed straight from the quad's 24-bit word (two shifts and
-// two masks) instead of four bit-field extracts and a shift-or assembly of four
-// chars. 8 KB of LDS, allocated only by kernels whose encode is on the clock.
-struct alignas(16) B64Pairs {
-  uint16_t p[4096];
-};
-static_assert(sizeof(B64Pairs) % 16 == 0, "copied as uint4");
-FLEET_HDC B64Pairs make_b64_pairs() {
-  B64Pairs t{};
-  for (int i = 0; i < 4096; ++i) t.p[i] = (uint16_t)(b64_to_value(i >> 6) | (b64_to_value(i & 63) << 8));
-  return t;
-}
-static __constant__ B64Pairs g_b64_pairs = make_b64_pairs();
-template <int NT = 256>
-__device__ __forceinline__ void b64_pairs_init(B64Pairs* t) {
-  constexpr int n16 = (int)(sizeof(B64Pairs) / 16);
-  const uint4* src = reinterpret_cast<const uint4*>(&g_b64_pairs);
-  uint4* dst = reinterpret_cast<uint4*>(t);
-#pragma unroll
-  for (int i0 = 0; i0 < n16; i0 += NT) {
-    const int i = i0 + (int)threadIdx.x;
-    if (i < n16) dst[i] = src[i];
-  }
-}
-// b64_encode_group on the pair table: identical bytes.
-__device__ __forceinline__ uint4 b64_encode_group_pairs(const int32_t codes[3], const B64Pairs* t) {
-  const uint32_t c0 = (uint32_t)codes[0], c1 = (uint32_t)codes[1], c2 = (uint32_t)codes[2];
-  uint32_t V[4];
-  V[0] = __builtin_amdgcn_perm(0u, c0, 0x0c000102u);
-  V[1] = __builtin_amdgcn_perm(c1, c0, 0x0c030405u);
-  V[2] = __builtin_amdgcn_perm(c2, c1, 0x0c020304u);
-  V[3] = __builtin_amdgcn_perm(0u, c2, 0x0c010203u);
-  uint32_t out[4];
-#pragma unroll
-  for (int qd = 0; qd < 4; ++qd) out[qd] = (uint32_t)t->p[V[qd] >> 12] | ((uint32_t)t->p[V[qd] & 0xfffu] << 16);
   return make_uint4(out[0], out[1], out[2], out[3]);
 }
 

@@ -19,13 +19,9 @@ struct DescentSegs {
 };
 hipError_t launch_descent(float* weights, float* fc_bias, const float* grad, const DescentSegs& segs, float lr,
                           hipStream_t s);
-// The stream update of many clients runs as several launches of at most
-// update_chunk_clients(M) clients each, the running sums kept in `merged` between them.
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s);
-// clients per launch of the chunked stream update (0: every client in one launch)
-int update_chunk_clients(int M);
 // Kardam's side outputs of the fused update (k_update<1, true>): per client c and
 // flat value (upload positions that are neither header slots nor past the walk)
 //   G = Q(f32(f64(p) lr))            the decoded Kardam.setGrad text (p = stage B)

@@ -584,118 +584,17 @@ constexpr bool kTileXcd = FLEET_TILE_XCD != 0;
 #endif
 constexpr bool kStageCVar = FLEET_STAGEC_VAR != 0;
 
-// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
-// One group (3 values) of one row: float2int (fixed chains when the wave is
-// in |x| < 1, multiplier-table chains otherwise, the general codec for values
-// outside the q_gen domain) and the 16 Base64 chars.
-__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab,
-                                              const D16Table* dt, const B64Pairs* pairs = nullptr) {
-  int32_t codes[3];
-  // |x| < 1 for the whole wave iff the largest |x| bit pattern is (integer max,
-  // not three 6-cycle e64 compares)
-  uint32_t amax = 0;
-#pragma unroll
-  for (int e = 0; e < 3; ++e) amax = max(amax, f2u(x[e]) & 0x7fffffffu);
-  if (__ballot(amax >= 0x3f800000u) == 0) {  // wave-uniform: gradients, |x| < 1
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
-  } else {
-    // byte-table digit counts (codec_math.h d16_entry): one byte load per value;
-    // the power-of-ten slices take the compare, values outside the q_gen
-    // domain (|x| >= 1e8/1e9, inf, NaN) the general codec -- both rare, per lane
-    uint32_t ofs[3], omax = 0;
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      ofs[e] = dt->d16[f2u(x[e]) >> 19];
-      omax = max(omax, ofs[e]);
-    }
-    if (__ballot(omax >= kD16Out) != 0) {
-      omax = 0;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        if (ofs[e] == kD16Cmp) ofs[e] = d16_fix(x[e], tab->var);
-        omax = max(omax, ofs[e]);
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
-    if (__ballot(omax >= kD16Out) != 0) {
-#pragma unroll
-      for (int e = 0; e < 3; ++e)
-        if (ofs[e] >= kD16Out) codes[e] = enc(x[e]);
-    }
-  }
-  return pad_group(pairs ? b64_encode_group_pairs(codes, pairs) : b64_encode_group(codes, tab), r);
-}
-
-// The same with the VarEntry digit counts (kernels that keep only B64Tables in LDS)
-__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
-  int32_t codes[3];
-  const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
-  if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab->var, tab->mt);
-    if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
-#pragma unroll
-      for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
-    }
-  }
-  return pad_group(b64_encode_group(codes, tab), r);
-}
-
-// The client encode of the next batch riding inside the stream update's waves
-// (k_update_encode_inline): lane g also encodes group g of every row of `values`
-// into `out`, one row per client step, its loads issued with the next client's
-// upload group.
-struct InlineEnc {
-  const float* values;
-  int64_t n;
-  size_t vpitch;
-  uint8_t* out;
-  size_t pitch;
-};
-
-// One launch of a client-chunked stream update (launch_update / launch_update_encode
-// for large M): clients [c0, c1) of the M picked uploads. The running sums A carry
-// over between launches in the merged output itself: `acc` = the merged text as
-// floats, a group's three sums in the first 12 of its 16 bytes (read at c0 > 0,
-// written at c1 < M, by the lanes that own the group; the last chunk reads them
-// before it writes the group's merged chars). A lane whose chain has left the q_gen
-// domain writes NaN, which keeps every later chunk out of the domain too, so the
-// last chunk recomputes it exactly over all M clients. c1 <= 0: the whole range
-// [0, M) in one launch.
-struct ClientChunk {
-  int c0 = 0, c1 = 0;
-  float* acc = nullptr;
-};
-
-// Client groups in flight ahead of the one being aggregated by a stream lane
-// (FLEET_UPDATE_PF: 1 = the next client's, 2 = the next two clients').
-#ifndef FLEET_UPDATE_PF
-#define FLEET_UPDATE_PF 1
-#endif
-constexpr int kUpdatePF = FLEET_UPDATE_PF;
-
 // One lane's share of the fused update (the non-Kardam stream path): the values
 // [e0, e0 + S) of group g, S = 3 (the whole group) or S = 1 (one value; three
 // lanes of a wave share a group). Returns the lane's merged codes in out[S] and
 // its Base64 / layout error bits; tables already in LDS.
-//   ENC (S = 3 only): also the client encode of group g of every row of ie
-// (InlineEnc), row c encoded in client c's step.
-template <int S, bool ENC = false>
+template <int S>
 __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table& dtab,
                                             const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                             const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                             int64_t g, int e0, bool live, int64_t g_safe,
                                             const int32_t* __restrict__ hdr_block, int32_t (&out)[S],
-                                            uint32_t& bad, uint32_t& layout_bad, InlineEnc ie = InlineEnc{},
-                                            ClientChunk ck = ClientChunk{}) {
-  static_assert(!ENC || S == 3, "the inline encode needs whole groups");
-  const int c0 = ck.c1 > 0 ? ck.c0 : 0, c1 = ck.c1 > 0 ? ck.c1 : M;
-  float* acc_at = ck.c1 > 0 ? ck.acc + 4 * (live ? g : g_safe) + e0 : nullptr;  // this lane's running sums
+                                            uint32_t& bad, uint32_t& layout_bad) {
   const int n_hdr = hdr_block[1];
   const int64_t walk_end = hdr_block[2];
   const int32_t* hdr = hdr_block + 4;
@@ -711,33 +610,7 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // bytes (chars 4e..4e+7); the group's three lanes together cover all 16 chars
   const uint32_t sel = b64_pair_selector(e0), need_pair = (need >> (4 * e0)) & 0xffu;
   using Row = typename std::conditional<S == 3, uint4, uint2>::type;
-  // the inline encode: group g's three values of row c (one 12-byte load per full group)
-  typedef float f3 __attribute__((ext_vector_type(3)));
-  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
-  const int er = live ? (int)min<int64_t>(3, ie.n - 3 * g) : 3;
-  const float* ev = ENC ? ie.values + 3 * (live ? g : g_safe) : nullptr;
-  auto vals_of = [&](int c) -> f3 {
-    const float* q = ev + (size_t)c * ie.vpitch;
-    if (er == 3) return *reinterpret_cast<const f3u*>(q);
-    return f3{q[0], er > 1 ? q[1] : 0.0f, 0.0f};
-  };
-  f3 xv{0.0f, 0.0f, 0.0f};  // row c's values while client c's step runs
-  if (c0 > 0) {  // a later chunk: the running sums so far, and (header waves) client 0's header codes
-#pragma unroll
-    for (int i = 0; i < S; ++i) acc[i] = live ? acc_at[i] : 0.0f;
-    if (wave_hdr) {
-      int32_t h0[3];
-      b64_decode_group(*reinterpret_cast<const uint4*>(uploads + 16 * (live ? g : g_safe)), &tab, h0);
-#pragma unroll
-      for (int i = 0; i < S; ++i) hfirst[i] = h0[e0 + i];
-    }
-  }
   auto client = [&](int c, const Row& cur) {
-    if constexpr (ENC) {
-      const float x[3] = {xv.x, xv.y, xv.z};
-      const uint4 t = encode_group(x, er, &tab, &dtab);
-      if (live) store_stream16(ie.out + (size_t)c * ie.pitch + 16 * g, t);
-    }
     if constexpr (S == 3) {
       if (need == 0xffffu) bad |= b64_decode_group_full(cur, &tab, codes);
       else bad |= b64_decode_group(cur, &tab, codes) & need;
@@ -777,61 +650,16 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
     }
   };
   // two clients per trip, the next client's group always in flight, in alternating
-  // registers (no copies between trips); with ENC the next row's values ride along
-  Row b0 = group_of(c0), b1;
-  f3 x0{0.0f, 0.0f, 0.0f}, x1{0.0f, 0.0f, 0.0f};
-  if constexpr (ENC) x0 = vals_of(c0);
-  int c = c0;
-  if constexpr (kUpdatePF == 2 && !ENC) {
-    // three clients per trip, the next TWO clients' groups in flight (rotating registers)
-    Row b2;
-    if (c0 + 1 < c1) b1 = group_of(c0 + 1);
-    for (; c + 2 < c1; c += 3) {
-      b2 = group_of(c + 2);
-      client(c, b0);
-      if (c + 3 < c1) b0 = group_of(c + 3);
-      client(c + 1, b1);
-      if (c + 4 < c1) b1 = group_of(c + 4);
-      client(c + 2, b2);
-    }
-    if (c < c1) client(c, b0);
-    if (c + 1 < c1) client(c + 1, b1);
-    c = c1;
-  }
-  // kUpdatePF == 3 (experiment): every lane also touches one dword of its group
-  // three clients ahead, warming the translation and the DRAM page for the row
-  uint32_t touch = 0;
-  for (; c + 1 < c1; c += 2) {
+  // registers (no copies between trips)
+  Row b0 = group_of(0), b1;
+  int c = 0;
+  for (; c + 1 < M; c += 2) {
     b1 = group_of(c + 1);
-    if constexpr (kUpdatePF == 3) {
-      if (c + 3 < c1) touch |= *reinterpret_cast<const uint32_t*>(rowp + (size_t)(c + 3) * pitch);
-    }
-    if constexpr (ENC) { x1 = vals_of(c + 1); xv = x0; }
     client(c, b0);
-    if (c + 2 < c1) {
-      b0 = group_of(c + 2);
-      if constexpr (ENC) x0 = vals_of(c + 2);
-    }
-    if constexpr (ENC) xv = x1;
+    if (c + 2 < M) b0 = group_of(c + 2);
     client(c + 1, b1);
   }
-  if (c < c1) {
-    if constexpr (ENC) xv = x0;
-    client(c, b0);
-  }
-  if constexpr (kUpdatePF == 3) {
-    if (touch == 0x5a5a5a5au && g < 0) bad |= 1u;  // keeps the touches (never true: g >= 0)
-  }
-  if (c1 < M) {  // not the last chunk: hand the running sums on (NaN: left the domain)
-    if (live) {
-      const bool od = dmax >= kD16Out;
-#pragma unroll
-      for (int i = 0; i < S; ++i) acc_at[i] = od ? __builtin_nanf("") : acc[i];
-    }
-#pragma unroll
-    for (int i = 0; i < S; ++i) out[i] = 0;
-    return;
-  }
+  if (c < M) client(c, b0);
   if (__ballot(dmax >= kD16Out) != 0) {  // left the q_gen domain: recompute exactly (never for gradients)
     if (dmax >= kD16Out && live) {
 #pragma unroll
@@ -847,27 +675,23 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
 }
 
 // Block `bid` of the SIMD-balanced stream grid (tables already in LDS).
-// ENC: the group-per-lane blocks also encode their groups of every row of ie.
-template <int NT, bool ENC = false>
+template <int NT>
 __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D16Table& dtab, int64_t bid,
                                                    const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                    const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                                    int64_t g_begin, int64_t g_end,
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
-                                                   float* __restrict__ merged_f32, int* __restrict__ err, int nA,
-                                                   InlineEnc ie = InlineEnc{}, ClientChunk ck = ClientChunk{}) {
+                                                   float* __restrict__ merged_f32, int* __restrict__ err, int nA) {
   uint32_t bad = 0, layout_bad = 0;
-  const bool last = ck.c1 <= 0 || ck.c1 >= M;  // this launch ends the client loop: merged codes out
   if (bid < nA) {  // block-uniform: one group per lane
     const int64_t g = g_begin + bid * NT + threadIdx.x;
     const bool live = g < g_end;
     int32_t out[3];
-    update_lane<3, ENC>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out,
-                        bad, layout_bad, ie, ck);
+    update_lane<3>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out, bad,
+                   layout_bad);
     if (!live) return;
     if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
-    if (!last) return;
     const int r = (int)min<int64_t>(3, n_up - 3 * g);
     *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &tab), r);
     if (merged_f32)
@@ -879,13 +703,12 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
     const bool live = lane < 63 && g < g_end;
     int32_t out[1];
     update_lane<1>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, e, live, g_begin, hdr_block, out, bad,
-                   layout_bad, InlineEnc{}, ck);
+                   layout_bad);
     const int base = lane - e;  // the group's three lanes (lane 63 reads its own)
     const int32_t o0 = __shfl(out[0], base), o1 = __shfl(out[0], base + 1), o2 = __shfl(out[0], base + 2);
     if (!live) return;
     if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
-    if (!last) return;
     const int r = (int)min<int64_t>(3, n_up - 3 * g);
     if (e == 0) {
       const int32_t o3[3] = {o0, r > 1 ? o1 : 0, r > 2 ? o2 : 0};
@@ -908,18 +731,80 @@ __global__ void __launch_bounds__(NT) k_update_mixed(const uint8_t* __restrict__
                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
                                                      const int32_t* __restrict__ hdr_block,
                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                     int* __restrict__ err, int nA, ClientChunk ck) {
+                                                     int* __restrict__ err, int nA) {
   __shared__ B64Tables tab;
   __shared__ D16Table dtab;
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
   __syncthreads();
   update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block,
-                         merged, merged_f32, err, nA, InlineEnc{}, ck);
+                         merged, merged_f32, err, nA);
 }
 
 // Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
 // of NW waves.
+// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
+// One group (3 values) of one row: float2int (fixed chains when the wave is
+// in |x| < 1, multiplier-table chains otherwise, the general codec for values
+// outside the q_gen domain) and the 16 Base64 chars.
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab,
+                                              const D16Table* dt) {
+  int32_t codes[3];
+  // |x| < 1 for the whole wave iff the largest |x| bit pattern is (integer max,
+  // not three 6-cycle e64 compares)
+  uint32_t amax = 0;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) amax = max(amax, f2u(x[e]) & 0x7fffffffu);
+  if (__ballot(amax >= 0x3f800000u) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+    // byte-table digit counts (codec_math.h d16_entry): one byte load per value;
+    // the power-of-ten slices take the compare, values outside the q_gen
+    // domain (|x| >= 1e8/1e9, inf, NaN) the general codec -- both rare, per lane
+    uint32_t ofs[3], omax = 0;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      ofs[e] = dt->d16[f2u(x[e]) >> 19];
+      omax = max(omax, ofs[e]);
+    }
+    if (__ballot(omax >= kD16Out) != 0) {
+      omax = 0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        if (ofs[e] == kD16Cmp) ofs[e] = d16_fix(x[e], tab->var);
+        omax = max(omax, ofs[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
+    if (__ballot(omax >= kD16Out) != 0) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if (ofs[e] >= kD16Out) codes[e] = enc(x[e]);
+    }
+  }
+  return pad_group(b64_encode_group(codes, tab), r);
+}
+
+// The same with the VarEntry digit counts (kernels that keep only B64Tables in LDS)
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
+  int32_t codes[3];
+  const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
+  if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab->var, tab->mt);
+    if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
+#pragma unroll
+      for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
+    }
+  }
+  return pad_group(b64_encode_group(codes, tab), r);
+}
+
 // A client-encode job riding in an aggregation launch (k_update_encode,
 // k_update_tiled_encode, k_update_pipe): k_encode_f32's grid, flattened x-fastest
 // (the tiles' inline form, k_update_tiled_encode<..., INL>, uses values / n / vpitch /
@@ -1415,7 +1300,7 @@ template <bool D16, int NT = 256, bool ROT = false>
 __device__ __forceinline__ void encode_rows(const float* __restrict__ values, int64_t n, size_t vpitch,
                                             uint8_t* __restrict__ out, size_t pitch, int64_t groups, int rows,
                                             int rpb, int64_t bx, int by, const B64Tables* tab,
-                                            const D16Table* dt, const B64Pairs* pairs = nullptr) {
+                                            const D16Table* dt) {
   const int64_t g = bx * NT + threadIdx.x;
   if (g >= groups) return;
   const int row0 = by * rpb, row1 = min(rows, row0 + rpb);
@@ -1433,7 +1318,7 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
     return f3{p[0], r > 1 ? p[1] : 0.0f, 0.0f};
   };
   auto emit = [&](int rr, const float (&x)[3]) {
-    if constexpr (D16) store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab, dt, pairs));
+    if constexpr (D16) store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab, dt));
     else store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab));
   };
   if constexpr (ROT) {
@@ -1660,66 +1545,27 @@ __global__ void __launch_bounds__(256) k_encode_f32_d16(const float* __restrict_
 // aggregation's blocks first (they fit the chip in one round) and streams the
 // encode's blocks through the wave slots and issue cycles they leave. Each
 // block's results are those of the separate kernels.
-#ifndef FLEET_FUSED_PAIRS
-#define FLEET_FUSED_PAIRS 0
-#endif
-constexpr bool kFusedPairs = FLEET_FUSED_PAIRS != 0;
 template <int NT>
 __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                       const double* __restrict__ dampen, double inv_avg,
                                                       int64_t n_up, int64_t g_begin, int64_t g_end,
                                                       const int32_t* __restrict__ hdr_block,
                                                       uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                      int* __restrict__ err, int nA, int nU, EncodeJob ej,
-                                                      ClientChunk ck) {
+                                                      int* __restrict__ err, int nA, int nU, EncodeJob ej) {
   static_assert(NT == 256, "the encode blocks are 256 lanes");
   __shared__ B64Tables tab;
   __shared__ D16Table dtab;
-  __shared__ B64Pairs pairs;  // the encode's Base64 by sextet pairs (kFusedPairs)
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
-  if (kFusedPairs && (int)blockIdx.x >= nU) b64_pairs_init<NT>(&pairs);
   __syncthreads();
   if ((int)blockIdx.x < nU) {  // block-uniform
     update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
-                           hdr_block, merged, merged_f32, err, nA, InlineEnc{}, ck);
+                           hdr_block, merged, merged_f32, err, nA);
   } else {
     set_wave_prio(ej.prio);
     const int64_t e = (int64_t)blockIdx.x - nU;
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
-                     (int)(e / ej.gx), &tab, &dtab, kFusedPairs ? &pairs : nullptr);
-  }
-}
-
-// The pipelined step with the client encode INSIDE the update's waves: blocks
-// [0, nA) are k_update_mixed's group-per-lane blocks, each lane also encoding its
-// group of every row of the next batch (InlineEnc: one row per client step, the
-// values loaded with the next client's upload group), so the encode's VALU work
-// and its HBM traffic are spread over the whole aggregation instead of queueing
-// behind it; blocks [nA, nU) the value-per-lane remainder of the update, blocks
-// [nU, ...) k_encode_f32's grid over the remainder's groups (ej: values / out
-// already offset to the first of them). Each block's results are those of the
-// separate kernels.
-template <int NT>
-__global__ void __launch_bounds__(NT) k_update_encode_inline(const uint8_t* __restrict__ uploads, size_t pitch, int M,
-                                                             const double* __restrict__ dampen, double inv_avg,
-                                                             int64_t n_up, int64_t g_begin, int64_t g_end,
-                                                             const int32_t* __restrict__ hdr_block,
-                                                             uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                             int* __restrict__ err, int nA, int nU, InlineEnc ie,
-                                                             EncodeJob ej) {
-  __shared__ B64Tables tab;
-  __shared__ D16Table dtab;
-  b64_tables_init<NT>(&tab);
-  d16_table_init<NT>(&dtab);
-  __syncthreads();
-  if ((int)blockIdx.x < nU) {  // block-uniform
-    update_mixed_block<NT, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
-                                 hdr_block, merged, merged_f32, err, nA, ie);
-  } else {
-    const int64_t e = (int64_t)blockIdx.x - nU;
-    encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
-                      (int)(e / ej.gx), &tab, &dtab);
+                     (int)(e / ej.gx), &tab, &dtab);
   }
 }
 
@@ -1735,17 +1581,11 @@ template __global__ void k_update<1, true, 256>(const uint8_t* __restrict__, siz
                                                KardamOut);
 template __global__ void k_update_mixed<256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
                                              double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
-                                             uint8_t* __restrict__, float* __restrict__, int* __restrict__, int,
-                                             ClientChunk);
+                                             uint8_t* __restrict__, float* __restrict__, int* __restrict__, int);
 template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
                                               double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
                                               uint8_t* __restrict__, float* __restrict__, int* __restrict__, int, int,
-                                              EncodeJob, ClientChunk);
-template __global__ void k_update_encode_inline<256>(const uint8_t* __restrict__, size_t, int,
-                                                     const double* __restrict__, double, int64_t, int64_t, int64_t,
-                                                     const int32_t* __restrict__, uint8_t* __restrict__,
-                                                     float* __restrict__, int* __restrict__, int, int, InlineEnc,
-                                                     EncodeJob);
+                                              EncodeJob);
 #else
 extern template __global__ void k_update<1, true, 256>(const uint8_t* __restrict__, size_t, int,
                                                       const double* __restrict__, double, int64_t, int64_t, int64_t,
@@ -1754,17 +1594,11 @@ extern template __global__ void k_update<1, true, 256>(const uint8_t* __restrict
 extern template __global__ void k_update_mixed<256>(const uint8_t* __restrict__, size_t, int,
                                                     const double* __restrict__, double, int64_t, int64_t, int64_t,
                                                     const int32_t* __restrict__, uint8_t* __restrict__,
-                                                    float* __restrict__, int* __restrict__, int, ClientChunk);
+                                                    float* __restrict__, int* __restrict__, int);
 extern template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_t, int,
                                                      const double* __restrict__, double, int64_t, int64_t, int64_t,
                                                      const int32_t* __restrict__, uint8_t* __restrict__,
-                                                     float* __restrict__, int* __restrict__, int, int, EncodeJob,
-                                                     ClientChunk);
-extern template __global__ void k_update_encode_inline<256>(const uint8_t* __restrict__, size_t, int,
-                                                            const double* __restrict__, double, int64_t, int64_t,
-                                                            int64_t, const int32_t* __restrict__,
-                                                            uint8_t* __restrict__, float* __restrict__,
-                                                            int* __restrict__, int, int, InlineEnc, EncodeJob);
+                                                     float* __restrict__, int* __restrict__, int, int, EncodeJob);
 #endif
 
 #ifndef FLEET_STREAM_TU
@@ -2386,8 +2220,9 @@ static UpdatePlan plan_update(int64_t groups) {
     // 64-group tiles down to 2 per CU (32 k groups): below 4 per CU they still beat
     // the 32-group tiles, whose phase 2 runs 1.5 waves of serial chains per tile
     // against 3 (synth1m_256's strong-scaling windows, scripts/gpu_r03_d13.sh: update
-    // alone 221 -> 195 us at 58,255 groups, 164 -> 153 us at 43,691); the narrow
-    // tiles are pipelined (producer waves + one consumer wave)
+    // alone 221 -> 195 us at 58,255 groups, 164 -> 153 us at 43,691; the fused step
+    // 287 -> 254, 214 -> 192 us); the narrow tiles are pipelined (producer waves +
+    // one consumer wave)
     p.tg = groups >= 32LL * 1024 ? 64 : 16;
     if (const char* e = getenv("FLEET_TILE_G")) p.tg = atoi(e);
     if (p.tg != 8 && p.tg != 16 && p.tg != 32 && p.tg != 64) p.tg = 16;
@@ -2453,23 +2288,6 @@ static void launch_pipe(const UpdatePlan& p, const uint8_t* uploads, size_t pitc
 #undef FLEET_LAUNCH_PIPE
 }
 
-// Client chunks of the stream update: a launch walks at most ~256 clients (the
-// chunks evenly sized), the running sums handed on through the merged output
-// (ClientChunk). A wave of
-// the stream grid walks every client of its groups; over thousands of clients the
-// waves of one round drift apart and each client step of the round touches rows
-// the others left long ago: configs[4]'s column window at N = 4 (349,526 groups,
-// one round of 5.3 waves per SIMD) took 6.4 us per client at M = 1024..4096
-// against 3.4 at M = 256 (scripts/strong_probe.py). FLEET_UPDATE_CHUNK overrides
-// (0 = one launch).
-int update_chunk_clients(int M) {
-  int ch = 0;
-  if (const char* e = getenv("FLEET_UPDATE_CHUNK")) ch = atoi(e);
-  if (ch <= 0 || M <= ch + ch / 2) return 0;
-  const int k = (M + ch - 1) / ch;
-  return (M + k - 1) / k;
-}
-
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
@@ -2503,12 +2321,8 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
       } else {
         const int64_t rem = groups - (int64_t)nA * 256;
         const int64_t nB = (rem + 83) / 84;
-        const int per = update_chunk_clients(M);
-        for (int c0 = 0; c0 < M; c0 += per ? per : M) {
-          const ClientChunk ck{c0, per ? std::min(M, c0 + per) : 0, reinterpret_cast<float*>(merged)};
-          hipLaunchKernelGGL((k_update_mixed<256>), dim3((unsigned)(nA + nB)), dim3(256), 0, s, uploads, pitch, M,
-                             d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, nA, ck);
-        }
+        hipLaunchKernelGGL((k_update_mixed<256>), dim3((unsigned)(nA + nB)), dim3(256), 0, s, uploads, pitch, M,
+                           d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, nA);
       }
 #undef FLEET_LAUNCH_NT
     }
@@ -2731,26 +2545,6 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     if (e != hipSuccess) return e;
     return launch_encode_f32(values, n_up, vpitch, M, enc_out, pitch, s);
   }
-  // FLEET_FUSED_INLINE=1: the encode inside the update's waves (k_update_encode_inline)
-  // on the SIMD-balanced grid -- an experiment, slower than the separate encode blocks
-  // below (synth1m_256: 1167-1177 vs 1134-1136 us per step, three same-box pairs,
-  // scripts/gpu_r03_d2.sh): 79 VGPRs (6 waves per SIMD) and the encode's VALU work
-  // on every update wave's critical path
-  const char* fin = getenv("FLEET_FUSED_INLINE");
-  if (fin && atoi(fin)) {
-    const int64_t nB = (groups - (int64_t)nA * 256 + 83) / 84;
-    const int64_t g0 = std::min<int64_t>(groups, (int64_t)nA * 256);  // first group of the remainder
-    const int64_t rg = groups - g0;
-    const int64_t gxr = blocks_for(rg, 256);
-    const int rpb = std::min(M, 12);
-    const int64_t nE = rg > 0 ? gxr * ((M + rpb - 1) / rpb) : 0;
-    const InlineEnc ie{values, n_up, vpitch, enc_out, pitch};
-    const EncodeJob ej{values + 3 * g0, n_up - 3 * g0, vpitch, enc_out + 16 * g0, pitch, rg, gxr, M, rpb};
-    hipLaunchKernelGGL((k_update_encode_inline<256>), dim3((unsigned)(nA + nB + nE)), dim3(256), 0, s, uploads, pitch,
-                       M, d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nA,
-                       (int)(nA + nB), ie, ej);
-    return hipGetLastError();
-  }
   // the plain stream grid (every update block group-per-lane): the encode's blocks
   // fill the SIMDs the last round of update waves leaves idle, so the value-per-lane
   // balancing of k_update_mixed only adds instructions here (same-box A/B on
@@ -2769,21 +2563,14 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   // 12 rows per block with enc_mt, 1179 / 1170 with enc_d16 (the blocks also copy
   // the 9 KB byte table); synth4m_4096 79.1 ms at 12, 64 or 684. FLEET_FUSED_RPB
   // overrides.
-  // client chunks (update_chunk_clients): launch k aggregates clients [c0, c1) and
-  // encodes rows [c0, c1) of the next batch
-  const int per = update_chunk_clients(M);
-  for (int c0 = 0; c0 < M; c0 += per ? per : M) {
-    const int c1 = per ? std::min(M, c0 + per) : M, rows = c1 - c0;
-    int rpb = std::min(rows, 12);
-    if (const char* e = getenv("FLEET_FUSED_RPB")) rpb = std::max(1, std::min(rows, atoi(e)));
-    const int64_t nE = gx * ((rows + rpb - 1) / rpb);
-    EncodeJob ej{values + (size_t)c0 * vpitch, n_up, vpitch, enc_out + (size_t)c0 * pitch, pitch, groups, gx, rows, rpb};
-    if (const char* e = getenv("FLEET_FUSED_ENC_PRIO")) ej.prio = atoi(e);
-    const ClientChunk ck{c0, per ? c1 : 0, reinterpret_cast<float*>(merged)};
-    hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nAf + nB + nE)), dim3(256), 0, s, uploads, pitch, M,
-                       d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf,
-                       (int)(nAf + nB), ej, ck);
-  }
+  int rpb = std::min(M, 12);
+  if (const char* e = getenv("FLEET_FUSED_RPB")) rpb = std::max(1, std::min(M, atoi(e)));
+  const int64_t nE = gx * ((M + rpb - 1) / rpb);
+  EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+  if (const char* e = getenv("FLEET_FUSED_ENC_PRIO")) ej.prio = atoi(e);
+  hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nAf + nB + nE)), dim3(256), 0, s, uploads, pitch, M,
+                     d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf,
+                     (int)(nAf + nB), ej);
   return hipGetLastError();
 }
 

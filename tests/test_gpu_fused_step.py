@@ -108,12 +108,3 @@ def test_update_encode_inline_tiles(codec, monkeypatch, lay_name, M, n_values):
     assert F.update_encode_kernel(L).endswith(", true, true>")
     test_update_encode_equals_two_calls(codec, lay_name, M, n_values)
 
-
-@pytest.mark.parametrize("lay_name,M,n_values", [("synth1m", 6, None), ("synth1m", 3, 1_000_003),
-                                                  ("synth1m", 2, 150_001)])
-def test_update_encode_inline_equals_two_calls(codec, monkeypatch, lay_name, M, n_values):
-    """The opt-in encode inside the update's waves (FLEET_FUSED_INLINE=1,
-    k_update_encode_inline: group-per-lane blocks encode their groups, the
-    remainder's groups get encode blocks of their own): the same bytes."""
-    monkeypatch.setenv("FLEET_FUSED_INLINE", "1")
-    test_update_encode_equals_two_calls(codec, lay_name, M, n_values)
