@@ -674,6 +674,13 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   }
 }
 
+// s_setprio takes an immediate: the wave's issue priority from a uniform value
+__device__ __forceinline__ void set_wave_prio(int prio) {
+  if (prio == 1) __builtin_amdgcn_s_setprio(1);
+  else if (prio == 2) __builtin_amdgcn_s_setprio(2);
+  else if (prio >= 3) __builtin_amdgcn_s_setprio(3);
+}
+
 // Block `bid` of the SIMD-balanced stream grid (tables already in LDS).
 template <int NT>
 __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D16Table& dtab, int64_t bid,
@@ -820,12 +827,6 @@ struct EncodeJob {
   int prio = 0;  // s_setprio of the encode's waves (experiments: FLEET_FUSED_ENC_PRIO)
 };
 
-// s_setprio takes an immediate: the wave's issue priority from a uniform value
-__device__ __forceinline__ void set_wave_prio(int prio) {
-  if (prio == 1) __builtin_amdgcn_s_setprio(1);
-  else if (prio == 2) __builtin_amdgcn_s_setprio(2);
-  else if (prio >= 3) __builtin_amdgcn_s_setprio(3);
-}
 
 // D16: the tile also holds the byte-table digit counts (D16Table, 9 KB), and the
 // epilogue assembles its merged codes in the tile's p buffer instead of outcodes.
