@@ -53,6 +53,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 # workload name -> (layout, clients M, BASELINE.json config index or note)
+# timed steps of the small extra workloads at least (see main)
+EXTRA_MIN_STEPS = {"mnist64": 200, "cifar10_256": 20}
+
 WORKLOADS = {
     "mnist64": ("mnist", 64, "configs[1]: MNIST cppNN gradient buckets, 64 simulated clients"),
     "cifar10_256": ("cifar10", 256, "configs[2]: CIFAR-10 cppNN gradient buckets, 256 clients"),
@@ -407,7 +410,7 @@ def time_workload(torch, dist, codec, name, steps, warmup, rank, world, graph=Tr
     res = {
         "workload": name, "note": note, "layout": lay_name, "clients": M, "n_up_per_rank": sh.n_local,
         "ms_per_step": ms, "gib_s": gib_s, "update_kernel_ms": upd_ms, "encode_kernel_ms": enc_ms,
-        "graph": graph, "steps_per_graph": G, "eager_ms_per_step": eager_ms, "exchange_ms": exchange_ms,
+        "graph": graph, "steps": steps, "steps_per_graph": G, "eager_ms_per_step": eager_ms, "exchange_ms": exchange_ms,
         "update_kernel": F.update_kernel(sh.L),
         "update_bytes": upd_b, "encode_bytes": enc_b,
         "update_gbs": upd_b / (upd_ms * 1e-3) / 1e9, "encode_gbs": enc_b / (enc_ms * 1e-3) / 1e9,
@@ -792,7 +795,11 @@ def main():
     extras = {}
     if world == 1 and args.extras:
         for w in [x for x in args.extras.split(",") if x and x != args.workload]:
-            extras[w] = time_workload(torch, dist, codec, w, max(4, args.steps // 8 * 2), 2, rank, world, args.graph)
+            # a few steps of the large extras; the small ones get enough steps that the
+            # timed region is not one or two graph launches (mnist64's 17 us step: 4 steps
+            # timed 22 us per step, 200 steps 17 us)
+            n = max(4, args.steps // 8 * 2, EXTRA_MIN_STEPS.get(w, 0))
+            extras[w] = time_workload(torch, dist, codec, w, n, 2, rank, world, args.graph)
 
     strong = None
     if args.strong or not args.no_strong_block:
