@@ -27,6 +27,9 @@ def main():
     base = None
     for N in ns:
         sh = bench.Shard(codec, torch, layout, M, 0, N, strong=True)
+        pm = int(os.environ.get("PROBE_PITCH_MULT", "1"))  # experiments: rows pm times wider than the window
+        if pm > 1:
+            sh.text = torch.zeros((M, sh.pitch * pm), dtype=torch.uint8, device=sh.text.device)  # pitch = pm x window
         v0 = 3 * sh.gb
         hloc = sh.hpos_global[(sh.hpos_global >= v0) & (sh.hpos_global < v0 + sh.n_local)] - v0
         L_loc = F.b64_len(sh.n_local)
@@ -47,7 +50,7 @@ def main():
         codec.check()
         ms = bench.kernel_ms(torch, lambda: (local(0), local(1)), reps=5) / 2
         base = base or ms
-        print(f"{name} M={M} {mode} N={N} groups/rank={sh.groups} kernel={F.update_encode_kernel(L_loc)} {ms * 1e3:.1f} us  "
+        print(f"{name} M={M} pitch x{pm} {mode} N={N} groups/rank={sh.groups} kernel={F.update_encode_kernel(L_loc)} {ms * 1e3:.1f} us  "
               f"speedup {base / ms:.2f} (x{N} ideal)", flush=True)
         del bufs, sh
         torch.cuda.empty_cache()
