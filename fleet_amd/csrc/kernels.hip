@@ -33,6 +33,13 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
+// Dev-only per-wave progress trace of the stream kernels' client loop
+// (scripts/ubench_window.hip defines it); compiled out of the library.
+#ifndef FLEET_CLIENT_HOOK
+#define FLEET_CLIENT_HOOK(c, M) \
+  do {                          \
+  } while (0)
+#endif
 
 // 16-byte store of data no later access in this kernel touches and that is far
 // larger than the caches (the client texts): a non-temporal store
@@ -292,16 +299,43 @@ __device__ __forceinline__ int32_t merged_code(float A, double inv, int32_t last
   return enc(q(r));
 }
 
+// Keep slots: layout header slots and slots past network::flatGrad's walk take the
+// last upload's code in the merged output (mergeFlatGradient, cppNN_backend.cpp:722-750),
+// so their running sums are never read. The chain runs on 0 there (Q(0) = 0): a header
+// value summed over thousands of clients (configs[4]: the bucket size 4,194,304 at
+// position 1) would otherwise leave the codec's fast domain and send its lane through
+// chain_general -- one straggler wave that doubled the configs[4] window kernels
+// (DESIGN.md §5). Bit i of the result = slot p0 + i of the lane is a keep slot.
+template <int S>
+__device__ __forceinline__ uint32_t keep_bits(uint32_t hbits, bool live, int64_t p0, int64_t walk_end) {
+  uint32_t k = hbits;
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+    if (live && p0 + i >= walk_end) k |= 1u << i;
+  return k;
+}
+template <int S>
+__device__ __forceinline__ void keep_zero(float (&y)[S], uint32_t kbits) {
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+    if ((kbits >> i) & 1u) y[i] = 0.0f;
+}
+
 // The exact chain of one value recomputed from global memory with the general
-// codec: the fallback when the serial accumulation leaves the q_lat domain
-// (|A| >= 1e8; never for gradients). Per lane, divergent, slow, exact.
+// codec: the fallback when the serial accumulation leaves the fast domain
+// (|A| >= 1e8 or 1e9; never for gradients). Per lane, divergent, slow, exact; the
+// next client's group is loaded while the current one is computed.
 __device__ __noinline__ float chain_general(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                             const double* __restrict__ dampen, int64_t g, int e,
                                             const B64Tables* tab) {
   float A = 0.f;
+  const uint8_t* row = uploads + 16 * g;
+  uint4 nxt = *reinterpret_cast<const uint4*>(row);
   for (int c = 0; c < M; ++c) {
+    const uint4 cur = nxt;
+    if (c + 1 < M) nxt = *reinterpret_cast<const uint4*>(row + (size_t)(c + 1) * pitch);
     int32_t cc[3];
-    b64_decode_group(*reinterpret_cast<const uint4*>(uploads + (size_t)c * pitch + 16 * g), tab, cc);
+    b64_decode_group(cur, tab, cc);
     const float y = q(dec(cc[e]));
     const float p = q((float)((double)y * dampen[c]));
     A = c == 0 ? p : q(A + p);
@@ -393,6 +427,10 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
   for (int k = 0; k < K; ++k)
     if (live[k]) hbits |= header_bits(hdr, n_hdr, 3 * g[k]) << (3 * k);
   const bool wave_hdr = __ballot(hbits != 0) != 0;
+  uint32_t kbits = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) kbits |= keep_bits<3>((hbits >> (3 * k)) & 7u, live[k], 3 * g[k], walk_end) << (3 * k);
+  const bool wave_keep = __ballot(kbits != 0) != 0;
   int32_t hfirst[S];
   uint32_t layout_bad = 0;
   // Kardam: value slots of the flat gradient (neither header slots nor past the walk)
@@ -448,6 +486,7 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
     // stage A: y = Q(int2float(code))
     float y0[S], y[S];
     dec_stage_d16<S>(y0, codes, &dtab);
+    if (wave_keep) keep_zero<S>(y0, kbits);
     if constexpr (KD) q_stage_d16x<S>(y, y0, &dtab, tab.var);
     else q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
 
@@ -602,6 +641,8 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   const uint32_t need = needed_chars_mask((int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g)));
   const uint32_t hbits = live ? (header_bits(hdr, n_hdr, 3 * g) >> e0) & ((1u << S) - 1u) : 0u;
   const bool wave_hdr = __ballot(hbits != 0) != 0;
+  const uint32_t kbits = keep_bits<S>(hbits, live, 3 * g + e0, walk_end);
+  const bool wave_keep = __ballot(kbits != 0) != 0;
   int32_t hfirst[S], codes[S];
   float acc[S];
   uint32_t dmax = 0;
@@ -627,6 +668,7 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
     }
     float y0[S], y[S], p[S];
     dec_stage_d16<S>(y0, codes, &dtab);
+    if (wave_keep) keep_zero<S>(y0, kbits);
     q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
     dampen_stage<S>(y, dampen[c]);
     q_stage_d16<S>(p, y, &dtab, tab.var, dmax);
@@ -654,12 +696,14 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   Row b0 = group_of(0), b1;
   int c = 0;
   for (; c + 1 < M; c += 2) {
+    FLEET_CLIENT_HOOK(c, M);
     b1 = group_of(c + 1);
     client(c, b0);
     if (c + 2 < M) b0 = group_of(c + 2);
     client(c + 1, b1);
   }
   if (c < M) client(c, b0);
+  FLEET_CLIENT_HOOK(M, M);
   if (__ballot(dmax >= kD16Out) != 0) {  // left the q_gen domain: recompute exactly (never for gradients)
     if (dmax >= kD16Out && live) {
 #pragma unroll
@@ -988,11 +1032,22 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const T
 
 template <int TG, int IPT, int NW, bool KD = false, bool D16 = false>
 __device__ __forceinline__ void tile_compute(TileShared<TG, NW, D16>& sh, const TileItems<TG, IPT>& it, int M,
-                                             const double* __restrict__ dampen, int64_t n_up, int64_t g0,
-                                             float* __restrict__ pdst, uint32_t& badacc,
+                                             const double* __restrict__ dampen, int64_t n_up, int64_t walk_end,
+                                             int64_t g0, float* __restrict__ pdst, uint32_t& badacc,
                                              const TileKd& tk = TileKd{}) {
   constexpr int E = 3 * TG, S = 3 * IPT;
   int32_t codes[S];
+  // keep slots (header slots, slots past the walk) run the chain on 0 (keep_bits)
+  uint32_t kbits = 0;
+  const bool tile_past = 3 * (g0 + TG) > walk_end;  // block-uniform
+#pragma unroll
+  for (int h = 0; h < IPT; ++h) {
+    if (it.live[h]) {
+      uint32_t k = sh.hmask[it.gl[h]];
+      if (tile_past) k = keep_bits<3>(k, true, 3 * (g0 + it.gl[h]), walk_end);
+      kbits |= k << (3 * h);
+    }
+  }
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
     const int r = (int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * (g0 + it.gl[h])));
@@ -1017,13 +1072,11 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW, D16>& sh, const 
   }
   // stage A: y = Q(int2float(code)); D16: the stream kernel's byte-table stages
   float y0[S], y[S];
-  if constexpr (D16) {
-    dec_stage_d16<S>(y0, codes, &sh.dt);
-    q_stage_d16x<S>(y, y0, &sh.dt, sh.tab.var);
-  } else {
-    dec_stage<S>(y0, codes, &sh.tab);
-    q_stage<S>(y, y0, &sh.tab);
-  }
+  if constexpr (D16) dec_stage_d16<S>(y0, codes, &sh.dt);
+  else dec_stage<S>(y0, codes, &sh.tab);
+  if (__ballot(kbits != 0) != 0) keep_zero<S>(y0, kbits);
+  if constexpr (D16) q_stage_d16x<S>(y, y0, &sh.dt, sh.tab.var);
+  else q_stage<S>(y, y0, &sh.tab);
   // stage B: p = Q(f32(f64(y) * d)), per-item client
   float r[S], p[S];
 #pragma unroll
@@ -1054,12 +1107,12 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW, D16>& sh, const 
 
 template <int TG, int IPT, int NW, bool KD = false, bool D16 = false>
 __device__ __forceinline__ void tile_produce(TileShared<TG, NW, D16>& sh, const uint8_t* __restrict__ uploads, size_t pitch,
-                                             int M, const double* __restrict__ dampen, int64_t n_up, int64_t g0,
-                                             int ng, int c_base, int nitems, int it0, int stride,
+                                             int M, const double* __restrict__ dampen, int64_t n_up, int64_t walk_end,
+                                             int64_t g0, int ng, int c_base, int nitems, int it0, int stride,
                                              float* __restrict__ pdst, uint32_t& badacc, const TileKd& tk) {
   TileItems<TG, IPT> it;
   tile_load<TG, IPT>(it, uploads, pitch, g0, ng, c_base, nitems, it0, stride);
-  tile_compute<TG, IPT, NW, KD>(sh, it, M, dampen, n_up, g0, pdst, badacc, tk);
+  tile_compute<TG, IPT, NW, KD>(sh, it, M, dampen, n_up, walk_end, g0, pdst, badacc, tk);
 }
 
 // Final values of the tile (vals[0..E)) -> merged Base64 (+ fp32), layout
@@ -1156,8 +1209,8 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
     const int cm = min(CM, M - c0);
     const int nitems = cm * TG;
     for (int base = 0; base < nitems; base += 512) {
-      tile_produce<TG, 2, 4, KD>(sh, uploads, pitch, M, dampen, n_up, g0, ng, c0, nitems, base + tid, 256, ptile,
-                                 badacc, tk);
+      tile_produce<TG, 2, 4, KD>(sh, uploads, pitch, M, dampen, n_up, hdr_block[2], g0, ng, c0, nitems, base + tid,
+                                 256, ptile, badacc, tk);
       if (base == 0) FLEET_TSTAMP(2);
     }
     // ENC: the chunk's rows of the next batch over this tile's groups (a wave: one
@@ -1422,8 +1475,8 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
         while (__hip_atomic_load(&consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < pass - RING + 1)
           __builtin_amdgcn_s_sleep(1);
       }
-      tile_compute<TG, IPT, NW, KD>(sh, cur, M, dampen, n_up, g0, ptile + (pass % RING) * CPP * E, badacc,
-                                    TileKd{kd, (int64_t)blockIdx.x, (int64_t)gridDim.x, (int64_t)hdr_block[2]});
+      tile_compute<TG, IPT, NW, KD>(sh, cur, M, dampen, n_up, hdr_block[2], g0, ptile + (pass % RING) * CPP * E,
+                                    badacc, TileKd{kd, (int64_t)blockIdx.x, (int64_t)gridDim.x, (int64_t)hdr_block[2]});
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       ++done;
       if (lane == 0) __hip_atomic_store(&prog[w], done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
