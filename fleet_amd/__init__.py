@@ -106,6 +106,9 @@ def lib() -> C.CDLL:
         "fleet_update_kardam_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, C.c_double, vp, vp, vp, sz, vp, vp,
                                              vp, vp, vp]),
         "fleet_update_kernel": (C.c_char_p, [sz]),
+        "fleet_update_encode_kernel": (C.c_char_p, [sz]),
+        "fleet_set_plan": (i32, [C.c_char_p, vp, sz]),
+        "fleet_plan": (C.c_char_p, []),
         "fleet_model_quantize_index": (i32, [vp, vp, vp, i32, vp, vp, vp, vp]),
         "fleet_model_weights_text": (i32, [vp, vp, vp, i32, vp, sz, szp]),
         "fleet_model_read_weights": (i32, [vp, vp, sz, vp, i32, vp]),
@@ -146,7 +149,7 @@ def lib() -> C.CDLL:
         "fleet_sampler_create_from": (i32, [vp, vp, vp, sz, i32, i32, i32, i32, i32, i32, i32, C.POINTER(vp)]),
         "fleet_sampler_destroy": (None, [vp]),
         "fleet_sampler_last_error": (C.c_char_p, [vp]),
-        "fleet_updater_reseed": (None, [i32]),
+        "fleet_updater_reseed": (None, [i32, i32]),
         "fleet_sampler_set_hyper": (i32, [vp, i32, C.c_double, C.c_double]),
         "fleet_sampler_set_teacher": (i32, [vp, vp, sz, vp, sz]),
         "fleet_sampler_minibatch": (i32, [vp, i32, C.c_float, vp, sz, szp]),
@@ -190,24 +193,42 @@ def update_kernel(length: int) -> str:
 
 
 def update_encode_kernel(length: int) -> str:
-    """What fleet_update_encode_device launches: the fused k_update_encode on the
-    stream grid, k_update_tiled_encode on the wide tiles, k_update_pipe with the
-    encode's blocks appended on the pipelined tiles."""
-    k = update_kernel(length)
-    if not os.environ.get("FLEET_FUSED_STEP_OFF"):
-        if k == "k_update_mixed<256>":
-            return "k_update_encode<256>"
-        if k.startswith(("k_update_tiled<64", "k_update_tiled<32")):
-            # k_update_tiled<TG, KD, TG2, D16> -> k_update_tiled_encode<TG, TG2, D16, INL>: one
-            # width unless FLEET_FUSED_TILE_MIX=1; the inline encode (FLEET_FUSED_TILE_INLINE=1,
-            # byte-table tiles only) keeps the update's two-width grid
-            tg, _, tg2, d16 = [a.strip() for a in k[len("k_update_tiled<"):].rstrip(">").split(",")]
-            inl = d16 == "true" and os.environ.get("FLEET_FUSED_TILE_INLINE", "") == "1"
-            mix = inl or os.environ.get("FLEET_FUSED_TILE_MIX", "") == "1"
-            return "k_update_tiled_encode<%s, %s, %s, %s>" % (tg, tg2 if mix else "0", d16, "true" if inl else "false")
-        if k.startswith("k_update_pipe"):
-            return k + " (with the encode's blocks)"
-    return k + " + k_encode_f32"
+    """What fleet_update_encode_device launches for uploads of `length` bytes: the fused
+    k_update_encode on the stream grid, k_update_tiled_encode on the wide tiles,
+    k_update_pipe with the encode's blocks appended on the pipelined tiles."""
+    return lib().fleet_update_encode_kernel(length).decode()
+
+
+def set_plan(spec: str = "") -> None:
+    """Launch-plan overrides (fleet_set_plan; process-wide): "update=auto|stream|tiled|pipe",
+    "grid=auto|plain|lanes", "tile_mix=auto|off", "fused=on|off", "stage_threads=N",
+    "stage_pieces=N", comma-separated; "" restores the measured default. Results are
+    identical under every plan; an invalid spec raises and changes nothing."""
+    err = C.create_string_buffer(256)
+    rc = lib().fleet_set_plan(spec.encode(), err, 256)
+    if rc != FLEET_OK:
+        raise FleetError(rc, err.value.decode())
+
+
+def plan() -> str:
+    """The active launch-plan overrides ("" = the measured default)."""
+    return lib().fleet_plan().decode()
+
+
+class plan_override:
+    """Context manager: `with plan_override("update=tiled"): ...` restores the previous plan."""
+
+    def __init__(self, spec: str):
+        self.spec = spec
+
+    def __enter__(self):
+        self.prev = plan()
+        set_plan(self.spec)
+        return self
+
+    def __exit__(self, *exc):
+        set_plan(self.prev)
+        return False
 
 
 def layout_from_sizes(w_sizes: Sequence[int], b_sizes: Sequence[int]):

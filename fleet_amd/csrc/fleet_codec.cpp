@@ -264,10 +264,10 @@ int finish_text(fleet_ctx* c, size_t out_len, char* out, size_t cap, size_t* out
   return rc;
 }
 
-// Host staging copy threads: FLEET_STAGE_THREADS, else one per ~2 MiB of
-// staging, at most 8 and at most the CPUs this process may run on.
+// Host staging copy threads: the plan's stage_threads (fleet_set_plan), else one per
+// ~2 MiB of staging, at most 8 and at most the CPUs this process may run on.
 int stage_threads(size_t bytes) {
-  if (const char* e = getenv("FLEET_STAGE_THREADS")) return std::max(1, std::min(64, atoi(e)));
+  if (const int t = fleet::plan_overrides().stage_threads) return t;
   int n = 1;
   cpu_set_t set;
   if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
@@ -307,7 +307,7 @@ int stage_uploads(fleet_ctx* c, const char* const* uploads, size_t col0, size_t 
   const size_t total = pitch * (size_t)M;
   int pieces = 3;
   if (total >= (256u << 20)) pieces = (int)std::min<size_t>(16, total / (24u << 20));
-  if (const char* e = getenv("FLEET_STAGE_PIECES")) pieces = std::max(1, atoi(e));
+  if (const int k = fleet::plan_overrides().stage_pieces) pieces = k;
   if (total < (4u << 20)) pieces = 1;
   pieces = std::min(pieces, M);
   for (int k = 0; k < pieces; ++k) {
@@ -1688,7 +1688,28 @@ int fleet_model_version(fleet_ctx* c, const float* weights, const int32_t* dims,
 }
 
 const char* fleet_update_kernel(size_t len) {
-  return fleet::update_kernel_name((int64_t)groups_of(fleet_b64_count(len)));
+  static thread_local std::string name;
+  name = fleet::update_kernel_name((int64_t)groups_of(fleet_b64_count(len)));
+  return name.c_str();
+}
+
+const char* fleet_update_encode_kernel(size_t len) {
+  static thread_local std::string name;
+  name = fleet::update_encode_kernel_name((int64_t)groups_of(fleet_b64_count(len)));
+  return name.c_str();
+}
+
+int fleet_set_plan(const char* spec, char* err, size_t cap) {
+  std::string e;
+  if (fleet::set_plan_overrides(spec, &e) == 0) return FLEET_OK;
+  if (err && cap) std::snprintf(err, cap, "%s", e.c_str());
+  return FLEET_ERR_ARG;
+}
+
+const char* fleet_plan(void) {
+  static thread_local std::string spec;
+  spec = fleet::plan_spec();
+  return spec.c_str();
 }
 
 int fleet_selftest_digest(fleet_ctx* c, int fn, uint64_t* out) {

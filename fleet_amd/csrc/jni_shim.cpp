@@ -24,6 +24,8 @@
 //   the offline sampler (fleet_sampler; dataset, buckets, client rotation, E/sigma/C)
 //     Java_apps_cppNN_CppNNOfflineSampler_initSampler  :385-551
 //     Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch :677-699
+//   plus boolean apps.cppNN.FleetSampler.setTeacherNative(float[] w, float[] b): the
+//   mode-1 teacher's trained weights (below)
 // so no native of libnative.so is reached any more: every global the
 // reference's natives share (the model, E/sigma/C, the libc rand() stream that
 // initSampler and initUpdater reseed) lives behind this one library;
@@ -39,9 +41,16 @@
 // FLEET_DISTILLATION_MODE = the reference's compile-time DISTILLATION_MODE (default 1);
 // FLEET_SAMPLER_IID / FLEET_SAMPLER_OUTLIER / FLEET_SAMPLER_CLIENTS = the
 // reference's source-edited sampler globals iid / outlier / numClients
-// (cppNN_backend.cpp:59-61; defaults 0, 0, 10). DISTILLATION_MODE=1 with iid
-// sampling is refused at initSampler: its mini-batches carry the outputs of a
-// teacher network initSampler trains (:480-546), which is not rebuilt.
+// (cppNN_backend.cpp:59-61; defaults 0, 0, 10). In DISTILLATION_MODE=1 the
+// reference's initSampler, after the buckets and whatever the sampler, parses the
+// MNIST test set (returning early when it is missing, :485) and trains a teacher
+// network (:481-545: 300 rand()-drawn samples through mojo's backward pass). Only
+// iid mini-batches carry the teacher's outputs (uniformSample :593-620); nonIIDSample
+// sends none. The training is not rebuilt here (it is client-side model compute,
+// not the codec path): iid mode-1 mini-batches need the trained weights from the
+// JVM through FleetSampler.setTeacherNative, and until then getMiniBatch fails with
+// that reason. Its rand() draws do not move the sampler's indices: initUpdater
+// reseeds after initSampler.
 //
 // Same argument meaning and results as the reference; failures return null / 0
 // (Java sees a NullPointerException at the caller) and print the C-ABI error
@@ -370,14 +379,21 @@ JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_fetchParamsNative(JNIEnv* en
   g_model = m;
 }
 
-// initUpdater (:161-225): srand(seed) and the two rand() draws of its
-// cnn.train_class (fleet_updater_reseed), E / sigma / C for the sampler's
-// mini-batch headers, and the model part (lrates, the first version).
+// initUpdater (:161-225): srand(seed) and the rand() draws of its
+// cnn.train_class (fleet_updater_reseed: two, for the random shift that
+// fetchParamsNative's set_random_augmentation enables; none before a fetch), E /
+// sigma / C for the sampler's mini-batch headers, and the model part (lrates, the
+// first version).
 JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_initUpdater(JNIEnv* env, jobject, jdoubleArray lrates, jint E,
                                                                 jdouble sigma, jdouble C) {
+  bool fetched;
+  {
+    std::lock_guard<std::mutex> lk(g_model_mu);
+    fetched = g_model != nullptr;
+  }
   {
     std::lock_guard<std::mutex> lk(g_sampler_mu);
-    fleet_updater_reseed(kSeed);
+    fleet_updater_reseed(kSeed, fetched ? 1 : 0);
     g_E = E;
     g_sigma = sigma;
     g_C = C;
@@ -484,8 +500,21 @@ JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_printParamsNative(JNIEnv* en
 
 // ----------------------------------------------------------------- sampler
 
+// the MNIST test set parse_test_data reads (mnist_parser.h:153-161: the two file-name spellings)
+static bool mnist_test_set_present(const std::string& dir) {
+  auto readable = [](const std::string& p) {
+    FILE* f = std::fopen(p.c_str(), "rb");
+    if (f) std::fclose(f);
+    return f != nullptr;
+  };
+  return (readable(dir + "/t10k-images.idx3-ubyte") || readable(dir + "/t10k-images-idx3-ubyte")) &&
+         (readable(dir + "/t10k-labels.idx1-ubyte") || readable(dir + "/t10k-labels-idx1-ubyte"));
+}
+
 // initSampler (:385-551) with the reference's source-edited globals taken from
-// the environment (FLEET_SAMPLER_*); the dataset stays in this library.
+// the environment (FLEET_SAMPLER_*); the dataset stays in this library. The
+// sampler lock is held from the srand(seed) on, so its rand() draws (the bucket
+// shuffles) cannot interleave with another thread's getMiniBatch / initUpdater.
 JNIEXPORT void JNICALL Java_apps_cppNN_CppNNOfflineSampler_initSampler(JNIEnv* env, jobject, jstring prefix) {
   fleet_ctx* c = ctx();
   if (!c || !prefix) return;
@@ -493,25 +522,54 @@ JNIEXPORT void JNICALL Java_apps_cppNN_CppNNOfflineSampler_initSampler(JNIEnv* e
   const int clients = env_int("FLEET_SAMPLER_CLIENTS", 10), mode = distillation_mode();
   std::printf("IID: %d\nOutlier: %d\n", iid, outlier);
   std::fflush(stdout);
-  if (iid && mode) {
-    std::fprintf(stderr,
-                 "[fleet] initSampler: DISTILLATION_MODE=1 with iid sampling is not supported (its mini-batches "
-                 "carry the outputs of the teacher initSampler trains, cppNN_backend.cpp:480-546, not rebuilt)\n");
-    return;
-  }
   const char* path = env->GetStringUTFChars(prefix, nullptr);
   if (!path) return;
   const std::string data_path(path);
   env->ReleaseStringUTFChars(prefix, path);
+  std::lock_guard<std::mutex> lk(g_sampler_mu);
   fleet_sampler* s = nullptr;
   const int rc = fleet_sampler_create(c, data_path.c_str(), iid, outlier, clients, mode, kSeed, &s);
   if (rc != FLEET_OK) return;  // fleet_sampler_create printed the reason
-  std::lock_guard<std::mutex> lk(g_sampler_mu);
   fleet_sampler_set_hyper(s, g_E, g_sigma, g_C);
   if (g_sampler) fleet_sampler_destroy(g_sampler);
-  g_sampler = s;
+  g_sampler = s;  // the buckets exist from here on, as the reference's globals do
+  if (mode) {
+    if (!mnist_test_set_present(data_path)) {  // :485: the early return, after the buckets
+      std::fprintf(stderr, "error: could not parse test data.\n");
+      return;
+    }
+    std::fprintf(stderr,
+                 "[fleet] initSampler: the mode-1 teacher's training (:481-545) is not rebuilt%s\n",
+                 iid ? "; iid mini-batches need its trained weights (FleetSampler.setTeacherNative)" : "");
+  }
   std::printf("Train data size: %zu\n", fleet_sampler_num_samples(s));
   std::fflush(stdout);
+}
+
+// The mode-1 teacher's trained weights (initSampler's network: conv 5x5x8, conv
+// 1x1x16, conv 5x5x48, softmax 10; fleet_teacher_weight_count / _bias_count floats in
+// mojo's layer order), from a JVM that trained or loaded it. iid mini-batches then
+// append its outputs at TEMPERATURE 2 (uniformSample :593-620, k_teacher_forward).
+// False (and the reason on stderr) without a sampler or with the wrong sizes.
+JNIEXPORT jboolean JNICALL Java_apps_cppNN_FleetSampler_setTeacherNative(JNIEnv* env, jobject, jfloatArray w,
+                                                                         jfloatArray b) {
+  if (!w || !b) return JNI_FALSE;
+  const jsize nw = env->GetArrayLength(w), nb = env->GetArrayLength(b);
+  std::vector<float> wv((size_t)std::max<jsize>(nw, 0)), bv((size_t)std::max<jsize>(nb, 0));
+  if (nw > 0) env->GetFloatArrayRegion(w, 0, nw, wv.data());
+  if (nb > 0) env->GetFloatArrayRegion(b, 0, nb, bv.data());
+  std::lock_guard<std::mutex> lk(g_sampler_mu);
+  if (!g_sampler) {
+    std::fprintf(stderr, "[fleet] setTeacherNative: no sampler (initSampler failed or was not called)\n");
+    return JNI_FALSE;
+  }
+  const int rc = fleet_sampler_set_teacher(g_sampler, wv.data(), wv.size(), bv.data(), bv.size());
+  if (rc != FLEET_OK) {
+    std::fprintf(stderr, "[fleet] setTeacherNative failed (%d): %s (expected %zu weights, %zu biases)\n", rc,
+                 fleet_sampler_last_error(g_sampler), fleet_teacher_weight_count(), fleet_teacher_bias_count());
+    return JNI_FALSE;
+  }
+  return JNI_TRUE;
 }
 
 // getMiniBatch (:677-699): batch_size * E samples of the current client, the

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 // device error bits (atomicOr into the context's error word, read back by fleet_check)
 #define FLEET_ERRBIT_BASE64 1
 #define FLEET_ERRBIT_LAYOUT 2
@@ -40,8 +42,25 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
                                 int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
                                 double* norms, hipStream_t s);
-// name of the aggregation kernel launch_update picks for `groups` groups
-const char* update_kernel_name(int64_t groups);
+// Launch-plan overrides: experiments, and the tests that run every launch variant on
+// small inputs. Process-wide; set by fleet_set_plan (spec "key=value,..." -- update=
+// auto|stream|tiled|pipe, grid=auto|plain|lanes, tile_mix=auto|off, fused=on|off,
+// stage_threads=N, stage_pieces=N) or, once at first use, from FLEET_EXPERIMENTS (the
+// same spec). The default (empty spec) is the measured plan.
+struct PlanOverrides {
+  int update = 0;         // 0 auto, 1 stream grid, 2 64-group tiles, 3 16-group pipelined tiles
+  int grid = 0;           // stream grid: 0 auto, 1 a group per lane everywhere, 2 a value per lane everywhere
+  int tile_mix = 0;       // 0 auto (two widths when a partial round of tiles remains), 1 one width
+  int fused = 1;          // 0: the pipelined step as two launches (update, then encode)
+  int stage_threads = 0;  // host staging copy threads (0 auto)
+  int stage_pieces = 0;   // host staging H2D parts (0 auto)
+};
+PlanOverrides plan_overrides();
+int set_plan_overrides(const char* spec, std::string* err);  // 0, or -1 (nothing changed)
+std::string plan_spec();                                     // normalised active spec, "" = default
+// names of the kernels launch_update / launch_update_encode pick for `groups` groups
+std::string update_kernel_name(int64_t groups);
+std::string update_encode_kernel_name(int64_t groups);
 hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                                 int64_t n_up, const int32_t* d_hdr_block, uint8_t* merged, float* merged_f32,
                                 int* d_err, const float* values, size_t vpitch, uint8_t* enc_out, hipStream_t s);

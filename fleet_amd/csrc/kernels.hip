@@ -12,6 +12,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <string>
 #include <type_traits>
 
 #include "codec_device.h"
@@ -613,16 +615,6 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
   }
 }
 
-#ifndef FLEET_TILE_XCD
-#define FLEET_TILE_XCD 1
-#endif
-constexpr bool kTileXcd = FLEET_TILE_XCD != 0;
-
-#ifndef FLEET_STAGEC_VAR
-#define FLEET_STAGEC_VAR 1
-#endif
-constexpr bool kStageCVar = FLEET_STAGEC_VAR != 0;
-
 // One lane's share of the fused update (the non-Kardam stream path): the values
 // [e0, e0 + S) of group g, S = 3 (the whole group) or S = 1 (one value; three
 // lanes of a wave share a group). Returns the lane's merged codes in out[S] and
@@ -679,8 +671,7 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       float sm[S];
 #pragma unroll
       for (int i = 0; i < S; ++i) sm[i] = acc[i] + p[i];
-      if (kStageCVar) q_stage_v16<S>(acc, sm, &dtab, tab.var, dmax);
-      else q_stage_d16<S>(acc, sm, &dtab, tab.var, dmax);
+      q_stage_v16<S>(acc, sm, &dtab, tab.var, dmax);
     }
   };
   auto group_of = [&](int c) {
@@ -716,13 +707,6 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
     const bool keep_last = ((hbits >> i) & 1u) || pos >= walk_end;
     out[i] = (live && pos < n_up) ? merged_code(acc[i], inv_avg, codes[i], keep_last, &tab) : 0;
   }
-}
-
-// s_setprio takes an immediate: the wave's issue priority from a uniform value
-__device__ __forceinline__ void set_wave_prio(int prio) {
-  if (prio == 1) __builtin_amdgcn_s_setprio(1);
-  else if (prio == 2) __builtin_amdgcn_s_setprio(2);
-  else if (prio >= 3) __builtin_amdgcn_s_setprio(3);
 }
 
 // Block `bid` of the SIMD-balanced stream grid (tables already in LDS).
@@ -857,9 +841,7 @@ __device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const 
 }
 
 // A client-encode job riding in an aggregation launch (k_update_encode,
-// k_update_tiled_encode, k_update_pipe): k_encode_f32's grid, flattened x-fastest
-// (the tiles' inline form, k_update_tiled_encode<..., INL>, uses values / n / vpitch /
-// out / pitch only).
+// k_update_tiled_encode, k_update_pipe): k_encode_f32's grid, flattened x-fastest.
 struct EncodeJob {
   const float* values;
   int64_t n;
@@ -868,7 +850,6 @@ struct EncodeJob {
   size_t pitch;
   int64_t groups, gx;
   int rows, rpb;
-  int prio = 0;  // s_setprio of the encode's waves (experiments: FLEET_FUSED_ENC_PRIO)
 };
 
 
@@ -1178,20 +1159,16 @@ template <int TG, bool D16 = false>
 constexpr int tiled_chunk_clients() { return TG > 0 ? (D16 ? FLEET_TILED_PT_D16 : FLEET_TILED_PT) / (3 * TG) : 0; }
 
 // Tile `bid` of k_update_tiled (LDS state in sh / ptile)
-// ENC: the next batch's client encode of the tile's column range rides in the tile
-// (k_update_tiled_encode's inline form): each chunk's phase 1 also encodes the
-// chunk's rows of ej->values into ej->out.
-template <int TG, bool KD = false, bool D16 = false, bool ENC = false>
+template <int TG, bool KD = false, bool D16 = false>
 __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, float* ptile, int64_t bid,
                                                    const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                    const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                                    int64_t g_begin, int64_t g_end,
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
                                                    float* __restrict__ merged_f32, int* __restrict__ err,
-                                                   const TileKd& tk = TileKd{}, const EncodeJob* ej = nullptr) {
+                                                   const TileKd& tk = TileKd{}) {
   constexpr int E = 3 * TG;
   static_assert(E <= 256, "phase 2 is one thread per value");
-  static_assert(!ENC || D16, "the inline encode uses the tile's byte table");
   constexpr int CM = tiled_chunk_clients<TG, D16>();
   static_assert(CM >= 2, "the epilogue's codes go after the E final values in ptile");
   FLEET_TSTAMP(0);
@@ -1212,26 +1189,6 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
       tile_produce<TG, 2, 4, KD>(sh, uploads, pitch, M, dampen, n_up, hdr_block[2], g0, ng, c0, nitems, base + tid,
                                  256, ptile, badacc, tk);
       if (base == 0) FLEET_TSTAMP(2);
-    }
-    // ENC: the chunk's rows of the next batch over this tile's groups (a wave: one
-    // row's 64), at most 2 items per thread (CM * TG <= 512): the values are loaded
-    // here, encoded after phase 2, so the loads fly during the serial phase
-    constexpr int EI = ENC ? 2 : 0;
-    float ex[EI > 0 ? EI : 1][3];
-    if constexpr (ENC) {
-      static_assert(CM * TG <= 512, "two encode items per thread and chunk");
-#pragma unroll
-      for (int h = 0; h < EI; ++h) {
-        const int it = tid + 256 * h, row = c0 + it / TG, gl = it % TG;
-        const int64_t g = g0 + gl;
-        const int r = (int)min<int64_t>(3, ej->n - 3 * g);
-        if (it < nitems && gl < ng) {
-          const float* v = ej->values + (size_t)row * ej->vpitch + 3 * g;
-          ex[h][0] = v[0];
-          ex[h][1] = r > 1 ? v[1] : 0.0f;
-          ex[h][2] = r > 2 ? v[2] : 0.0f;
-        }
-      }
     }
     __syncthreads();
     FLEET_TSTAMP(3);
@@ -1263,16 +1220,6 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
             A = q_mt_d(s, d, sh.tab.mt);
           }
         }
-      }
-    }
-    if constexpr (ENC) {
-#pragma unroll
-      for (int h = 0; h < EI; ++h) {
-        const int it = tid + 256 * h, row = c0 + it / TG, gl = it % TG;
-        const int64_t g = g0 + gl;
-        const int r = (int)min<int64_t>(3, ej->n - 3 * g);
-        if (it < nitems && gl < ng)
-          store_stream16(ej->out + (size_t)row * ej->pitch + 16 * g, encode_group(ex[h], r, &sh.tab, &sh.dt));
       }
     }
     __syncthreads();
@@ -1331,13 +1278,13 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
     if ((int)blockIdx.x >= nW) {  // block-uniform: a narrow tile after the wide rounds
       const int64_t nN = (int64_t)gridDim.x - nW, b = (int64_t)blockIdx.x - nW;
       update_tiled_block<TG2, KD, D16>(reinterpret_cast<TileShared<TG2, 4, D16>&>(sh), ptile,
-                                       kTileXcd ? xcd_tile(b, nN) : b, uploads, pitch, M, dampen, inv_avg, n_up,
+                                       xcd_tile(b, nN), uploads, pitch, M, dampen, inv_avg, n_up,
                                        g_begin + (int64_t)nW * TG, g_end, hdr_block, merged, merged_f32, err, tk);
       return;
     }
   }
   const int64_t nw = TG2 > 0 ? (int64_t)nW : (int64_t)gridDim.x;
-  update_tiled_block<TG, KD, D16>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nw) : blockIdx.x, uploads, pitch, M,
+  update_tiled_block<TG, KD, D16>(sh, ptile, xcd_tile(blockIdx.x, nw), uploads, pitch, M,
                                   dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged, merged_f32, err, tk);
 }
 
@@ -1546,11 +1493,7 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
       for (; k < cm; ++k) {
         const float s = A + pt[k * E + col];
         amax = __builtin_fmaxf(amax, __builtin_fabsf(s));  // s is finite: p and A are Q outputs
-#ifdef FLEET_PIPE_TRIVIAL_CONSUMER  // dev experiment: producer-bound time
-        A = s * 0.5f;
-#else
         A = q_xl(s, xl.x);
-#endif
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&consumed, pass + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1577,17 +1520,6 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
   b64_tables_init(&tab);
   __syncthreads();
   encode_rows<false, 256, true>(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab, nullptr);
-}
-// the same on the byte-table digit counts (experiments: FLEET_ENCODE_D16=1)
-__global__ void __launch_bounds__(256) k_encode_f32_d16(const float* __restrict__ values, int64_t n, size_t vpitch,
-                                                        uint8_t* __restrict__ out, size_t pitch, int64_t groups,
-                                                        int rows, int rpb) {
-  __shared__ B64Tables tab;
-  __shared__ D16Table dtab;
-  b64_tables_init(&tab);
-  d16_table_init(&dtab);
-  __syncthreads();
-  encode_rows<true, 256, true>(values, n, vpitch, out, pitch, groups, rows, rpb, blockIdx.x, blockIdx.y, &tab, &dtab);
 }
 #endif
 
@@ -1616,7 +1548,6 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
     update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                            hdr_block, merged, merged_f32, err, nA);
   } else {
-    set_wave_prio(ej.prio);
     const int64_t e = (int64_t)blockIdx.x - nU;
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                      (int)(e / ej.gx), &tab, &dtab);
@@ -1658,51 +1589,30 @@ extern template __global__ void k_update_encode<256>(const uint8_t* __restrict__
 #ifndef FLEET_STREAM_TU
 
 // The same pairing for the tiled sizes (CIFAR buckets): blocks [0, nU) are
-// k_update_tiled<TG>'s tiles (under two waves per SIMD at these sizes, so most
-// wave slots are free), the rest the client encode's blocks on the tile's B64Tables
-// (VarEntry digit counts: the tile state leaves no room for the byte table).
-// TG2 > 0: the update's tiles on k_update_tiled's two-width grid (blocks [0, nW)
-// wide, [nW, nU) TG2-wide). D16: tiles and encode blocks on the byte-table digit
-// counts (the encode as in k_update_encode: enc_d16). INL (with D16): no encode
-// blocks -- every tile encodes the next batch's rows of its own column range, a
-// chunk's rows in each chunk's phase 1 (nU = the tiles).
-template <int TG, int TG2 = 0, bool D16 = false, bool INL = false>
+// k_update_tiled<TG>'s byte-table tiles on one width (every tile is resident at
+// once there and the encode's blocks fill the CUs the last partial round leaves:
+// the two-width grid measured slower in the fused step), the rest
+// the client encode's blocks on the tile's tables (enc_d16, as in k_update_encode).
+template <int TG>
 __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                              const double* __restrict__ dampen, double inv_avg,
                                                              int64_t n_up, int64_t g_begin, int64_t g_end,
                                                              const int32_t* __restrict__ hdr_block,
                                                              uint8_t* __restrict__ merged,
                                                              float* __restrict__ merged_f32, int* __restrict__ err,
-                                                             int nU, EncodeJob ej, int nW = INT32_MAX) {
-  __shared__ TileShared<TG, 4, D16> sh;
-  __shared__ float ptile[tiled_chunk_clients<TG, D16>() * 3 * TG];
+                                                             int nU, EncodeJob ej) {
+  __shared__ TileShared<TG, 4, true> sh;
+  __shared__ float ptile[tiled_chunk_clients<TG, true>() * 3 * TG];
   if ((int)blockIdx.x < nU) {  // block-uniform
-    if constexpr (TG2 > 0) {
-      if ((int)blockIdx.x >= nW) {
-        const int64_t nN = (int64_t)nU - nW, b = (int64_t)blockIdx.x - nW;
-        update_tiled_block<TG2, false, D16, INL>(reinterpret_cast<TileShared<TG2, 4, D16>&>(sh), ptile,
-                                                 kTileXcd ? xcd_tile(b, nN) : b, uploads, pitch, M, dampen, inv_avg,
-                                                 n_up, g_begin + (int64_t)nW * TG, g_end, hdr_block, merged,
-                                                 merged_f32, err, TileKd{}, &ej);
-        return;
-      }
-    }
-    const int64_t nw = TG2 > 0 ? (int64_t)nW : (int64_t)nU;
-    update_tiled_block<TG, false, D16, INL>(sh, ptile, kTileXcd ? xcd_tile(blockIdx.x, nw) : blockIdx.x, uploads,
-                                            pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged,
-                                            merged_f32, err, TileKd{}, &ej);
+    update_tiled_block<TG, false, true>(sh, ptile, xcd_tile(blockIdx.x, nU), uploads, pitch, M, dampen, inv_avg, n_up,
+                                        g_begin, g_end, hdr_block, merged, merged_f32, err);
   } else {
     b64_tables_init(&sh.tab);
-    if constexpr (D16) d16_table_init(&sh.dt);
+    d16_table_init(&sh.dt);
     __syncthreads();
-    set_wave_prio(ej.prio);
     const int64_t e = (int64_t)blockIdx.x - nU;
-    if constexpr (D16)
-      encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
-                        (int)(e / ej.gx), &sh.tab, &sh.dt);
-    else
-      encode_rows<false>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
-                         (int)(e / ej.gx), &sh.tab, nullptr);
+    encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                      (int)(e / ej.gx), &sh.tab, &sh.dt);
   }
 }
 
@@ -2121,267 +2031,256 @@ hipError_t launch_descent(float* weights, float* fc_bias, const float* grad, con
   return hipGetLastError();
 }
 
-// ---------------------------------------------------------------- launchers
+// ---------------------------------------------------------------- launch plan
+
+// Launch-plan overrides (kernels.h): process-wide, set by fleet_set_plan or, once at
+// first use, from FLEET_EXPERIMENTS (the same spec) -- the only environment read of
+// the launch path. Validated: an unknown key or value rejects the whole spec.
+namespace {
+std::mutex g_plan_mu;
+PlanOverrides g_plan;
+std::string g_plan_spec;  // normalised, "" = the measured default plan
+std::once_flag g_plan_env_once;
+
+bool parse_int(const std::string& v, int lo, int hi, int* out) {
+  if (v.empty() || v.size() > 6 || v.find_first_not_of("0123456789") != std::string::npos) return false;
+  const int x = atoi(v.c_str());
+  if (x < lo || x > hi) return false;
+  *out = x;
+  return true;
+}
+
+int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::string* err) {
+  *o = PlanOverrides{};
+  norm->clear();
+  std::string s = spec ? spec : "";
+  for (char& ch : s)
+    if (ch == ';' || ch == ' ') ch = ',';
+  size_t p = 0;
+  while (p <= s.size()) {
+    size_t q = s.find(',', p);
+    if (q == std::string::npos) q = s.size();
+    const std::string item = s.substr(p, q - p);
+    p = q + 1;
+    if (item.empty()) continue;
+    const size_t eq = item.find('=');
+    if (eq == std::string::npos) {
+      *err = "plan item '" + item + "' is not key=value";
+      return -1;
+    }
+    const std::string k = item.substr(0, eq), v = item.substr(eq + 1);
+    bool ok = true;
+    if (k == "update") {
+      if (v == "auto") o->update = 0;
+      else if (v == "stream") o->update = 1;
+      else if (v == "tiled") o->update = 2;
+      else if (v == "pipe") o->update = 3;
+      else ok = false;
+    } else if (k == "grid") {
+      if (v == "auto") o->grid = 0;
+      else if (v == "plain") o->grid = 1;
+      else if (v == "lanes") o->grid = 2;
+      else ok = false;
+    } else if (k == "tile_mix") {
+      if (v == "auto") o->tile_mix = 0;
+      else if (v == "off") o->tile_mix = 1;
+      else ok = false;
+    } else if (k == "fused") {
+      if (v == "on") o->fused = 1;
+      else if (v == "off") o->fused = 0;
+      else ok = false;
+    } else if (k == "stage_threads") {
+      ok = parse_int(v, 1, 64, &o->stage_threads);
+    } else if (k == "stage_pieces") {
+      ok = parse_int(v, 1, 64, &o->stage_pieces);
+    } else {
+      *err = "unknown plan key '" + k + "' (update, grid, tile_mix, fused, stage_threads, stage_pieces)";
+      return -1;
+    }
+    if (!ok) {
+      *err = "bad value '" + v + "' for plan key '" + k + "'";
+      return -1;
+    }
+    if (!norm->empty()) *norm += ",";
+    *norm += k + "=" + v;
+  }
+  return 0;
+}
+
+void plan_env_init() {
+  std::call_once(g_plan_env_once, [] {
+    const char* e = getenv("FLEET_EXPERIMENTS");
+    if (!e || !*e) return;
+    PlanOverrides o;
+    std::string norm, err;
+    if (parse_plan(e, &o, &norm, &err) != 0) {
+      fprintf(stderr, "[fleet] FLEET_EXPERIMENTS rejected (%s): the default launch plan is used\n", err.c_str());
+      return;
+    }
+    std::lock_guard<std::mutex> lk(g_plan_mu);
+    g_plan = o;
+    g_plan_spec = norm;
+  });
+}
+}  // namespace
+
+PlanOverrides plan_overrides() {
+  plan_env_init();
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  return g_plan;
+}
+
+int set_plan_overrides(const char* spec, std::string* err) {
+  plan_env_init();
+  PlanOverrides o;
+  std::string norm;
+  if (parse_plan(spec, &o, &norm, err) != 0) return -1;
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  g_plan = o;
+  g_plan_spec = norm;
+  return 0;
+}
+
+std::string plan_spec() {
+  plan_env_init();
+  std::lock_guard<std::mutex> lk(g_plan_mu);
+  return g_plan_spec;
+}
 
 static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
-// k_update_mixed's split: the blocks of whole rounds of one-group-per-lane waves
-// (a multiple of one wave per SIMD of the current device), or -1 when the grid is
-// under one round (the plain stream grid then).
+
+// SIMDs of the current device (4 per CU), cached per device (a process may drive
+// several GPUs, one launching thread each; concurrent first calls store the same value)
 static int device_simds() {
-  // per device (a process may drive several GPUs, one launching thread each), set
-  // once per device with an atomic store: concurrent first calls compute the same value
   static std::atomic<int> simds[64];
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+  if (hipGetDevice(&dev) != hipSuccess) {
     (void)hipGetLastError();
-    return 4 * 256;
+    dev = 0;
   }
-  int v = simds[dev].load(std::memory_order_relaxed);
+  const bool cached = dev >= 0 && dev < 64;
+  int v = cached ? simds[dev].load(std::memory_order_relaxed) : 0;
   if (!v) {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) {
       (void)hipGetLastError();
+      fprintf(stderr, "[fleet] no CU count for device %d: planning for 256 CUs\n", dev);
       cus = 256;
     }
     v = 4 * cus;
-    simds[dev].store(v, std::memory_order_relaxed);
+    if (cached) simds[dev].store(v, std::memory_order_relaxed);
   }
   return v;
 }
-static int stream_full_rounds_blocks(int64_t groups) {
-  const int simds = device_simds();
-  const int64_t waves = (groups + 63) / 64;
-  if (waves < simds) return -1;
-  const int64_t full = waves / simds * simds;  // waves in whole rounds
-  return (int)(full * 64 / 256);
-}
-// The two-width split of k_update_tiled's TG-wide grid over `groups` groups: nW
-// wide tiles (whole rounds over the CUs: the same count on every CU) and nN tiles
-// of TG2 groups for the rest; nW = -1 (the one-width grid) when there is no whole
-// round or no partial one. FLEET_TILE_MIX = 0 turns it off, 16 / 32 pick TG2
-// (default 16 for TG = 64; experiments).
+
+// The two-width split of k_update_tiled's 64-group grid over `groups` groups: nW
+// wide tiles (whole rounds over the CUs: the same count on every CU) and nN 16-group
+// tiles for the rest; nW = -1 (one width) when there is no whole round or no partial one.
 struct TileSplit {
-  int nW, tg2;
+  int nW;
   int64_t nN;
 };
-static TileSplit tile_split(int64_t groups, int tg) {
-  TileSplit t{-1, 0, 0};
-  int tg2 = tg == 64 ? 16 : 0;
-  if (const char* e = getenv("FLEET_TILE_MIX")) tg2 = atoi(e);
-  if (tg != 64 || (tg2 != 16 && tg2 != 32)) return t;
+static TileSplit tile_split(int64_t groups, const PlanOverrides& o) {
+  TileSplit t{-1, 0};
+  if (o.tile_mix == 1) return t;
   const int cus = device_simds() / 4;
-  const int64_t tiles = (groups + tg - 1) / tg, rounds = tiles / cus;
+  const int64_t tiles = (groups + 63) / 64, rounds = tiles / cus;
   if (rounds < 1 || tiles % cus == 0) return t;
   t.nW = (int)(rounds * cus);
-  t.tg2 = tg2;
-  t.nN = (groups - (int64_t)t.nW * tg + tg2 - 1) / tg2;
+  t.nN = (groups - (int64_t)t.nW * 64 + 15) / 16;
   return t;
 }
 
-// The wide tiles (TG = 32 / 64) on the byte-table digit counts (FLEET_TILE_D16=0:
-// the VarEntry compare, experiments).
-static bool tile_d16(int tg) {
-  if (tg != 32 && tg != 64) return false;
-  const char* e = getenv("FLEET_TILE_D16");
-  return !(e && atoi(e) == 0);
-}
-
-// k_update_tiled in the variant the plan picked: width tg, the two-width split
-// (tile_split), the byte-table tiles (tile_d16); KD: with Kardam's side outputs.
-// Returns the block count (= Kardam's partial slots per client).
-template <bool KD>
-static unsigned launch_tiled(int tg, int64_t groups, const uint8_t* uploads, size_t pitch, int M,
-                             const double* d_dampen, double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end,
-                             const int32_t* d_hdr_block, uint8_t* merged, float* merged_f32, int* d_err,
-                             const KardamOut& kd, hipStream_t s, bool launch = true) {
-  const TileSplit t = tile_split(groups, tg);
-  const bool d16 = tile_d16(tg);
-  const unsigned blocks = t.nW >= 0 ? (unsigned)(t.nW + t.nN) : (unsigned)((groups + tg - 1) / tg);
-  if (!launch) return blocks;
-  const int nW = t.nW >= 0 ? t.nW : INT32_MAX;
-#define FLEET_TL(TG, TG2, D)                                                                                     \
-  hipLaunchKernelGGL((k_update_tiled<TG, KD, TG2, D>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, \
-                     inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd, nW)
-  if (tg == 64) {
-    if (t.nW >= 0 && t.tg2 == 32) {
-      if (d16) FLEET_TL(64, 32, true);
-      else FLEET_TL(64, 32, false);
-    } else if (t.nW >= 0) {
-      if (d16) FLEET_TL(64, 16, true);
-      else FLEET_TL(64, 16, false);
-    } else {
-      if (d16) FLEET_TL(64, 0, true);
-      else FLEET_TL(64, 0, false);
-    }
-  } else if (tg == 32) {
-    if (d16) FLEET_TL(32, 0, true);
-    else FLEET_TL(32, 0, false);
-  } else if (tg == 16) {
-    FLEET_TL(16, 0, false);
-  } else if constexpr (!KD) {  // Kardam's tile sums need TG >= 16
-    FLEET_TL(8, 0, false);
-  }
-#undef FLEET_TL
-  return blocks;
-}
-
-// the split in use: FLEET_UPDATE_MIXED=0 the plain stream grid (-1), =2 every group
-// one value per lane (0; experiments)
-static int mixed_split(int64_t groups) {
-  if (const char* mx = getenv("FLEET_UPDATE_MIXED")) {
-    if (atoi(mx) == 0) return -1;
-    if (atoi(mx) == 2) return 0;
-  }
-  return stream_full_rounds_blocks(groups);
-}
-
-// groups per lane of the stream kernel: 1 at every size measured -- 1M floats
-// x 256: 1.64 / 1.85 / 2.63 ms for K = 1 / 2 / 4 (before the multiplier-table
-// codec); 4M floats x 4096: 59.2 / 83.5 / 115.7 ms. More lanes in flight beat
-// fewer table copies (a lane walks all M clients, the copy is amortised anyway).
-int update_groups_per_lane(int64_t groups) {
-  (void)groups;
-  if (const char* e = getenv("FLEET_UPDATE_K")) return atoi(e);
-  return 1;
-}
-
-// FLEET_UPDATE_MODE = stream | tiled | auto (default: tiled below ~2 waves per SIMD of stream lanes)
-static bool use_tiled(int64_t groups) {
-  if (const char* e = getenv("FLEET_UPDATE_MODE")) {
-    if (!strcmp(e, "tiled")) return true;
-    if (!strcmp(e, "stream")) return false;
-  }
-  return groups < 256LL * 4 * 2 * 64;
-}
-
-// Kernel choice for a bucket of `groups` 3-value groups (environment
-// overrides for experiments: FLEET_UPDATE_MODE=stream|tiled, FLEET_TILE_G,
-// FLEET_UPDATE_PIPE=0, FLEET_UPDATE_K).
+// The aggregation's launch plan for a bucket (or window) of `groups` 3-value groups.
+//   pipe   -- k_update_pipe<16, 1, 5, 0>: 16-group tiles, 4 producer waves + one
+//             consumer wave (MNIST-size buckets: the serial chain is the critical path);
+//   tiled  -- k_update_tiled<64, ..., TG2 = 16 | 0, D16>: two-phase 64-group tiles on the
+//             byte-table digit counts, two widths when a partial round remains (CIFAR);
+//   stream -- k_update_mixed<256>: a lane walks its group down all M rows (from ~2 waves
+//             per SIMD up), whole rounds group-per-lane and the rest a value per lane.
+// Measured rules: the stream grid from 131,072 groups (2 waves per SIMD),
+// 64-group tiles from 32 k groups (below 4 per CU they still beat 32-group tiles, whose
+// phase 2 has half the serial lanes per tile), the pipelined tiles below.
 struct UpdatePlan {
-  int kind;  // 0 stream k_update<k>, 1 k_update_tiled<tg>, 2 k_update_pipe<tg, ipt, nw, wp>
-  int tg, k, ipt, nw, wp;
+  int kind;       // 0 stream, 1 tiled, 2 pipe
+  int nA;         // stream: blocks of group-per-lane waves (the rest a value per lane)
+  int64_t blocks; // stream / tiled / pipe grid
+  TileSplit t;    // tiled
 };
-static UpdatePlan plan_update(int64_t groups) {
-  // measured best on MNIST-64 (scripts/ubench_tiled.hip, profiles/r01/ubench_tiled.log):
-  // 5 waves (4 producers keep ahead of the q_xl consumer), block-wide passes, 1 item per thread
-  UpdatePlan p{0, 0, 1, 1, 5, 0};
-  if (const char* e = getenv("FLEET_PIPE_WAVEPASS")) p.wp = atoi(e) != 0;
-  if (const char* e = getenv("FLEET_PIPE_IPT")) p.ipt = atoi(e) == 2 ? 2 : 1;
-  if (const char* e = getenv("FLEET_PIPE_WAVES")) p.nw = atoi(e) == 8 ? 8 : atoi(e) == 4 ? 4 : 5;
-  if (p.ipt == 2) p.nw = 4, p.wp = 0;
-  if (p.wp && p.nw == 5) p.nw = 4;
-  if (use_tiled(groups)) {
-    // 64-group tiles down to 2 per CU (32 k groups): below 4 per CU they still beat
-    // the 32-group tiles, whose phase 2 runs 1.5 waves of serial chains per tile
-    // against 3 (synth1m_256's strong-scaling windows, scripts/gpu_r03_d13.sh: update
-    // alone 221 -> 195 us at 58,255 groups, 164 -> 153 us at 43,691; the fused step
-    // 287 -> 254, 214 -> 192 us); the narrow tiles are pipelined (producer waves +
-    // one consumer wave)
-    p.tg = groups >= 32LL * 1024 ? 64 : 16;
-    if (const char* e = getenv("FLEET_TILE_G")) p.tg = atoi(e);
-    if (p.tg != 8 && p.tg != 16 && p.tg != 32 && p.tg != 64) p.tg = 16;
-    const char* pe = getenv("FLEET_UPDATE_PIPE");
-    p.kind = (p.tg <= 16 && !(pe && !strcmp(pe, "0"))) ? 2 : 1;
-    return p;
+static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o) {
+  UpdatePlan p{0, 0, 0, TileSplit{-1, 0}};
+  if (o.update == 1) p.kind = 0;
+  else if (o.update == 2) p.kind = 1;
+  else if (o.update == 3) p.kind = 2;
+  else p.kind = groups >= 256LL * 4 * 2 * 64 ? 0 : groups >= 32LL * 1024 ? 1 : 2;
+  if (p.kind == 2) {
+    p.blocks = (groups + 15) / 16;
+  } else if (p.kind == 1) {
+    p.t = tile_split(groups, o);
+    p.blocks = p.t.nW >= 0 ? p.t.nW + p.t.nN : (groups + 63) / 64;
+  } else {
+    const int64_t plain = (groups + 255) / 256;
+    if (o.grid == 1) {
+      p.nA = (int)plain;
+    } else if (o.grid == 2) {
+      p.nA = 0;
+    } else {  // whole rounds of group-per-lane waves (a multiple of one wave per SIMD)
+      const int simds = device_simds();
+      const int64_t waves = (groups + 63) / 64;
+      p.nA = waves < simds ? (int)plain : (int)(waves / simds * simds * 64 / 256);
+    }
+    p.blocks = p.nA + (groups - (int64_t)p.nA * 256 + 83) / 84;
   }
-  p.k = update_groups_per_lane(groups);
-  p.k = p.k >= 4 ? 4 : p.k == 2 ? 2 : 1;
   return p;
 }
 
-const char* update_kernel_name(int64_t groups) {
-  static thread_local char buf[48];
-  const UpdatePlan p = plan_update(groups);
-  if (p.kind == 0 && p.k == 1 && !getenv("FLEET_UPDATE_NT") && mixed_split(groups) >= 0)
-    snprintf(buf, sizeof buf, "k_update_mixed<256>");
-  else if (p.kind == 0)
-    snprintf(buf, sizeof buf, "k_update<%d, false, 256>", p.k);  // as rocprofv3 names it
-  else if (p.kind == 2)
-    snprintf(buf, sizeof buf, "k_update_pipe<%d, %d, %d, %d>", p.tg, p.ipt, p.nw, p.wp);
-  else {  // as rocprofv3 names it (every template argument)
-    const TileSplit t = tile_split(groups, p.tg);
-    snprintf(buf, sizeof buf, "k_update_tiled<%d, false, %d, %s>", p.tg, t.nW >= 0 ? t.tg2 : 0,
-             tile_d16(p.tg) ? "true" : "false");
-  }
+std::string update_kernel_name(int64_t groups) {
+  const UpdatePlan p = plan_update(groups, plan_overrides());
+  char buf[64];
+  if (p.kind == 0) snprintf(buf, sizeof buf, "k_update_mixed<256>");
+  else if (p.kind == 2) snprintf(buf, sizeof buf, "k_update_pipe<16, 1, 5, 0>");
+  else snprintf(buf, sizeof buf, "k_update_tiled<64, false, %d, true>", p.t.nW >= 0 ? 16 : 0);  // as rocprofv3 names it
   return buf;
 }
 
-// k_update_pipe in the variant the plan picked, with `nE` client-encode blocks
-// after its tiles (nE = 0: none)
-static void launch_pipe(const UpdatePlan& p, const uint8_t* uploads, size_t pitch, int M, const double* d_dampen,
-                        double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
-                        uint8_t* merged, float* merged_f32, int* d_err, int64_t nE, const EncodeJob& ej,
-                        hipStream_t s) {
-  const int64_t groups = g_end - g_begin;
-  const int64_t nU = (groups + p.tg - 1) / p.tg;
-#define FLEET_LAUNCH_PIPE(TG, IPT, NW, WP)                                                                       \
-  hipLaunchKernelGGL((k_update_pipe<TG, IPT, NW, WP>), dim3((unsigned)(nU + nE)), dim3(64 * NW), 0, s, uploads,    \
-                     pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err,       \
-                     nE ? (int)nU : INT32_MAX, ej)
-    if (p.wp) {
-      if (p.nw == 8) {
-        if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 8, 1);
-        else FLEET_LAUNCH_PIPE(16, 1, 8, 1);
-      } else {
-        if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 4, 1);
-        else FLEET_LAUNCH_PIPE(16, 1, 4, 1);
-      }
-    } else if (p.nw == 8) {
-      if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 8, 0);
-      else FLEET_LAUNCH_PIPE(16, 1, 8, 0);
-    } else if (p.ipt == 2) {
-      if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 2, 4, 0);
-      else FLEET_LAUNCH_PIPE(16, 2, 4, 0);
-    } else if (p.nw == 5) {
-      if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 5, 0);
-      else FLEET_LAUNCH_PIPE(16, 1, 5, 0);
-    } else {
-      if (p.tg == 8) FLEET_LAUNCH_PIPE(8, 1, 4, 0);
-      else FLEET_LAUNCH_PIPE(16, 1, 4, 0);
-    }
-#undef FLEET_LAUNCH_PIPE
+std::string update_encode_kernel_name(int64_t groups) {
+  const PlanOverrides o = plan_overrides();
+  const UpdatePlan p = plan_update(groups, o);
+  if (!o.fused) return update_kernel_name(groups) + " + k_encode_f32";
+  if (p.kind == 0) return "k_update_encode<256>";
+  if (p.kind == 1) return "k_update_tiled_encode<64>";
+  return "k_update_pipe<16, 1, 5, 0> (with the encode's blocks)";
+}
+
+// k_update_tiled on the plan's grid; KD: with Kardam's side outputs.
+template <bool KD>
+static void launch_tiled(const UpdatePlan& p, const uint8_t* uploads, size_t pitch, int M, const double* d_dampen,
+                         double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
+                         uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, hipStream_t s) {
+  if (p.t.nW >= 0)
+    hipLaunchKernelGGL((k_update_tiled<64, KD, 16, true>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch,
+                       M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd, p.t.nW);
+  else
+    hipLaunchKernelGGL((k_update_tiled<64, KD, 0, true>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch,
+                       M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd,
+                       INT32_MAX);
 }
 
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
   if (g_end <= g_begin) return hipSuccess;
-  const int64_t groups = g_end - g_begin;
-  const UpdatePlan p = plan_update(groups);
-#define FLEET_LAUNCH(KERNEL, PER_BLOCK)                                                                         \
-  hipLaunchKernelGGL(KERNEL, dim3((unsigned)((groups + (PER_BLOCK)-1) / (PER_BLOCK))), dim3(256), 0, s, uploads, \
-                     pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
-  if (p.kind == 2) {
-    launch_pipe(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, 0,
-                EncodeJob{}, s);
-  } else if (p.kind == 1) {
-    (void)launch_tiled<false>(p.tg, groups, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block,
-                              merged, merged_f32, d_err, KardamOut{}, s);
-  } else {
-    if (p.k == 4) FLEET_LAUNCH(k_update<4>, 256 * 4);
-    else if (p.k == 2) FLEET_LAUNCH(k_update<2>, 256 * 2);
-    else {
-      const char* nt = getenv("FLEET_UPDATE_NT");  // experiments: block size of the stream kernel
-      const int v = nt ? atoi(nt) : 256;
-#define FLEET_LAUNCH_NT(N)                                                                                      \
-  hipLaunchKernelGGL((k_update<1, false, N>), dim3((unsigned)((groups + (N)-1) / (N))), dim3(N), 0, s, uploads, \
-                     pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
-      const int nA = mixed_split(groups);
-      if (nt || nA < 0) {
-        if (v == 64) FLEET_LAUNCH_NT(64);
-        else if (v == 128) FLEET_LAUNCH_NT(128);
-        else if (v == 512) FLEET_LAUNCH_NT(512);
-        else FLEET_LAUNCH_NT(256);
-      } else {
-        const int64_t rem = groups - (int64_t)nA * 256;
-        const int64_t nB = (rem + 83) / 84;
-        hipLaunchKernelGGL((k_update_mixed<256>), dim3((unsigned)(nA + nB)), dim3(256), 0, s, uploads, pitch, M,
-                           d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, nA);
-      }
-#undef FLEET_LAUNCH_NT
-    }
-  }
-#undef FLEET_LAUNCH
+  const UpdatePlan p = plan_update(g_end - g_begin, plan_overrides());
+  if (p.kind == 2)
+    hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0>), dim3((unsigned)p.blocks), dim3(64 * 5), 0, s, uploads, pitch, M,
+                       d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
+                       EncodeJob{});
+  else if (p.kind == 1)
+    launch_tiled<false>(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
+                        d_err, KardamOut{}, s);
+  else
+    hipLaunchKernelGGL((k_update_mixed<256>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
+                       inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.nA);
   return hipGetLastError();
 }
 
@@ -2443,40 +2342,24 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
                                 double* norms, hipStream_t s) {
   const int64_t groups = g_end - g_begin;
-  // the update's own launch plan (plan_update): the stream kernel, the wide tiles or the
-  // pipelined tiles, each with the side outputs; partial slots per client = waves of the
-  // stream grid or the tiles. Launch variants the plan takes only under experiment
-  // overrides fall back to the stream kernel.
-  const UpdatePlan p = plan_update(groups);
-  const bool pipe = p.kind == 2 && p.ipt == 1 && p.nw == 5 && !p.wp && p.tg == 16;
-  // the side outputs double the producers' work: more producer waves per tile
-  // (FLEET_KARDAM_PIPE_NW = 5 keeps the plain update's four)
-  const char* knw = getenv("FLEET_KARDAM_PIPE_NW");
-  const int pnw = knw && atoi(knw) == 5 ? 5 : 8;
-  const bool tiled = p.kind == 1 && (p.tg == 16 || p.tg == 32 || p.tg == 64);
-  const int64_t per = pipe ? p.tg : 256;
-  const unsigned blocks = tiled ? launch_tiled<true>(p.tg, groups, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin,
-                                                     g_end, d_hdr_block, merged, merged_f32, d_err, kd, s, false)
-                                : (unsigned)((groups + per - 1) / per);
-  *n_waves = pipe || tiled ? (int)blocks : (int)blocks * 4;
+  // the update's own launch plan with the side outputs: the pipelined tiles with 7
+  // producer waves (the side outputs double the producers' work), the wide tiles, or
+  // the stream grid group-per-lane; partial slots per client = tiles or stream waves
+  const UpdatePlan p = plan_update(groups, plan_overrides());
+  const unsigned blocks = p.kind == 0 ? blocks_for(groups, 256) : (unsigned)p.blocks;
+  *n_waves = p.kind == 0 ? (int)blocks * 4 : (int)blocks;
   if (groups <= 0) return hipSuccess;
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
-  if (pipe) {
-    if (pnw == 8)
-      hipLaunchKernelGGL((k_update_pipe<16, 1, 8, 0, true>), dim3(blocks), dim3(64 * 8), 0, s, uploads, pitch, M,
-                         d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
-                         EncodeJob{}, kd);
-    else
-      hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0, true>), dim3(blocks), dim3(64 * 5), 0, s, uploads, pitch, M,
-                         d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
-                         EncodeJob{}, kd);
-  } else if (tiled) {
-    (void)launch_tiled<true>(p.tg, groups, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block,
-                             merged, merged_f32, d_err, kd, s);
-  } else {
+  if (p.kind == 2)
+    hipLaunchKernelGGL((k_update_pipe<16, 1, 8, 0, true>), dim3(blocks), dim3(64 * 8), 0, s, uploads, pitch, M,
+                       d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
+                       EncodeJob{}, kd);
+  else if (p.kind == 1)
+    launch_tiled<true>(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
+                       d_err, kd, s);
+  else
     hipLaunchKernelGGL((k_update<1, true>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
                        g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd);
-  }
   if (*n_waves <= 2048)
     hipLaunchKernelGGL(k_kardam_reduce<64>, dim3((unsigned)M), dim3(64), 0, s, kd.partials, (int64_t)*n_waves, norms);
   else
@@ -2485,146 +2368,78 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   return hipGetLastError();
 }
 
-// The standalone client encode's digit counts: the VarEntry compare (enc_mt) by
-// default, the byte table (enc_d16; FLEET_ENCODE_D16=1) for experiments. The
-// encode is HBM-bound on its own, and the byte table's 9 KB copy per block costs
-// more than its VALU saving (same-box A/B on synth1m_256: 460 vs 476 us at 6 rows
-// per block, 468 vs 470 at 12); k_update_encode, where the VALU is the limit,
-// uses the byte table.
-static bool encode_d16() {
-  const char* e = getenv("FLEET_ENCODE_D16");
-  return e && atoi(e) != 0;
-}
-// rows per block of the client encode: about 65,536 blocks in all (a lane walks its
-// group down rpb rows, so the LDS table copy is paid once per rpb rows)
+// rows per block of the standalone client encode: about 65,536 blocks in all (a
+// lane walks its group down rpb rows, so the LDS table copy is paid once per rpb
+// rows). Measured on one box (scripts/gpu_encode_rpb.sh, two rows of loads in
+// flight): synth1m_256 encodes in 478-480 us at 4-8 rows per block, 483 at 16, 501
+// at 2 and 32, 595 at 1; the same access pattern without the codec arithmetic
+// (scripts/ubench_stream.hip, 12 B in / 16 B out per lane) runs 452-486 us.
 static int encode_rows_per_block(int64_t gx, int rows) {
-  int rpb = (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 65535) / 65536));
-  if (const char* e = getenv("FLEET_ENCODE_RPB")) rpb = std::max(1, std::min(rows, atoi(e)));  // experiments
-  return rpb;
+  return (int)std::min<int64_t>(rows, std::max<int64_t>(1, (gx * rows + 65535) / 65536));
 }
 
+// The standalone client encode keeps the VarEntry digit counts: it is HBM-bound, and
+// the byte table's 9 KB copy per block costs it more than the VALU it saves (same-box
+// A/B on synth1m_256: 460 vs 476 us); k_update_encode, where the VALU is the limit,
+// uses the byte table.
 hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int rows, uint8_t* out, size_t pitch,
                              hipStream_t s) {
   int64_t groups = (n + 2) / 3;
   if (groups == 0 || rows == 0) return hipSuccess;
   const int64_t gx = blocks_for(groups, 256);
-  // rows per block: about 65,536 blocks in all (a lane walks its group down
-  // rpb rows, so the LDS table copy is paid once per rpb rows). Measured on
-  // one box (scripts/gpu_encode_rpb.sh, two rows of loads in flight):
-  // synth1m_256 encodes in 478-480 us at 4-8 rows per block, 483 at 16, 501 at
-  // 2 and 32, 595 at 1; the same access pattern without the codec arithmetic
-  // (scripts/ubench_stream.hip, 12 B in / 16 B out per lane) runs 452-486 us.
   const int rpb = encode_rows_per_block(gx, rows);
-  if (encode_d16())
-    hipLaunchKernelGGL(k_encode_f32_d16, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s,
-                       values, n, vpitch, out, pitch, groups, rows, rpb);
-  else
-    hipLaunchKernelGGL(k_encode_f32, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s,
-                       values, n, vpitch, out, pitch, groups, rows, rpb);
+  hipLaunchKernelGGL(k_encode_f32, dim3((unsigned)gx, (unsigned)((rows + rpb - 1) / rpb)), dim3(256), 0, s, values, n,
+                     vpitch, out, pitch, groups, rows, rpb);
   return hipGetLastError();
 }
 
 // The aggregation of `uploads` and the client encode of `values` into `enc_out`
-// (another buffer) in one k_update_encode launch when the update runs on the
-// SIMD-balanced stream grid; otherwise the two kernels back to back.
+// (another buffer) in one launch (the pipelined step): k_update_encode on the stream
+// grid, k_update_tiled_encode on the wide tiles, the pipelined tiles with the encode's
+// blocks after them; plan fused=off runs the two kernels back to back.
 hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                                 int64_t n_up, const int32_t* d_hdr_block, uint8_t* merged, float* merged_f32,
                                 int* d_err, const float* values, size_t vpitch, uint8_t* enc_out, hipStream_t s) {
   const int64_t groups = (n_up + 2) / 3;
-  const UpdatePlan p = plan_update(groups);
-  const int nA = mixed_split(groups);
-  const int64_t gx = blocks_for(groups, 256);
-  if (groups > 0 && p.kind == 1 && (p.tg == 32 || p.tg == 64) && !getenv("FLEET_FUSED_STEP_OFF")) {
-    const int rpb = encode_rows_per_block(gx, M);
-    int64_t nU = (groups + p.tg - 1) / p.tg;
-    const int64_t nE = gx * ((M + rpb - 1) / rpb);
-    EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
-    if (const char* e = getenv("FLEET_FUSED_ENC_PRIO")) ej.prio = atoi(e);
-    // one-width tiles here: the encode's blocks already fill the CUs the last partial
-    // round of tiles leaves idle, and the narrow tiles' extra work then costs step time
-    // (two-width grid, FLEET_FUSED_TILE_MIX=1: cifar10_256 415 -> 441 us, cifar100_1024
-    // 1623 -> 1734 us per step, same box)
-    const char* fm = getenv("FLEET_FUSED_TILE_MIX");
-    const TileSplit t = (fm && atoi(fm) == 1) ? tile_split(groups, p.tg) : TileSplit{-1, 0, 0};
-    if (t.nW >= 0) nU = t.nW + t.nN;
-    const bool d16 = tile_d16(p.tg);
-    // FLEET_FUSED_TILE_INLINE=1: the encode inside the tiles (experiment)
-    const char* fi = getenv("FLEET_FUSED_TILE_INLINE");
-    if (d16 && fi && atoi(fi) == 1) {
-      const TileSplit t2 = tile_split(groups, p.tg);
-      const int64_t nT = t2.nW >= 0 ? t2.nW + t2.nN : nU;
-#define FLEET_LAUNCH_TI(TG, TG2)                                                                                     \
-  hipLaunchKernelGGL((k_update_tiled_encode<TG, TG2, true, true>), dim3((unsigned)nT), dim3(256), 0, s, uploads,    \
-                     pitch, M, d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err,  \
-                     (int)nT, ej, t2.nW)
-      if (p.tg == 64 && t2.nW >= 0 && t2.tg2 == 32) FLEET_LAUNCH_TI(64, 32);
-      else if (p.tg == 64 && t2.nW >= 0) FLEET_LAUNCH_TI(64, 16);
-      else if (p.tg == 64) FLEET_LAUNCH_TI(64, 0);
-      else FLEET_LAUNCH_TI(32, 0);
-#undef FLEET_LAUNCH_TI
-      return hipGetLastError();
-    }
-#define FLEET_LAUNCH_TE(TG, TG2, D)                                                                                 \
-  hipLaunchKernelGGL((k_update_tiled_encode<TG, TG2, D>), dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads,     \
-                     pitch, M, d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, \
-                     (int)nU, ej, t.nW)
-    if (p.tg == 64 && t.nW >= 0 && t.tg2 == 32) {
-      if (d16) FLEET_LAUNCH_TE(64, 32, true);
-      else FLEET_LAUNCH_TE(64, 32, false);
-    } else if (p.tg == 64 && t.nW >= 0) {
-      if (d16) FLEET_LAUNCH_TE(64, 16, true);
-      else FLEET_LAUNCH_TE(64, 16, false);
-    } else if (p.tg == 64) {
-      if (d16) FLEET_LAUNCH_TE(64, 0, true);
-      else FLEET_LAUNCH_TE(64, 0, false);
-    } else {
-      if (d16) FLEET_LAUNCH_TE(32, 0, true);
-      else FLEET_LAUNCH_TE(32, 0, false);
-    }
-#undef FLEET_LAUNCH_TE
-    return hipGetLastError();
-  }
-  if (groups > 0 && p.kind == 2 && !getenv("FLEET_FUSED_STEP_OFF")) {  // small buckets: the pipelined tiles
-    const int nt = 64 * p.nw;
-    const int64_t gxp = (groups + nt - 1) / nt;
-    const int rpb = encode_rows_per_block(gxp, M);
-    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gxp, M, rpb};
-    launch_pipe(p, uploads, pitch, M, d_dampen, inv_avg, n_up, 0, groups, d_hdr_block, merged, merged_f32, d_err,
-                gxp * ((M + rpb - 1) / rpb), ej, s);
-    return hipGetLastError();
-  }
-  if (groups == 0 || p.kind != 0 || p.k != 1 || nA < 0 || getenv("FLEET_UPDATE_NT") || getenv("FLEET_FUSED_STEP_OFF")) {
+  const PlanOverrides o = plan_overrides();
+  const UpdatePlan p = plan_update(groups, o);
+  if (groups == 0 || !o.fused) {
     hipError_t e = launch_update(uploads, pitch, M, d_dampen, inv_avg, n_up, 0, groups, d_hdr_block, merged, merged_f32,
                                  d_err, s);
     if (e != hipSuccess) return e;
     return launch_encode_f32(values, n_up, vpitch, M, enc_out, pitch, s);
   }
-  // the plain stream grid (every update block group-per-lane): the encode's blocks
-  // fill the SIMDs the last round of update waves leaves idle, so the value-per-lane
-  // balancing of k_update_mixed only adds instructions here (same-box A/B on
-  // synth1m_256: 1172.7 vs 1181.3 us, scripts/gpu_fused_ab.sh); FLEET_FUSED_PLAIN=0
-  // restores the balanced grid
-  int nAf = (int)((groups + 255) / 256);
-  int64_t nB = 0;
-  if (const char* e = getenv("FLEET_FUSED_PLAIN"); e && !atoi(e)) {
-    nAf = nA;
-    nB = (groups - (int64_t)nA * 256 + 83) / 84;
+  if (p.kind == 1) {  // the wide tiles on one width, then the encode's blocks
+    const int64_t gx = blocks_for(groups, 256);
+    const int rpb = encode_rows_per_block(gx, M);
+    const int64_t nU = (groups + 63) / 64, nE = gx * ((M + rpb - 1) / rpb);
+    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+    hipLaunchKernelGGL((k_update_tiled_encode<64>), dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, M,
+                       d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)nU, ej);
+    return hipGetLastError();
   }
-  // 12 rows per encode block: short blocks that fill the slots the update's waves
-  // leave (a lane walks its group down the rows with two loads in flight, so a
-  // block of hundreds of rows -- the standalone rule at configs[4] -- is a
-  // latency-bound straggler); same-box A/B on synth1m_256: 1188 / 1177 us at 6 /
-  // 12 rows per block with enc_mt, 1179 / 1170 with enc_d16 (the blocks also copy
-  // the 9 KB byte table); synth4m_4096 79.1 ms at 12, 64 or 684. FLEET_FUSED_RPB
-  // overrides.
-  int rpb = std::min(M, 12);
-  if (const char* e = getenv("FLEET_FUSED_RPB")) rpb = std::max(1, std::min(M, atoi(e)));
+  if (p.kind == 2) {  // small buckets: the pipelined tiles, the encode's 320-lane blocks after them
+    const int64_t gxp = (groups + 319) / 320;
+    const int rpb = encode_rows_per_block(gxp, M);
+    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gxp, M, rpb};
+    hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0>), dim3((unsigned)(p.blocks + gxp * ((M + rpb - 1) / rpb))),
+                       dim3(64 * 5), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block,
+                       merged, merged_f32, d_err, (int)p.blocks, ej);
+    return hipGetLastError();
+  }
+  // the stream grid group-per-lane everywhere: the encode's blocks fill the SIMDs the
+  // last round of update waves leaves idle, so the value-per-lane balancing of
+  // k_update_mixed only adds instructions here (same-box A/B on synth1m_256: 1172.7 vs
+  // 1181.3 us, scripts/gpu_fused_ab.sh). 12 rows per encode block: short blocks that
+  // fill the slots the update's waves leave (a lane walks its group down the rows with
+  // two loads in flight, so a block of hundreds of rows is a latency-bound straggler);
+  // same-box A/B on synth1m_256: 1179 / 1170 us at 6 / 12 rows per block.
+  const int64_t gx = blocks_for(groups, 256);
+  const int nAf = (int)gx, rpb = std::min(M, 12);
   const int64_t nE = gx * ((M + rpb - 1) / rpb);
-  EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
-  if (const char* e = getenv("FLEET_FUSED_ENC_PRIO")) ej.prio = atoi(e);
-  hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nAf + nB + nE)), dim3(256), 0, s, uploads, pitch, M,
-                     d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf,
-                     (int)(nAf + nB), ej);
+  const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+  hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nAf + nE)), dim3(256), 0, s, uploads, pitch, M, d_dampen,
+                     inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf, nAf, ej);
   return hipGetLastError();
 }
 

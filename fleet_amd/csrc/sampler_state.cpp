@@ -9,7 +9,7 @@
 //                           training set (commonLib/cppNN/mnist_parser.h), the
 //                           non-IID buckets
 //   fleet_updater_reseed    initUpdater's srand(seed) (:163) and the rand()
-//                           draws of its one cnn.train_class (:216/:222)
+//                           draws of its one cnn.train_class (:216/:222) after a fetch
 //   fleet_sampler_set_hyper initUpdater's E, sigma, C (:169-171)
 //   fleet_sampler_minibatch getMiniBatch (:677-699) = uniformSample (:553-634)
 //                           / nonIIDSample (:636-675) + Base64::encode
@@ -217,13 +217,16 @@ void fleet_sampler_destroy(fleet_sampler* s) { delete s; }
 
 const char* fleet_sampler_last_error(const fleet_sampler* s) { return s ? s->err.c_str() : "no sampler"; }
 
-void fleet_updater_reseed(int seed) {
+void fleet_updater_reseed(int seed, int fetched) {
   std::srand((unsigned)seed);
   // cnn.train_class(train_images[0], ...) after it: the random shift of
   // set_random_augmentation(1, 1, 0, 0, edge) (fetchParamsNative :293) draws
-  // rand() twice (network.h:1840; no flips, no OpenCV transform, no dropout)
-  (void)std::rand();
-  (void)std::rand();
+  // rand() twice (network.h:1840; no flips, no OpenCV transform, no dropout in
+  // the reference's MNIST network). Without a fetched model use_augmentation is 0.
+  if (fetched) {
+    (void)std::rand();
+    (void)std::rand();
+  }
 }
 
 int fleet_sampler_set_hyper(fleet_sampler* s, int E, double sigma, double C) {

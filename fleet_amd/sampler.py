@@ -186,10 +186,11 @@ class NativeSampler:
             raise FleetError(rc, self._L.fleet_sampler_last_error(self._h).decode())
 
     @staticmethod
-    def reseed_updater(seed: int = 1) -> None:
-        """initUpdater's srand(seed) and its train_class's two rand() draws."""
+    def reseed_updater(seed: int = 1, fetched: bool = True) -> None:
+        """initUpdater's srand(seed) and, after fetchParamsNative (fetched), its
+        train_class's two rand() draws."""
         from . import lib
-        lib().fleet_updater_reseed(seed)
+        lib().fleet_updater_reseed(seed, int(bool(fetched)))
 
     def set_hyper(self, E: int, sigma: float, C: float) -> None:
         self._check(self._L.fleet_sampler_set_hyper(self._h, int(E), float(sigma), float(C)))

@@ -437,8 +437,9 @@ typedef struct fleet_sampler fleet_sampler;
  * a first bucket of the label-0 samples, then 2*(num_clients - outliers) shards
  * shuffled and dealt two per client, every bucket shuffled (std::random_shuffle
  * over rand() % i). iid, outlier and num_clients are the reference's
- * compile-time globals (:59-61; defaults 0, 0, 10). The teacher's training in
- * DISTILLATION_MODE=1 (:480-546) is not rebuilt: fleet_sampler_set_teacher.
+ * compile-time globals (:59-61; defaults 0, 0, 10). The teacher's training that
+ * follows in DISTILLATION_MODE=1 whatever the sampler (:481-545) is not rebuilt:
+ * iid mini-batches take the trained weights from fleet_sampler_set_teacher.
  * ctx may be NULL (host state only; fleet_sampler_minibatch then fails). */
 int fleet_sampler_create(fleet_ctx* ctx, const char* data_path, int iid, int outlier, int num_clients,
                          int distillation_mode, int seed, fleet_sampler** out);
@@ -448,9 +449,12 @@ int fleet_sampler_create_from(fleet_ctx* ctx, const float* images, const int32_t
                               fleet_sampler** out);
 void fleet_sampler_destroy(fleet_sampler* s);
 const char* fleet_sampler_last_error(const fleet_sampler* s);
-/* initUpdater's generator side effects (:163, :216/:222): srand(seed), then the
- * two rand() draws of cnn.train_class's random shift (network.h:1840). */
-void fleet_updater_reseed(int seed);
+/* initUpdater's generator side effects (:163, :216/:222): srand(seed), then, when
+ * a model was fetched (fetched != 0: fetchParamsNative's set_random_augmentation
+ * enabled the random shift, :293), the two rand() draws of cnn.train_class's shift
+ * (network.h:1840). Assumes the reference's MNIST network: no dropout layer (whose
+ * training forward would draw more, layer.h:608-617) and no flips. */
+void fleet_updater_reseed(int seed, int fetched);
 /* initUpdater's E, sigma, C (:169-171), read by every later mini-batch header */
 int fleet_sampler_set_hyper(fleet_sampler* s, int E, double sigma, double C);
 /* DISTILLATION_MODE=1 with iid sampling: the trained teacher's weights
@@ -474,9 +478,25 @@ int fleet_sampler_sorted_index(fleet_sampler* s, int32_t* out, size_t cap, size_
 int fleet_sampler_last_indices(fleet_sampler* s, int32_t* out, size_t cap, size_t* n);
 
 /* Name of the aggregation kernel fleet_update / fleet_update_device launch for
- * an upload of `len` Base64 bytes (or a group window of that many bytes):
- * "k_update<K>", "k_update_tiled<TG>" or "k_update_pipe<TG>" (profiling aid). */
+ * an upload of `len` Base64 bytes (or a group window of that many bytes), as
+ * rocprofv3 names it: "k_update_mixed<256>", "k_update_tiled<64, false, TG2, true>"
+ * or "k_update_pipe<16, 1, 5, 0>"; and what fleet_update_encode_device launches
+ * (profiling aid; thread-local storage, valid until the thread's next call). */
 const char* fleet_update_kernel(size_t len);
+const char* fleet_update_encode_kernel(size_t len);
+
+/* Launch-plan overrides, process-wide (experiments, and tests that run every
+ * launch variant on small inputs; results are identical under every plan). spec =
+ * comma-separated key=value items: update=auto|stream|tiled|pipe, grid=auto|plain|
+ * lanes (the stream grid), tile_mix=auto|off, fused=on|off (the pipelined step as
+ * one launch or two), stage_threads=1..64, stage_pieces=1..64 (host staging); ""
+ * restores the measured default. An unknown key or value rejects the whole spec
+ * (FLEET_ERR_ARG, the reason in err) and leaves the plan unchanged. The environment
+ * variable FLEET_EXPERIMENTS, read once at first use, takes the same spec; no other
+ * environment variable changes a launch. fleet_plan returns the active spec ("" =
+ * default; thread-local storage). */
+int fleet_set_plan(const char* spec, char* err, size_t cap);
+const char* fleet_plan(void);
 
 #ifdef __cplusplus
 }

@@ -30,3 +30,12 @@ def codec():
     import fleet_amd
     fleet_amd.build_if_needed = None
     return fleet_amd.Codec(0)
+
+
+@pytest.fixture
+def plan():
+    """plan("update=tiled,...") sets launch-plan overrides (fleet_set_plan) for the
+    test; the measured default plan is restored afterwards."""
+    import fleet_amd
+    yield fleet_amd.set_plan
+    fleet_amd.set_plan("")

@@ -69,6 +69,11 @@ def new_doubles(values) -> int:
     return fakejvm().fakejvm_new_array(4, a.ctypes.data, len(a))
 
 
+def new_floats(values) -> int:
+    a = np.ascontiguousarray(values, np.float32)
+    return fakejvm().fakejvm_new_array(3, a.ctypes.data, len(a))
+
+
 def new_object_array(ptrs) -> int:
     arr = (C.c_void_p * len(ptrs))(*ptrs)
     return fakejvm().fakejvm_new_object_array(arr, len(ptrs))

@@ -61,3 +61,23 @@ def test_null_context_rejected():
     assert L.fleet_update_device(None, None, 0, 0, 0, None, None, 0, 0, 0, None, None, None) == F.FLEET_ERR_ARG
     assert L.fleet_update_encode_device(None, None, 0, 0, 0, None, None, 0, None, None, None, 0, None,
                                         None) == F.FLEET_ERR_ARG
+
+
+def test_plan_overrides_validated_on_host():
+    """fleet_set_plan is host-only: a spec with an unknown key or value is rejected
+    as a whole (the plan stays as it was), a valid one is normalised, "" restores
+    the default. No environment variable other than FLEET_EXPERIMENTS (read once)
+    reaches the launch path (kernels.hip reads no other)."""
+    import os
+    F.set_plan("")
+    for bad in ("update=fast", "k_update=stream", "grid", "stage_pieces=0", "fused=1", "update=stream,tile_mix=no"):
+        with pytest.raises(F.FleetError):
+            F.set_plan(bad)
+        assert F.plan() == ""
+    F.set_plan(" update=pipe ;fused=off,stage_threads=3")
+    assert F.plan() == "update=pipe,fused=off,stage_threads=3"
+    F.set_plan("")
+    assert F.plan() == ""
+    src = open(os.path.join(F.ROOT, "fleet_amd", "csrc", "kernels.hip")).read()
+    assert src.count("getenv(") == 1 and 'getenv("FLEET_EXPERIMENTS")' in src
+    assert "getenv(" not in open(os.path.join(F.ROOT, "fleet_amd", "csrc", "fleet_codec.cpp")).read()

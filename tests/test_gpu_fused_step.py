@@ -89,22 +89,29 @@ def test_update_encode_rejects_overlap_and_bad_text(codec):
         codec.check()
 
 
-def test_update_encode_two_width_tiles(codec, monkeypatch):
-    """The fused tile step on the two-width grid (FLEET_FUSED_TILE_MIX=1, an
-    experiment: wide tiles, narrow tiles, then the encode's blocks)."""
-    monkeypatch.setenv("FLEET_FUSED_TILE_MIX", "1")
-    assert F.update_encode_kernel(F.b64_len(LAYOUTS["cifar10"].n_up)) == "k_update_tiled_encode<64, 16, true, false>"
+@pytest.mark.parametrize("spec,kernel", [("fused=off", " + k_encode_f32"), ("update=tiled", "k_update_tiled_encode<64>"),
+                                         ("update=pipe", "(with the encode's blocks)"),
+                                         ("update=stream", "k_update_encode<256>")])
+def test_update_encode_under_plans(codec, plan, spec, kernel):
+    """The pipelined step on each launch plan, forced on sizes the planner gives
+    another kernel (fused=off: the two launches back to back)."""
+    plan(spec)
+    assert F.update_encode_kernel(F.b64_len(LAYOUTS["cifar10"].n_up)).endswith(kernel)
     test_update_encode_equals_two_calls(codec, "cifar10", 3, None)
+    test_update_encode_equals_two_calls(codec, "synth1m", 2, 150_001)
 
 
-@pytest.mark.parametrize("lay_name,M,n_values", [("cifar10", 5, None), ("cifar100", 3, None), ("synth1m", 4, 150_001),
-                                                  ("synth1m", 9, 250_001)])
-def test_update_encode_inline_tiles(codec, monkeypatch, lay_name, M, n_values):
-    """The encode inside the tiles (FLEET_FUSED_TILE_INLINE=1): every tile encodes
-    the next batch's rows of its own column range; ragged groups, both tile
-    widths of the two-width grid, chunks of 8 rows with M not a multiple of 8."""
-    monkeypatch.setenv("FLEET_FUSED_TILE_INLINE", "1")
-    L = F.b64_len(LAYOUTS[lay_name].n_up if n_values is None else n_values)
-    assert F.update_encode_kernel(L).endswith(", true, true>")
-    test_update_encode_equals_two_calls(codec, lay_name, M, n_values)
-
+def test_plan_overrides_are_validated():
+    """fleet_set_plan rejects an unknown key or value as a whole and leaves the plan
+    unchanged; the default is the empty spec."""
+    F.set_plan("")
+    assert F.plan() == ""
+    for bad in ("update=fast", "k_update=stream", "grid", "stage_threads=0", "stage_threads=65", "fused=1",
+                "update=stream,tile_mix=maybe"):
+        with pytest.raises(F.FleetError):
+            F.set_plan(bad)
+        assert F.plan() == ""
+    with F.plan_override("update=tiled; grid=plain"):
+        assert F.plan() == "update=tiled,grid=plain"
+        assert F.update_kernel(F.b64_len(LAYOUTS["mnist"].n_up)).startswith("k_update_tiled<64")
+    assert F.plan() == ""

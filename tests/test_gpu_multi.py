@@ -75,10 +75,9 @@ def test_update_multi_errors(contexts, oracle):
 
 
 @pytest.mark.parametrize("threads,pieces", [("4", "5"), ("3", "1"), ("8", "16")])
-def test_update_threaded_staging(contexts, oracle, monkeypatch, threads, pieces):
+def test_update_threaded_staging(contexts, oracle, plan, threads, pieces):
     # the host-buffer path's parallel staging copy (large batches) on a small batch
-    monkeypatch.setenv("FLEET_STAGE_THREADS", threads)
-    monkeypatch.setenv("FLEET_STAGE_PIECES", pieces)
+    plan(f"stage_threads={threads},stage_pieces={pieces}")
     ups = uploads_for(oracle, CIFAR10, 7, seed=9)
     d = [1.0 / ((c % 3) + 1) for c in range(7)]
     hm = oracle.header_mask(list(CIFAR10.w_sizes), list(CIFAR10.b_sizes))

@@ -315,36 +315,26 @@ def test_device_codec_exhaustive_digest(codec, fn):
     assert f"{codec.selftest_digest(fn):016x}" == ref[f"fn{SAME_DIGEST.get(fn, fn)}"]
 
 
-@pytest.mark.parametrize("K", [1, 2, 4])
-def test_update_groups_per_lane_variants(codec, oracle, monkeypatch, K):
-    """k_update<K> (K groups per lane, chosen by problem size) on ragged sizes."""
-    monkeypatch.setenv("FLEET_UPDATE_K", str(K))
+@pytest.mark.parametrize("grid", ["auto", "plain", "lanes"])
+def test_update_stream_grids(codec, oracle, plan, grid):
+    """The stream kernel's grids (a group per lane, a value per lane, and the
+    balanced mix the planner picks from one round of waves up) on ragged sizes."""
+    plan(f"update=stream,grid={grid}")
     for lay, M in ((synthetic(300001), 3), (synthetic(20000), 7), (MNIST, 5)):
-        ups = uploads_for(oracle, lay, M, seed=21 + K)
+        ups = uploads_for(oracle, lay, M, seed=21)
         d = policy("exp", M)
         hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
         assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
-@pytest.mark.parametrize("env", [{"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "8"},
-                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16"},
-                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "8", "FLEET_UPDATE_PIPE": "0"},
-                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_UPDATE_PIPE": "0"},
-                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_PIPE_IPT": "2"},
-                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_PIPE_WAVES": "8"},
-                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_PIPE_WAVES": "4"},
-                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "16", "FLEET_PIPE_WAVEPASS": "1"},
-                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "32"},
-                                 {"FLEET_UPDATE_MODE": "tiled", "FLEET_TILE_G": "64"},
-                                 {"FLEET_UPDATE_MODE": "stream", "FLEET_UPDATE_K": "1"},
-                                 {"FLEET_UPDATE_MODE": "stream", "FLEET_UPDATE_K": "4"}])
-def test_update_large_magnitudes_slow_path(codec, oracle, monkeypatch, env):
+@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile_mix=off", "update=stream",
+                                  "update=stream,grid=plain", "update=stream,grid=lanes"])
+def test_update_large_magnitudes_slow_path(codec, oracle, plan, spec):
     """Values far outside the fast path (|x| >= 1, digits != 0, >= 2^31) force
     every compaction pass and the tiled kernel's general-chain fallback (the
     accumulator leaves the q_lat domain); dampening > 1 (class-aware policy) too.
     Ragged tiles (4000 values = 1334 groups) for every tile width."""
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
+    plan(spec)
     rng = np.random.default_rng(8)
     lay = synthetic(4000)
     M = 6
@@ -361,18 +351,13 @@ def test_update_large_magnitudes_slow_path(codec, oracle, monkeypatch, env):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm) == oracle.update_faithful(ups, d)
 
 
-@pytest.mark.parametrize("d16", ["1", "0"])
-@pytest.mark.parametrize("mix", ["16", "32", "0"])
-def test_update_two_width_tiles(codec, oracle, monkeypatch, mix, d16):
+@pytest.mark.parametrize("mix", ["auto", "off"])
+def test_update_two_width_tiles(codec, oracle, plan, mix):
     """k_update_tiled's two-width grid (whole rounds of 64-group tiles, the rest in
-    16- or 32-group tiles; FLEET_TILE_MIX=0 the one-width grid): 16,668 groups =
-    one round of 256 wide tiles + 284 groups, the last narrow tile ragged; large
-    magnitudes force the in-stage fallbacks and the general-chain recompute in
-    both tile widths."""
-    monkeypatch.setenv("FLEET_UPDATE_MODE", "tiled")
-    monkeypatch.setenv("FLEET_TILE_G", "64")
-    monkeypatch.setenv("FLEET_TILE_MIX", mix)
-    monkeypatch.setenv("FLEET_TILE_D16", d16)
+    16-group tiles; tile_mix=off the one-width grid): 16,668 groups = one round of
+    256 wide tiles + 284 groups, the last narrow tile ragged; large magnitudes force
+    the in-stage fallbacks and the general-chain recompute in both tile widths."""
+    plan(f"update=tiled,tile_mix={mix}")
     lay = synthetic(50_003)
     hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
     rng = np.random.default_rng(11)
@@ -385,30 +370,18 @@ def test_update_two_width_tiles(codec, oracle, monkeypatch, mix, d16):
         v[-5:-1] = [9.99e8, -9.99e8, 2.1e9, 0.999999]
         ups.append(oracle.encode_floats(v))
     d = [1.0, 7.5, 0.25, 10.0, 1 / 3, 1.0]
-    want = "k_update_tiled<64, false, %s, %s>" % (mix, "true" if d16 == "1" else "false")
+    want = "k_update_tiled<64, false, %s, true>" % ("16" if mix == "auto" else "0")
     assert F.update_kernel(len(ups[0])) == want
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
-@pytest.mark.parametrize("mode", ["tiled", "tiled-nopipe", "tiled-wide", "tiled-ipt2", "tiled-8waves",
-                                  "tiled-4waves", "tiled-wavepass", "stream"])
-def test_update_modes(codec, oracle, monkeypatch, mode):
+@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile_mix=off", "update=stream",
+                                  "update=stream,grid=plain", "update=stream,grid=lanes"])
+def test_update_modes(codec, oracle, plan, spec):
     """Every aggregation kernel (pipelined and two-phase tiles for small
     buckets, streaming for large ones) on ragged tiles, client counts that wrap
     the LDS ring / chunk several times, and every layout."""
-    monkeypatch.setenv("FLEET_UPDATE_MODE", mode.split("-")[0])
-    if mode == "tiled-nopipe":
-        monkeypatch.setenv("FLEET_UPDATE_PIPE", "0")
-    if mode == "tiled-wide":
-        monkeypatch.setenv("FLEET_TILE_G", "64")
-    if mode == "tiled-ipt2":
-        monkeypatch.setenv("FLEET_PIPE_IPT", "2")
-    if mode == "tiled-8waves":
-        monkeypatch.setenv("FLEET_PIPE_WAVES", "8")
-    if mode == "tiled-4waves":
-        monkeypatch.setenv("FLEET_PIPE_WAVES", "4")
-    if mode == "tiled-wavepass":
-        monkeypatch.setenv("FLEET_PIPE_WAVEPASS", "1")
+    plan(spec)
     for lay, M in ((MNIST, 70), (synthetic(1000), 1), (synthetic(3001), 129), (synthetic(5002), 2),
                    (synthetic(700), 300), (CIFAR10, 3)):
         ups = uploads_for(oracle, lay, M, seed=M)
@@ -656,16 +629,15 @@ def test_model_version_matches_reference_fixture(codec):
     assert np.array_equal(b.view(np.uint32), f["b_out"].view(np.uint32))
 
 
-@pytest.mark.parametrize("mixed", ["1", "0", "2"])
-def test_stream_update_mixed_grid(codec, oracle, monkeypatch, mixed):
+@pytest.mark.parametrize("grid", ["auto", "plain", "lanes"])
+def test_stream_update_mixed_grid(codec, oracle, plan, grid):
     """The stream kernel's SIMD-balanced grid (k_update_mixed: whole rounds of
     group-per-lane waves, the remaining groups one value per lane) against the
     oracle and against the plain grid: a ragged size whose remainder groups and
     last partial group fall in the value-per-lane blocks, with values outside the
     q_gen domain (1e9, -1e8, inf, NaN, 3e38) and power-of-ten boundaries
     planted in both parts, under the two dampening kinds (binary32-exact and not)."""
-    monkeypatch.setenv("FLEET_UPDATE_MODE", "stream")
-    monkeypatch.setenv("FLEET_UPDATE_MIXED", mixed)
+    plan(f"update=stream,grid={grid}")
     lay = synthetic(3 * 70000 + 2)  # 70,001 groups: one round of 65,536 + 4,465 in value-per-lane blocks
     M = 4
     n = lay.n_up
@@ -688,17 +660,15 @@ def test_stream_update_mixed_grid(codec, oracle, monkeypatch, mixed):
         assert np.array_equal(f32.view(np.uint32), oracle.decode_floats(exp).view(np.uint32))
 
 
-@pytest.mark.parametrize("mode,mixed", [("stream", "1"), ("stream", "0"), ("tiled", "1")])
-def test_update_dampen_kinds(codec, oracle, monkeypatch, mode, mixed):
+@pytest.mark.parametrize("spec", ["update=stream", "update=stream,grid=plain", "update=tiled"])
+def test_update_dampen_kinds(codec, oracle, plan, spec):
     """The dampen step takes one binary32 multiply when d is a binary32 normal
     value (tested on d's bits with scalar instructions where d is wave-uniform:
     the stream kernels, 64-group tiles) and the reference's f64 product
     otherwise: both kinds and their edges (+-0, binary32 subnormal and extreme
     binary32 values, values just off binary32, products that overflow) against
     the oracle, in both parts of the balanced grid and in the tiled kernel."""
-    monkeypatch.setenv("FLEET_UPDATE_MODE", mode)
-    monkeypatch.setenv("FLEET_UPDATE_MIXED", mixed)
-    monkeypatch.setenv("FLEET_TILE_G", "64")
+    plan(spec)
     f32 = lambda x: float(np.float32(x))  # noqa: E731
     d = [1.0, 0.0, -0.0, -0.5, 2.0 ** -126, 2.0 ** -149, 2.0 ** 127, f32(3.4028235e38), 1 / 3, 1e-300, 0.1,
          f32(0.1), 3.0, -7.25, f32(0.1) * (1 + 2.0 ** -40), 2.0 ** -127]
@@ -708,14 +678,13 @@ def test_update_dampen_kinds(codec, oracle, monkeypatch, mode, mixed):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
-def test_value_per_lane_decode_checks_every_char(codec, oracle, monkeypatch):
+def test_value_per_lane_decode_checks_every_char(codec, oracle, plan):
     """Lanes that own one value of a group decode only the two quads holding its
-    bytes (FLEET_UPDATE_MIXED=2: every group one value per lane): a char outside
+    bytes (grid=lanes: every group one value per lane): a char outside
     the alphabet at any of a full group's 16 positions, or at a needed position
     of the last partial group, is still reported; the partial group's '='
     padding is not."""
-    monkeypatch.setenv("FLEET_UPDATE_MODE", "stream")
-    monkeypatch.setenv("FLEET_UPDATE_MIXED", "2")
+    plan("update=stream,grid=lanes")
     lay = synthetic(3 * 200 + 2)
     M = 3
     ups = uploads_for(oracle, lay, M, seed=23)
@@ -739,13 +708,13 @@ def test_value_per_lane_decode_checks_every_char(codec, oracle, monkeypatch):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
-def test_window_update_on_mixed_grid(codec, oracle, monkeypatch):
+def test_window_update_on_mixed_grid(codec, oracle, plan):
     """Element windows (the N-GPU shards of fleet_update_multi / torch.distributed)
     through the SIMD-balanced stream grid: each window's merged slice equals the
     same bytes of the whole update."""
     torch = pytest.importorskip("torch")
     from fleet_amd.shard import byte_range, group_range
-    monkeypatch.setenv("FLEET_UPDATE_MODE", "stream")
+    plan("update=stream")
     lay = synthetic(3 * 150001 + 1)
     M = 3
     ups = uploads_for(oracle, lay, M, seed=41)

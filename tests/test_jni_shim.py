@@ -28,7 +28,8 @@ SYMBOLS = list(BYTES_OUT) + ["Java_utils_ByteVec_getNorm", UPDATER + "fetchParam
                              UPDATER + "getLrate", UPDATER + "getNumLabels", UPDATER + "hasOutlier",
                              UPDATER + "printParamsNative", SAMPLER + "initSampler", SAMPLER + "getMiniBatch",
                              "Java_apps_cppNN_FleetUpdater_registerDirectNative",
-                             "Java_apps_cppNN_FleetUpdater_unregisterDirectNative"]
+                             "Java_apps_cppNN_FleetUpdater_unregisterDirectNative",
+                             "Java_apps_cppNN_FleetSampler_setTeacherNative"]
 
 
 def load():
@@ -54,6 +55,7 @@ def load():
         UPDATER + "getNumLabels": [vp, vp], UPDATER + "hasOutlier": [vp, vp], UPDATER + "printParamsNative": [vp, vp, vp],
         SAMPLER + "initSampler": [vp, vp, vp], SAMPLER + "getMiniBatch": [vp, vp, i32],
         "Java_apps_cppNN_FleetUpdater_unregisterDirectNative": [vp, vp, vp],
+        "Java_apps_cppNN_FleetSampler_setTeacherNative": [vp, vp, vp, vp],
     }
     for s, a in sig.items():
         getattr(L, s).argtypes = a
@@ -61,6 +63,7 @@ def load():
     L.Java_apps_cppNN_CppNNUpdater_getLrate.restype = f64
     L.Java_apps_cppNN_FleetUpdater_registerDirectNative.restype = C.c_uint8
     L.Java_apps_cppNN_CppNNUpdater_hasOutlier.restype = C.c_uint8
+    L.Java_apps_cppNN_FleetSampler_setTeacherNative.restype = C.c_uint8
     L.Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch.restype = vp
     L.Java_apps_cppNN_FleetUpdater_unregisterDirectNative.restype = None
     L.Java_apps_cppNN_CppNNUpdater_printParamsNative.restype = None

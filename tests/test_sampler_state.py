@@ -182,8 +182,20 @@ def test_shim_server_session_sampler_and_updater(tmp_path, oracle, monkeypatch):
         bytes(s["newest_text2"])
 
 
+def _write_test_set(path, n=10):
+    """The MNIST test files parse_test_data reads (mnist_parser.h:153-161)."""
+    with open(os.path.join(path, "t10k-images.idx3-ubyte"), "wb") as f:
+        f.write(np.array([2051, n, 28, 28], ">i4").tobytes() + bytes(784 * n))
+    with open(os.path.join(path, "t10k-labels.idx1-ubyte"), "wb") as f:
+        f.write(np.array([2049, n], ">i4").tobytes() + bytes(n))
+
+
 @pytest.mark.gpu
-def test_shim_refuses_iid_with_distillation_and_empty_batches(tmp_path, monkeypatch, capfd):
+def test_shim_mode1_test_set_and_empty_batches(tmp_path, monkeypatch, capfd):
+    """DISTILLATION_MODE=1 initSampler without the MNIST test set: the reference
+    returns after building the buckets (cppNN_backend.cpp:485), so the non-IID
+    sampler still serves and "Train data size" is not printed; getMiniBatch with
+    batch * E = 0 is refused instead of reading sample 0 of an empty batch."""
     import jnifake as J
     from test_jni_shim import load
     L = load()
@@ -191,18 +203,90 @@ def test_shim_refuses_iid_with_distillation_and_empty_batches(tmp_path, monkeypa
     pix, labels = _dataset(100, 3)
     d = str(tmp_path / "m")
     _write_mnist(d, pix, labels)
-    monkeypatch.setenv("FLEET_SAMPLER_IID", "1")
+    monkeypatch.setenv("FLEET_SAMPLER_IID", "0")
+    monkeypatch.setenv("FLEET_SAMPLER_CLIENTS", "2")
     monkeypatch.setenv("FLEET_DISTILLATION_MODE", "1")
     J.begin()
     L.Java_apps_cppNN_CppNNOfflineSampler_initSampler(env, None, J.new_string(d))
-    assert "DISTILLATION_MODE=1 with iid sampling is not supported" in capfd.readouterr().err
-    monkeypatch.setenv("FLEET_SAMPLER_IID", "0")
-    monkeypatch.setenv("FLEET_SAMPLER_CLIENTS", "2")
-    L.Java_apps_cppNN_CppNNOfflineSampler_initSampler(env, None, J.new_string(d))
+    out = capfd.readouterr()
+    assert "error: could not parse test data." in out.err and "Train data size" not in out.out
     L.Java_apps_cppNN_CppNNUpdater_initUpdater(env, None, J.new_doubles([0.1]), 0, 0.0, 0.0)  # E = 0
     J.begin()
     assert L.Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch(env, None, 4) is None  # batch*E = 0: no read of sample 0
     assert "batch_size * E = 0" in capfd.readouterr().err
+    L.Java_apps_cppNN_CppNNUpdater_initUpdater(env, None, J.new_doubles([0.1]), 1, 0.0, 0.0)
+    J.begin()
+    assert L.Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch(env, None, 4)  # the buckets serve
+    _write_test_set(d)
+    L.Java_apps_cppNN_CppNNOfflineSampler_initSampler(env, None, J.new_string(d))
+    assert "Train data size: 100" in capfd.readouterr().out
+
+
+@pytest.mark.gpu
+def test_shim_iid_mode1_session_with_teacher(tmp_path, oracle, monkeypatch, capfd):
+    """iid sampling in DISTILLATION_MODE=1 through the JNI table, in the server's call
+    order: initSampler (test set present; the teacher's training is not rebuilt) ->
+    fetchParamsNative -> initUpdater -> getMiniBatch refused until the JVM hands over
+    the trained teacher (FleetSampler.setTeacherNative) -> getMiniBatch x2: indices =
+    rand() % N after srand(1) and initUpdater's two train_class draws, teacher outputs
+    = the teacher's forward pass, the 1234567 sentinel (uniformSample :553-634)."""
+    import jnifake as J
+    import pyoracle
+    from test_jni_shim import check_rules, load
+    L = load()
+    env = J.env()
+    n, E, batch = 300, 2, 3
+    pix, labels = _dataset(n, 19)
+    d = str(tmp_path / "iid")
+    _write_mnist(d, pix, labels)
+    _write_test_set(d)
+    images = _pixels(pix)
+    monkeypatch.setenv("FLEET_SAMPLER_IID", "1")
+    monkeypatch.setenv("FLEET_DISTILLATION_MODE", "1")
+    s = np.load(os.path.join(HERE, "golden", "session_mnist.npz"))
+    lrates = np.asarray(s["lrates"], np.float64)
+    J.begin()
+    L.Java_apps_cppNN_CppNNOfflineSampler_initSampler(env, None, J.new_string(d))
+    assert "Train data size: 300" in capfd.readouterr().out
+    L.Java_apps_cppNN_CppNNUpdater_fetchParamsNative(env, None, J.new_bytes(bytes(s["init"])))
+    L.Java_apps_cppNN_CppNNUpdater_initUpdater(env, None, J.new_doubles(lrates), E, 0.5, 2.0)
+    J.begin()
+    assert L.Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch(env, None, batch) is None
+    assert "trained teacher" in capfd.readouterr().err
+    z = np.load(os.path.join(HERE, "golden", "teacher_mnist.npz"))
+    w, b = z["w0"], z["b0"]
+    J.begin()
+    assert L.Java_apps_cppNN_FleetSampler_setTeacherNative(env, None, J.new_floats(w[:-1]), J.new_floats(b)) == 0
+    assert L.Java_apps_cppNN_FleetSampler_setTeacherNative(env, None, J.new_floats(w), J.new_floats(b)) == 1
+    check_rules(J)
+    # the generator: initUpdater's srand(1) + two draws, then B = batch * E draws per request
+    lc = _libc()
+    lc.srand(1)
+    lc.rand(), lc.rand()
+    B = batch * E
+    hdr = np.array([E, 0.5, 2.0, np.float32(lrates[0]), B, 784, 10], np.float64).astype(np.float32)
+    for _ in range(2):
+        want = [lc.rand() % n for _ in range(B)]
+        J.begin()
+        text = J.read_bytes(L.Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch(env, None, batch))
+        check_rules(J)
+        teacher = oracle.teacher_forward(w, b, images[want])
+        assert text == oracle.encode_floats(pyoracle.minibatch_vector(images, labels, want, hdr, teacher))
+
+
+def test_reseed_without_a_fetched_model_draws_nothing():
+    """initUpdater before any fetchParamsNative: the reference's train_class draws its
+    random shift only with use_augmentation > 0, which the fetch sets."""
+    lc = _libc()
+    NativeSampler.reseed_updater(1, fetched=False)
+    got = lc.rand()
+    lc.srand(1)
+    assert got == lc.rand()
+    NativeSampler.reseed_updater(1, fetched=True)
+    got = lc.rand()
+    lc.srand(1)
+    lc.rand(), lc.rand()
+    assert got == lc.rand()
 
 
 def _libc():
