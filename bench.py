@@ -87,9 +87,10 @@ class Shard:
     """One rank's device-resident slice of a workload.
 
     weak (default): a full-size bucket slice per rank.
-    strong: the rank's column window [gb, ge) of the ONE fixed problem; the
-    window's values are synthesised in place (same value mix), and the update
-    runs in window mode with the fixed problem's whole-upload coordinates."""
+    strong: the rank's column window [gb, ge) of the ONE fixed problem, synthesised
+    in place as that problem's columns (the same seed on every rank, the global
+    element index as the generator's counter, the header slots that fall inside),
+    so the N windows together hold exactly the N = 1 problem's uploads."""
 
     def __init__(self, codec, torch, layout, M, rank, world, seed=1, strong=False):
         import fleet_amd as F
@@ -125,7 +126,8 @@ class Shard:
         self.merged = torch.zeros((self.pitch,), dtype=torch.uint8, device=dev)
         self.merged_f32 = torch.empty((self.vpitch,), dtype=torch.float32, device=dev)
         if self.n_local:
-            codec.synth_device(seed + rank * 1000003, self.values, self.n_local, syn_pos, syn_val)
+            codec.synth_device(seed, self.values, self.n_local, syn_pos, syn_val,
+                               elem0=3 * self.gb if strong else 0)
         self.dampen = np.asarray(dampen_policy(M), dtype=np.float64)
         torch.cuda.synchronize()
 
@@ -342,6 +344,15 @@ def strong_pipelined(torch, dist, codec, name, steps, warmup, rank, world):
     kl = (steps - 1) % 2
     if world > 1 and not torch.equal(outs[kl][rank * 16 * wmax: rank * 16 * wmax + nb], srcs[kl][:nb]):
         raise RuntimeError("all_gather returned a different merged slice")
+    # rank 0's merged text of the whole problem: every rank's slice, trimmed to its width
+    gathered = None
+    if rank == 0:
+        parts = []
+        for r in range(world):
+            a, b = group_range(G, world, r)
+            base = r * 16 * wmax if world > 1 else 0
+            parts.append((outs[kl] if world > 1 else srcs[kl])[base: base + 16 * (b - a)])
+        gathered = torch.cat(parts).cpu().numpy()
     kern_ms = kernel_ms(torch, lambda: (local(0), local(1)), reps=5) / 2
     res = {"workload": name, "note": note, "clients": M, "n_up_total": layout.n_up, "n_up_per_rank": sh.n_local,
            "groups_per_rank_max": wmax, "ms_per_step": elapsed / steps * 1e3,
@@ -350,6 +361,81 @@ def strong_pipelined(torch, dist, codec, name, steps, warmup, rank, world):
            "step": "pipelined launch on the rank's column window + all_gather of the merged slices (inside; "
                    + ("issued async, overlapping the next step's launch)" if overlap else "in line)")}
     del graphs, bufs, sh, srcs, outs
+    torch.cuda.empty_cache()
+    res["gathered"] = gathered  # popped by main (rank 0: the parity check)
+    return res
+
+
+def full_width_merged(torch, codec, name):
+    """The fixed problem of `name` aggregated at full width on ONE GPU -- the N = 1
+    problem (the same synthetic uploads, one fleet_update_device over every group):
+    its merged Base64 bytes [16 * groups], the reference the N-rank text is held to."""
+    from fleet_amd.layouts import LAYOUTS
+    lay_name, M, _ = WORKLOADS[name]
+    sh = Shard(codec, torch, LAYOUTS[lay_name], M, 0, 1)
+    sh.encode()
+    sh.aggregate()
+    torch.cuda.synchronize()
+    codec.check()
+    out = sh.merged.cpu().numpy().copy()
+    del sh
+    torch.cuda.empty_cache()
+    return out
+
+
+def approx_client_sharded(torch, dist, codec, name, steps, warmup, rank, world, exact):
+    """SURVEY.md §8e's opt-in approximate mode timed on the same problem: rank r holds
+    the full-width uploads of its block of clients (group_range over clients), runs the
+    exact chain on them (fleet_update_device, averaged by its own M_r), one float64
+    all_reduce (RCCL) sums the weighted partials, and every rank encodes the sum
+    (fleet_amd.shard.ClientShardedUpdater.device_step). Rank 0 reports deviation() of
+    its text from the exact text (`exact`: the full-width merged bytes); at N = 1 the
+    mode is the exact chain itself."""
+    import fleet_amd as F
+    from fleet_amd.layouts import LAYOUTS
+    from fleet_amd.shard import ClientShardedUpdater, deviation
+    lay_name, M, _ = WORKLOADS[name]
+    layout = LAYOUTS[lay_name]
+    cb, ce = group_range(M, world, rank)
+    Mr = ce - cb
+    n = layout.n_up
+    groups = (n + 2) // 3
+    L = F.b64_len(n)
+    hpos = np.asarray(layout.header_positions(), dtype=np.int32)
+    hval = np.asarray(layout.header_values(), dtype=np.float32)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    values = torch.empty((Mr, 3 * groups), dtype=torch.float32, device=dev)
+    text = torch.zeros((Mr, 16 * groups), dtype=torch.uint8, device=dev)
+    codec.synth_device(1, values, n, hpos, hval, client0=cb)
+    codec.encode_device(values, n, text)
+    del values
+    merged = torch.zeros(16 * groups, dtype=torch.uint8, device=dev)
+    f32 = torch.zeros(3 * groups, dtype=torch.float32, device=dev)
+    out = torch.zeros(16 * groups, dtype=torch.uint8, device=dev)
+    vals = torch.zeros((1, 3 * groups), dtype=torch.float32, device=dev)
+    cs = ClientShardedUpdater(codec, approx=True)
+    d = dampen_policy(M)[cb:ce]
+
+    def step():
+        cs.device_step(text, L, d, hpos, M, cb, merged, f32, out, vals)
+
+    for _ in range(max(1, warmup)):
+        step()
+    torch.cuda.synchronize()
+    codec.check()
+    el = run_timed(torch, dist, world, step, steps) / steps
+    codec.check()
+    res = {"workload": name, "clients": M, "clients_per_rank": [e - b for b, e in
+                                                                 (group_range(M, world, r) for r in range(world))],
+           "ms_per_step": el * 1e3, "gib_s": M * n * 4 / el / 2**30,
+           "step": "rank's block of clients through the exact chain (full width) + float64 all_reduce of the "
+                   "weighted partial averages + encode of the sum; NOT the reference's bytes"}
+    if rank == 0 and exact is not None:
+        got = out.cpu().numpy()[:L].tobytes()
+        want = bytes(exact[:L])
+        res["deviation"] = deviation(codec.decode_floats(got), codec.decode_floats(want))
+        res["equals_exact_bytes"] = got == want
+    del text, merged, f32, out, vals
     torch.cuda.empty_cache()
     return res
 
@@ -456,6 +542,10 @@ def strong_device(torch, dist, codec, name, steps, warmup, rank, world):
     if world > 1 and not torch.equal(out[rank * 16 * wmax: rank * 16 * wmax + 16 * sh.groups],
                                      sh.merged[: 16 * sh.groups]):
         raise RuntimeError("all_gather returned a different merged slice")
+    gathered = None
+    if rank == 0 and world > 1:
+        gathered = torch.cat([out[r * 16 * wmax: r * 16 * wmax + 16 * (b - a)]
+                              for r, (a, b) in enumerate(group_range(G, world, q) for q in range(world))]).cpu().numpy()
     fp32 = M * layout.n_up * 4
     res = {"workload": name, "note": note, "clients": M, "n_up_total": layout.n_up,
            "groups_per_rank_max": wmax,
@@ -463,6 +553,10 @@ def strong_device(torch, dist, codec, name, steps, warmup, rank, world):
            "gather_outside": {"ms_per_step": outside * 1e3, "gib_s": fp32 / outside / 2**30}}
     del sh, src, out
     torch.cuda.empty_cache()
+    if gathered is not None:  # rank 0: the N windows' text against the 1-GPU full-width text
+        res["parity"] = bool(np.array_equal(gathered, full_width_merged(torch, codec, name)))
+    if world > 1:
+        dist.barrier()
     return res
 
 
@@ -783,8 +877,21 @@ def main():
 
     main_res = time_workload(torch, dist, codec, args.workload, args.steps, args.warmup, rank, world, args.graph)
     strong_value = None
+    exact = None  # rank 0: the N = 1 problem's merged bytes (full width, one GPU)
     if world > 1 and args.graph:
         strong_value = strong_pipelined(torch, dist, codec, args.workload, args.steps, args.warmup, rank, world)
+        gathered = strong_value.pop("gathered")
+        if rank == 0:
+            exact = full_width_merged(torch, codec, args.workload)
+            strong_value["parity"] = bool(gathered is not None and np.array_equal(gathered, exact))
+            strong_value["parity_check"] = ("rank 0's gathered merged text (every rank's slice) == the full-width "
+                                            "1-GPU update of the same problem, byte for byte")
+            if not strong_value["parity"]:
+                print("bench.py: the N-rank merged text differs from the 1-GPU text of the same problem",
+                      file=sys.stderr)
+    elif rank == 0:
+        exact = full_width_merged(torch, codec, args.workload)
+    approx = approx_client_sharded(torch, dist, codec, args.workload, max(3, args.steps // 4), 1, rank, world, exact)
     # the host-buffer paths before the extras: after the 150 GiB synth4m_4096 extra the
     # process's small pinned-host copies run 2-3x slower (measured on MNIST-64: 0.81 vs
     # 0.30 ms), an allocator-state effect that is not the path's
@@ -899,6 +1006,9 @@ def main():
         "strong": strong,
         "weak": weak,
         "strong_value": strong_value,
+        "parity": None if strong_value is None else {"n_rank_equals_1_gpu": strong_value["parity"],
+                                                     "check": strong_value["parity_check"]},
+        "approx": approx,
         "extra": extras,
         # the extras in the headline's own form (the pipelined step), beside their sequential step
         "extra_steps": {w: {"pipelined_ms": (x["pipelined"] or {}).get("ms_per_step"),

@@ -115,6 +115,7 @@ def lib() -> C.CDLL:
         "fleet_encode_device": (i32, [vp, vp, sz, sz, i32, vp, sz, vp]),
         "fleet_decode_device": (i32, [vp, vp, sz, sz, i32, vp, sz, vp]),
         "fleet_synth_device": (i32, [vp, C.c_uint64, i32, i32, vp, vp, i32, sz, vp, sz, vp]),
+        "fleet_synth_window_device": (i32, [vp, C.c_uint64, i32, i32, sz, vp, vp, i32, sz, vp, sz, vp]),
         "fleet_selftest_digest": (i32, [vp, i32, C.POINTER(C.c_uint64)]),
         "fleet_descent_device": (i32, [vp, vp, vp, vp, vp, vp, i32, vp, vp, i32, C.c_float, vp]),
         "fleet_descent": (i32, [vp, vp, sz, vp, sz, vp, sz, vp, vp, i32, vp, vp, i32, C.c_float]),
@@ -505,12 +506,14 @@ class Codec:
         self._check(rc)
 
     def synth_device(self, seed: int, values_f32, n_up: int, header_pos, header_val, client0: int = 0,
-                     stream=None):
+                     stream=None, elem0: int = 0):
+        """Synthetic buckets (fleet_synth_window_device): rows client0.. of a problem whose
+        elements elem0 .. elem0 + n_up this tensor holds; header_pos in its coordinates."""
         M, vpitch = values_f32.shape
         hp = np.ascontiguousarray(header_pos, dtype=np.int32)
         hv = np.ascontiguousarray(header_val, dtype=np.float32)
-        rc = self._L.fleet_synth_device(self._h, seed, M, client0, hp.ctypes.data, hv.ctypes.data, len(hp), n_up,
-                                        values_f32.data_ptr(), vpitch, _stream(stream))
+        rc = self._L.fleet_synth_window_device(self._h, seed, M, client0, elem0, hp.ctypes.data, hv.ctypes.data,
+                                               len(hp), n_up, values_f32.data_ptr(), vpitch, _stream(stream))
         self._check(rc)
 
     def selftest_digest(self, fn: int) -> int:

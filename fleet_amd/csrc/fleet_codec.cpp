@@ -1099,6 +1099,13 @@ int fleet_decode_device(fleet_ctx* c, const void* d_text, size_t len, size_t pit
 int fleet_synth_device(fleet_ctx* c, uint64_t seed, int M, int client0, const int32_t* header_pos,
                        const float* header_val, int n_headers, size_t n_up, void* d_values, size_t vpitch,
                        void* stream) {
+  return fleet_synth_window_device(c, seed, M, client0, 0, header_pos, header_val, n_headers, n_up, d_values, vpitch,
+                                   stream);
+}
+
+int fleet_synth_window_device(fleet_ctx* c, uint64_t seed, int M, int client0, size_t elem0,
+                              const int32_t* header_pos, const float* header_val, int n_headers, size_t n_up,
+                              void* d_values, size_t vpitch, void* stream) {
   if (!c || !d_values || M <= 0 || n_headers < 0 || n_headers > FLEET_MAX_HEADERS || vpitch < n_up)
     return FLEET_ERR_ARG;
   std::lock_guard<std::mutex> lk(c->mu);
@@ -1112,8 +1119,8 @@ int fleet_synth_device(fleet_ctx* c, uint64_t seed, int M, int client0, const in
     HIP_TRY(c, hipMemcpy(d_pos, header_pos, sizeof(int32_t) * (size_t)n_headers, hipMemcpyHostToDevice));
     HIP_TRY(c, hipMemcpy(d_val, header_val, sizeof(float) * (size_t)n_headers, hipMemcpyHostToDevice));
   }
-  HIP_TRY(c, fleet::launch_synth(seed, client0, M, (int64_t)n_up, (float*)d_values, vpitch, d_pos, d_val, n_headers,
-                                 s));
+  HIP_TRY(c, fleet::launch_synth(seed, client0, (int64_t)elem0, M, (int64_t)n_up, (float*)d_values, vpitch, d_pos,
+                                 d_val, n_headers, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   if (d_pos) (void)hipFree(d_pos);
   if (d_val) (void)hipFree(d_val);

@@ -94,7 +94,7 @@ hipError_t launch_flat(const uint8_t* up, const int32_t* d_hdr, int n_hdr, int64
 hipError_t launch_merge(const uint8_t* up, const uint8_t* flat, const int32_t* d_hdr, int n_hdr, int64_t walk_end,
                         int64_t n_up, uint8_t* out, int* d_err, hipStream_t s);
 hipError_t launch_layout_parse(const uint8_t* up, int64_t n, int cap, int32_t* out, hipStream_t s);
-hipError_t launch_synth(uint64_t seed, int client0, int rows, int64_t n_up, float* out, size_t vpitch,
+hipError_t launch_synth(uint64_t seed, int client0, int64_t elem0, int rows, int64_t n_up, float* out, size_t vpitch,
                         const int32_t* d_hpos, const float* d_hval, int n_hdr, hipStream_t s);
 hipError_t launch_digest(int fn, unsigned long long* out, hipStream_t s);
 }  // namespace fleet

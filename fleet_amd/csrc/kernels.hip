@@ -1970,12 +1970,13 @@ __global__ void k_layout_parse(const uint8_t* __restrict__ up, int64_t n, int ca
 }
 
 // synthetic buckets + layout header values
-__global__ void __launch_bounds__(256) k_synth(uint64_t seed, int client0, int64_t n_up, float* __restrict__ out,
-                                               size_t vpitch, const int32_t* __restrict__ hpos,
-                                               const float* __restrict__ hval, int n_hdr) {
+// elem0: the first element of a column window of a larger problem (its values are
+// that problem's columns: the counter is the global element index)
+__global__ void __launch_bounds__(256) k_synth(uint64_t seed, int client0, int64_t elem0, int64_t n_up,
+                                               float* __restrict__ out, size_t vpitch) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int c = blockIdx.y;
-  if (i < n_up) out[(size_t)c * vpitch + i] = synth_value(seed, (uint32_t)(client0 + c), (uint32_t)i);
+  if (i < n_up) out[(size_t)c * vpitch + i] = synth_value(seed, (uint32_t)(client0 + c), (uint32_t)(elem0 + i));
 }
 
 __global__ void k_synth_headers(float* __restrict__ out, size_t vpitch, const int32_t* __restrict__ hpos,
@@ -2513,11 +2514,11 @@ hipError_t launch_layout_parse(const uint8_t* up, int64_t n, int cap, int32_t* o
   return hipGetLastError();
 }
 
-hipError_t launch_synth(uint64_t seed, int client0, int rows, int64_t n_up, float* out, size_t vpitch,
+hipError_t launch_synth(uint64_t seed, int client0, int64_t elem0, int rows, int64_t n_up, float* out, size_t vpitch,
                         const int32_t* d_hpos, const float* d_hval, int n_hdr, hipStream_t s) {
   if (rows == 0 || n_up == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_synth, dim3(blocks_for(n_up, 256), rows), dim3(256), 0, s, seed, client0, n_up, out, vpitch,
-                     d_hpos, d_hval, n_hdr);
+  hipLaunchKernelGGL(k_synth, dim3(blocks_for(n_up, 256), rows), dim3(256), 0, s, seed, client0, elem0, n_up, out,
+                     vpitch);
   if (n_hdr > 0)
     hipLaunchKernelGGL(k_synth_headers, dim3(blocks_for(n_hdr, 256), rows), dim3(256), 0, s, out, vpitch, d_hpos,
                        d_hval, n_hdr);

@@ -153,7 +153,52 @@ class ClientShardedUpdater(ShardedUpdater):
     re-quantising after every add (CppNNUpdater.java:490-493); here each rank's
     block is summed that way and the blocks are added in float64 at the end, then
     quantised once. Use `deviation(approx, exact)` to report the difference; the
-    exact, byte-identical default is ShardedUpdater (element sharding)."""
+    exact, byte-identical default is ShardedUpdater (element sharding). Construct
+    with approx=True to accept that: without it update() raises, so the mode is
+    never mistaken for the exact path."""
+
+    def __init__(self, codec, group=None, device=None, approx: bool = False):
+        super().__init__(codec, group, device)
+        self.approx = bool(approx)
+
+    def _require_approx(self):
+        if not self.approx:
+            raise ValueError("ClientShardedUpdater is not the reference's bytes: construct it with approx=True "
+                             "(the exact sharded update is ShardedUpdater)")
+
+    def device_step(self, text_rows, length: int, dampen_block, header_pos, M: int, cb: int, merged, merged_f32,
+                    out_text, values_buf=None):
+        """The same step on device-resident uploads: text_rows [M_r, pitch] holds picked
+        uploads [cb, cb + M_r) of M (rows of the full-width texts); dampen_block their
+        factors. The rank's exact chain (fleet_update_device, averaged by M_r), the
+        float64 all_reduce of its weighted partial (header slots: the last upload's
+        values from the rank holding client M-1) and the encode of the float32 sum into
+        out_text [>= 16 * groups] (fleet_encode_device). One rank: the exact chain's
+        merged text itself. Returns nothing; every rank's out_text holds the result."""
+        import torch
+        import torch.distributed as dist
+        self._require_approx()
+        Mr = int(text_rows.shape[0])
+        n = b64_count(length)
+        if Mr:  # a rank without clients (M < world) still joins the all_reduce
+            self.codec.update_device(text_rows, length, dampen_block, header_pos, merged, merged_f32)
+        if self.world == 1:
+            out_text[: merged.numel()].copy_(merged)
+            return
+        last = Mr > 0 and cb + Mr == M
+        part = merged_f32[:n].double() if Mr else torch.zeros(n, dtype=torch.float64, device=merged_f32.device)
+        keep = getattr(self, "_keep", None)
+        if keep is None or keep.numel() != n:
+            keep = torch.zeros(n, dtype=torch.bool, device=part.device)
+            if len(header_pos):
+                keep[torch.as_tensor(np.asarray(header_pos), dtype=torch.long, device=part.device)] = True
+            self._keep = keep
+        acc = torch.where(keep, part if last else torch.zeros_like(part), part * (Mr / M))
+        dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=self.group)
+        vals = values_buf if values_buf is not None else torch.empty((1, 3 * ((n + 2) // 3)), dtype=torch.float32,
+                                                                       device=part.device)
+        vals[0, :n].copy_(acc)
+        self.codec.encode_device(vals, n, out_text.view(1, -1))
 
     def local_partial(self, uploads: Sequence[bytes], dampen: Sequence[float], header_pos):
         """This rank's block of uploads through the exact chain: (merged_f32 as a
@@ -178,6 +223,7 @@ class ClientShardedUpdater(ShardedUpdater):
     def update(self, uploads: Sequence[bytes], dampen: Sequence[float]) -> bytes:
         import torch
         import torch.distributed as dist
+        self._require_approx()
         M = len(uploads)
         if M == 0 or len(dampen) != M:
             raise ValueError("need one dampening factor per upload")

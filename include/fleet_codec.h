@@ -208,6 +208,12 @@ int fleet_decode_device(fleet_ctx* ctx, const void* d_text, size_t len, size_t p
 int fleet_synth_device(fleet_ctx* ctx, uint64_t seed, int M, int client0, const int32_t* header_pos,
                        const float* header_val, int n_headers, size_t n_up, void* d_values, size_t vpitch,
                        void* stream);
+/* The same for a column window of a larger synthetic problem: values n_up columns
+ * from element elem0 (the counter is the global element index, so a rank's window
+ * holds exactly the fixed problem's values there); header_pos in window coordinates. */
+int fleet_synth_window_device(fleet_ctx* ctx, uint64_t seed, int M, int client0, size_t elem0,
+                              const int32_t* header_pos, const float* header_val, int n_headers, size_t n_up,
+                              void* d_values, size_t vpitch, void* stream);
 /* Returns FLEET_ERR_BASE64 / FLEET_ERR_LAYOUT if a device-resident call
  * (fleet_*_device) since the last check saw malformed text or a header that
  * differs from the last upload's (synchronises the stream), and clears the

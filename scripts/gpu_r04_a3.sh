@@ -1,7 +1,7 @@
 # r04 a3: the launch-plan refactor (validated plan overrides, dropped variants) -- GPU suite, smoke, default bench
 set -u
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/a3; mkdir -p $O
+O=${OUTROOT:-$GRAFT_REPO_ROOT/gpurun_out}/a3; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1; rc=$?
 tail -15 $O/tests.log
 [ $rc -eq 0 ] || exit 1

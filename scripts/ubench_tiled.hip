@@ -80,7 +80,7 @@ void run(int64_t n_up, int M, int reps = 1) {
     hipMemcpy(dpos, g_hpos.data(), sizeof(int32_t) * nh, hipMemcpyHostToDevice);
     hipMemcpy(dval, g_hval.data(), sizeof(float) * nh, hipMemcpyHostToDevice);
   }
-  launch_synth(1, 0, M, n_up, vals, vpitch, dpos, dval, nh, 0);
+  launch_synth(1, 0, 0, M, n_up, vals, vpitch, dpos, dval, nh, 0);
   launch_encode_f32(vals, n_up, vpitch, M, text, pitch, 0);
   const unsigned blocks = (unsigned)((groups + TG - 1) / TG);
   for (int rep = 0; rep < 3; ++rep)
@@ -143,7 +143,7 @@ static void time_encode(int64_t n_up, int M, int reps) {
   uint8_t* text;
   hipMalloc(&vals, sizeof(float) * vpitch * M);
   hipMalloc(&text, pitch * M);
-  launch_synth(1, 0, M, n_up, vals, vpitch, nullptr, nullptr, 0, 0);
+  launch_synth(1, 0, 0, M, n_up, vals, vpitch, nullptr, nullptr, 0, 0);
   for (int r = 0; r < 3; ++r) launch_encode_f32(vals, n_up, vpitch, M, text, pitch, 0);
   hipEvent_t a, b;
   hipEventCreate(&a);

@@ -110,7 +110,7 @@ static void run(int64_t groups, int M, bool plain, const char* tag) {
   const int32_t h[8] = {0, 0, (int32_t)n_up, 0, 0, 0, 0, 0};
   CHK(hipMemcpy(hdr, h, sizeof h, hipMemcpyHostToDevice));
   CHK(hipMemset(err, 0, sizeof(int)));
-  CHK(launch_synth(1, 0, M, n_up, vals, vpitch, nullptr, nullptr, 0, 0));
+  CHK(launch_synth(1, 0, 0, M, n_up, vals, vpitch, nullptr, nullptr, 0, 0));
   CHK(launch_encode_f32(vals, n_up, vpitch, M, text, pitch, 0));
   CHK(hipDeviceSynchronize());
   CHK(hipFree(vals));

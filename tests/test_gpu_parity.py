@@ -436,7 +436,7 @@ def test_client_sharded_partials_on_device(codec, oracle):
     ups = uploads_for(oracle, lay, M, seed=23)
     d = policy("inverse", M)
     hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
-    cs = ClientShardedUpdater(codec)
+    cs = ClientShardedUpdater(codec, approx=True)
     hp = cs.layout(ups[-1])
     for cb, ce in ((0, 3), (3, 7)):
         part, text = cs.local_partial(ups[cb:ce], d[cb:ce], hp)
@@ -444,6 +444,19 @@ def test_client_sharded_partials_on_device(codec, oracle):
         assert text == want
         assert np.array_equal(part.float().cpu().numpy().view(np.uint32), oracle.decode_floats(want).view(np.uint32))
     assert cs.update(ups, d) == oracle.update_fused(ups, d, hm)
+    # the device-resident step (bench.py's approx block) with one rank: the exact chain's text
+    torch = pytest.importorskip("torch")
+    L = len(ups[0])
+    groups = (F.b64_count(L) + 2) // 3
+    rows = torch.zeros((M, 16 * groups), dtype=torch.uint8, device="cuda")
+    rows[:, :L] = torch.from_numpy(np.frombuffer(b"".join(ups), np.uint8).reshape(M, L).copy()).cuda()
+    merged = torch.zeros(16 * groups, dtype=torch.uint8, device="cuda")
+    f32 = torch.zeros(3 * groups, dtype=torch.float32, device="cuda")
+    out = torch.zeros(16 * groups, dtype=torch.uint8, device="cuda")
+    cs.device_step(rows, L, d, hp, M, 0, merged, f32, out)
+    torch.cuda.synchronize()
+    codec.check()
+    assert out.cpu().numpy()[:L].tobytes() == oracle.update_fused(ups, d, hm)
 
 
 # ---- DISTILLATION_MODE=1 model codec ---------------------------------

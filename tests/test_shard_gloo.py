@@ -117,13 +117,13 @@ def _client_rank_main(rank, world, port, cases, out_dir):
     import torch
 
     import pyoracle
-    from fleet_amd.shard import ClientShardedUpdater, deviation
+    from fleet_amd.shard import ClientShardedUpdater, deviation, group_range
 
     o = pyoracle.Oracle()
 
     class OracleClientRank(ClientShardedUpdater):
         def __init__(self, layout):
-            super().__init__(codec=None, device="cpu")
+            super().__init__(codec=None, device="cpu", approx=True)
             self.mask = o.header_mask(list(layout.w_sizes), list(layout.b_sizes))
 
         def layout(self, last_upload):
@@ -136,6 +136,24 @@ def _client_rank_main(rank, world, port, cases, out_dir):
         def encode(self, values):
             return o.encode_floats(values.float().numpy())
 
+    class OracleDeviceCodec:
+        """update_device / encode_device of the C-ABI on CPU tensors, by the oracle:
+        drives ClientShardedUpdater.device_step (bench.py's approx block) under gloo."""
+
+        def __init__(self, mask):
+            self.mask = mask
+
+        def update_device(self, rows, length, dampen, header_pos, merged, merged_f32):
+            ups = [rows[c, :length].numpy().tobytes() for c in range(rows.shape[0])]
+            text = o.update_fused(ups, list(dampen), self.mask, threads=1)
+            merged[: len(text)] = torch.from_numpy(np.frombuffer(text, np.uint8).copy())
+            f = o.decode_floats(text)
+            merged_f32[: len(f)] = torch.from_numpy(f)
+
+        def encode_device(self, vals, n, out):
+            text = o.encode_floats(vals[0, :n].numpy())
+            out[0, : len(text)] = torch.from_numpy(np.frombuffer(text, np.uint8).copy())
+
     lines = []
     for name, M in cases:
         lay = MNIST if name == "mnist" else synthetic(int(name))
@@ -144,6 +162,20 @@ def _client_rank_main(rank, world, port, cases, out_dir):
         hm = o.header_mask(list(lay.w_sizes), list(lay.b_sizes))
         exact = o.update_fused(ups, d, hm)
         got = OracleClientRank(lay).update(ups, d)
+        # the device-resident form (bench.py's approx block) gives the same text
+        cb, ce = group_range(M, world, rank)
+        if True:  # every rank joins the all_reduce, with or without clients
+            L = len(ups[0])
+            groups = (len(o.decode_floats(ups[0])) + 2) // 3
+            rows = torch.zeros((ce - cb, 16 * groups), dtype=torch.uint8)
+            for i, c in enumerate(range(cb, ce)):
+                rows[i, :L] = torch.from_numpy(np.frombuffer(ups[c], np.uint8).copy())
+            dev = ClientShardedUpdater(OracleDeviceCodec(hm), device="cpu", approx=True)
+            out = torch.zeros(16 * groups, dtype=torch.uint8)
+            dev.device_step(rows, L, d[cb:ce], np.nonzero(hm)[0].tolist(), M, cb,
+                            torch.zeros(16 * groups, dtype=torch.uint8), torch.zeros(3 * groups),
+                            out)
+            assert out.numpy()[:L].tobytes() == got, (name, M)
         a, e = o.decode_floats(got), o.decode_floats(exact)
         dv = deviation(a, e)
         ok = (len(got) == len(exact) and np.array_equal(a[hm != 0], e[hm != 0])
@@ -152,6 +184,14 @@ def _client_rank_main(rank, world, port, cases, out_dir):
     with open(os.path.join(out_dir, f"crank{rank}.txt"), "w") as f:
         f.write("\n".join(lines))
     dist.destroy_process_group()
+
+
+def test_client_sharded_needs_explicit_approx():
+    """The approximate mode refuses to run unless asked for by name (approx=True)."""
+    from fleet_amd.shard import ClientShardedUpdater
+    cs = ClientShardedUpdater(codec=None, device="cpu")
+    with pytest.raises(ValueError, match="approx=True"):
+        cs.update([b"AAAA"], [1.0])
 
 
 @pytest.mark.parametrize("world", [2, 3])
