@@ -303,7 +303,8 @@ __device__ __forceinline__ int32_t merged_code(float A, double inv, int32_t last
 
 // Keep slots: layout header slots and slots past network::flatGrad's walk take the
 // last upload's code in the merged output (mergeFlatGradient, cppNN_backend.cpp:722-750),
-// so their running sums are never read. The chain runs on 0 there (Q(0) = 0): a header
+// so their running sums are never read. The chain runs on code 0 there (Q(0) = 0; the
+// stream kernels keep the last client's codes, which the merged output needs): a header
 // value summed over thousands of clients (configs[4]: the bucket size 4,194,304 at
 // position 1) would otherwise leave the codec's fast domain and send its lane through
 // chain_general -- one straggler wave that doubled the configs[4] window kernels
@@ -315,12 +316,6 @@ __device__ __forceinline__ uint32_t keep_bits(uint32_t hbits, bool live, int64_t
   for (int i = 0; i < S; ++i)
     if (live && p0 + i >= walk_end) k |= 1u << i;
   return k;
-}
-template <int S>
-__device__ __forceinline__ void keep_zero(float (&y)[S], uint32_t kbits) {
-#pragma unroll
-  for (int i = 0; i < S; ++i)
-    if ((kbits >> i) & 1u) y[i] = 0.0f;
 }
 
 // The exact chain of one value recomputed from global memory with the general
@@ -428,11 +423,10 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
 #pragma unroll
   for (int k = 0; k < K; ++k)
     if (live[k]) hbits |= header_bits(hdr, n_hdr, 3 * g[k]) << (3 * k);
-  const bool wave_hdr = __ballot(hbits != 0) != 0;
   uint32_t kbits = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) kbits |= keep_bits<3>((hbits >> (3 * k)) & 7u, live[k], 3 * g[k], walk_end) << (3 * k);
-  const bool wave_keep = __ballot(kbits != 0) != 0;
+  const bool wave_keep = __ballot(kbits != 0) != 0;  // as in update_lane
   int32_t hfirst[S];
   uint32_t layout_bad = 0;
   // Kardam: value slots of the flat gradient (neither header slots nor past the walk)
@@ -473,11 +467,12 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
       else  // the partial last group: only the chars carrying its values must be valid
         bad[k] |= b64_decode_group(cur[k], &tab, codes + 3 * k) & need[k];
     }
-    if (wave_hdr) {  // wave-uniform
+    if (wave_keep) {  // wave-uniform
 #pragma unroll
       for (int i = 0; i < S; ++i) {
         if (c == 0) hfirst[i] = codes[i];
         layout_bad |= (((hbits >> i) & 1u) & (uint32_t)(codes[i] != hfirst[i])) << i;
+        if (((kbits >> i) & 1u) && c + 1 < M) codes[i] = 0;
       }
     }
 
@@ -488,7 +483,6 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
     // stage A: y = Q(int2float(code))
     float y0[S], y[S];
     dec_stage_d16<S>(y0, codes, &dtab);
-    if (wave_keep) keep_zero<S>(y0, kbits);
     if constexpr (KD) q_stage_d16x<S>(y, y0, &dtab, tab.var);
     else q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
 
@@ -604,7 +598,7 @@ __global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploa
     int32_t out[3];
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
-      const bool keep_last = ((hbits >> (3 * k + e)) & 1u) || p0 + e >= walk_end;
+      const bool keep_last = ((kbits >> (3 * k + e)) & 1u) != 0;  // header slot or past the walk
       const int32_t o = merged_code(acc[3 * k + e], inv_avg, codes[3 * k + e], keep_last, &tab);
       out[e] = e < r ? o : 0;
     }
@@ -632,9 +626,9 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   const uint8_t* rowp = uploads + 16 * (live ? g : g_safe);
   const uint32_t need = needed_chars_mask((int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g)));
   const uint32_t hbits = live ? (header_bits(hdr, n_hdr, 3 * g) >> e0) & ((1u << S) - 1u) : 0u;
-  const bool wave_hdr = __ballot(hbits != 0) != 0;
-  const uint32_t kbits = keep_bits<S>(hbits, live, 3 * g + e0, walk_end);
-  const bool wave_keep = __ballot(kbits != 0) != 0;
+  // waves holding header slots (layout check) or keep slots (keep_bits: their chains run
+  // on code 0 up to the last client, whose codes the merged output keeps): wave-uniform
+  const bool wave_keep = __ballot(keep_bits<S>(hbits, live, 3 * g + e0, walk_end) != 0) != 0;
   int32_t hfirst[S], codes[S];
   float acc[S];
   uint32_t dmax = 0;
@@ -651,16 +645,17 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       if (need == 0xffffu) bad |= b64_decode_pair_full(cur.x, cur.y, sel, &tab, codes[0]);
       else bad |= b64_decode_pair(cur.x, cur.y, sel, &tab, codes[0]) & need_pair;
     }
-    if (wave_hdr) {
+    if (wave_keep) {
+      const uint32_t kbits = keep_bits<S>(hbits, live, 3 * g + e0, walk_end);
 #pragma unroll
       for (int i = 0; i < S; ++i) {
         if (c == 0) hfirst[i] = codes[i];
         layout_bad |= (((hbits >> i) & 1u) & (uint32_t)(codes[i] != hfirst[i])) << i;
+        if (((kbits >> i) & 1u) && c + 1 < M) codes[i] = 0;
       }
     }
     float y0[S], y[S], p[S];
     dec_stage_d16<S>(y0, codes, &dtab);
-    if (wave_keep) keep_zero<S>(y0, kbits);
     q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
     dampen_stage<S>(y, dampen[c]);
     q_stage_d16<S>(p, y, &dtab, tab.var, dmax);
@@ -1018,17 +1013,6 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW, D16>& sh, const 
                                              const TileKd& tk = TileKd{}) {
   constexpr int E = 3 * TG, S = 3 * IPT;
   int32_t codes[S];
-  // keep slots (header slots, slots past the walk) run the chain on 0 (keep_bits)
-  uint32_t kbits = 0;
-  const bool tile_past = 3 * (g0 + TG) > walk_end;  // block-uniform
-#pragma unroll
-  for (int h = 0; h < IPT; ++h) {
-    if (it.live[h]) {
-      uint32_t k = sh.hmask[it.gl[h]];
-      if (tile_past) k = keep_bits<3>(k, true, 3 * (g0 + it.gl[h]), walk_end);
-      kbits |= k << (3 * h);
-    }
-  }
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
     const int r = (int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * (g0 + it.gl[h])));
@@ -1042,20 +1026,27 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW, D16>& sh, const 
       if (it.c_base + it.cc[h] == M - 1)
         for (int e = 0; e < 3; ++e) sh.last_codes[3 * it.gl[h] + e] = codes[3 * h + e];
       const uint32_t hm = sh.hmask[it.gl[h]];
-      if (hm) {
+      if (hm) {  // header slots (rare lanes): the layout check, then the chain runs on code 0 (keep_bits)
         for (int e = 0; e < 3; ++e)
           if ((hm >> e) & 1u) {
             atomicMin(&sh.hmin[3 * it.gl[h] + e], codes[3 * h + e]);
             atomicMax(&sh.hmax[3 * it.gl[h] + e], codes[3 * h + e]);
+            codes[3 * h + e] = 0;
           }
       }
     }
+  }
+  if (3 * (g0 + TG) > walk_end) {  // block-uniform, rare: slots past the walk run on code 0 too
+#pragma unroll
+    for (int h = 0; h < IPT; ++h)
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if (3 * (g0 + it.gl[h]) + e >= walk_end) codes[3 * h + e] = 0;
   }
   // stage A: y = Q(int2float(code)); D16: the stream kernel's byte-table stages
   float y0[S], y[S];
   if constexpr (D16) dec_stage_d16<S>(y0, codes, &sh.dt);
   else dec_stage<S>(y0, codes, &sh.tab);
-  if (__ballot(kbits != 0) != 0) keep_zero<S>(y0, kbits);
   if constexpr (D16) q_stage_d16x<S>(y, y0, &sh.dt, sh.tab.var);
   else q_stage<S>(y, y0, &sh.tab);
   // stage B: p = Q(f32(f64(y) * d)), per-item client
