@@ -780,8 +780,9 @@ namespace {
 
 // Ranges page-locked by fleet_host_register (process-wide: every context's
 // device DMAs from them). The copy-free row path requires the WHOLE row range
-// to lie inside ONE live registration -- not just its two end bytes, which a
-// freed and reallocated buffer could still satisfy.
+// to lie inside ONE recorded registration. A record cannot tell whether its
+// memory was freed and reused since (the caller's contract, fleet_codec.h:
+// unregister before freeing); it only stops rows that straddle two ranges.
 std::mutex g_reg_mu;
 std::vector<std::pair<uintptr_t, size_t>> g_registered;  // (base, bytes)
 

@@ -348,10 +348,10 @@ JNIEXPORT jboolean JNICALL Java_apps_cppNN_FleetUpdater_registerDirectNative(JNI
   return rc == FLEET_OK ? JNI_TRUE : JNI_FALSE;
 }
 
-// Releases the page lock before the buffer is dropped (its Cleaner frees the
-// memory). A registration left behind is released anyway when a later
-// registerDirectNative covers the same memory (fleet_host_register), and rows
-// are only DMA'd copy-free from inside one live registration.
+// Releases the page lock; the Java side must call it before the buffer is dropped
+// (its Cleaner frees the memory): a registration left behind still looks live to
+// the library until a later registerDirectNative covers the same memory
+// (fleet_host_register), and rows inside it would be DMA'd from the old pages.
 JNIEXPORT void JNICALL Java_apps_cppNN_FleetUpdater_unregisterDirectNative(JNIEnv* env, jobject, jobject buf) {
   fleet_ctx* c = ctx();
   if (!c || !buf) return;

@@ -140,9 +140,12 @@ int fleet_update_rows_multi(fleet_ctx* const* ctxs, int n_ctx, const char* rows,
                             const double* dampen, char* merged, size_t cap, size_t* out_len, float* merged_f32);
 /* Page-lock (hipHostRegister, portable to every device) / release a long-lived
  * host buffer, e.g. the upload rows of fleet_update_rows. The registrations
- * are tracked process-wide: registering a range that overlaps a live
- * registration releases the old one first (its memory was freed and reused,
- * e.g. a collected Java direct buffer). */
+ * are tracked process-wide: registering a range that overlaps a recorded
+ * registration releases the old one first. Contract: unregister BEFORE the
+ * memory is freed. The library cannot tell a registration whose memory was
+ * freed and reused (a collected Java direct buffer, a new allocation at the
+ * same addresses) from a live one: rows inside it would be DMA'd from the
+ * stale pinned pages. */
 int fleet_host_register(fleet_ctx* ctx, void* ptr, size_t bytes);
 int fleet_host_unregister(fleet_ctx* ctx, void* ptr);
 

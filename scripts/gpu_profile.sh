@@ -3,7 +3,7 @@
 set -u
 TAG=${1:-r02}; shift || true
 WL=${*:-"synth1m_256 cifar10_256 mnist64"}
-O=$PWD/gpurun_out/$TAG; mkdir -p $O
+O=${OUTROOT:-$PWD/gpurun_out}/$TAG; mkdir -p $O
 R=$PWD
 export TMPDIR=/tmp
 B="--extras= --no-cpu-baseline --no-e2e --no-strong-block"
