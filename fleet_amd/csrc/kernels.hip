@@ -35,6 +35,9 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
+#ifndef FLEET_PRIO_LADDER
+#define FLEET_PRIO_LADDER 0
+#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -681,8 +684,20 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // registers (no copies between trips)
   Row b0 = group_of(0), b1;
   int c = 0;
+#if FLEET_PRIO_LADDER
+  // experiment: issue priority falls as a wave gets ahead (3 -> 0 at quarters of the
+  // client loop), so the waves of a SIMD keep step instead of finishing one by one
+  // in age order (the tail of a single-round grid, profiles/r04/window_traces.txt)
+  const int q1 = M / 4, q2 = M / 2, q3 = 3 * M / 4;
+  __builtin_amdgcn_s_setprio(3);
+#endif
   for (; c + 1 < M; c += 2) {
     FLEET_CLIENT_HOOK(c, M);
+#if FLEET_PRIO_LADDER
+    if (c == (q1 & ~1)) __builtin_amdgcn_s_setprio(2);
+    if (c == (q2 & ~1)) __builtin_amdgcn_s_setprio(1);
+    if (c == (q3 & ~1)) __builtin_amdgcn_s_setprio(0);
+#endif
     b1 = group_of(c + 1);
     client(c, b0);
     if (c + 2 < M) b0 = group_of(c + 2);
@@ -1550,7 +1565,7 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
 // machine scheduler, which helps them (VALU-issue bound at 5-6 waves per SIMD)
 // and hurts the tiled and pipelined kernels; the main unit only
 // declares their instantiations.
-#ifdef FLEET_STREAM_TU
+#if defined(FLEET_STREAM_TU) || defined(FLEET_DEV_ALL_KERNELS)  // (dev tools that include this file: all here)
 template __global__ void k_update<1, true, 256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
                                                double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
                                                uint8_t* __restrict__, float* __restrict__, int* __restrict__,

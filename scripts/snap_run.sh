@@ -7,7 +7,7 @@ set -u
 script=$1; tmo=$2; log=$3
 cd /root/repo
 rm -rf .snap && mkdir .snap
-tar --exclude ./.git --exclude ./.snap --exclude ./gpurun_out --exclude ./ab --exclude '__pycache__' --exclude '*.pyc' \
+tar --exclude ./.git --exclude ./.snap --exclude ./gpurun_out --exclude './ab/*.objs' --exclude '__pycache__' --exclude '*.pyc' \
   -cf - . | tar -xf - -C .snap
 cmd="export OUTROOT=\$GRAFT_REPO_ROOT/gpurun_out; cd .snap && export GRAFT_REPO_ROOT=\$PWD && bash $script"
 for i in $(seq 1 12); do

@@ -31,6 +31,7 @@ __device__ __forceinline__ void fleet_trace_hook(int c, int M) {
   }
 }
 #define FLEET_CLIENT_HOOK(c, M) fleet_trace_hook(c, M)
+#define FLEET_DEV_ALL_KERNELS 1
 #include "../fleet_amd/csrc/kernels.hip"
 
 #include <algorithm>
@@ -43,20 +44,7 @@ __device__ __forceinline__ void fleet_trace_hook(int c, int M) {
 
 using namespace fleet;
 
-// the stream kernels live in stream_kernels.hip's unit in the library: instantiate them here
-namespace fleet {
-template __global__ void k_update<1, true, 256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
-                                               double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
-                                               uint8_t* __restrict__, float* __restrict__, int* __restrict__,
-                                               KardamOut);
-template __global__ void k_update_mixed<256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
-                                             double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
-                                             uint8_t* __restrict__, float* __restrict__, int* __restrict__, int);
-template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
-                                              double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
-                                              uint8_t* __restrict__, float* __restrict__, int* __restrict__, int, int,
-                                              EncodeJob);
-}  // namespace fleet
+
 
 __global__ void __launch_bounds__(256) k_probe(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                const double* __restrict__ dampen, double inv_avg, int64_t n_up,
