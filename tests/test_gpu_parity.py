@@ -390,6 +390,46 @@ def test_update_modes(codec, oracle, plan, spec):
         assert codec.update(ups, d) == oracle.update_fused(ups, d, hm), (lay.name, M)
 
 
+@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile_mix=off", "update=stream",
+                                  "update=stream,grid=plain", "update=stream,grid=lanes"])
+@pytest.mark.parametrize("extra", [200, 201])
+def test_update_keep_slots_past_the_walk(codec, oracle, plan, spec, extra):
+    """Uploads longer than their layout: mergeFlatGradient (CppNNUpdater.java:508)
+    keeps the last upload's values past the header walk, like the header slots. The
+    kernels still run the chain on those lanes (on code 0, so no lane of a wave leaves
+    the fast path); the values there are large enough (3e8..9.9e8) that a chain on
+    the real codes would overflow the digit domain within a few clients. Same bytes
+    as the per-op chain and as the fused oracle with those slots masked; the Kardam
+    update's merged text too. extra = 201 leaves the last group ragged."""
+    torch = pytest.importorskip("torch")
+    plan(spec)
+    lay = synthetic(1000)
+    rng = np.random.default_rng(extra)
+    M = 8
+    ups = []
+    for c in range(M):
+        v = oracle.synth_upload(17, c, list(lay.w_sizes), list(lay.b_sizes))
+        tail = (rng.uniform(3e8, 9.9e8, extra) * rng.choice([-1, 1], extra)).astype(np.float32)
+        ups.append(oracle.encode_floats(np.concatenate([v, tail])))
+    d = [1.0, 7.5, 0.25, 10.0, 1 / 3, 1.0, 2.0, 0.5]
+    hm = np.concatenate([oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes)), np.ones(extra, np.uint8)])
+    exp = oracle.update_faithful(ups, d)
+    assert exp == oracle.update_fused(ups, d, hm)
+    assert codec.update(ups, d) == exp
+    L = len(ups[0])
+    pitch = 16 * ((L + 15) // 16)
+    host = np.zeros((M, pitch), np.uint8)
+    for c, u in enumerate(ups):
+        host[c, :L] = np.frombuffer(u, np.uint8)
+    merged = torch.zeros(pitch, dtype=torch.uint8, device="cuda")
+    g_out = torch.zeros((M, lay.n_up + extra + 3), dtype=torch.float32, device="cuda")
+    codec.update_kardam_device(torch.from_numpy(host).cuda(), L, d, lay.header_positions(), 0.05, merged, None,
+                               None, None, g_out)
+    codec.check()
+    torch.cuda.synchronize()
+    assert merged.cpu().numpy()[:L].tobytes() == exp
+
+
 def test_device_window_update(codec, oracle):
     """A rank holding only its column window of every upload (fleet_amd.shard)."""
     torch = pytest.importorskip("torch")
