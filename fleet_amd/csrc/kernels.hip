@@ -352,14 +352,14 @@ __device__ __noinline__ float chain_general(const uint8_t* __restrict__ uploads,
 // then r = Q((float)((double)A * inv)) (scalarMultiply(1/avgSize) + merge decode) and
 // merged code = enc(r); header slots take enc(dec(code_{M-1})) (mergeFlatGradient).
 //
-// Layout: lane owns K groups (3K values) g = g_begin + (blockIdx*K + k)*256 + tid,
-// so every wave-wide load of a client row is 1 KiB contiguous; the next
-// client's K loads are in flight while the current one computes.
-//
+// The stream form (update_lane, k_update_mixed): a lane walks one group (or one
+// value) down all M client rows, so every wave-wide load of a client row is 1 KiB
+// contiguous; the next client's loads are in flight while the current one computes.
 // KD = true adds Kardam's bookkeeping of the same picked uploads (CppNNUpdater.java:
 // 463-481, Kardam.java:48-106) as side outputs of the client loop
 // (KardamOut), so it costs no second pass over the uploads; stages A and B then
 // use the exact in-stage fallback (their values feed the side outputs).
+//
 // Sum of v over each aligned group of TG lanes (16, 32 or 64), valid in the
 // group's last lane, by DPP lane moves inside the VALU (no LDS crossbar):
 // row_half_mirror + two quad_perms + row_mirror give every lane its 16-lane row's
@@ -384,251 +384,104 @@ __device__ __forceinline__ double group_sum_f64(double v) {
   return v;
 }
 
-template <int K, bool KD = false, int NT = 256>
-__global__ void __launch_bounds__(NT) k_update(const uint8_t* __restrict__ uploads, size_t pitch, int M,
-                                                const double* __restrict__ dampen, double inv_avg,
-                                                int64_t n_up, int64_t g_begin, int64_t g_end,
-                                                const int32_t* __restrict__ hdr_block,
-                                                uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                int* __restrict__ err, KardamOut kd = KardamOut{}) {
-  constexpr int S = 3 * K;
-  __shared__ B64Tables tab;
-  __shared__ D16Table dtab;
-  const int lane = threadIdx.x & 63;
-
-  // hdr_block = {status, n_headers, walk_end, 0, positions...} (k_layout_parse / host-built);
-  // slots at or after walk_end are outside network::flatGrad's walk and, like
-  // header slots, come from the last upload in mergeFlatGrad.
-  const int n_hdr = hdr_block[1];
-  const int64_t walk_end = hdr_block[2];
-  const int32_t* hdr = hdr_block + 4;
-
-  int64_t g[K];
-  bool live[K];
-  const uint8_t* rowp[K];
+// Kardam's bookkeeping of one client step in a stream lane (KD = true; SURVEY.md f2,
+// CppNNUpdater.java:463-481, Kardam.java:48-106): G = Q(f32(f64(p) * lr)) -- the
+// picked gradient scalarMultiply(getLrate()) --, its squared norm and that of
+// Q(G - prev) (getNorm: float products summed in double), G stored in upload
+// coordinates for the next round's difference. `flat` bit i = value slot pos0 + i
+// is in the flat gradient (neither a header slot nor past the walk). The wave's
+// two sums go to its partial slot `part` (lane 63; k_kardam_reduce sums the waves).
+template <int S>
+__device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uint32_t flat, bool live, int64_t pos0,
+                                                 int64_t n_up, const KardamOut& kd, const D16Table& dtab,
+                                                 const B64Tables& tab, double* __restrict__ part) {
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+  float rg[S], G[S];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    g[k] = g_begin + ((int64_t)blockIdx.x * K + k) * NT + threadIdx.x;
-    live[k] = g[k] < g_end;
-    rowp[k] = uploads + 16 * (live[k] ? g[k] : g_begin);
-  }
-
-  float acc[S];
-  int32_t codes[S];
-  uint32_t bad[K], need[K];
-  uint32_t dmax = 0;  // largest digit-table offset seen (>= kD16Out: left the q_gen domain)
+  for (int i = 0; i < S; ++i) rg[i] = p[i];
+  dampen_stage<S>(rg, kd.lr);  // lr is uniform
+  q_stage_d16x<S>(G, rg, &dtab, tab.var);
+  double sg = 0.0, sd = 0.0;
 #pragma unroll
-  for (int k = 0; k < K; ++k) need[k] = needed_chars_mask((int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g[k])));
-  // layout consistency (every upload carries the last one's header codes) is
-  // checked while walking the clients, only in the few waves holding header
-  // slots: hbits bit i = value slot i of this lane is a header slot
-  uint32_t hbits = 0;
+  for (int i = 0; i < S; ++i)
+    if ((flat >> i) & 1u) sg += (double)(G[i] * G[i]);
+  const bool whole = live && pos0 + S - 1 < n_up;
+  if (kd.prev && kd.has_prev[c]) {  // uniform
+    const float* pr = kd.prev + (size_t)c * kd.vpitch + pos0;
+    float pv[S], dv[S], D[S];
+    if constexpr (S == 3) {
+      if (whole) {  // one 12-byte access per group (rows are 4-byte aligned)
+        const f3u t = *reinterpret_cast<const f3u*>(pr);
+        pv[0] = t.x;
+        pv[1] = t.y;
+        pv[2] = t.z;
+      } else {
 #pragma unroll
-  for (int k = 0; k < K; ++k)
-    if (live[k]) hbits |= header_bits(hdr, n_hdr, 3 * g[k]) << (3 * k);
-  uint32_t kbits = 0;
-#pragma unroll
-  for (int k = 0; k < K; ++k) kbits |= keep_bits<3>((hbits >> (3 * k)) & 7u, live[k], 3 * g[k], walk_end) << (3 * k);
-  const bool wave_keep = __ballot(kbits != 0) != 0;  // as in update_lane
-  int32_t hfirst[S];
-  uint32_t layout_bad = 0;
-  // Kardam: value slots of the flat gradient (neither header slots nor past the walk)
-  uint32_t flatbits = 0;
-  if constexpr (KD) {
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        const int64_t pos = 3 * g[k] + e;
-        if (live[k] && pos < n_up && pos < walk_end && !((hbits >> (3 * k + e)) & 1u)) flatbits |= 1u << (3 * k + e);
+        for (int i = 0; i < S; ++i) pv[i] = ((flat >> i) & 1u) ? pr[i] : 0.0f;
       }
+    } else {
+      pv[0] = (flat & 1u) ? pr[0] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < S; ++i) dv[i] = ((flat >> i) & 1u) ? G[i] - pv[i] : 0.0f;
+    q_stage_d16x<S>(D, dv, &dtab, tab.var);
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      if ((flat >> i) & 1u) sd += (double)(D[i] * D[i]);
   }
+  if (kd.g_out) {
+    float* go = kd.g_out + (size_t)c * kd.vpitch + pos0;
+    float gv[S];
 #pragma unroll
-  for (int i = 0; i < S; ++i) acc[i] = 0.f;
-#pragma unroll
-  for (int k = 0; k < K; ++k) bad[k] = 0;
-
-  uint4 nxt[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) nxt[k] = *reinterpret_cast<const uint4*>(rowp[k]);
-  // tables copied while the first client's groups are in flight
-  b64_tables_init<NT>(&tab);
-  d16_table_init<NT>(&dtab);
-  __syncthreads();
-  for (int c = 0; c < M; ++c) {
-    uint4 cur[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) cur[k] = nxt[k];
-    if (c + 1 < M) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) nxt[k] = *reinterpret_cast<const uint4*>(rowp[k] + (size_t)(c + 1) * pitch);
-    }
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (need[k] == 0xffffu)
-        bad[k] |= b64_decode_group_full(cur[k], &tab, codes + 3 * k);
-      else  // the partial last group: only the chars carrying its values must be valid
-        bad[k] |= b64_decode_group(cur[k], &tab, codes + 3 * k) & need[k];
-    }
-    if (wave_keep) {  // wave-uniform
-#pragma unroll
-      for (int i = 0; i < S; ++i) {
-        if (c == 0) hfirst[i] = codes[i];
-        layout_bad |= (((hbits >> i) & 1u) & (uint32_t)(codes[i] != hfirst[i])) << i;
-        if (((kbits >> i) & 1u) && c + 1 < M) codes[i] = 0;
-      }
-    }
-
-    // Per stage and wave: if every value of the wave is inside the |x| < 1
-    // fast domain, run the fixed 9-step chains; otherwise the 2+1+2+4-step
-    // variable chains (numDigits <= 9). Values outside both are recomputed
-    // with the general codec at the end (|x| >= 1e8: never for gradients).
-    // stage A: y = Q(int2float(code))
-    float y0[S], y[S];
-    dec_stage_d16<S>(y0, codes, &dtab);
-    if constexpr (KD) q_stage_d16x<S>(y, y0, &dtab, tab.var);
-    else q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
-
-    // stage B: p = Q((float)((double)y * d))
-    const double d = dampen[c];
-    float r[S], p[S];
-#pragma unroll
-    for (int i = 0; i < S; ++i) r[i] = y[i];
-    dampen_stage<S>(r, d);
-    if constexpr (KD) q_stage_d16x<S>(p, r, &dtab, tab.var);
-    else q_stage_d16<S>(p, r, &dtab, tab.var, dmax);
-
-    if constexpr (KD) {
-      // Kardam.setGrad(id, pickedGrad.scalarMultiply(getLrate())) and updateLip's
-      // g.subtract(prev).getNorm() (getNorm: float products summed in double)
-      float rg[S], G[S];
-#pragma unroll
-      for (int i = 0; i < S; ++i) rg[i] = p[i];
-      dampen_stage<S>(rg, kd.lr);  // (float)((double)p * lr); lr is uniform
-      q_stage_d16x<S>(G, rg, &dtab, tab.var);
-      double sg = 0.0, sd = 0.0;
-#pragma unroll
-      for (int i = 0; i < S; ++i)
-        if ((flatbits >> i) & 1u) sg += (double)(G[i] * G[i]);
-      // prev / G rows: one 12-byte access per whole group (rows are 4-byte aligned)
-      typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
-      if (kd.prev && kd.has_prev[c]) {  // uniform
-        float dv[S], D[S];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          const float* pr = kd.prev + (size_t)c * kd.vpitch + 3 * g[k];
-          float pv[3] = {0.0f, 0.0f, 0.0f};
-          if (live[k] && 3 * g[k] + 2 < n_up) {
-            const f3u t = *reinterpret_cast<const f3u*>(pr);
-            pv[0] = t.x;
-            pv[1] = t.y;
-            pv[2] = t.z;
-          } else {
-#pragma unroll
-            for (int e = 0; e < 3; ++e)
-              if ((flatbits >> (3 * k + e)) & 1u) pv[e] = pr[e];
-          }
-#pragma unroll
-          for (int e = 0; e < 3; ++e) {
-            const int i = 3 * k + e;
-            dv[i] = ((flatbits >> i) & 1u) ? G[i] - pv[e] : 0.0f;
-          }
-        }
-        q_stage_d16x<S>(D, dv, &dtab, tab.var);
+    for (int i = 0; i < S; ++i) gv[i] = ((flat >> i) & 1u) ? G[i] : 0.0f;
+    if constexpr (S == 3) {
+      if (whole) {
+        *reinterpret_cast<f3u*>(go) = f3u{gv[0], gv[1], gv[2]};
+      } else {
 #pragma unroll
         for (int i = 0; i < S; ++i)
-          if ((flatbits >> i) & 1u) sd += (double)(D[i] * D[i]);
+          if (live && pos0 + i < n_up) go[i] = gv[i];
       }
-      if (kd.g_out) {
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          float* go = kd.g_out + (size_t)c * kd.vpitch + 3 * g[k];
-          float gv[3];
-#pragma unroll
-          for (int e = 0; e < 3; ++e) gv[e] = ((flatbits >> (3 * k + e)) & 1u) ? G[3 * k + e] : 0.0f;
-          if (live[k] && 3 * g[k] + 2 < n_up) {
-            *reinterpret_cast<f3u*>(go) = f3u{gv[0], gv[1], gv[2]};
-          } else {
-#pragma unroll
-            for (int e = 0; e < 3; ++e)
-              if (live[k] && 3 * g[k] + e < n_up) go[e] = gv[e];
-          }
-        }
-      }
-      // the wave's sums by DPP lane moves in the VALU (the xor shuffles were
-      // ds_bpermute round trips through the LDS crossbar: 24 per client and lane)
-      sg = group_sum_f64<64>(sg);
-      sd = group_sum_f64<64>(sd);
-      if (lane == 63) {
-        const size_t w = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) / 64;
-        const size_t nw = (size_t)gridDim.x * (blockDim.x / 64);
-        kd.partials[((size_t)c * nw + w) * 2] = sg;
-        kd.partials[((size_t)c * nw + w) * 2 + 1] = sd;
-      }
-    }
-
-    // stage C: A = Q(A + p)
-    if (c == 0) {
-#pragma unroll
-      for (int i = 0; i < S; ++i) acc[i] = p[i];
     } else {
-      float sm[S];
-#pragma unroll
-      for (int i = 0; i < S; ++i) sm[i] = acc[i] + p[i];
-      q_stage_d16<S>(acc, sm, &dtab, tab.var, dmax);
+      if (live && pos0 < n_up) go[0] = gv[0];
     }
   }
-  // a value left the q_gen domain somewhere in this lane's chains (|x| >= 1e8,
-  // inf, NaN -- never for gradients): recompute the lane's values exactly.
-  // dmax holds the largest table offset (q_stage_d16) of the serial accumulation.
-  const bool out_of_domain = dmax >= kD16Out;
-  if (__ballot(out_of_domain) != 0) {
-    if (out_of_domain) {
-#pragma unroll
-      for (int k = 0; k < K; ++k)
-        if (live[k])
-          for (int e = 0; e < 3; ++e) acc[3 * k + e] = chain_general(uploads, pitch, M, dampen, g[k], e, &tab);
-    }
-  }
-
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    if (!live[k]) continue;
-    const int64_t p0 = 3 * g[k];
-    const int r = (int)min<int64_t>(3, n_up - p0);
-    if (bad[k]) atomicOr(err, FLEET_ERRBIT_BASE64);
-    if ((layout_bad >> (3 * k)) & 7u) atomicOr(err, FLEET_ERRBIT_LAYOUT);
-    int32_t out[3];
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      const bool keep_last = ((kbits >> (3 * k + e)) & 1u) != 0;  // header slot or past the walk
-      const int32_t o = merged_code(acc[3 * k + e], inv_avg, codes[3 * k + e], keep_last, &tab);
-      out[e] = e < r ? o : 0;
-    }
-    *reinterpret_cast<uint4*>(merged + 16 * g[k]) = pad_group(b64_encode_group(out, &tab), r);
-    if (merged_f32) {
-      for (int e = 0; e < r; ++e) merged_f32[p0 + e] = dec_mt(out[e], tab.mt);
-    }
+  sg = group_sum_f64<64>(sg);  // DPP lane moves: every lane of the wave is here
+  sd = group_sum_f64<64>(sd);
+  if ((threadIdx.x & 63) == 63) {
+    part[0] = sg;
+    part[1] = sd;
   }
 }
 
-// One lane's share of the fused update (the non-Kardam stream path): the values
-// [e0, e0 + S) of group g, S = 3 (the whole group) or S = 1 (one value; three
-// lanes of a wave share a group). Returns the lane's merged codes in out[S] and
-// its Base64 / layout error bits; tables already in LDS.
-template <int S>
+// One lane's share of the fused update (the stream path): the values [e0, e0 + S)
+// of group g, S = 3 (the whole group) or S = 1 (one value; three lanes of a wave
+// share a group). Returns the lane's merged codes in out[S] and its Base64 / layout
+// error bits; tables already in LDS. KD: Kardam's side outputs per client
+// (kardam_lane_step; kd_part = this wave's slot of client 0, kd_stride between clients).
+template <int S, bool KD = false>
 __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table& dtab,
                                             const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                             const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                             int64_t g, int e0, bool live, int64_t g_safe,
                                             const int32_t* __restrict__ hdr_block, int32_t (&out)[S],
-                                            uint32_t& bad, uint32_t& layout_bad) {
+                                            uint32_t& bad, uint32_t& layout_bad, const KardamOut& kd = KardamOut{},
+                                            double* __restrict__ kd_part = nullptr, size_t kd_stride = 0) {
   const int n_hdr = hdr_block[1];
   const int64_t walk_end = hdr_block[2];
   const int32_t* hdr = hdr_block + 4;
   const uint8_t* rowp = uploads + 16 * (live ? g : g_safe);
   const uint32_t need = needed_chars_mask((int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g)));
   const uint32_t hbits = live ? (header_bits(hdr, n_hdr, 3 * g) >> e0) & ((1u << S) - 1u) : 0u;
+  // Kardam: the lane's value slots in the flat gradient
+  uint32_t flatbits = 0;
+  if constexpr (KD) {
+#pragma unroll
+    for (int i = 0; i < S; ++i) {
+      const int64_t pos = 3 * g + e0 + i;
+      if (live && pos < n_up && pos < walk_end && !((hbits >> i) & 1u)) flatbits |= 1u << i;
+    }
+  }
   // waves holding header slots (layout check) or keep slots (keep_bits: their chains run
   // on code 0 up to the last client, whose codes the merged output keeps): wave-uniform
   const bool wave_keep = __ballot(keep_bits<S>(hbits, live, 3 * g + e0, walk_end) != 0) != 0;
@@ -659,9 +512,16 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
     }
     float y0[S], y[S], p[S];
     dec_stage_d16<S>(y0, codes, &dtab);
-    q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
-    dampen_stage<S>(y, dampen[c]);
-    q_stage_d16<S>(p, y, &dtab, tab.var, dmax);
+    if constexpr (KD) {  // stages A and B feed the side outputs: the exact in-stage fallback
+      q_stage_d16x<S>(y, y0, &dtab, tab.var);
+      dampen_stage<S>(y, dampen[c]);
+      q_stage_d16x<S>(p, y, &dtab, tab.var);
+      kardam_lane_step<S>(p, c, flatbits, live, 3 * g + e0, n_up, kd, dtab, tab, kd_part + (size_t)c * kd_stride);
+    } else {
+      q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
+      dampen_stage<S>(y, dampen[c]);
+      q_stage_d16<S>(p, y, &dtab, tab.var, dmax);
+    }
     if (c == 0) {
 #pragma unroll
       for (int i = 0; i < S; ++i) acc[i] = p[i];
@@ -720,20 +580,24 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
 }
 
 // Block `bid` of the SIMD-balanced stream grid (tables already in LDS).
-template <int NT>
+template <int NT, bool KD = false>
 __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D16Table& dtab, int64_t bid,
                                                    const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                    const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                                    int64_t g_begin, int64_t g_end,
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
-                                                   float* __restrict__ merged_f32, int* __restrict__ err, int nA) {
+                                                   float* __restrict__ merged_f32, int* __restrict__ err, int nA,
+                                                   const KardamOut& kd = KardamOut{}) {
   uint32_t bad = 0, layout_bad = 0;
+  // Kardam: this wave's partial slot of client 0; one slot per wave of the grid
+  const size_t nw = (size_t)gridDim.x * (NT / 64);
+  double* kd_part = KD ? kd.partials + 2 * ((size_t)bid * (NT / 64) + (threadIdx.x >> 6)) : nullptr;
   if (bid < nA) {  // block-uniform: one group per lane
     const int64_t g = g_begin + bid * NT + threadIdx.x;
     const bool live = g < g_end;
     int32_t out[3];
-    update_lane<3>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out, bad,
-                   layout_bad);
+    update_lane<3, KD>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out, bad,
+                       layout_bad, kd, kd_part, 2 * nw);
     if (!live) return;
     if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
@@ -747,8 +611,8 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
     const int e = lane % 3;
     const bool live = lane < 63 && g < g_end;
     int32_t out[1];
-    update_lane<1>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, e, live, g_begin, hdr_block, out, bad,
-                   layout_bad);
+    update_lane<1, KD>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, e, live, g_begin, hdr_block, out, bad,
+                       layout_bad, kd, kd_part, 2 * nw);
     const int base = lane - e;  // the group's three lanes (lane 63 reads its own)
     const int32_t o0 = __shfl(out[0], base), o1 = __shfl(out[0], base + 1), o2 = __shfl(out[0], base + 2);
     if (!live) return;
@@ -769,21 +633,27 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
 // blocks [0, nA) run whole rounds of group-per-lane waves, and the remaining
 // groups go to blocks of one value per lane (21 groups = 63 lanes per wave):
 // three times the waves at a third of the work each, spread over every SIMD
-// instead of a sixth full wave on some. Bit-identical to k_update<1>.
-template <int NT>
-__global__ void __launch_bounds__(NT) k_update_mixed(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+// instead of a sixth full wave on some. nA = gridDim.x: the plain grid.
+// KD = true adds Kardam's side outputs (kardam_lane_step; partial slots per wave);
+// its register budget asks for at least 6 waves per SIMD (the allocator lands on
+// 68 VGPRs: 7 waves, no scratch; unconstrained it takes 86 VGPRs: 5 waves).
+#ifndef FLEET_KD_STREAM_WAVES
+#define FLEET_KD_STREAM_WAVES 6  // A/B builds: -DFLEET_KD_STREAM_WAVES=1 (unconstrained)
+#endif
+template <int NT, bool KD>
+__global__ void __launch_bounds__(NT, KD ? FLEET_KD_STREAM_WAVES : 1) k_update_mixed(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                      const double* __restrict__ dampen, double inv_avg,
                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
                                                      const int32_t* __restrict__ hdr_block,
                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                     int* __restrict__ err, int nA) {
+                                                     int* __restrict__ err, int nA, KardamOut kd) {
   __shared__ B64Tables tab;
   __shared__ D16Table dtab;
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
   __syncthreads();
-  update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block,
-                         merged, merged_f32, err, nA);
+  update_mixed_block<NT, KD>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+                             hdr_block, merged, merged_f32, err, nA, kd);
 }
 
 // Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
@@ -1566,26 +1436,27 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
 // and hurts the tiled and pipelined kernels; the main unit only
 // declares their instantiations.
 #if defined(FLEET_STREAM_TU) || defined(FLEET_DEV_ALL_KERNELS)  // (dev tools that include this file: all here)
-template __global__ void k_update<1, true, 256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
-                                               double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
-                                               uint8_t* __restrict__, float* __restrict__, int* __restrict__,
-                                               KardamOut);
-template __global__ void k_update_mixed<256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
-                                             double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
-                                             uint8_t* __restrict__, float* __restrict__, int* __restrict__, int);
+template __global__ void k_update_mixed<256, false>(const uint8_t* __restrict__, size_t, int,
+                                                    const double* __restrict__, double, int64_t, int64_t, int64_t,
+                                                    const int32_t* __restrict__, uint8_t* __restrict__,
+                                                    float* __restrict__, int* __restrict__, int, KardamOut);
+template __global__ void k_update_mixed<256, true>(const uint8_t* __restrict__, size_t, int,
+                                                   const double* __restrict__, double, int64_t, int64_t, int64_t,
+                                                   const int32_t* __restrict__, uint8_t* __restrict__,
+                                                   float* __restrict__, int* __restrict__, int, KardamOut);
 template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_t, int, const double* __restrict__,
                                               double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
                                               uint8_t* __restrict__, float* __restrict__, int* __restrict__, int, int,
                                               EncodeJob);
 #else
-extern template __global__ void k_update<1, true, 256>(const uint8_t* __restrict__, size_t, int,
-                                                      const double* __restrict__, double, int64_t, int64_t, int64_t,
-                                                      const int32_t* __restrict__, uint8_t* __restrict__,
-                                                      float* __restrict__, int* __restrict__, KardamOut);
-extern template __global__ void k_update_mixed<256>(const uint8_t* __restrict__, size_t, int,
-                                                    const double* __restrict__, double, int64_t, int64_t, int64_t,
-                                                    const int32_t* __restrict__, uint8_t* __restrict__,
-                                                    float* __restrict__, int* __restrict__, int);
+extern template __global__ void k_update_mixed<256, false>(const uint8_t* __restrict__, size_t, int,
+                                                           const double* __restrict__, double, int64_t, int64_t,
+                                                           int64_t, const int32_t* __restrict__, uint8_t* __restrict__,
+                                                           float* __restrict__, int* __restrict__, int, KardamOut);
+extern template __global__ void k_update_mixed<256, true>(const uint8_t* __restrict__, size_t, int,
+                                                          const double* __restrict__, double, int64_t, int64_t,
+                                                          int64_t, const int32_t* __restrict__, uint8_t* __restrict__,
+                                                          float* __restrict__, int* __restrict__, int, KardamOut);
 extern template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_t, int,
                                                      const double* __restrict__, double, int64_t, int64_t, int64_t,
                                                      const int32_t* __restrict__, uint8_t* __restrict__,
@@ -2244,7 +2115,7 @@ static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o) {
 std::string update_kernel_name(int64_t groups) {
   const UpdatePlan p = plan_update(groups, plan_overrides());
   char buf[64];
-  if (p.kind == 0) snprintf(buf, sizeof buf, "k_update_mixed<256>");
+  if (p.kind == 0) snprintf(buf, sizeof buf, "k_update_mixed<256, false>");
   else if (p.kind == 2) snprintf(buf, sizeof buf, "k_update_pipe<16, 1, 5, 0>");
   else snprintf(buf, sizeof buf, "k_update_tiled<64, false, %d, true>", p.t.nW >= 0 ? 16 : 0);  // as rocprofv3 names it
   return buf;
@@ -2286,48 +2157,45 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
     launch_tiled<false>(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
                         d_err, KardamOut{}, s);
   else
-    hipLaunchKernelGGL((k_update_mixed<256>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
-                       inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.nA);
+    hipLaunchKernelGGL((k_update_mixed<256, false>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M,
+                       d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.nA,
+                       KardamOut{});
   return hipGetLastError();
 }
 
 // per client: the (client, wave or tile) partials of the update summed in a fixed
-// order. A lane sums a strided run of partial pairs (8 independent 16-byte loads in
-// flight), the wave folds its lanes by butterfly shuffles, the block's waves meet
-// in LDS. One wave per client for the tiles' few hundred partials (no barrier on
-// the path: the reduce is latency, 6 us with a 256-thread LDS tree on MNIST-64),
-// four for the stream grid's thousands.
-template <int NT>
+// order. The reduce is pure latency (a few hundred to a few thousand 16-byte pairs
+// per client), so a lane issues all of its U loads before the first add (one HBM
+// round trip, not one per 8 loads), the pairs fold in a fixed tree, the wave by DPP
+// lane moves (group_sum_f64: no LDS crossbar round trips), and the block's waves meet
+// in LDS. One wave per client up to 2,048 partials (the tiles), four beyond (the
+// stream grid's thousands of waves); past U * NT a strided loop takes the rest.
+template <int NT, int U>
 __global__ void __launch_bounds__(NT) k_kardam_reduce(const double* __restrict__ partials, int64_t n_waves,
                                                       double* __restrict__ norms) {
   typedef double d2 __attribute__((ext_vector_type(2)));
   const int c = blockIdx.x;
   const d2* p = reinterpret_cast<const d2*>(partials) + (size_t)c * n_waves;
-  d2 acc[8];
+  d2 v[U];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) acc[u] = d2{0.0, 0.0};
-  int64_t w = threadIdx.x;
-  for (; w + 7 * NT < n_waves; w += 8 * NT)
-#pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] += p[w + u * NT];
-#pragma unroll
-  for (int u = 0; u < 8; ++u)
-    if (w + u * NT < n_waves) acc[u] += p[w + u * NT];
-  double a = ((acc[0].x + acc[1].x) + (acc[2].x + acc[3].x)) + ((acc[4].x + acc[5].x) + (acc[6].x + acc[7].x));
-  double b = ((acc[0].y + acc[1].y) + (acc[2].y + acc[3].y)) + ((acc[4].y + acc[5].y) + (acc[6].y + acc[7].y));
-#pragma unroll
-  for (int s = 32; s > 0; s >>= 1) {
-    a += __shfl_xor(a, s);
-    b += __shfl_xor(b, s);
+  for (int u = 0; u < U; ++u) {
+    const int64_t w = threadIdx.x + (int64_t)u * NT;
+    v[u] = w < n_waves ? p[w] : d2{0.0, 0.0};
   }
+  for (int64_t w = threadIdx.x + (int64_t)U * NT; w < n_waves; w += NT) v[0] += p[w];
+#pragma unroll
+  for (int h = U / 2; h > 0; h /= 2)
+#pragma unroll
+    for (int u = 0; u < h; ++u) v[u] += v[u + h];
+  const double a = group_sum_f64<64>(v[0].x), b = group_sum_f64<64>(v[0].y);  // valid in lane 63
   if constexpr (NT == 64) {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 63) {
       norms[2 * c] = a;
       norms[2 * c + 1] = b;
     }
   } else {
     __shared__ double red[2][NT / 64];
-    if ((threadIdx.x & 63) == 0) {
+    if ((threadIdx.x & 63) == 63) {
       red[0][threadIdx.x / 64] = a;
       red[1][threadIdx.x / 64] = b;
     }
@@ -2351,10 +2219,10 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   const int64_t groups = g_end - g_begin;
   // the update's own launch plan with the side outputs: the pipelined tiles with 7
   // producer waves (the side outputs double the producers' work), the wide tiles, or
-  // the stream grid group-per-lane; partial slots per client = tiles or stream waves
+  // the stream kernel's SIMD-balanced grid; partial slots per client = tiles or stream waves
   const UpdatePlan p = plan_update(groups, plan_overrides());
-  const unsigned blocks = p.kind == 0 ? blocks_for(groups, 256) : (unsigned)p.blocks;
-  *n_waves = p.kind == 0 ? (int)blocks * 4 : (int)blocks;
+  const unsigned blocks = (unsigned)p.blocks;
+  *n_waves = p.kind == 0 ? (int)blocks * 4 : (int)blocks;  // stream: a slot per wave; tiles: per tile
   if (groups <= 0) return hipSuccess;
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
   if (p.kind == 2)
@@ -2365,13 +2233,17 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
     launch_tiled<true>(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
                        d_err, kd, s);
   else
-    hipLaunchKernelGGL((k_update<1, true>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
-                       g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd);
-  if (*n_waves <= 2048)
-    hipLaunchKernelGGL(k_kardam_reduce<64>, dim3((unsigned)M), dim3(64), 0, s, kd.partials, (int64_t)*n_waves, norms);
-  else
-    hipLaunchKernelGGL(k_kardam_reduce<256>, dim3((unsigned)M), dim3(256), 0, s, kd.partials, (int64_t)*n_waves,
+    hipLaunchKernelGGL((k_update_mixed<256, true>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
+                       inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.nA, kd);
+  if (*n_waves <= 512)
+    hipLaunchKernelGGL((k_kardam_reduce<64, 8>), dim3((unsigned)M), dim3(64), 0, s, kd.partials, (int64_t)*n_waves,
                        norms);
+  else if (*n_waves <= 2048)
+    hipLaunchKernelGGL((k_kardam_reduce<64, 32>), dim3((unsigned)M), dim3(64), 0, s, kd.partials, (int64_t)*n_waves,
+                       norms);
+  else
+    hipLaunchKernelGGL((k_kardam_reduce<256, 32>), dim3((unsigned)M), dim3(256), 0, s, kd.partials,
+                       (int64_t)*n_waves, norms);
   return hipGetLastError();
 }
 

@@ -29,6 +29,21 @@ def scatter_flat(flat, layout):
 @pytest.mark.parametrize("layout,M", [(MNIST, 6), (synthetic(3001), 4), (CIFAR10, 5), (synthetic(120_001), 3),
                                       (synthetic(1_048_576), 2)])
 def test_kardam_side_outputs(codec, oracle, layout, M):
+    check_side_outputs(codec, oracle, layout, M)
+
+
+@pytest.mark.parametrize("spec", ["update=stream,grid=plain", "update=stream,grid=lanes", "update=stream",
+                                  "update=tiled", "update=tiled,tile_mix=off", "update=pipe"])
+def test_kardam_side_outputs_under_plans(codec, oracle, plan, spec):
+    """Every launch plan's Kardam form on ragged sizes: the stream kernel's group-per-
+    lane and value-per-lane blocks (k_update_mixed<256, true>), both tile grids, the
+    pipelined tiles."""
+    plan(spec)
+    for layout, M in ((synthetic(3001), 4), (synthetic(50_003), 3), (MNIST, 5)):
+        check_side_outputs(codec, oracle, layout, M)
+
+
+def check_side_outputs(codec, oracle, layout, M):
     dev = torch.device("cuda", 0)
     lr = 0.05
     d = [1.0 / ((c % 3) + 1) for c in range(M)]
