@@ -24,8 +24,8 @@ hipError_t launch_descent(float* weights, float* fc_bias, const float* grad, con
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s);
-// Kardam's side outputs of the fused update (k_update<1, true>): per client c and
-// flat value (upload positions that are neither header slots nor past the walk)
+// Kardam's side outputs of the fused update (k_update_mixed<256, true>, the tiles, the
+// pipelined tiles): per client c and flat value (upload positions that are neither header slots nor past the walk)
 //   G = Q(f32(f64(p) lr))            the decoded Kardam.setGrad text (p = stage B)
 //   D = Q(G - prev[c])               the decoded g.subtract(prev) text (has_prev[c])
 // partials[(c * n_waves + w) * 2 + {0, 1}] = per-wave sums of (double)(G*G), (double)(D*D);
