@@ -2238,7 +2238,10 @@ static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o) {
       const int64_t waves = (groups + 63) / 64;
       p.nA = waves < simds ? (int)plain : (int)(waves / simds * simds * 64 / 256);
     }
-    p.blocks = p.nA + (groups - (int64_t)p.nA * 256 + 83) / 84;
+    // the value-per-lane blocks take what the group-per-lane rounds leave (none when
+    // the plain grid covers every group: its last block is ragged)
+    const int64_t rest = groups - (int64_t)p.nA * 256;
+    p.blocks = p.nA + (rest > 0 ? (rest + 83) / 84 : 0);
   }
   return p;
 }
