@@ -399,8 +399,12 @@ def test_update_keep_slots_past_the_walk(codec, oracle, plan, spec, extra):
     kernels still run the chain on those lanes (on code 0, so no lane of a wave leaves
     the fast path); the values there are large enough (3e8..9.9e8) that a chain on
     the real codes would overflow the digit domain within a few clients. Same bytes
-    as the per-op chain and as the fused oracle with those slots masked; the Kardam
-    update's merged text too. extra = 201 leaves the last group ragged."""
+    as the per-op chain and as the fused oracle with those slots masked. The device-
+    resident entry points take the caller's header positions as a layout that covers
+    the whole upload (fleet_codec.h), so there the tail is payload: the Kardam update's
+    merged text is the fused oracle's with only the header slots kept (the tail's
+    sums leave the fast domain: the exact general-codec recompute). extra = 201 leaves
+    the last group ragged."""
     torch = pytest.importorskip("torch")
     plan(spec)
     lay = synthetic(1000)
@@ -427,7 +431,8 @@ def test_update_keep_slots_past_the_walk(codec, oracle, plan, spec, extra):
                                None, None, g_out)
     codec.check()
     torch.cuda.synchronize()
-    assert merged.cpu().numpy()[:L].tobytes() == exp
+    hm_dev = np.concatenate([oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes)), np.zeros(extra, np.uint8)])
+    assert merged.cpu().numpy()[:L].tobytes() == oracle.update_fused(ups, d, hm_dev)
 
 
 def test_device_window_update(codec, oracle):
