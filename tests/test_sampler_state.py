@@ -259,14 +259,18 @@ def test_shim_iid_mode1_session_with_teacher(tmp_path, oracle, monkeypatch, capf
     assert L.Java_apps_cppNN_FleetSampler_setTeacherNative(env, None, J.new_floats(w[:-1]), J.new_floats(b)) == 0
     assert L.Java_apps_cppNN_FleetSampler_setTeacherNative(env, None, J.new_floats(w), J.new_floats(b)) == 1
     check_rules(J)
-    # the generator: initUpdater's srand(1) + two draws, then B = batch * E draws per request
+    # the generator: initUpdater's srand(1) + two draws, then B = batch * E draws per request.
+    # libc's rand() state is the process's, shared with the shim: replay the expected
+    # indices first, then put the state back where initUpdater left it
     lc = _libc()
+    B = batch * E
     lc.srand(1)
     lc.rand(), lc.rand()
-    B = batch * E
+    wants = [[lc.rand() % n for _ in range(B)] for _ in range(2)]
+    lc.srand(1)
+    lc.rand(), lc.rand()
     hdr = np.array([E, 0.5, 2.0, np.float32(lrates[0]), B, 784, 10], np.float64).astype(np.float32)
-    for _ in range(2):
-        want = [lc.rand() % n for _ in range(B)]
+    for want in wants:
         J.begin()
         text = J.read_bytes(L.Java_apps_cppNN_CppNNOfflineSampler_getMiniBatch(env, None, batch))
         check_rules(J)
