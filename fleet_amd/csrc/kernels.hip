@@ -891,11 +891,15 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const T
   }
 }
 
-template <int TG, int IPT, int NW, bool KD = false, bool D16 = false>
+// PS: also store every live item's p in the rows p_out (client c at c * p_pitch, upload
+// coordinates; 0 in header slots and past the walk) -- Kardam's pipelined form
+// (k_update_pipe<..., KD = true> + k_kardam_finish).
+template <int TG, int IPT, int NW, bool KD = false, bool D16 = false, bool PS = false>
 __device__ __forceinline__ void tile_compute(TileShared<TG, NW, D16>& sh, const TileItems<TG, IPT>& it, int M,
                                              const double* __restrict__ dampen, int64_t n_up, int64_t walk_end,
                                              int64_t g0, float* __restrict__ pdst, uint32_t& badacc,
-                                             const TileKd& tk = TileKd{}) {
+                                             const TileKd& tk = TileKd{}, float* __restrict__ p_out = nullptr,
+                                             size_t p_pitch = 0) {
   constexpr int E = 3 * TG, S = 3 * IPT;
   int32_t codes[S];
 #pragma unroll
@@ -960,6 +964,26 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW, D16>& sh, const 
 #pragma unroll
       for (int e = 0; e < 3; ++e) pdst[it.cc[h] * E + 3 * it.gl[h] + e] = p[3 * h + e];
   if constexpr (KD) tile_kardam<TG, IPT, NW>(sh, it, p, n_up, g0, tk);
+  if constexpr (PS) {
+    typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+#pragma unroll
+    for (int h = 0; h < IPT; ++h) {
+      if (!it.live[h]) continue;
+      const int64_t gp = 3 * (g0 + it.gl[h]);
+      const uint32_t hm = sh.hmask[it.gl[h]];
+      float v[3];
+#pragma unroll
+      for (int e = 0; e < 3; ++e) v[e] = (((hm >> e) & 1u) || gp + e >= walk_end) ? 0.0f : p[3 * h + e];
+      float* dst = p_out + (size_t)(it.c_base + it.cc[h]) * p_pitch + gp;
+      if (gp + 2 < n_up) {
+        *reinterpret_cast<f3u*>(dst) = f3u{v[0], v[1], v[2]};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+          if (gp + e < n_up) dst[e] = v[e];
+      }
+    }
+  }
 }
 
 template <int TG, int IPT, int NW, bool KD = false, bool D16 = false>
@@ -1225,130 +1249,6 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
   }
 }
 
-// Kardam's side outputs as blocks of their own riding in the pipelined update's
-// launch (k_update_pipe<..., KD = true>: the blocks past the tiles, as the client
-// encode rides in the pipelined step). The pipelined tiles are latency-bound -- one
-// serial consumer wave per tile, most issue slots of the chip idle
-// -- so Kardam's client-independent work (its own decode and stages A, B of the same
-// uploads, then G = Q(f32(f64(p) * lr)), D = Q(G - prev) and the two squared norms;
-// SURVEY.md f2, CppNNUpdater.java:463-481, Kardam.java:48-106) runs in those idle
-// slots instead of doubling the producers' work on the critical path. Block = (client
-// c, chunk of kKjGroupsPerLane * NT groups), kKjGroupsPerLane groups per lane (their
-// chains interleave); the block's sums meet in LDS in a fixed order: one partial slot
-// per (client, chunk), summed by k_kardam_reduce.
-constexpr int kKjGroupsPerLane = 2;
-__host__ __device__ constexpr int64_t kj_chunks(int64_t groups, int nt) {
-  return (groups + (int64_t)kKjGroupsPerLane * nt - 1) / ((int64_t)kKjGroupsPerLane * nt);
-}
-template <int NT>
-__device__ __forceinline__ void kardam_job_block(const B64Tables& tab, double* red, int64_t bid,
-                                                 const uint8_t* __restrict__ uploads, size_t pitch,
-                                                 const double* __restrict__ dampen, int64_t n_up, int64_t g_begin,
-                                                 int64_t g_end, const int32_t* __restrict__ hdr_block,
-                                                 const KardamOut& kd) {
-  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
-  constexpr int IPL = kKjGroupsPerLane, S = 3 * IPL;
-  const int64_t nchunk = kj_chunks(g_end - g_begin, NT);
-  const int c = (int)(bid / nchunk);
-  const int64_t ch = bid % nchunk;
-  const int n_hdr = hdr_block[1];
-  const int64_t walk_end = hdr_block[2];
-  const int32_t* hdr = hdr_block + 4;
-  int64_t g[IPL];
-  bool live[IPL];
-  uint4 w[IPL];
-#pragma unroll
-  for (int h = 0; h < IPL; ++h) {
-    g[h] = g_begin + ch * (IPL * NT) + h * NT + threadIdx.x;
-    live[h] = g[h] < g_end;
-    w[h] = *reinterpret_cast<const uint4*>(uploads + (size_t)c * pitch + 16 * (live[h] ? g[h] : g_begin));
-  }
-  // flat-gradient slots; the others (headers, past the walk, past n_up, dead lanes)
-  // run on code 0 and are masked out (the tiles report Base64 and layout errors)
-  int32_t codes[S];
-  uint32_t flat = 0;
-#pragma unroll
-  for (int h = 0; h < IPL; ++h) {
-    b64_decode_group(w[h], &tab, codes + 3 * h);
-    const uint32_t hb = live[h] ? header_bits(hdr, n_hdr, 3 * g[h]) : 7u;
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      const int64_t pos = 3 * g[h] + e;
-      if (live[h] && pos < n_up && pos < walk_end && !((hb >> e) & 1u)) flat |= 1u << (3 * h + e);
-      else codes[3 * h + e] = 0;
-    }
-  }
-  float y0[S], y[S], p[S], G[S];
-  dec_stage<S>(y0, codes, &tab);
-  q_stage<S>(y, y0, &tab);
-  dampen_stage<S>(y, dampen[c]);  // block-uniform client
-  q_stage<S>(p, y, &tab);
-  dampen_stage<S>(p, kd.lr);
-  q_stage<S>(G, p, &tab);
-  double sg = 0.0, sd = 0.0;
-#pragma unroll
-  for (int i = 0; i < S; ++i)
-    if ((flat >> i) & 1u) sg += (double)(G[i] * G[i]);
-  if (kd.prev && kd.has_prev[c]) {  // block-uniform
-    float dv[S], D[S];
-#pragma unroll
-    for (int h = 0; h < IPL; ++h) {
-      const float* pr = kd.prev + (size_t)c * kd.vpitch + 3 * g[h];
-      float pv[3] = {0.0f, 0.0f, 0.0f};
-      if (live[h] && 3 * g[h] + 2 < n_up) {
-        const f3u t = *reinterpret_cast<const f3u*>(pr);
-        pv[0] = t.x;
-        pv[1] = t.y;
-        pv[2] = t.z;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 3; ++e)
-          if ((flat >> (3 * h + e)) & 1u) pv[e] = pr[e];
-      }
-#pragma unroll
-      for (int e = 0; e < 3; ++e) dv[3 * h + e] = ((flat >> (3 * h + e)) & 1u) ? G[3 * h + e] - pv[e] : 0.0f;
-    }
-    q_stage<S>(D, dv, &tab);
-#pragma unroll
-    for (int i = 0; i < S; ++i)
-      if ((flat >> i) & 1u) sd += (double)(D[i] * D[i]);
-  }
-  if (kd.g_out) {
-#pragma unroll
-    for (int h = 0; h < IPL; ++h) {
-      float* go = kd.g_out + (size_t)c * kd.vpitch + 3 * g[h];
-      float gv[3];
-#pragma unroll
-      for (int e = 0; e < 3; ++e) gv[e] = ((flat >> (3 * h + e)) & 1u) ? G[3 * h + e] : 0.0f;
-      if (live[h] && 3 * g[h] + 2 < n_up) {
-        *reinterpret_cast<f3u*>(go) = f3u{gv[0], gv[1], gv[2]};
-      } else {
-#pragma unroll
-        for (int e = 0; e < 3; ++e)
-          if (live[h] && 3 * g[h] + e < n_up) go[e] = gv[e];
-      }
-    }
-  }
-  sg = group_sum_f64<64>(sg);  // every lane of the block is here
-  sd = group_sum_f64<64>(sd);
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 63) {
-    red[2 * wave] = sg;
-    red[2 * wave + 1] = sd;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double a = 0.0, b = 0.0;
-    for (int v = 0; v < NT / 64; ++v) {
-      a += red[2 * v];
-      b += red[2 * v + 1];
-    }
-    const size_t slot = ((size_t)c * nchunk + ch) * 2;
-    kd.partials[slot] = a;
-    kd.partials[slot + 1] = b;
-  }
-}
-
 // Pipelined tile variant (E = 3*TG <= 64): producer waves compute p for passes
 // of clients into an LDS ring while wave 0 consumes them in client order (the
 // serial A = Q(A + p_c)), so the client-independent work and the serial
@@ -1358,8 +1258,9 @@ __device__ __forceinline__ void kardam_job_block(const B64Tables& tab, double* r
 //           a pass is ready after one wave's work -- the consumer starts
 //           early -- while the NW-1 producer waves work on successive passes
 //           in parallel.
-// Blocks [nU, ...): the next batch's client encode (ej; the pipelined step) or,
-// KD = true, Kardam's side outputs (kardam_job_block, one per (client, chunk)).
+// Blocks [nU, ...): the next batch's client encode (ej; the pipelined step).
+// KD = true: the producers also store every item's p in Kardam's G rows (kd.g_out or
+// scratch), which k_kardam_finish turns into G, D and the norms (launch_update_kardam).
 // Hand-off through LDS: a producer wave publishes its count of finished passes
 // with a workgroup release after its p writes; the consumer acquires it before
 // reading a pass, and publishes "passes consumed" so producers never overwrite
@@ -1385,7 +1286,6 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   __shared__ float finals[E];
   __shared__ int prog[NPW];  // passes finished by each producer wave
   __shared__ int consumed;   // passes finished by the consumer
-  __shared__ double kred[KD ? 2 * NW : 1];  // Kardam job blocks: the waves' sums
   // wave index made wave-uniform (readfirstlane), so the producer/consumer
   // split below is a scalar branch and the consumer's s_setprio is its own
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
@@ -1393,10 +1293,6 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
     b64_tables_init<64 * NW>(&sh.tab);
     __syncthreads();
     const int64_t e = (int64_t)blockIdx.x - nU;
-    if constexpr (KD) {
-      kardam_job_block<64 * NW>(sh.tab, kred, e, uploads, pitch, dampen, n_up, g_begin, g_end, hdr_block, kd);
-      return;
-    }
     // the next batch's client encode (fleet_update_encode_device)
     encode_rows<false, 64 * NW>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                                 (int)(e / ej.gx), &sh.tab, nullptr);
@@ -1430,7 +1326,9 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
         while (__hip_atomic_load(&consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < pass - RING + 1)
           __builtin_amdgcn_s_sleep(1);
       }
-      tile_compute<TG, IPT, NW>(sh, cur, M, dampen, n_up, hdr_block[2], g0, ptile + (pass % RING) * CPP * E, badacc);
+      tile_compute<TG, IPT, NW, false, false, KD>(sh, cur, M, dampen, n_up, hdr_block[2], g0,
+                                                  ptile + (pass % RING) * CPP * E, badacc, TileKd{}, kd.g_out,
+                                                  kd.vpitch);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       ++done;
       if (lane == 0) __hip_atomic_store(&prog[w], done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2346,26 +2244,151 @@ __global__ void __launch_bounds__(NT) k_kardam_reduce(const double* __restrict__
   }
 }
 
+// Kardam's side outputs of the pipelined form (CppNNUpdater.java:463-481,
+// Kardam.java:48-106). The pipelined tiles are latency-bound -- one serial consumer
+// wave per tile -- so Kardam's two extra Q stages stay off them:
+// their producers only store each (client, value)'s p in `rows` (k_update_pipe<...,
+// KD = true>), and this kernel, one block per client, turns the row into G =
+// Q(f32(f64(p) * lr)) (into g_out when given: 0 off the flat gradient), ||G||^2 and,
+// with the worker's previous G, ||Q(G - prev)||^2. The norms come out directly in a
+// fixed order (a lane's groups in turn, the wave by DPP, the block's waves in LDS):
+// no partial slots and no separate reduce. rows may be g_out (each lane reads its p
+// before writing its G); prev must not overlap rows (it may be g_out: a lane reads
+// prev before writing G at the same slots).
+template <int NT>
+__global__ void __launch_bounds__(NT) k_kardam_finish(const float* rows, size_t rpitch, float* g_out,
+                                                      int64_t n_up, const int32_t* __restrict__ hdr_block,
+                                                      const float* prev, size_t gpitch,
+                                                      const uint8_t* __restrict__ has_prev, double lr,
+                                                      double* __restrict__ norms) {
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+  __shared__ B64Tables tab;
+  __shared__ double red[2][NT / 64];
+  b64_tables_init<NT>(&tab);
+  __syncthreads();
+  const int c = blockIdx.x;
+  const int n_hdr = hdr_block[1];
+  const int64_t walk_end = hdr_block[2];
+  const int32_t* hdr = hdr_block + 4;
+  const bool hasp = prev && has_prev[c];  // block-uniform
+  const float* row = rows + (size_t)c * rpitch;
+  const float* prow = hasp ? prev + (size_t)c * gpitch : nullptr;
+  float* grow = g_out ? g_out + (size_t)c * gpitch : nullptr;
+  const int64_t groups = (n_up + 2) / 3;
+  double sg = 0.0, sd = 0.0;
+  for (int64_t base = 0; base < groups; base += NT) {  // uniform trip count: every lane in every ballot
+    const int64_t g = base + threadIdx.x;
+    const bool live = g < groups;
+    const int64_t gp = 3 * g;
+    const bool whole = live && gp + 2 < n_up;
+    const uint32_t hb = live ? header_bits(hdr, n_hdr, gp) : 7u;
+    uint32_t flat = 0;
+#pragma unroll
+    for (int e = 0; e < 3; ++e)
+      if (live && gp + e < n_up && gp + e < walk_end && !((hb >> e) & 1u)) flat |= 1u << e;
+    float pv[3] = {0.0f, 0.0f, 0.0f};
+    if (whole) {
+      const f3u t = *reinterpret_cast<const f3u*>(row + gp);
+      pv[0] = t.x;
+      pv[1] = t.y;
+      pv[2] = t.z;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if ((flat >> e) & 1u) pv[e] = row[gp + e];
+    }
+#pragma unroll
+    for (int e = 0; e < 3; ++e)
+      if (!((flat >> e) & 1u)) pv[e] = 0.0f;
+    float G[3];
+    dampen_stage<3>(pv, lr);  // lr is uniform
+    q_stage<3>(G, pv, &tab);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      if (!((flat >> e) & 1u)) G[e] = 0.0f;
+      sg += (double)(G[e] * G[e]);
+    }
+    if (hasp) {
+      float qv[3] = {0.0f, 0.0f, 0.0f}, dv[3], D[3];
+      if (whole) {
+        const f3u t = *reinterpret_cast<const f3u*>(prow + gp);
+        qv[0] = t.x;
+        qv[1] = t.y;
+        qv[2] = t.z;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+          if ((flat >> e) & 1u) qv[e] = prow[gp + e];
+      }
+#pragma unroll
+      for (int e = 0; e < 3; ++e) dv[e] = ((flat >> e) & 1u) ? G[e] - qv[e] : 0.0f;
+      q_stage<3>(D, dv, &tab);
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if ((flat >> e) & 1u) sd += (double)(D[e] * D[e]);
+    }
+    if (grow) {
+      if (whole) {
+        *reinterpret_cast<f3u*>(grow + gp) = f3u{G[0], G[1], G[2]};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+          if (live && gp + e < n_up) grow[gp + e] = G[e];
+      }
+    }
+  }
+  sg = group_sum_f64<64>(sg);  // valid in lane 63
+  sd = group_sum_f64<64>(sd);
+  if ((threadIdx.x & 63) == 63) {
+    red[0][threadIdx.x / 64] = sg;
+    red[1][threadIdx.x / 64] = sd;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0;
+    for (int i = 0; i < NT / 64; ++i) {
+      a += red[0][i];
+      b += red[1][i];
+    }
+    norms[2 * c] = a;
+    norms[2 * c + 1] = b;
+  }
+}
+
 hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                                 int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
                                 double* norms, hipStream_t s) {
   const int64_t groups = g_end - g_begin;
-  // the update's own launch plan with the side outputs: the pipelined tiles with
-  // Kardam's job blocks riding after them, the wide tiles (side outputs from the tile
-  // producers), or the stream kernel's SIMD-balanced grid
+  // the update's own launch plan with the side outputs: the pipelined tiles (their
+  // producers store p; k_kardam_finish does the rest), the wide tiles (side outputs
+  // from the tile producers), or the stream kernel's SIMD-balanced grid
   const UpdatePlan p = plan_update(groups, plan_overrides());
   const unsigned blocks = (unsigned)p.blocks;
-  // partial slots per client: a wave of the stream grid, a tile, or a Kardam job block
-  // of the pipelined launch (a chunk of groups)
-  *n_waves = p.kind == 0 ? (int)blocks * 4 : p.kind == 1 ? (int)blocks : (int)kj_chunks(groups, 64 * 5);
+  // partial slots per client: a wave of the stream grid or a tile; the pipelined form
+  // uses the slots' bytes as its p rows (4 floats a slot) unless they can go straight
+  // into the caller's G rows
+  *n_waves = p.kind == 0 ? (int)blocks * 4 : p.kind == 1 ? (int)blocks : (int)((n_up + 3) / 4);
   if (groups <= 0) return hipSuccess;
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
-  if (p.kind == 2)
-    hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0, true>), dim3((unsigned)(blocks + (int64_t)M * *n_waves)),
-                       dim3(64 * 5), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block,
-                       merged, merged_f32, d_err, (int)blocks, EncodeJob{}, kd);
-  else if (p.kind == 1)
+  if (p.kind == 2) {
+    // p rows: the caller's G rows, unless there are none or they overlap prev (G may
+    // replace prev in place: prev must stay intact until k_kardam_finish reads it)
+    const size_t span = (size_t)M * kd.vpitch;
+    const bool overlap = kd.g_out && kd.prev && kd.g_out < kd.prev + span && kd.prev < kd.g_out + span;
+    KardamOut kp = kd;
+    if (!kd.g_out || overlap) {
+      kp.g_out = reinterpret_cast<float*>(kd.partials);
+      kp.vpitch = (size_t)((n_up + 3) / 4 * 4);
+    }
+    hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0, true>), dim3(blocks), dim3(64 * 5), 0, s, uploads, pitch, M,
+                       d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
+                       EncodeJob{}, kp);
+    hipLaunchKernelGGL(k_kardam_finish<1024>, dim3((unsigned)M), dim3(1024), 0, s, kp.g_out, kp.vpitch, kd.g_out,
+                       n_up, d_hdr_block, kd.prev, kd.vpitch, kd.has_prev, kd.lr, norms);
+    return hipGetLastError();
+  }
+  if (p.kind == 1)
     launch_tiled<true>(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
                        d_err, kd, s);
   else

@@ -191,7 +191,8 @@ int fleet_update_encode_device(fleet_ctx* ctx, const void* d_uploads, size_t pit
  * with prev_c = the worker's previous G (d_prev: M rows of vpitch floats in
  * upload coordinates, header slots ignored; NULL = none) and, when d_g_out is
  * given, this round's G written there in the same layout (the next round's
- * prev). Whole uploads (all groups); synchronous (the norms are host outputs);
+ * prev; d_g_out may be d_prev itself: G then replaces prev in place). Whole
+ * uploads (all groups); synchronous (the norms are host outputs);
  * not for graph capture. Norms: fixed-order partial sums of the reference's
  * fp64 loop (1e-12 relative, like fleet_norm). */
 int fleet_update_kardam_device(fleet_ctx* ctx, const void* d_uploads, size_t pitch, size_t len, int M,

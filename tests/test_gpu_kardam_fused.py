@@ -52,7 +52,7 @@ def check_side_outputs(codec, oracle, layout, M):
     vpitch = layout.n_up + 3
     hpos = layout.header_positions()
 
-    def round_(seed, prev_texts, prev_dev, has):
+    def round_(seed, prev_texts, prev_dev, has, in_place=False):
         ups = [oracle.encode_floats(oracle.synth_upload(seed, c, list(layout.w_sizes), list(layout.b_sizes)))
                for c in range(M)]
         host = np.zeros((M, pitch), np.uint8)
@@ -60,7 +60,8 @@ def check_side_outputs(codec, oracle, layout, M):
             host[c, :L] = np.frombuffer(u, np.uint8)
         t = torch.from_numpy(host).to(dev)
         merged = torch.zeros(pitch, dtype=torch.uint8, device=dev)
-        g_out = torch.zeros((M, vpitch), dtype=torch.float32, device=dev)
+        # in_place: this round's G replaces prev in the same rows
+        g_out = prev_dev if in_place else torch.zeros((M, vpitch), dtype=torch.float32, device=dev)
         ng, nd = codec.update_kardam_device(t, L, d, hpos, lr, merged, None, prev_dev, has, g_out)
         codec.check()
         print(layout.n_up, M, F.update_kernel(L))
@@ -85,4 +86,5 @@ def check_side_outputs(codec, oracle, layout, M):
 
     g1, g1_dev = round_(31, None, None, None)
     has = [c % 2 == 0 for c in range(M)]
-    round_(32, g1, g1_dev, has)
+    g2, g2_dev = round_(32, g1, g1_dev, has)
+    round_(33, g2, g2_dev, [True] * M, in_place=True)
