@@ -11,6 +11,10 @@
 #define FLEET_ERRBIT_ARG 4
 
 namespace fleet {
+
+// FLEET_MAX_HEADERS of fleet_codec.h (checked there): header positions a kernel may
+// hold in LDS
+constexpr int kMaxHeaderSlots = 4096;
 // segments of descentNative's model step (k_descent): kind 0 = weight block,
 // 1 = fully-connected bias block; offsets in floats
 constexpr int kMaxDescentSegs = 64;

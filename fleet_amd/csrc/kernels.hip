@@ -35,9 +35,6 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
-#ifndef FLEET_PRIO_LADDER
-#define FLEET_PRIO_LADDER 0
-#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -459,7 +456,7 @@ __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uin
 // share a group). Returns the lane's merged codes in out[S] and its Base64 / layout
 // error bits; tables already in LDS. KD: Kardam's side outputs per client
 // (kardam_lane_step; kd_part = this wave's slot of client 0, kd_stride between clients).
-template <int S, bool KD = false>
+template <int S, bool KD = false, bool LADDER = false>
 __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table& dtab,
                                             const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                             const double* __restrict__ dampen, double inv_avg, int64_t n_up,
@@ -544,20 +541,21 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // registers (no copies between trips)
   Row b0 = group_of(0), b1;
   int c = 0;
-#if FLEET_PRIO_LADDER
-  // experiment: issue priority falls as a wave gets ahead (3 -> 0 at quarters of the
-  // client loop), so the waves of a SIMD keep step instead of finishing one by one
-  // in age order (the tail of a single-round grid, profiles/r04/window_traces.txt)
+  // LADDER: issue priority falls as a wave gets ahead (3 -> 0 at quarters of the
+  // client loop), so the waves of a SIMD keep step instead of finishing one by one in
+  // age order -- the tail of a one-round grid (profiles/r04/window_traces.txt). The
+  // aggregation alone: 828 -> 786 us on synth1m_256; inside k_update_encode it slows
+  // the step (1120 -> 1158 us: the encode's waves need the issue slots the ladder
+  // gives the late update waves), so that kernel runs without it (scripts/gpu_r04_a6.sh)
   const int q1 = M / 4, q2 = M / 2, q3 = 3 * M / 4;
-  __builtin_amdgcn_s_setprio(3);
-#endif
+  if constexpr (LADDER) __builtin_amdgcn_s_setprio(3);
   for (; c + 1 < M; c += 2) {
     FLEET_CLIENT_HOOK(c, M);
-#if FLEET_PRIO_LADDER
-    if (c == (q1 & ~1)) __builtin_amdgcn_s_setprio(2);
-    if (c == (q2 & ~1)) __builtin_amdgcn_s_setprio(1);
-    if (c == (q3 & ~1)) __builtin_amdgcn_s_setprio(0);
-#endif
+    if constexpr (LADDER) {
+      if (c == (q1 & ~1)) __builtin_amdgcn_s_setprio(2);
+      if (c == (q2 & ~1)) __builtin_amdgcn_s_setprio(1);
+      if (c == (q3 & ~1)) __builtin_amdgcn_s_setprio(0);
+    }
     b1 = group_of(c + 1);
     client(c, b0);
     if (c + 2 < M) b0 = group_of(c + 2);
@@ -580,7 +578,7 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
 }
 
 // Block `bid` of the SIMD-balanced stream grid (tables already in LDS).
-template <int NT, bool KD = false>
+template <int NT, bool KD = false, bool LADDER = false>
 __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D16Table& dtab, int64_t bid,
                                                    const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                    const double* __restrict__ dampen, double inv_avg, int64_t n_up,
@@ -596,8 +594,8 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
     const int64_t g = g_begin + bid * NT + threadIdx.x;
     const bool live = g < g_end;
     int32_t out[3];
-    update_lane<3, KD>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out, bad,
-                       layout_bad, kd, kd_part, 2 * nw);
+    update_lane<3, KD, LADDER>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out,
+                               bad, layout_bad, kd, kd_part, 2 * nw);
     if (!live) return;
     if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
@@ -611,8 +609,8 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
     const int e = lane % 3;
     const bool live = lane < 63 && g < g_end;
     int32_t out[1];
-    update_lane<1, KD>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, e, live, g_begin, hdr_block, out, bad,
-                       layout_bad, kd, kd_part, 2 * nw);
+    update_lane<1, KD, LADDER>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, e, live, g_begin, hdr_block, out,
+                               bad, layout_bad, kd, kd_part, 2 * nw);
     const int base = lane - e;  // the group's three lanes (lane 63 reads its own)
     const int32_t o0 = __shfl(out[0], base), o1 = __shfl(out[0], base + 1), o2 = __shfl(out[0], base + 2);
     if (!live) return;
@@ -635,6 +633,7 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
 // three times the waves at a third of the work each, spread over every SIMD
 // instead of a sixth full wave on some. nA = gridDim.x: the plain grid.
 // KD = true adds Kardam's side outputs (kardam_lane_step; partial slots per wave);
+// KD = false runs the issue-priority ladder (update_lane);
 // its register budget asks for at least 6 waves per SIMD (the allocator lands on
 // 68 VGPRs: 7 waves, no scratch; unconstrained it takes 86 VGPRs: 5 waves).
 #ifndef FLEET_KD_STREAM_WAVES
@@ -652,7 +651,7 @@ __global__ void __launch_bounds__(NT, KD ? FLEET_KD_STREAM_WAVES : 1) k_update_m
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
   __syncthreads();
-  update_mixed_block<NT, KD>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+  update_mixed_block<NT, KD, !KD>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                              hdr_block, merged, merged_f32, err, nA, kd);
 }
 
@@ -2255,85 +2254,98 @@ __global__ void __launch_bounds__(NT) k_kardam_reduce(const double* __restrict__
 // no partial slots and no separate reduce. rows may be g_out (each lane reads its p
 // before writing its G); prev must not overlap rows (it may be g_out: a lane reads
 // prev before writing G at the same slots).
-template <int NT>
+template <int NT, int IPL = 2>
 __global__ void __launch_bounds__(NT) k_kardam_finish(const float* rows, size_t rpitch, float* g_out,
                                                       int64_t n_up, const int32_t* __restrict__ hdr_block,
                                                       const float* prev, size_t gpitch,
                                                       const uint8_t* __restrict__ has_prev, double lr,
                                                       double* __restrict__ norms) {
   typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+  constexpr int S = 3 * IPL;
   __shared__ B64Tables tab;
+  __shared__ int32_t hdr[kMaxHeaderSlots];  // the header positions: searched per group in LDS
   __shared__ double red[2][NT / 64];
   b64_tables_init<NT>(&tab);
-  __syncthreads();
-  const int c = blockIdx.x;
   const int n_hdr = hdr_block[1];
   const int64_t walk_end = hdr_block[2];
-  const int32_t* hdr = hdr_block + 4;
+  for (int i = threadIdx.x; i < n_hdr; i += NT) hdr[i] = hdr_block[4 + i];
+  __syncthreads();
+  const int c = blockIdx.x;
   const bool hasp = prev && has_prev[c];  // block-uniform
   const float* row = rows + (size_t)c * rpitch;
   const float* prow = hasp ? prev + (size_t)c * gpitch : nullptr;
   float* grow = g_out ? g_out + (size_t)c * gpitch : nullptr;
   const int64_t groups = (n_up + 2) / 3;
   double sg = 0.0, sd = 0.0;
-  for (int64_t base = 0; base < groups; base += NT) {  // uniform trip count: every lane in every ballot
-    const int64_t g = base + threadIdx.x;
-    const bool live = g < groups;
-    const int64_t gp = 3 * g;
-    const bool whole = live && gp + 2 < n_up;
-    const uint32_t hb = live ? header_bits(hdr, n_hdr, gp) : 7u;
+  // IPL groups per lane per trip (their loads in flight together); a uniform trip
+  // count, so every lane is in every ballot
+  for (int64_t base = 0; base < groups; base += (int64_t)IPL * NT) {
+    int64_t gp[IPL];
+    bool whole[IPL], live[IPL];
     uint32_t flat = 0;
+    float pv[S], qv[S];
 #pragma unroll
-    for (int e = 0; e < 3; ++e)
-      if (live && gp + e < n_up && gp + e < walk_end && !((hb >> e) & 1u)) flat |= 1u << e;
-    float pv[3] = {0.0f, 0.0f, 0.0f};
-    if (whole) {
-      const f3u t = *reinterpret_cast<const f3u*>(row + gp);
-      pv[0] = t.x;
-      pv[1] = t.y;
-      pv[2] = t.z;
-    } else {
+    for (int h = 0; h < IPL; ++h) {
+      const int64_t g = base + h * NT + threadIdx.x;
+      live[h] = g < groups;
+      gp[h] = 3 * g;
+      whole[h] = live[h] && gp[h] + 2 < n_up;
+      const uint32_t hb = live[h] ? header_bits(hdr, n_hdr, gp[h]) : 7u;
 #pragma unroll
       for (int e = 0; e < 3; ++e)
-        if ((flat >> e) & 1u) pv[e] = row[gp + e];
+        if (live[h] && gp[h] + e < n_up && gp[h] + e < walk_end && !((hb >> e) & 1u)) flat |= 1u << (3 * h + e);
+      pv[3 * h] = pv[3 * h + 1] = pv[3 * h + 2] = 0.0f;
+      qv[3 * h] = qv[3 * h + 1] = qv[3 * h + 2] = 0.0f;
+      if (whole[h]) {
+        const f3u t = *reinterpret_cast<const f3u*>(row + gp[h]);
+        pv[3 * h] = t.x;
+        pv[3 * h + 1] = t.y;
+        pv[3 * h + 2] = t.z;
+        if (hasp) {
+          const f3u u = *reinterpret_cast<const f3u*>(prow + gp[h]);
+          qv[3 * h] = u.x;
+          qv[3 * h + 1] = u.y;
+          qv[3 * h + 2] = u.z;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 3; ++e)
+          if ((flat >> (3 * h + e)) & 1u) {
+            pv[3 * h + e] = row[gp[h] + e];
+            if (hasp) qv[3 * h + e] = prow[gp[h] + e];
+          }
+      }
     }
 #pragma unroll
-    for (int e = 0; e < 3; ++e)
-      if (!((flat >> e) & 1u)) pv[e] = 0.0f;
-    float G[3];
-    dampen_stage<3>(pv, lr);  // lr is uniform
-    q_stage<3>(G, pv, &tab);
+    for (int i = 0; i < S; ++i)
+      if (!((flat >> i) & 1u)) pv[i] = 0.0f;
+    float G[S];
+    dampen_stage<S>(pv, lr);  // lr is uniform
+    q_stage<S>(G, pv, &tab);
 #pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      if (!((flat >> e) & 1u)) G[e] = 0.0f;
-      sg += (double)(G[e] * G[e]);
+    for (int i = 0; i < S; ++i) {
+      if (!((flat >> i) & 1u)) G[i] = 0.0f;
+      sg += (double)(G[i] * G[i]);
     }
     if (hasp) {
-      float qv[3] = {0.0f, 0.0f, 0.0f}, dv[3], D[3];
-      if (whole) {
-        const f3u t = *reinterpret_cast<const f3u*>(prow + gp);
-        qv[0] = t.x;
-        qv[1] = t.y;
-        qv[2] = t.z;
-      } else {
+      float dv[S], D[S];
 #pragma unroll
-        for (int e = 0; e < 3; ++e)
-          if ((flat >> e) & 1u) qv[e] = prow[gp + e];
-      }
+      for (int i = 0; i < S; ++i) dv[i] = ((flat >> i) & 1u) ? G[i] - qv[i] : 0.0f;
+      q_stage<S>(D, dv, &tab);
 #pragma unroll
-      for (int e = 0; e < 3; ++e) dv[e] = ((flat >> e) & 1u) ? G[e] - qv[e] : 0.0f;
-      q_stage<3>(D, dv, &tab);
-#pragma unroll
-      for (int e = 0; e < 3; ++e)
-        if ((flat >> e) & 1u) sd += (double)(D[e] * D[e]);
+      for (int i = 0; i < S; ++i)
+        if ((flat >> i) & 1u) sd += (double)(D[i] * D[i]);
     }
     if (grow) {
-      if (whole) {
-        *reinterpret_cast<f3u*>(grow + gp) = f3u{G[0], G[1], G[2]};
-      } else {
 #pragma unroll
-        for (int e = 0; e < 3; ++e)
-          if (live && gp + e < n_up) grow[gp + e] = G[e];
+      for (int h = 0; h < IPL; ++h) {
+        if (whole[h]) {
+          *reinterpret_cast<f3u*>(grow + gp[h]) = f3u{G[3 * h], G[3 * h + 1], G[3 * h + 2]};
+        } else {
+#pragma unroll
+          for (int e = 0; e < 3; ++e)
+            if (live[h] && gp[h] + e < n_up) grow[gp[h] + e] = G[3 * h + e];
+        }
       }
     }
   }
@@ -2363,7 +2375,14 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   // the update's own launch plan with the side outputs: the pipelined tiles (their
   // producers store p; k_kardam_finish does the rest), the wide tiles (side outputs
   // from the tile producers), or the stream kernel's SIMD-balanced grid
-  const UpdatePlan p = plan_update(groups, plan_overrides());
+  UpdatePlan p = plan_update(groups, plan_overrides());
+  if (p.kind == 0 && plan_overrides().grid == 0) {
+    // the stream form on the plain grid unless a grid is asked for: value-per-lane waves
+    // pay the per-client wave sums for a third of the values (synth1m_256: 1747 vs
+    // 1724 us, scripts/gpu_r04_a6.sh)
+    p.nA = (int)((groups + 255) / 256);
+    p.blocks = p.nA;
+  }
   const unsigned blocks = (unsigned)p.blocks;
   // partial slots per client: a wave of the stream grid or a tile; the pipelined form
   // uses the slots' bytes as its p rows (4 floats a slot) unless they can go straight

@@ -12,7 +12,7 @@ for W in ${WORKLOADS:-mnist64 cifar10_256 synth1m_256}; do
 import csv
 for r in csv.DictReader(open('$O/${lab}_$W/run_kernel_stats.csv')):
     n = r['Name']
-    if 'k_update' in n or 'k_kardam_reduce' in n:
+    if 'k_update' in n or 'k_kardam_reduce' in n or 'k_kardam_finish' in n:
         print('%-8s %-12s %-44s calls %4s avg %9.1f us' % ('$lab', '$W', n.split('(')[0].replace('void fleet::', '').replace('fleet::', ''),
                                                    r['Calls'], float(r['AverageNs']) / 1e3), flush=True)
 "
