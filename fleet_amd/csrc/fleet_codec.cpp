@@ -1047,14 +1047,15 @@ int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch
   if ((d_prev || d_g_out) && vpitch < n) return fail(c, FLEET_ERR_ARG, "vpitch %zu < %zu values", vpitch, n);
   hipStream_t s = pick(c, stream);
   if ((rc = dev_params(c, s, n, M, dampen, header_pos, n_headers))) return rc;
-  int nw_sz = 0;  // partial slots per client of the launch plan (sizing call)
+  int nw_sz = 0, parts_sz = 1;  // partial slots and norm parts per client of the launch plan (sizing call)
   fleet::KardamOut kd0{lr, nullptr, nullptr, 0, nullptr, nullptr};
   (void)fleet::launch_update_kardam(nullptr, pitch, M, nullptr, 0.0, (int64_t)n, 0, (int64_t)ge, nullptr, nullptr,
-                                    nullptr, nullptr, kd0, &nw_sz, nullptr, s);
+                                    nullptr, nullptr, kd0, &nw_sz, nullptr, &parts_sz, s);
   (void)hipGetLastError();
-  const size_t n_waves = (size_t)std::max(nw_sz, 1);
-  // scratch: [partials M x slots x 2 | norms M x 2 | has_prev M]; synchronous call (host outputs)
-  const size_t o_norm = sizeof(double) * 2 * (size_t)M * n_waves, o_has = o_norm + sizeof(double) * 2 * (size_t)M;
+  const size_t n_waves = (size_t)std::max(nw_sz, 1), n_parts = (size_t)std::max(parts_sz, 1);
+  // scratch: [partials M x slots x 2 | norms M x parts x 2 | has_prev M]; synchronous call (host outputs)
+  const size_t o_norm = sizeof(double) * 2 * (size_t)M * n_waves;
+  const size_t o_has = o_norm + sizeof(double) * 2 * (size_t)M * n_parts;
   if ((rc = grow_dev(c, &c->d_b, &c->d_b_cap, o_has + (size_t)M + 64))) return rc;
   HIP_TRY(c, hipStreamSynchronize(s));
   double* d_part = reinterpret_cast<double*>(c->d_b);
@@ -1062,16 +1063,22 @@ int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch
   uint8_t* d_has = c->d_b + o_has;
   if (d_prev) HIP_TRY(c, hipMemcpy(d_has, has_prev, (size_t)M, hipMemcpyHostToDevice));
   fleet::KardamOut kd{lr, (const float*)d_prev, d_prev ? d_has : nullptr, vpitch, (float*)d_g_out, d_part};
-  int nw = 0;
+  int nw = 0, np = 1;
   HIP_TRY(c, fleet::launch_update_kardam((const uint8_t*)d_uploads, pitch, M, c->d_dev_dampen, (double)1 / M,
                                          (int64_t)n, 0, (int64_t)ge, c->d_dev_hdr, (uint8_t*)d_merged,
-                                         (float*)d_merged_f32, c->d_dev_err, kd, &nw, d_norm, s));
-  std::vector<double> norms(2 * (size_t)M);
+                                         (float*)d_merged_f32, c->d_dev_err, kd, &nw, d_norm, &np, s));
+  if ((size_t)np != n_parts) return fail(c, FLEET_ERR_HIP, "Kardam launch plan changed between sizing and launch");
+  std::vector<double> norms(2 * (size_t)M * n_parts);
   HIP_TRY(c, hipMemcpyAsync(norms.data(), d_norm, sizeof(double) * norms.size(), hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   for (int i = 0; i < M; ++i) {
-    norm_g[i] = std::sqrt(norms[2 * (size_t)i]);
-    norm_diff[i] = (d_prev && has_prev[i]) ? std::sqrt(norms[2 * (size_t)i + 1]) : std::nan("");
+    double a = 0.0, b = 0.0;  // the client's chunk sums, in order
+    for (size_t k = 0; k < n_parts; ++k) {
+      a += norms[2 * ((size_t)i * n_parts + k)];
+      b += norms[2 * ((size_t)i * n_parts + k) + 1];
+    }
+    norm_g[i] = std::sqrt(a);
+    norm_diff[i] = (d_prev && has_prev[i]) ? std::sqrt(b) : std::nan("");
   }
   return FLEET_OK;
 }

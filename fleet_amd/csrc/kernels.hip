@@ -2247,21 +2247,22 @@ __global__ void __launch_bounds__(NT) k_kardam_reduce(const double* __restrict__
 // Kardam.java:48-106). The pipelined tiles are latency-bound -- one serial consumer
 // wave per tile -- so Kardam's two extra Q stages stay off them:
 // their producers only store each (client, value)'s p in `rows` (k_update_pipe<...,
-// KD = true>), and this kernel, one block per client, turns the row into G =
-// Q(f32(f64(p) * lr)) (into g_out when given: 0 off the flat gradient), ||G||^2 and,
-// with the worker's previous G, ||Q(G - prev)||^2. The norms come out directly in a
-// fixed order (a lane's groups in turn, the wave by DPP, the block's waves in LDS):
-// no partial slots and no separate reduce. rows may be g_out (each lane reads its p
+// KD = true>), and this kernel turns the rows into G = Q(f32(f64(p) * lr)) (into g_out
+// when given: 0 off the flat gradient), ||G||^2 and, with the worker's previous G,
+// ||Q(G - prev)||^2. Block = (client c, chunk k of kKfGroups groups): a lane's groups,
+// the wave by DPP and the block's waves in LDS give the chunk's two sums, in a fixed
+// order, at parts[(c * kc + k) * 2]; the host adds a client's kc chunk sums in order
+// (a few per client: no reduce launch). rows may be g_out (each lane reads its p
 // before writing its G); prev must not overlap rows (it may be g_out: a lane reads
 // prev before writing G at the same slots).
-template <int NT, int IPL = 2>
-__global__ void __launch_bounds__(NT) k_kardam_finish(const float* rows, size_t rpitch, float* g_out,
-                                                      int64_t n_up, const int32_t* __restrict__ hdr_block,
-                                                      const float* prev, size_t gpitch,
-                                                      const uint8_t* __restrict__ has_prev, double lr,
-                                                      double* __restrict__ norms) {
+constexpr int kKfThreads = 256, kKfIpl = 2, kKfGroups = kKfThreads * kKfIpl;
+__global__ void __launch_bounds__(kKfThreads) k_kardam_finish(const float* rows, size_t rpitch, float* g_out,
+                                                              int64_t n_up, const int32_t* __restrict__ hdr_block,
+                                                              const float* prev, size_t gpitch,
+                                                              const uint8_t* __restrict__ has_prev, double lr,
+                                                              double* __restrict__ parts, int kc) {
   typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
-  constexpr int S = 3 * IPL;
+  constexpr int NT = kKfThreads, IPL = kKfIpl, S = 3 * IPL;
   __shared__ B64Tables tab;
   __shared__ int32_t hdr[kMaxHeaderSlots];  // the header positions: searched per group in LDS
   __shared__ double red[2][NT / 64];
@@ -2270,82 +2271,78 @@ __global__ void __launch_bounds__(NT) k_kardam_finish(const float* rows, size_t 
   const int64_t walk_end = hdr_block[2];
   for (int i = threadIdx.x; i < n_hdr; i += NT) hdr[i] = hdr_block[4 + i];
   __syncthreads();
-  const int c = blockIdx.x;
+  const int c = (int)(blockIdx.x / kc), k = (int)(blockIdx.x % kc);
   const bool hasp = prev && has_prev[c];  // block-uniform
   const float* row = rows + (size_t)c * rpitch;
   const float* prow = hasp ? prev + (size_t)c * gpitch : nullptr;
   float* grow = g_out ? g_out + (size_t)c * gpitch : nullptr;
   const int64_t groups = (n_up + 2) / 3;
-  double sg = 0.0, sd = 0.0;
-  // IPL groups per lane per trip (their loads in flight together); a uniform trip
-  // count, so every lane is in every ballot
-  for (int64_t base = 0; base < groups; base += (int64_t)IPL * NT) {
-    int64_t gp[IPL];
-    bool whole[IPL], live[IPL];
-    uint32_t flat = 0;
-    float pv[S], qv[S];
+  int64_t gp[IPL];
+  bool whole[IPL], live[IPL];
+  uint32_t flat = 0;
+  float pv[S], qv[S];
 #pragma unroll
-    for (int h = 0; h < IPL; ++h) {
-      const int64_t g = base + h * NT + threadIdx.x;
-      live[h] = g < groups;
-      gp[h] = 3 * g;
-      whole[h] = live[h] && gp[h] + 2 < n_up;
-      const uint32_t hb = live[h] ? header_bits(hdr, n_hdr, gp[h]) : 7u;
+  for (int h = 0; h < IPL; ++h) {  // the lane's groups: their loads in flight together
+    const int64_t g = (int64_t)k * kKfGroups + h * NT + threadIdx.x;
+    live[h] = g < groups;
+    gp[h] = 3 * g;
+    whole[h] = live[h] && gp[h] + 2 < n_up;
+    const uint32_t hb = live[h] ? header_bits(hdr, n_hdr, gp[h]) : 7u;
+#pragma unroll
+    for (int e = 0; e < 3; ++e)
+      if (live[h] && gp[h] + e < n_up && gp[h] + e < walk_end && !((hb >> e) & 1u)) flat |= 1u << (3 * h + e);
+    pv[3 * h] = pv[3 * h + 1] = pv[3 * h + 2] = 0.0f;
+    qv[3 * h] = qv[3 * h + 1] = qv[3 * h + 2] = 0.0f;
+    if (whole[h]) {
+      const f3u t = *reinterpret_cast<const f3u*>(row + gp[h]);
+      pv[3 * h] = t.x;
+      pv[3 * h + 1] = t.y;
+      pv[3 * h + 2] = t.z;
+      if (hasp) {
+        const f3u u = *reinterpret_cast<const f3u*>(prow + gp[h]);
+        qv[3 * h] = u.x;
+        qv[3 * h + 1] = u.y;
+        qv[3 * h + 2] = u.z;
+      }
+    } else {
 #pragma unroll
       for (int e = 0; e < 3; ++e)
-        if (live[h] && gp[h] + e < n_up && gp[h] + e < walk_end && !((hb >> e) & 1u)) flat |= 1u << (3 * h + e);
-      pv[3 * h] = pv[3 * h + 1] = pv[3 * h + 2] = 0.0f;
-      qv[3 * h] = qv[3 * h + 1] = qv[3 * h + 2] = 0.0f;
-      if (whole[h]) {
-        const f3u t = *reinterpret_cast<const f3u*>(row + gp[h]);
-        pv[3 * h] = t.x;
-        pv[3 * h + 1] = t.y;
-        pv[3 * h + 2] = t.z;
-        if (hasp) {
-          const f3u u = *reinterpret_cast<const f3u*>(prow + gp[h]);
-          qv[3 * h] = u.x;
-          qv[3 * h + 1] = u.y;
-          qv[3 * h + 2] = u.z;
+        if ((flat >> (3 * h + e)) & 1u) {
+          pv[3 * h + e] = row[gp[h] + e];
+          if (hasp) qv[3 * h + e] = prow[gp[h] + e];
         }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+    if (!((flat >> i) & 1u)) pv[i] = 0.0f;
+  float G[S];
+  dampen_stage<S>(pv, lr);  // lr is uniform
+  q_stage<S>(G, pv, &tab);
+  double sg = 0.0, sd = 0.0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    if (!((flat >> i) & 1u)) G[i] = 0.0f;
+    sg += (double)(G[i] * G[i]);
+  }
+  if (hasp) {
+    float dv[S], D[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) dv[i] = ((flat >> i) & 1u) ? G[i] - qv[i] : 0.0f;
+    q_stage<S>(D, dv, &tab);
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      if ((flat >> i) & 1u) sd += (double)(D[i] * D[i]);
+  }
+  if (grow) {
+#pragma unroll
+    for (int h = 0; h < IPL; ++h) {
+      if (whole[h]) {
+        *reinterpret_cast<f3u*>(grow + gp[h]) = f3u{G[3 * h], G[3 * h + 1], G[3 * h + 2]};
       } else {
 #pragma unroll
         for (int e = 0; e < 3; ++e)
-          if ((flat >> (3 * h + e)) & 1u) {
-            pv[3 * h + e] = row[gp[h] + e];
-            if (hasp) qv[3 * h + e] = prow[gp[h] + e];
-          }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < S; ++i)
-      if (!((flat >> i) & 1u)) pv[i] = 0.0f;
-    float G[S];
-    dampen_stage<S>(pv, lr);  // lr is uniform
-    q_stage<S>(G, pv, &tab);
-#pragma unroll
-    for (int i = 0; i < S; ++i) {
-      if (!((flat >> i) & 1u)) G[i] = 0.0f;
-      sg += (double)(G[i] * G[i]);
-    }
-    if (hasp) {
-      float dv[S], D[S];
-#pragma unroll
-      for (int i = 0; i < S; ++i) dv[i] = ((flat >> i) & 1u) ? G[i] - qv[i] : 0.0f;
-      q_stage<S>(D, dv, &tab);
-#pragma unroll
-      for (int i = 0; i < S; ++i)
-        if ((flat >> i) & 1u) sd += (double)(D[i] * D[i]);
-    }
-    if (grow) {
-#pragma unroll
-      for (int h = 0; h < IPL; ++h) {
-        if (whole[h]) {
-          *reinterpret_cast<f3u*>(grow + gp[h]) = f3u{G[3 * h], G[3 * h + 1], G[3 * h + 2]};
-        } else {
-#pragma unroll
-          for (int e = 0; e < 3; ++e)
-            if (live[h] && gp[h] + e < n_up) grow[gp[h] + e] = G[3 * h + e];
-        }
+          if (live[h] && gp[h] + e < n_up) grow[gp[h] + e] = G[3 * h + e];
       }
     }
   }
@@ -2362,15 +2359,15 @@ __global__ void __launch_bounds__(NT) k_kardam_finish(const float* rows, size_t 
       a += red[0][i];
       b += red[1][i];
     }
-    norms[2 * c] = a;
-    norms[2 * c + 1] = b;
+    parts[((size_t)c * kc + k) * 2] = a;
+    parts[((size_t)c * kc + k) * 2 + 1] = b;
   }
 }
 
 hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                                 int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
-                                double* norms, hipStream_t s) {
+                                double* norms, int* norm_parts, hipStream_t s) {
   const int64_t groups = g_end - g_begin;
   // the update's own launch plan with the side outputs: the pipelined tiles (their
   // producers store p; k_kardam_finish does the rest), the wide tiles (side outputs
@@ -2388,6 +2385,9 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   // uses the slots' bytes as its p rows (4 floats a slot) unless they can go straight
   // into the caller's G rows
   *n_waves = p.kind == 0 ? (int)blocks * 4 : p.kind == 1 ? (int)blocks : (int)((n_up + 3) / 4);
+  // norms: one pair per client (the reduce), or the finish kernel's chunk sums
+  const int kc = (int)(((n_up + 2) / 3 + kKfGroups - 1) / kKfGroups);
+  *norm_parts = p.kind == 2 ? std::max(kc, 1) : 1;
   if (groups <= 0) return hipSuccess;
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
   if (p.kind == 2) {
@@ -2403,8 +2403,8 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
     hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0, true>), dim3(blocks), dim3(64 * 5), 0, s, uploads, pitch, M,
                        d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
                        EncodeJob{}, kp);
-    hipLaunchKernelGGL(k_kardam_finish<1024>, dim3((unsigned)M), dim3(1024), 0, s, kp.g_out, kp.vpitch, kd.g_out,
-                       n_up, d_hdr_block, kd.prev, kd.vpitch, kd.has_prev, kd.lr, norms);
+    hipLaunchKernelGGL(k_kardam_finish, dim3((unsigned)((int64_t)M * kc)), dim3(kKfThreads), 0, s, kp.g_out,
+                       kp.vpitch, kd.g_out, n_up, d_hdr_block, kd.prev, kd.vpitch, kd.has_prev, kd.lr, norms, kc);
     return hipGetLastError();
   }
   if (p.kind == 1)
