@@ -2266,11 +2266,6 @@ __global__ void __launch_bounds__(kKfThreads) k_kardam_finish(const float* rows,
   __shared__ B64Tables tab;
   __shared__ int32_t hdr[kMaxHeaderSlots];  // the header positions: searched per group in LDS
   __shared__ double red[2][NT / 64];
-  b64_tables_init<NT>(&tab);
-  const int n_hdr = hdr_block[1];
-  const int64_t walk_end = hdr_block[2];
-  for (int i = threadIdx.x; i < n_hdr; i += NT) hdr[i] = hdr_block[4 + i];
-  __syncthreads();
   const int c = (int)(blockIdx.x / kc), k = (int)(blockIdx.x % kc);
   const bool hasp = prev && has_prev[c];  // block-uniform
   const float* row = rows + (size_t)c * rpitch;
@@ -2279,18 +2274,15 @@ __global__ void __launch_bounds__(kKfThreads) k_kardam_finish(const float* rows,
   const int64_t groups = (n_up + 2) / 3;
   int64_t gp[IPL];
   bool whole[IPL], live[IPL];
-  uint32_t flat = 0;
   float pv[S], qv[S];
+  // the lane's groups first (their loads in flight while the tables are copied; slots
+  // past n_up read as 0), the flat-gradient mask after
 #pragma unroll
-  for (int h = 0; h < IPL; ++h) {  // the lane's groups: their loads in flight together
+  for (int h = 0; h < IPL; ++h) {
     const int64_t g = (int64_t)k * kKfGroups + h * NT + threadIdx.x;
     live[h] = g < groups;
     gp[h] = 3 * g;
     whole[h] = live[h] && gp[h] + 2 < n_up;
-    const uint32_t hb = live[h] ? header_bits(hdr, n_hdr, gp[h]) : 7u;
-#pragma unroll
-    for (int e = 0; e < 3; ++e)
-      if (live[h] && gp[h] + e < n_up && gp[h] + e < walk_end && !((hb >> e) & 1u)) flat |= 1u << (3 * h + e);
     pv[3 * h] = pv[3 * h + 1] = pv[3 * h + 2] = 0.0f;
     qv[3 * h] = qv[3 * h + 1] = qv[3 * h + 2] = 0.0f;
     if (whole[h]) {
@@ -2304,14 +2296,27 @@ __global__ void __launch_bounds__(kKfThreads) k_kardam_finish(const float* rows,
         qv[3 * h + 1] = u.y;
         qv[3 * h + 2] = u.z;
       }
-    } else {
+    } else if (live[h]) {
 #pragma unroll
       for (int e = 0; e < 3; ++e)
-        if ((flat >> (3 * h + e)) & 1u) {
+        if (gp[h] + e < n_up) {
           pv[3 * h + e] = row[gp[h] + e];
           if (hasp) qv[3 * h + e] = prow[gp[h] + e];
         }
     }
+  }
+  b64_tables_init<NT>(&tab);
+  const int n_hdr = hdr_block[1];
+  const int64_t walk_end = hdr_block[2];
+  for (int i = threadIdx.x; i < n_hdr; i += NT) hdr[i] = hdr_block[4 + i];
+  __syncthreads();
+  uint32_t flat = 0;
+#pragma unroll
+  for (int h = 0; h < IPL; ++h) {
+    const uint32_t hb = live[h] ? header_bits(hdr, n_hdr, gp[h]) : 7u;
+#pragma unroll
+    for (int e = 0; e < 3; ++e)
+      if (live[h] && gp[h] + e < n_up && gp[h] + e < walk_end && !((hb >> e) & 1u)) flat |= 1u << (3 * h + e);
   }
 #pragma unroll
   for (int i = 0; i < S; ++i)
