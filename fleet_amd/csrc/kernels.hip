@@ -35,6 +35,9 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
+#ifndef FLEET_TILE_LADDER
+#define FLEET_TILE_LADDER 0
+#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -1081,7 +1084,20 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
   uint32_t off_domain = 0;
   float amax = 0.f;  // narrow tiles: max |A + p| (q_lat is exact below 1e8 for any sign)
   uint32_t badacc = 0;
+#if FLEET_TILE_LADDER  // experiment (A/B builds): the stream kernel's issue-priority ladder per chunk
+  int rung = -1;
+#endif
   for (int c0 = 0; c0 < M; c0 += CM) {
+#if FLEET_TILE_LADDER
+    const int q = (4 * c0) / M;  // block-uniform
+    if (q != rung) {
+      if (q == 0) __builtin_amdgcn_s_setprio(3);
+      else if (q == 1) __builtin_amdgcn_s_setprio(2);
+      else if (q == 2) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+      rung = q;
+    }
+#endif
     const int cm = min(CM, M - c0);
     const int nitems = cm * TG;
     for (int base = 0; base < nitems; base += 512) {
