@@ -1,4 +1,4 @@
-# r04 a9: Kardam A/B, alternating on one box: the a5 HEAD library (k_update<1, true>, the NW=8
+# r04 a9: Kardam A/B, alternating on one box (then the tile ladder A/B of a10): the a5 HEAD library (k_update<1, true>, the NW=8
 # pipelined producers + reduce) against the tree (the plain-grid stream form; the pipelined form's
 # p rows + chunked finish, its loads issued before the table copy)
 set -u
@@ -10,3 +10,6 @@ tail -2 $O/tests.log
 for r in 1 2 3; do
   OUT=$O/klibs$r LIBS="head=ab/libhead.so tree=fleet_amd/libfleetcodec.so" WORKLOADS="mnist64 synth1m_256 cifar10_256" bash scripts/gpu_kardam_libs.sh || exit 1
 done
+
+LIBS="base=fleet_amd/libfleetcodec.so tladder=ab/libtladder.so" REPS=3 WORKLOADS="cifar10_256 cifar100_1024" STEPS=20 bash scripts/gpu_ab_multi.sh > $O/tile_ladder.txt 2>&1 || { tail -5 $O/tile_ladder.txt; exit 1; }
+cat $O/tile_ladder.txt
