@@ -471,7 +471,8 @@ class Codec:
                              merged_u8, merged_f32=None, prev_f32=None, has_prev=None, g_out_f32=None, stream=None):
         """update_device plus Kardam's per-client norms in the same pass (fleet_update_kardam_device):
         returns (norm_g[M], norm_diff[M]); prev_f32 / g_out_f32: float32 CUDA tensors [M, vpitch]
-        of decoded Kardam gradients in upload coordinates."""
+        of decoded Kardam gradients in upload coordinates (g_out_f32 may be prev_f32 itself:
+        this round's G then replaces prev in place)."""
         M, pitch = uploads_u8.shape
         hp = np.ascontiguousarray(header_pos, dtype=np.int32)
         d = np.ascontiguousarray(dampen, dtype=np.float64)

@@ -2414,8 +2414,9 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   if (p.kind == 2) {
     // p rows: the caller's G rows, unless there are none or they overlap prev (G may
     // replace prev in place: prev must stay intact until k_kardam_finish reads it)
-    const size_t span = (size_t)M * kd.vpitch;
-    const bool overlap = kd.g_out && kd.prev && kd.g_out < kd.prev + span && kd.prev < kd.g_out + span;
+    const uintptr_t span = (uintptr_t)M * kd.vpitch * sizeof(float);
+    const uintptr_t go = reinterpret_cast<uintptr_t>(kd.g_out), pv = reinterpret_cast<uintptr_t>(kd.prev);
+    const bool overlap = kd.g_out && kd.prev && go < pv + span && pv < go + span;
     KardamOut kp = kd;
     if (!kd.g_out || overlap) {
       kp.g_out = reinterpret_cast<float*>(kd.partials);
