@@ -106,6 +106,8 @@ def lib() -> C.CDLL:
         "fleet_update_kardam_device": (i32, [vp, vp, sz, sz, i32, vp, vp, i32, C.c_double, vp, vp, vp, sz, vp, vp,
                                              vp, vp, vp]),
         "fleet_update_kernel": (C.c_char_p, [sz]),
+        "fleet_update_plan_grid": (i32, [sz, C.POINTER(C.c_int), C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                         C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "fleet_update_encode_kernel": (C.c_char_p, [sz]),
         "fleet_set_plan": (i32, [C.c_char_p, vp, sz]),
         "fleet_plan": (C.c_char_p, []),
@@ -191,6 +193,18 @@ def b64_count(length: int) -> int:
 def update_kernel(length: int) -> str:
     """Aggregation kernel the library launches for uploads of `length` bytes."""
     return lib().fleet_update_kernel(length).decode()
+
+
+def update_plan_grid(length: int) -> dict:
+    """The aggregation's launch grid for uploads of `length` bytes (fleet_update_plan_grid):
+    kind ("stream" / "tiled" / "pipe"), blocks, and n_a / n_w / n_n (see fleet_codec.h)."""
+    k = C.c_int()
+    b, a, w, n = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
+    rc = lib().fleet_update_plan_grid(length, C.byref(k), C.byref(b), C.byref(a), C.byref(w), C.byref(n))
+    if rc != 0:
+        raise FleetError(f"fleet_update_plan_grid: {rc}")
+    return {"kind": ("stream", "tiled", "pipe")[k.value], "blocks": b.value, "n_a": a.value, "n_w": w.value,
+            "n_n": n.value}
 
 
 def update_encode_kernel(length: int) -> str:

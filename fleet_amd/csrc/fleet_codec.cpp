@@ -1710,6 +1710,12 @@ const char* fleet_update_kernel(size_t len) {
   return name.c_str();
 }
 
+int fleet_update_plan_grid(size_t len, int* kind, int64_t* blocks, int64_t* n_a, int64_t* n_w, int64_t* n_n) {
+  if (!kind || !blocks || !n_a || !n_w || !n_n) return FLEET_ERR_ARG;
+  fleet::update_plan_grid((int64_t)groups_of(fleet_b64_count(len)), kind, blocks, n_a, n_w, n_n);
+  return FLEET_OK;
+}
+
 const char* fleet_update_encode_kernel(size_t len) {
   static thread_local std::string name;
   name = fleet::update_encode_kernel_name((int64_t)groups_of(fleet_b64_count(len)));

@@ -67,6 +67,7 @@ int set_plan_overrides(const char* spec, std::string* err);  // 0, or -1 (nothin
 std::string plan_spec();                                     // normalised active spec, "" = default
 // names of the kernels launch_update / launch_update_encode pick for `groups` groups
 std::string update_kernel_name(int64_t groups);
+void update_plan_grid(int64_t groups, int* kind, int64_t* blocks, int64_t* n_a, int64_t* n_w, int64_t* n_n);
 std::string update_encode_kernel_name(int64_t groups);
 hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                                 int64_t n_up, const int32_t* d_hdr_block, uint8_t* merged, float* merged_f32,

@@ -2168,6 +2168,15 @@ std::string update_kernel_name(int64_t groups) {
   return buf;
 }
 
+void update_plan_grid(int64_t groups, int* kind, int64_t* blocks, int64_t* n_a, int64_t* n_w, int64_t* n_n) {
+  const UpdatePlan p = plan_update(groups, plan_overrides());
+  *kind = p.kind;
+  *blocks = p.blocks;
+  *n_a = p.nA;
+  *n_w = p.t.nW;
+  *n_n = p.t.nN;
+}
+
 std::string update_encode_kernel_name(int64_t groups) {
   const PlanOverrides o = plan_overrides();
   const UpdatePlan p = plan_update(groups, o);

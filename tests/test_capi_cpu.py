@@ -81,3 +81,43 @@ def test_plan_overrides_validated_on_host():
     src = open(os.path.join(F.ROOT, "fleet_amd", "csrc", "kernels.hip")).read()
     assert src.count("getenv(") == 1 and 'getenv("FLEET_EXPERIMENTS")' in src
     assert "getenv(" not in open(os.path.join(F.ROOT, "fleet_amd", "csrc", "fleet_codec.cpp")).read()
+
+
+GRID_SIZES = [1, 2, 16, 17, 83, 84, 85, 255, 256, 257, 6_667, 7_654, 16_668, 32_768, 50_001, 65_537, 100_001,
+              104_623, 110_413, 131_072, 174_763, 349_526, 1_398_102]
+
+
+@pytest.mark.parametrize("spec", ["", "update=stream", "update=stream,grid=plain", "update=stream,grid=lanes",
+                                  "update=tiled", "update=tiled,tile_mix=off", "update=pipe"])
+def test_launch_grid_covers_every_group(spec):
+    """The aggregation's grid (fleet_update_plan_grid) covers every group of the
+    bucket exactly once and launches no block past it, under every plan: the stream
+    grid's group-per-lane blocks (256 groups) then value-per-lane blocks (84 groups:
+    4 waves x 21), the tiles' two widths, the pipelined 16-group tiles. (An r04 plan
+    change once dropped the stream grid's last ragged block when the plain grid
+    covered the bucket; found on the GPU, pinned here on the host.)"""
+    F.set_plan(spec)
+    try:
+        for groups in GRID_SIZES:
+            g = F.update_plan_grid(16 * groups)
+            b = g["blocks"]
+            if g["kind"] == "stream":
+                covered_a = 256 * g["n_a"]
+                if covered_a >= groups:
+                    assert b == g["n_a"] and 256 * (b - 1) < groups, (groups, g)
+                else:
+                    rest = groups - covered_a
+                    assert b - g["n_a"] == -(-rest // 84), (groups, g)
+            elif g["kind"] == "tiled":
+                if g["n_w"] >= 0:
+                    cov = 64 * g["n_w"] + 16 * g["n_n"]
+                    assert b == g["n_w"] + g["n_n"] and cov >= groups and cov - 16 < groups, (groups, g)
+                    assert 64 * g["n_w"] < groups, (groups, g)
+                else:
+                    assert b == -(-groups // 64), (groups, g)
+            else:
+                assert b == -(-groups // 16), (groups, g)
+            if spec.startswith("update="):
+                assert g["kind"] == spec.split(",")[0].split("=")[1], (spec, g)
+    finally:
+        F.set_plan("")
