@@ -35,8 +35,8 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
-#ifndef FLEET_TILE_LADDER
-#define FLEET_TILE_LADDER 0
+#ifndef FLEET_KD_ONE_PER_TRIP
+#define FLEET_KD_ONE_PER_TRIP 0
 #endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
@@ -544,6 +544,15 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // registers (no copies between trips)
   Row b0 = group_of(0), b1;
   int c = 0;
+#if FLEET_KD_ONE_PER_TRIP
+  if constexpr (KD) {  // experiment (A/B builds): one client per trip, the next one in flight
+    for (; c < M; ++c) {
+      const Row cur = b0;
+      if (c + 1 < M) b0 = group_of(c + 1);
+      client(c, cur);
+    }
+  }
+#endif
   // LADDER: issue priority falls as a wave gets ahead (3 -> 0 at quarters of the
   // client loop), so the waves of a SIMD keep step instead of finishing one by one in
   // age order -- the tail of a one-round grid (profiles/r04/window_traces.txt). The
@@ -1084,20 +1093,7 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
   uint32_t off_domain = 0;
   float amax = 0.f;  // narrow tiles: max |A + p| (q_lat is exact below 1e8 for any sign)
   uint32_t badacc = 0;
-#if FLEET_TILE_LADDER  // experiment (A/B builds): the stream kernel's issue-priority ladder per chunk
-  int rung = -1;
-#endif
   for (int c0 = 0; c0 < M; c0 += CM) {
-#if FLEET_TILE_LADDER
-    const int q = (4 * c0) / M;  // block-uniform
-    if (q != rung) {
-      if (q == 0) __builtin_amdgcn_s_setprio(3);
-      else if (q == 1) __builtin_amdgcn_s_setprio(2);
-      else if (q == 2) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-      rung = q;
-    }
-#endif
     const int cm = min(CM, M - c0);
     const int nitems = cm * TG;
     for (int base = 0; base < nitems; base += 512) {
