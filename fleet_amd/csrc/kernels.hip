@@ -35,8 +35,8 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
-#ifndef FLEET_KD_ONE_PER_TRIP
-#define FLEET_KD_ONE_PER_TRIP 0
+#ifndef FLEET_KD_LADDER
+#define FLEET_KD_LADDER 0  // experiment (A/B builds): the issue-priority ladder in the Kardam stream form
 #endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
@@ -544,15 +544,6 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // registers (no copies between trips)
   Row b0 = group_of(0), b1;
   int c = 0;
-#if FLEET_KD_ONE_PER_TRIP
-  if constexpr (KD) {  // experiment (A/B builds): one client per trip, the next one in flight
-    for (; c < M; ++c) {
-      const Row cur = b0;
-      if (c + 1 < M) b0 = group_of(c + 1);
-      client(c, cur);
-    }
-  }
-#endif
   // LADDER: issue priority falls as a wave gets ahead (3 -> 0 at quarters of the
   // client loop), so the waves of a SIMD keep step instead of finishing one by one in
   // age order -- the tail of a one-round grid (profiles/r04/window_traces.txt). The
@@ -561,6 +552,20 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // gives the late update waves), so that kernel runs without it (scripts/gpu_r04_a6.sh)
   const int q1 = M / 4, q2 = M / 2, q3 = 3 * M / 4;
   if constexpr (LADDER) __builtin_amdgcn_s_setprio(3);
+  if constexpr (KD) {
+    // Kardam: one client per trip, the next one in flight (two per trip: 1840 against
+    // 1795 us on synth1m_256, scripts/gpu_r04_a13.sh)
+    for (; c < M; ++c) {
+      if constexpr (LADDER) {
+        if (c == q1) __builtin_amdgcn_s_setprio(2);
+        if (c == q2) __builtin_amdgcn_s_setprio(1);
+        if (c == q3) __builtin_amdgcn_s_setprio(0);
+      }
+      const Row cur = b0;
+      if (c + 1 < M) b0 = group_of(c + 1);
+      client(c, cur);
+    }
+  }
   for (; c + 1 < M; c += 2) {
     FLEET_CLIENT_HOOK(c, M);
     if constexpr (LADDER) {
@@ -646,8 +651,8 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
 // instead of a sixth full wave on some. nA = gridDim.x: the plain grid.
 // KD = true adds Kardam's side outputs (kardam_lane_step; partial slots per wave);
 // KD = false runs the issue-priority ladder (update_lane);
-// its register budget asks for at least 6 waves per SIMD (the allocator lands on
-// 68 VGPRs: 7 waves, no scratch; unconstrained it takes 86 VGPRs: 5 waves).
+// its register budget asks for at least 6 waves per SIMD (73 VGPRs, no scratch;
+// unconstrained it takes 91 VGPRs: 5 waves, 1922 against 1795 us on synth1m_256).
 #ifndef FLEET_KD_STREAM_WAVES
 #define FLEET_KD_STREAM_WAVES 6  // A/B builds: -DFLEET_KD_STREAM_WAVES=1 (unconstrained)
 #endif
@@ -663,7 +668,7 @@ __global__ void __launch_bounds__(NT, KD ? FLEET_KD_STREAM_WAVES : 1) k_update_m
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
   __syncthreads();
-  update_mixed_block<NT, KD, !KD>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+  update_mixed_block<NT, KD, !KD || FLEET_KD_LADDER>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                              hdr_block, merged, merged_f32, err, nA, kd);
 }
 
