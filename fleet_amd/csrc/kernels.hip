@@ -35,8 +35,11 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
-#ifndef FLEET_KD_LADDER
-#define FLEET_KD_LADDER 0  // experiment (A/B builds): the issue-priority ladder in the Kardam stream form
+#ifndef FLEET_FUSED_LADDER
+#define FLEET_FUSED_LADDER 0  // experiment (A/B builds): the ladder in k_update_encode's update waves
+#endif
+#ifndef FLEET_FUSED_ENC_PRIO
+#define FLEET_FUSED_ENC_PRIO 0  // experiment (A/B builds): issue priority of k_update_encode's encode waves
 #endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
@@ -649,8 +652,9 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
 // groups go to blocks of one value per lane (21 groups = 63 lanes per wave):
 // three times the waves at a third of the work each, spread over every SIMD
 // instead of a sixth full wave on some. nA = gridDim.x: the plain grid.
-// KD = true adds Kardam's side outputs (kardam_lane_step; partial slots per wave);
-// KD = false runs the issue-priority ladder (update_lane);
+// KD = true adds Kardam's side outputs (kardam_lane_step; partial slots per wave).
+// Both forms run the issue-priority ladder (update_lane: synth1m_256 828 -> 786 us
+// plain, 1776 -> 1502-1546 us with Kardam's side outputs, scripts/gpu_r04_a14.sh);
 // its register budget asks for at least 6 waves per SIMD (73 VGPRs, no scratch;
 // unconstrained it takes 91 VGPRs: 5 waves, 1922 against 1795 us on synth1m_256).
 #ifndef FLEET_KD_STREAM_WAVES
@@ -668,7 +672,7 @@ __global__ void __launch_bounds__(NT, KD ? FLEET_KD_STREAM_WAVES : 1) k_update_m
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
   __syncthreads();
-  update_mixed_block<NT, KD, !KD || FLEET_KD_LADDER>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+  update_mixed_block<NT, KD, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                              hdr_block, merged, merged_f32, err, nA, kd);
 }
 
@@ -1466,10 +1470,13 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   d16_table_init<NT>(&dtab);
   __syncthreads();
   if ((int)blockIdx.x < nU) {  // block-uniform
-    update_mixed_block<NT>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
-                           hdr_block, merged, merged_f32, err, nA);
+    update_mixed_block<NT, false, FLEET_FUSED_LADDER != 0>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen,
+                                                           inv_avg, n_up, g_begin, g_end, hdr_block, merged,
+                                                           merged_f32, err, nA);
   } else {
     const int64_t e = (int64_t)blockIdx.x - nU;
+    if (FLEET_FUSED_ENC_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+    if (FLEET_FUSED_ENC_PRIO == 2) __builtin_amdgcn_s_setprio(2);
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                      (int)(e / ej.gx), &tab, &dtab);
   }
