@@ -35,11 +35,8 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
-#ifndef FLEET_FUSED_LADDER
-#define FLEET_FUSED_LADDER 0  // experiment (A/B builds): the ladder in k_update_encode's update waves
-#endif
 #ifndef FLEET_FUSED_ENC_PRIO
-#define FLEET_FUSED_ENC_PRIO 0  // experiment (A/B builds): issue priority of k_update_encode's encode waves
+#define FLEET_FUSED_ENC_PRIO 2  // issue priority of k_update_encode's encode waves (A/B builds: 3)
 #endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
@@ -550,9 +547,8 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // LADDER: issue priority falls as a wave gets ahead (3 -> 0 at quarters of the
   // client loop), so the waves of a SIMD keep step instead of finishing one by one in
   // age order -- the tail of a one-round grid (profiles/r04/window_traces.txt). The
-  // aggregation alone: 828 -> 786 us on synth1m_256; inside k_update_encode it slows
-  // the step (1120 -> 1158 us: the encode's waves need the issue slots the ladder
-  // gives the late update waves), so that kernel runs without it (scripts/gpu_r04_a6.sh)
+  // aggregation alone: 828 -> 786 us on synth1m_256 (scripts/gpu_r04_a6.sh); inside
+  // k_update_encode with the encode's waves at priority 2 (see there)
   const int q1 = M / 4, q2 = M / 2, q3 = 3 * M / 4;
   if constexpr (LADDER) __builtin_amdgcn_s_setprio(3);
   if constexpr (KD) {
@@ -1469,14 +1465,17 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
   __syncthreads();
+  // the update waves run the issue-priority ladder (3 -> 0 as they get ahead) and the
+  // encode's waves sit at priority 2: behind the update waves that lag, ahead of those
+  // that lead. synth1m_256 step 1129-1133 -> 1119-1120 us; the ladder with the encode
+  // waves at 0 (r04 a6: 1158 us) or 1 (1138-1142 us) was slower (scripts/gpu_r04_a15.sh)
   if ((int)blockIdx.x < nU) {  // block-uniform
-    update_mixed_block<NT, false, FLEET_FUSED_LADDER != 0>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen,
-                                                           inv_avg, n_up, g_begin, g_end, hdr_block, merged,
-                                                           merged_f32, err, nA);
+    update_mixed_block<NT, false, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin,
+                                        g_end, hdr_block, merged, merged_f32, err, nA);
   } else {
     const int64_t e = (int64_t)blockIdx.x - nU;
-    if (FLEET_FUSED_ENC_PRIO == 1) __builtin_amdgcn_s_setprio(1);
     if (FLEET_FUSED_ENC_PRIO == 2) __builtin_amdgcn_s_setprio(2);
+    if (FLEET_FUSED_ENC_PRIO == 3) __builtin_amdgcn_s_setprio(3);
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                      (int)(e / ej.gx), &tab, &dtab);
   }
