@@ -35,9 +35,6 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
-#ifndef FLEET_FUSED_ENC_PRIO
-#define FLEET_FUSED_ENC_PRIO 2  // issue priority of k_update_encode's encode waves (A/B builds: 3)
-#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -1466,16 +1463,16 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   d16_table_init<NT>(&dtab);
   __syncthreads();
   // the update waves run the issue-priority ladder (3 -> 0 as they get ahead) and the
-  // encode's waves sit at priority 2: behind the update waves that lag, ahead of those
-  // that lead. synth1m_256 step 1129-1133 -> 1119-1120 us; the ladder with the encode
-  // waves at 0 (r04 a6: 1158 us) or 1 (1138-1142 us) was slower (scripts/gpu_r04_a15.sh)
+  // encode's waves run at priority 3: the HBM-bound encode issues whenever it can, the
+  // update waves that lag next. synth1m_256 step 1129-1133 -> 1119-1120 us with the
+  // encode at 2 (scripts/gpu_r04_a15.sh), 1171-1176 -> 1153-1158 us from 2 to 3 on
+  // another box (gpu_r04_a16.sh); at 0 (r04 a6: 1158 us) or 1 (1138-1142 us) slower
   if ((int)blockIdx.x < nU) {  // block-uniform
     update_mixed_block<NT, false, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin,
                                         g_end, hdr_block, merged, merged_f32, err, nA);
   } else {
     const int64_t e = (int64_t)blockIdx.x - nU;
-    if (FLEET_FUSED_ENC_PRIO == 2) __builtin_amdgcn_s_setprio(2);
-    if (FLEET_FUSED_ENC_PRIO == 3) __builtin_amdgcn_s_setprio(3);
+    __builtin_amdgcn_s_setprio(3);
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                      (int)(e / ej.gx), &tab, &dtab);
   }
