@@ -35,6 +35,9 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
+#ifndef FLEET_LADDER_STEPS
+#define FLEET_LADDER_STEPS 0
+#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -546,7 +549,13 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // age order -- the tail of a one-round grid (profiles/r04/window_traces.txt). The
   // aggregation alone: 828 -> 786 us on synth1m_256 (scripts/gpu_r04_a6.sh); inside
   // k_update_encode with the encode's waves at priority 2 (see there)
+#if FLEET_LADDER_STEPS == 1  // experiment (A/B builds): early rungs
+  const int q1 = M / 8, q2 = M / 4, q3 = M / 2;
+#elif FLEET_LADDER_STEPS == 2  // experiment (A/B builds): late rungs
+  const int q1 = M / 2, q2 = 3 * M / 4, q3 = 7 * M / 8;
+#else
   const int q1 = M / 4, q2 = M / 2, q3 = 3 * M / 4;
+#endif
   if constexpr (LADDER) __builtin_amdgcn_s_setprio(3);
   if constexpr (KD) {
     // Kardam: one client per trip, the next one in flight (two per trip: 1840 against
