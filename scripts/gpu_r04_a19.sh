@@ -1,0 +1,7 @@
+# r04 a19: the CIFAR tiles' serial phase at issue priority 2 (ab/libtp2.so) against the tree, alternating
+set -u
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+O=${OUTROOT:-$GRAFT_REPO_ROOT/gpurun_out}/a19; mkdir -p $O
+LIBS="base=fleet_amd/libfleetcodec.so tp2=ab/libtp2.so" REPS=3 WORKLOADS="cifar10_256 cifar100_1024" STEPS=20 bash scripts/gpu_ab_multi.sh > $O/tile_p2prio.txt 2>&1 || { tail -5 $O/tile_p2prio.txt; exit 1; }
+cat $O/tile_p2prio.txt
