@@ -662,11 +662,8 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
 // plain, 1776 -> 1502-1546 us with Kardam's side outputs, scripts/gpu_r04_a14.sh);
 // its register budget asks for at least 6 waves per SIMD (73 VGPRs, no scratch;
 // unconstrained it takes 91 VGPRs: 5 waves, 1922 against 1795 us on synth1m_256).
-#ifndef FLEET_KD_STREAM_WAVES
-#define FLEET_KD_STREAM_WAVES 6  // A/B builds: -DFLEET_KD_STREAM_WAVES=1 (unconstrained)
-#endif
 template <int NT, bool KD>
-__global__ void __launch_bounds__(NT, KD ? FLEET_KD_STREAM_WAVES : 1) k_update_mixed(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+__global__ void __launch_bounds__(NT, KD ? 6 : 1) k_update_mixed(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                      const double* __restrict__ dampen, double inv_avg,
                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
                                                      const int32_t* __restrict__ hdr_block,
