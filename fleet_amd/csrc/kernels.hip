@@ -35,9 +35,6 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
-#ifndef FLEET_LADDER_STEPS
-#define FLEET_LADDER_STEPS 0
-#endif
 #ifndef FLEET_TILE_P2_PRIO
 #define FLEET_TILE_P2_PRIO 0
 #endif
@@ -552,13 +549,10 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // age order -- the tail of a one-round grid (profiles/r04/window_traces.txt). The
   // aggregation alone: 828 -> 786 us on synth1m_256 (scripts/gpu_r04_a6.sh); inside
   // k_update_encode with the encode's waves at priority 2 (see there)
-#if FLEET_LADDER_STEPS == 1  // experiment (A/B builds): early rungs
-  const int q1 = M / 8, q2 = M / 4, q3 = M / 2;
-#elif FLEET_LADDER_STEPS == 2  // experiment (A/B builds): late rungs
-  const int q1 = M / 2, q2 = 3 * M / 4, q3 = 7 * M / 8;
-#else
-  const int q1 = M / 4, q2 = M / 2, q3 = 3 * M / 4;
-#endif
+  // rungs at quarters of the loop; the Kardam form's longer client steps settle later
+  // (rungs at 1/2, 3/4, 7/8: 1561 -> 1517 us on synth1m_256, where they cost the fused
+  // step 1.8 % and rungs at 1/8, 1/4, 1/2 lose everywhere; scripts/gpu_r04_a18.sh)
+  const int q1 = KD ? M / 2 : M / 4, q2 = KD ? 3 * M / 4 : M / 2, q3 = KD ? 7 * M / 8 : 3 * M / 4;
   if constexpr (LADDER) __builtin_amdgcn_s_setprio(3);
   if constexpr (KD) {
     // Kardam: one client per trip, the next one in flight (two per trip: 1840 against
