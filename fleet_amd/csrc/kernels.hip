@@ -35,9 +35,6 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
-#ifndef FLEET_TILE_P2_PRIO
-#define FLEET_TILE_P2_PRIO 0
-#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -1109,9 +1106,6 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
     __syncthreads();
     FLEET_TSTAMP(3);
     // phase 2: serial accumulation, one value per thread
-#if FLEET_TILE_P2_PRIO  // experiment (A/B builds): the serial phase at a higher issue priority
-    if (tid < E) __builtin_amdgcn_s_setprio(2);
-#endif
     if (tid < E) {
       int k = 0;
       if (c0 == 0) {
@@ -1141,9 +1135,6 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
         }
       }
     }
-#if FLEET_TILE_P2_PRIO
-    __builtin_amdgcn_s_setprio(0);
-#endif
     __syncthreads();
   }
   FLEET_TSTAMP(4);
