@@ -2526,12 +2526,14 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   // fill the slots the update's waves leave (a lane walks its group down the rows with
   // two loads in flight, so a block of hundreds of rows is a latency-bound straggler);
   // same-box A/B on synth1m_256: 1179 / 1170 us at 6 / 12 rows per block.
+  // (grid=lanes: the update's blocks a value per lane, for experiments on small windows)
   const int64_t gx = blocks_for(groups, 256);
-  const int nAf = (int)gx, rpb = std::min(M, 12);
+  const bool lanes = o.grid == 2;
+  const int nAf = lanes ? 0 : (int)gx, nUf = lanes ? (int)((groups + 83) / 84) : (int)gx, rpb = std::min(M, 12);
   const int64_t nE = gx * ((M + rpb - 1) / rpb);
   const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
-  hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nAf + nE)), dim3(256), 0, s, uploads, pitch, M, d_dampen,
-                     inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf, nAf, ej);
+  hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nUf + nE)), dim3(256), 0, s, uploads, pitch, M, d_dampen,
+                     inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf, nUf, ej);
   return hipGetLastError();
 }
 
