@@ -35,6 +35,9 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
+#ifndef FLEET_KD_WAVES
+#define FLEET_KD_WAVES 6  // experiment (A/B builds): the Kardam stream form's wave cap
+#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -654,7 +657,7 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
 // its register budget asks for at least 6 waves per SIMD (73 VGPRs, no scratch;
 // unconstrained it takes 91 VGPRs: 5 waves, 1922 against 1795 us on synth1m_256).
 template <int NT, bool KD>
-__global__ void __launch_bounds__(NT, KD ? 6 : 1) k_update_mixed(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+__global__ void __launch_bounds__(NT, KD ? FLEET_KD_WAVES : 1) k_update_mixed(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                      const double* __restrict__ dampen, double inv_avg,
                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
                                                      const int32_t* __restrict__ hdr_block,
