@@ -35,9 +35,6 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
-#ifndef FLEET_KD_WAVES
-#define FLEET_KD_WAVES 6  // experiment (A/B builds): the Kardam stream form's wave cap
-#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -655,9 +652,10 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
 // Both forms run the issue-priority ladder (update_lane: synth1m_256 828 -> 786 us
 // plain, 1776 -> 1502-1546 us with Kardam's side outputs, scripts/gpu_r04_a14.sh);
 // its register budget asks for at least 6 waves per SIMD (73 VGPRs, no scratch;
-// unconstrained it takes 91 VGPRs: 5 waves, 1922 against 1795 us on synth1m_256).
+// unconstrained it takes 91 VGPRs: 5 waves, 1922 against 1795 us on synth1m_256; at 7
+// or 8 waves it spills 16 / 64 B a lane and runs no faster, scripts/gpu_r04_a24.sh).
 template <int NT, bool KD>
-__global__ void __launch_bounds__(NT, KD ? FLEET_KD_WAVES : 1) k_update_mixed(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+__global__ void __launch_bounds__(NT, KD ? 6 : 1) k_update_mixed(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                      const double* __restrict__ dampen, double inv_avg,
                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
                                                      const int32_t* __restrict__ hdr_block,
