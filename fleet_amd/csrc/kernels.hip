@@ -35,6 +35,9 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
+#ifndef FLEET_FUSED_LADDER_TOP
+#define FLEET_FUSED_LADDER_TOP 3  // experiment (A/B builds): the fused step's first rung
+#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -456,7 +459,7 @@ __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uin
 // share a group). Returns the lane's merged codes in out[S] and its Base64 / layout
 // error bits; tables already in LDS. KD: Kardam's side outputs per client
 // (kardam_lane_step; kd_part = this wave's slot of client 0, kd_stride between clients).
-template <int S, bool KD = false, bool LADDER = false>
+template <int S, bool KD = false, int LADDER = 0>
 __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table& dtab,
                                             const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                             const double* __restrict__ dampen, double inv_avg, int64_t n_up,
@@ -550,14 +553,16 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // (rungs at 1/2, 3/4, 7/8: 1561 -> 1517 us on synth1m_256, where they cost the fused
   // step 1.8 % and rungs at 1/8, 1/4, 1/2 lose everywhere; scripts/gpu_r04_a18.sh)
   const int q1 = KD ? M / 2 : M / 4, q2 = KD ? 3 * M / 4 : M / 2, q3 = KD ? 7 * M / 8 : 3 * M / 4;
-  if constexpr (LADDER) __builtin_amdgcn_s_setprio(3);
+  // LADDER = the first rung's priority (0: no ladder); each rung one lower, floor 0
+  constexpr int P0 = LADDER, P1 = LADDER > 1 ? LADDER - 1 : 0, P2 = LADDER > 2 ? LADDER - 2 : 0;
+  if constexpr (LADDER > 0) __builtin_amdgcn_s_setprio(P0);
   if constexpr (KD) {
     // Kardam: one client per trip, the next one in flight (two per trip: 1840 against
     // 1795 us on synth1m_256, scripts/gpu_r04_a13.sh)
     for (; c < M; ++c) {
-      if constexpr (LADDER) {
-        if (c == q1) __builtin_amdgcn_s_setprio(2);
-        if (c == q2) __builtin_amdgcn_s_setprio(1);
+      if constexpr (LADDER > 0) {
+        if (c == q1) __builtin_amdgcn_s_setprio(P1);
+        if (c == q2) __builtin_amdgcn_s_setprio(P2);
         if (c == q3) __builtin_amdgcn_s_setprio(0);
       }
       const Row cur = b0;
@@ -567,9 +572,9 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   }
   for (; c + 1 < M; c += 2) {
     FLEET_CLIENT_HOOK(c, M);
-    if constexpr (LADDER) {
-      if (c == (q1 & ~1)) __builtin_amdgcn_s_setprio(2);
-      if (c == (q2 & ~1)) __builtin_amdgcn_s_setprio(1);
+    if constexpr (LADDER > 0) {
+      if (c == (q1 & ~1)) __builtin_amdgcn_s_setprio(P1);
+      if (c == (q2 & ~1)) __builtin_amdgcn_s_setprio(P2);
       if (c == (q3 & ~1)) __builtin_amdgcn_s_setprio(0);
     }
     b1 = group_of(c + 1);
@@ -594,7 +599,7 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
 }
 
 // Block `bid` of the SIMD-balanced stream grid (tables already in LDS).
-template <int NT, bool KD = false, bool LADDER = false>
+template <int NT, bool KD = false, int LADDER = 0>
 __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D16Table& dtab, int64_t bid,
                                                    const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                    const double* __restrict__ dampen, double inv_avg, int64_t n_up,
@@ -666,7 +671,7 @@ __global__ void __launch_bounds__(NT, KD ? 6 : 1) k_update_mixed(const uint8_t* 
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
   __syncthreads();
-  update_mixed_block<NT, KD, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+  update_mixed_block<NT, KD, 3>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                              hdr_block, merged, merged_f32, err, nA, kd);
 }
 
@@ -1469,8 +1474,9 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   // encode at 2 (scripts/gpu_r04_a15.sh), 1171-1176 -> 1153-1158 us from 2 to 3 on
   // another box (gpu_r04_a16.sh); at 0 (r04 a6: 1158 us) or 1 (1138-1142 us) slower
   if ((int)blockIdx.x < nU) {  // block-uniform
-    update_mixed_block<NT, false, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin,
-                                        g_end, hdr_block, merged, merged_f32, err, nA);
+    update_mixed_block<NT, false, FLEET_FUSED_LADDER_TOP>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg,
+                                                          n_up, g_begin, g_end, hdr_block, merged, merged_f32, err,
+                                                          nA);
   } else {
     const int64_t e = (int64_t)blockIdx.x - nU;
     __builtin_amdgcn_s_setprio(3);
