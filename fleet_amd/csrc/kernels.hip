@@ -35,9 +35,6 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
-#ifndef FLEET_FUSED_LADDER_TOP
-#define FLEET_FUSED_LADDER_TOP 3  // experiment (A/B builds): the fused step's first rung
-#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -1472,11 +1469,12 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   // encode's waves run at priority 3: the HBM-bound encode issues whenever it can, the
   // update waves that lag next. synth1m_256 step 1129-1133 -> 1119-1120 us with the
   // encode at 2 (scripts/gpu_r04_a15.sh), 1171-1176 -> 1153-1158 us from 2 to 3 on
-  // another box (gpu_r04_a16.sh); at 0 (r04 a6: 1158 us) or 1 (1138-1142 us) slower
+  // another box (gpu_r04_a16.sh); at 0 (r04 a6: 1158 us) or 1 (1138-1142 us) slower, and
+  // so were update waves laddered from 2 under the encode's 3 (1134-1141 against
+  // 1118-1129 us, gpu_r04_a26.sh)
   if ((int)blockIdx.x < nU) {  // block-uniform
-    update_mixed_block<NT, false, FLEET_FUSED_LADDER_TOP>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg,
-                                                          n_up, g_begin, g_end, hdr_block, merged, merged_f32, err,
-                                                          nA);
+    update_mixed_block<NT, false, 3>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+                                     hdr_block, merged, merged_f32, err, nA);
   } else {
     const int64_t e = (int64_t)blockIdx.x - nU;
     __builtin_amdgcn_s_setprio(3);
