@@ -852,17 +852,21 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const T
   dampen_stage<S>(rg, kd.lr);  // (float)((double)p * lr), lr uniform
   if constexpr (D16) q_stage_d16x<S>(G, rg, &sh.dt, sh.tab.var);  // exact (in-stage fallback)
   else q_stage<S>(G, rg, &sh.tab);
+  // per item: the flat slots, ||G||^2, prev and G - prev, the G row out; then one D stage
+  // for all the lane's items (one ballot / fix-up pass, not one per item)
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+  double sg[IPT], sd[IPT];
+  float dv[S], D[S];
+  uint32_t flat = 0, hasps = 0;
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
     const int c = it.c_base + it.cc[h];
     const int64_t gp = 3 * (g0 + it.gl[h]);
     const uint32_t hm = it.live[h] ? sh.hmask[it.gl[h]] : 7u;
     const bool hasp = kd.prev && it.live[h] && kd.has_prev[c];
-    double sg = 0.0, sd = 0.0;
-    float dv[3], D[3];
-    bool flat[3];
+    hasps |= (uint32_t)hasp << h;
+    sg[h] = 0.0;
     // prev / G rows: one 12-byte access per whole group (rows are 4-byte aligned)
-    typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
     const bool whole = it.live[h] && gp + 2 < n_up;
     float pv[3] = {0.0f, 0.0f, 0.0f};
     if (hasp && whole) {
@@ -875,12 +879,13 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const T
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
       const int64_t pos = gp + e;
-      flat[e] = it.live[h] && !((hm >> e) & 1u) && pos < n_up && pos < tk.walk_end;
+      const bool f = it.live[h] && !((hm >> e) & 1u) && pos < n_up && pos < tk.walk_end;
+      flat |= (uint32_t)f << (3 * h + e);
       const float g = G[3 * h + e];
-      if (flat[e]) sg += (double)(g * g);
-      if (hasp && !whole && flat[e]) pv[e] = kd.prev[(size_t)c * kd.vpitch + pos];
-      dv[e] = (flat[e] && hasp) ? g - pv[e] : 0.0f;
-      gv[e] = flat[e] ? g : 0.0f;
+      if (f) sg[h] += (double)(g * g);
+      if (hasp && !whole && f) pv[e] = kd.prev[(size_t)c * kd.vpitch + pos];
+      dv[3 * h + e] = (f && hasp) ? g - pv[e] : 0.0f;
+      gv[e] = f ? g : 0.0f;
     }
     if (kd.g_out) {
       float* go = kd.g_out + (size_t)c * kd.vpitch + gp;
@@ -892,17 +897,20 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const T
           if (it.live[h] && gp + e < n_up) go[e] = gv[e];
       }
     }
-    if constexpr (D16) q_stage_d16x<3>(D, dv, &sh.dt, sh.tab.var);
-    else q_stage<3>(D, dv, &sh.tab);
+  }
+  if constexpr (D16) q_stage_d16x<S>(D, dv, &sh.dt, sh.tab.var);
+  else q_stage<S>(D, dv, &sh.tab);
+#pragma unroll
+  for (int h = 0; h < IPT; ++h) {
+    sd[h] = 0.0;
 #pragma unroll
     for (int e = 0; e < 3; ++e)
-      if (flat[e] && hasp) sd += (double)(D[e] * D[e]);
-    sg = group_sum_f64<TG>(sg);
-    sd = group_sum_f64<TG>(sd);
+      if (((flat >> (3 * h + e)) & 1u) && ((hasps >> h) & 1u)) sd[h] += (double)(D[3 * h + e] * D[3 * h + e]);
+    const double a = group_sum_f64<TG>(sg[h]), b = group_sum_f64<TG>(sd[h]);
     if (it.cvalid[h] && (threadIdx.x & (TG - 1)) == TG - 1) {  // the group's last lane: its client's tile sum
       const size_t slot = ((size_t)(it.c_base + it.cl[h]) * tk.ntiles + tk.tile) * 2;
-      kd.partials[slot] = sg;
-      kd.partials[slot + 1] = sd;
+      kd.partials[slot] = a;
+      kd.partials[slot + 1] = b;
     }
   }
 }
