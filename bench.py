@@ -609,8 +609,8 @@ def newest_profile(name: str):
 
 def kernel_key(kern: dict, kernel: str):
     """The entry of `kernel` in a profile summary: the exact rocprofv3 name, else the
-    same kernel with default template arguments spelled differently (k_update<1> /
-    k_update<1, false> / k_update<1, false, 256>; k_update_tiled_encode<64> /
+    same kernel with default template arguments spelled differently (k_update_mixed<256> /
+    k_update_mixed<256, false>; k_update_tiled_encode<64> /
     k_update_tiled_encode<64, 0>)."""
     if kernel in kern:
         return kernel
