@@ -35,6 +35,9 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
+#ifndef FLEET_FUSED_RPB
+#define FLEET_FUSED_RPB 12  // experiment (A/B builds): rows per encode block of the fused stream step
+#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -2542,7 +2545,8 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   // (grid=lanes: the update's blocks a value per lane, for experiments on small windows)
   const int64_t gx = blocks_for(groups, 256);
   const bool lanes = o.grid == 2;
-  const int nAf = lanes ? 0 : (int)gx, nUf = lanes ? (int)((groups + 83) / 84) : (int)gx, rpb = std::min(M, 12);
+  const int nAf = lanes ? 0 : (int)gx, nUf = lanes ? (int)((groups + 83) / 84) : (int)gx;
+  const int rpb = std::min(M, FLEET_FUSED_RPB);
   const int64_t nE = gx * ((M + rpb - 1) / rpb);
   const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
   hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nUf + nE)), dim3(256), 0, s, uploads, pitch, M, d_dampen,
