@@ -36,7 +36,7 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   } while (0)
 #endif
 #ifndef FLEET_FUSED_RPB
-#define FLEET_FUSED_RPB 12  // experiment (A/B builds): rows per encode block of the fused stream step
+#define FLEET_FUSED_RPB 24  // experiment (A/B builds): rows per encode block of the fused stream step
 #endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
@@ -2538,10 +2538,12 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   // the stream grid group-per-lane everywhere: the encode's blocks fill the SIMDs the
   // last round of update waves leaves idle, so the value-per-lane balancing of
   // k_update_mixed only adds instructions here (same-box A/B on synth1m_256: 1172.7 vs
-  // 1181.3 us, scripts/gpu_fused_ab.sh). 12 rows per encode block: short blocks that
+  // 1181.3 us, scripts/gpu_fused_ab.sh). 24 rows per encode block: short blocks that
   // fill the slots the update's waves leave (a lane walks its group down the rows with
   // two loads in flight, so a block of hundreds of rows is a latency-bound straggler);
-  // same-box A/B on synth1m_256: 1179 / 1170 us at 6 / 12 rows per block.
+  // same-box A/B on synth1m_256: 1179 / 1170 us at 6 / 12 rows per block in r03; with
+  // the encode's waves at priority 3 (r04) 1130 / 1097-1100 / 1084-1090 us at 6 / 12 /
+  // 24 (scripts/gpu_r04_a31.sh).
   // (grid=lanes: the update's blocks a value per lane, for experiments on small windows)
   const int64_t gx = blocks_for(groups, 256);
   const bool lanes = o.grid == 2;
