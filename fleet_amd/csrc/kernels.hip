@@ -35,9 +35,6 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
-#ifndef FLEET_FUSED_RPB
-#define FLEET_FUSED_RPB 24  // experiment (A/B builds): rows per encode block of the fused stream step
-#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -2543,12 +2540,12 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   // two loads in flight, so a block of hundreds of rows is a latency-bound straggler);
   // same-box A/B on synth1m_256: 1179 / 1170 us at 6 / 12 rows per block in r03; with
   // the encode's waves at priority 3 (r04) 1130 / 1097-1100 / 1084-1090 us at 6 / 12 /
-  // 24 (scripts/gpu_r04_a31.sh).
+  // 24, and 48 no better (scripts/gpu_r04_a31.sh, a32.sh).
   // (grid=lanes: the update's blocks a value per lane, for experiments on small windows)
   const int64_t gx = blocks_for(groups, 256);
   const bool lanes = o.grid == 2;
   const int nAf = lanes ? 0 : (int)gx, nUf = lanes ? (int)((groups + 83) / 84) : (int)gx;
-  const int rpb = std::min(M, FLEET_FUSED_RPB);
+  const int rpb = std::min(M, 24);
   const int64_t nE = gx * ((M + rpb - 1) / rpb);
   const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
   hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nUf + nE)), dim3(256), 0, s, uploads, pitch, M, d_dampen,
