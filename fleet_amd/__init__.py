@@ -152,7 +152,9 @@ def lib() -> C.CDLL:
         "fleet_sampler_create_from": (i32, [vp, vp, vp, sz, i32, i32, i32, i32, i32, i32, i32, C.POINTER(vp)]),
         "fleet_sampler_destroy": (None, [vp]),
         "fleet_sampler_last_error": (C.c_char_p, [vp]),
-        "fleet_updater_reseed": (None, [i32, i32]),
+        "fleet_last_ingress": (i32, [vp]),
+        "fleet_updater_reseed_ex": (None, [i32, i32]),
+        "fleet_updater_reseed": (None, [i32]),
         "fleet_sampler_set_hyper": (i32, [vp, i32, C.c_double, C.c_double]),
         "fleet_sampler_set_teacher": (i32, [vp, vp, sz, vp, sz]),
         "fleet_sampler_minibatch": (i32, [vp, i32, C.c_float, vp, sz, szp]),
@@ -188,7 +190,7 @@ def exported_symbols_from_header(path: str = HEADER_PATH):
 
 
 def b64_len(n_values: int) -> int:
-    """Base64 length of n int32 values: 4*ceil(4n/3) (Base64.cpp:166-175)."""
+    """Base64 length of n int32 values: 4*ceil(4n/3) (Base64.cpp:129-136)."""
     return 4 * ((4 * n_values + 2) // 3)
 
 
@@ -342,17 +344,17 @@ class Codec:
 
     # -- Base64.cpp -------------------------------------------------------------
     def encode_floats(self, v) -> bytes:
-        """Base64::encode(std::vector<float>) (Base64.cpp:140-142)."""
+        """Base64::encode(std::vector<float>) (Base64.cpp:104-106)."""
         v = np.ascontiguousarray(v, dtype=np.float32)
         return self._text_call(self._L.fleet_encode_f32, (v.ctypes.data, len(v)), b64_len(len(v)))
 
     def encode_ints(self, v) -> bytes:
-        """Base64::encode(std::vector<int>) (Base64.cpp:145-151)."""
+        """Base64::encode(std::vector<int>) (Base64.cpp:109-115)."""
         v = np.ascontiguousarray(v, dtype=np.int32)
         return self._text_call(self._L.fleet_encode_i32, (v.ctypes.data, len(v)), b64_len(len(v)))
 
     def decode_floats(self, text) -> np.ndarray:
-        """Base64::decodeFloat (Base64.cpp:207-209)."""
+        """Base64::decodeFloat (Base64.cpp:171-173)."""
         s = _as_bytes(text)
         out = np.empty(b64_count(len(s)) + 1, np.float32)
         n = C.c_size_t(0)
@@ -360,7 +362,7 @@ class Codec:
         return out[: n.value].copy()
 
     def decode_ints(self, text) -> np.ndarray:
-        """Base64::decodeInt (Base64.cpp:211-219)."""
+        """Base64::decodeInt (Base64.cpp:175-183)."""
         s = _as_bytes(text)
         out = np.empty(b64_count(len(s)) + 1, np.int32)
         n = C.c_size_t(0)

@@ -1,6 +1,6 @@
 // fleet_amd/csrc/codec_device.h -- device-side FLeet codec pieces for gfx950:
-//   decimal fixed-point arithmetic (codec_math.h, Base64.cpp:73-139)
-//   Base64 text <-> bytes           (Base64.cpp:56-68,160-205,221-253)
+//   decimal fixed-point arithmetic (codec_math.h, Base64.cpp:37-103)
+//   Base64 text <-> bytes           (Base64.cpp:20-27,124-169,185-217)
 //   Philox synthetic gradient source
 #pragma once
 
@@ -13,13 +13,13 @@ namespace fleet {
 
 // ------------------------------------------------------------------ Base64
 
-// Base64.cpp:56-68 `from_base64`, extended with 0xff for bytes >= 0x80
+// Base64.cpp:20-27 `from_base64`, extended with 0xff for bytes >= 0x80
 // (the reference indexes out of bounds there; such text is rejected here).
 // Every kernel copies this block of tables into LDS at start (b64_tables_init).
 struct B64Tables {
   MulEntry mt[16];    // step multipliers by digit count (codec_math.h)
   VarEntry var[512];  // digit count by sign + biased exponent (codec_math.h)
-  uint8_t from[256];  // Base64.cpp:56-68, 0xff = not in the alphabet
+  uint8_t from[256];  // Base64.cpp:20-27, 0xff = not in the alphabet
   uint8_t to[64];
 };
 static_assert(sizeof(B64Tables) % 16 == 0, "copied as uint4");
@@ -199,7 +199,7 @@ __device__ __forceinline__ uint32_t b64_decode_pair(uint32_t w0, uint32_t w1, ui
   return bad;
 }
 
-// 3 codes -> 12 bytes -> 16 chars (Base64.cpp:176-195).
+// 3 codes -> 12 bytes -> 16 chars (Base64.cpp:141-162).
 __device__ __forceinline__ uint4 b64_encode_group(const int32_t codes[3], const B64Tables* t) {
   const uint32_t c0 = (uint32_t)codes[0], c1 = (uint32_t)codes[1], c2 = (uint32_t)codes[2];
   // inverse of the perms above: V[q] = 24-bit big-endian view of bytes 3q..3q+2

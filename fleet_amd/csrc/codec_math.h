@@ -2,7 +2,7 @@
 // host+device (the host build exists only so tests/native can check the fast
 // paths exhaustively against the oracle on CPU).
 //
-// Bit-exact restatement of commonLib/cpp_utils/Base64.cpp:73-139 as the
+// Bit-exact restatement of commonLib/cpp_utils/Base64.cpp:37-103 as the
 // reference's x86-64 SSE build computes it: one IEEE binary32 RNE rounding per
 // multiply/divide, `(int)` = cvttss2si. Compile with -ffp-contract=off; every
 // fused multiply-add below is explicit.
@@ -52,7 +52,7 @@ FLEET_HD f2 div10x2(f2 t) {
 // x86-64 `(int)x` (cvttss2si): INT_MIN when |x| >= 2^31 or x is NaN.
 FLEET_HD int32_t cvtt(float x) { return __builtin_fabsf(x) < 2147483648.0f ? (int32_t)x : INT32_MIN; }
 
-// Base64::numDigits (Base64.cpp:73-82): decimal digits of n, '-' counted.
+// Base64::numDigits (Base64.cpp:37-46): decimal digits of n, '-' counted.
 FLEET_HD int num_digits(int32_t n) {
   uint32_t a = n < 0 ? 0u - (uint32_t)n : (uint32_t)n;
   int d = n < 0;
@@ -71,7 +71,7 @@ FLEET_HD int num_digits(int32_t n) {
 
 // ------------------------------------------------------------ general, exact
 
-// Base64::int2float (Base64.cpp:127-134): k = 9 - |c % 10| divisions of (float)c.
+// Base64::int2float (Base64.cpp:91-98): k = 9 - |c % 10| divisions of (float)c.
 FLEET_HD float dec(int32_t c) {
   int dd = c % 10;
   dd = dd < 0 ? -dd : dd;
@@ -84,7 +84,7 @@ FLEET_HD float dec(int32_t c) {
   return t;
 }
 
-// Base64::float2int (Base64.cpp:96-109): 9 - d multiplications by 10,
+// Base64::float2int (Base64.cpp:60-73): 9 - d multiplications by 10,
 // truncation, last decimal digit replaced by d.
 FLEET_HD int32_t enc(float x) {
   int d = num_digits(cvtt(x));
@@ -271,7 +271,7 @@ FLEET_HD f2 steps_div10x2(f2 t, Steps s0, Steps s1) {
   return sel2(s0.b2, s1.b2, u, t);
 }
 
-// |code| = 10*(n/10) + d with n = trunc(|x| * 10^(9-d)) (Base64.cpp:104-108)
+// |code| = 10*(n/10) + d with n = trunc(|x| * 10^(9-d)) (Base64.cpp:64-70)
 FLEET_HD float signed_code_float(uint32_t n, int d, float x) {
   uint32_t c = (n / 10u) * 10u + (uint32_t)d;
   return u2f(f2u((float)c) | (f2u(x) & 0x80000000u));
@@ -398,7 +398,7 @@ FLEET_HDC MulEntry mul_entry(uint32_t d) {  // d = numDigits; d > 9 (slow marker
 
 // Digit table entry i = (sign << 8) | biased exponent of x. The binade holds at
 // most one power of ten, thr: numDigits((int)x) is dlo for |x| < thr and dhi =
-// dlo + 1 for |x| >= thr ('-' counts, Base64.cpp:73-82). The entry keeps
+// dlo + 1 for |x| >= thr ('-' counts, Base64.cpp:37-46). The entry keeps
 // base = dlo + 1, so d = base - (|x| < thr) is three integer ops (sub, shift,
 // sub) with no select or bit-field extract. d > 9 marks values outside the
 // q_gen domain (-1e8 < x < 1e9), NaN and inf (callers send those through the

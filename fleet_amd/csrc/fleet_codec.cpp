@@ -133,6 +133,7 @@ struct fleet_ctx {
   int32_t* h_hdr = nullptr;
   int* h_err = nullptr;
   std::unique_ptr<WorkerPool> pool;  // staging copy threads (stage_uploads)
+  int last_ingress = FLEET_INGRESS_NONE;  // how the last host-buffer update reached HBM
 };
 
 namespace {
@@ -477,6 +478,16 @@ void fleet_destroy(fleet_ctx* c) {
 
 const char* fleet_last_error(const fleet_ctx* c) { return c ? c->err.c_str() : "no context"; }
 
+namespace {
+std::atomic<int> g_last_ingress{FLEET_INGRESS_NONE};  // the process's most recent one
+}
+
+int fleet_last_ingress(fleet_ctx* c) {
+  if (!c) return g_last_ingress.load();
+  std::lock_guard<std::mutex> lk(c->mu);
+  return c->last_ingress;
+}
+
 int fleet_sync(fleet_ctx* c, void* stream) {
   if (!c) return FLEET_ERR_ARG;
   HIP_TRY(c, hipStreamSynchronize(pick(c, stream)));
@@ -732,6 +743,8 @@ int update_window(fleet_ctx* c, const char* const* uploads, size_t len, int M, c
   std::memcpy(c->h_stage + o_hdr, hw, sizeof(int32_t) * kHdrWords);
   std::memcpy(c->h_stage + o_damp, dampen, sizeof(double) * (size_t)M);
   std::memset(c->h_stage + o_err, 0, 16);
+  c->last_ingress = pinned_rows ? FLEET_INGRESS_PINNED : FLEET_INGRESS_STAGED;
+  g_last_ingress.store(c->last_ingress);
   if (pinned_rows) {
     HIP_TRY(c, hipMemcpy2DAsync(c->d_a, wpitch, pinned_rows + col0, row_pitch, width, (size_t)M,
                                 hipMemcpyHostToDevice, c->stream));
@@ -1047,10 +1060,13 @@ int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch
   if ((d_prev || d_g_out) && vpitch < n) return fail(c, FLEET_ERR_ARG, "vpitch %zu < %zu values", vpitch, n);
   hipStream_t s = pick(c, stream);
   if ((rc = dev_params(c, s, n, M, dampen, header_pos, n_headers))) return rc;
+  // one snapshot of the launch plan for the sizing call and the launch (a concurrent
+  // fleet_set_plan must not give the launch more partial slots than were sized)
+  const fleet::PlanOverrides plan = fleet::plan_overrides();
   int nw_sz = 0, parts_sz = 1;  // partial slots and norm parts per client of the launch plan (sizing call)
   fleet::KardamOut kd0{lr, nullptr, nullptr, 0, nullptr, nullptr};
   (void)fleet::launch_update_kardam(nullptr, pitch, M, nullptr, 0.0, (int64_t)n, 0, (int64_t)ge, nullptr, nullptr,
-                                    nullptr, nullptr, kd0, &nw_sz, nullptr, &parts_sz, s);
+                                    nullptr, nullptr, kd0, &nw_sz, nullptr, &parts_sz, plan, s);
   (void)hipGetLastError();
   const size_t n_waves = (size_t)std::max(nw_sz, 1), n_parts = (size_t)std::max(parts_sz, 1);
   // scratch: [partials M x slots x 2 | norms M x parts x 2 | has_prev M]; synchronous call (host outputs)
@@ -1066,8 +1082,9 @@ int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch
   int nw = 0, np = 1;
   HIP_TRY(c, fleet::launch_update_kardam((const uint8_t*)d_uploads, pitch, M, c->d_dev_dampen, (double)1 / M,
                                          (int64_t)n, 0, (int64_t)ge, c->d_dev_hdr, (uint8_t*)d_merged,
-                                         (float*)d_merged_f32, c->d_dev_err, kd, &nw, d_norm, &np, s));
-  if ((size_t)np != n_parts) return fail(c, FLEET_ERR_HIP, "Kardam launch plan changed between sizing and launch");
+                                         (float*)d_merged_f32, c->d_dev_err, kd, &nw, d_norm, &np, plan, s));
+  if ((size_t)np != n_parts || (size_t)std::max(nw, 1) != n_waves)
+    return fail(c, FLEET_ERR_HIP, "Kardam launch plan changed between sizing and launch");
   std::vector<double> norms(2 * (size_t)M * n_parts);
   HIP_TRY(c, hipMemcpyAsync(norms.data(), d_norm, sizeof(double) * norms.size(), hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));

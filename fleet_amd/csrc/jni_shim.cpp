@@ -159,6 +159,50 @@ int update_ptrs(const std::vector<fleet_ctx*>& cs, const char* const* ups, const
   return fleet_update(cs[0], ups, lens, M, d, out, cap, n, nullptr);
 }
 
+// Direct ByteBuffers page-locked by registerDirectNative, each with a weak global
+// reference to its Java object. The library's registration record only knows an
+// address range; the weak reference tells whether the buffer that owns the range is
+// still alive. A buffer the JVM collected without unregisterDirectNative (its Cleaner
+// freed the memory; a later buffer may sit at the same address) leaves a stale page
+// lock: aggregateDirectNative finds it by address, sees the referent gone, releases
+// the registration and stages the rows instead of DMAing from the stale pages.
+struct DirectReg {
+  uintptr_t base;
+  size_t bytes;
+  jweak ref;
+};
+std::mutex g_direct_mu;
+std::vector<DirectReg> g_direct;
+
+// drop the shim's records overlapping [a, a + bytes) (the library released their page
+// locks when a new registration covered them)
+void forget_overlapping(JNIEnv* env, uintptr_t a, size_t bytes) {
+  for (size_t i = g_direct.size(); i-- > 0;) {
+    const DirectReg& r = g_direct[i];
+    if (r.base < a + bytes && a < r.base + r.bytes) {
+      env->DeleteWeakGlobalRef(r.ref);
+      g_direct.erase(g_direct.begin() + (long)i);
+    }
+  }
+}
+
+// Before rows [p, p + bytes) of `buf` go to fleet_update_rows: every registration
+// they touch must belong to a live buffer. One whose buffer was collected is released
+// (library page lock and record), so the library stages those rows.
+void release_stale(JNIEnv* env, fleet_ctx* c, jobject buf, const char* p, size_t bytes) {
+  const uintptr_t a = (uintptr_t)p;
+  std::lock_guard<std::mutex> lk(g_direct_mu);
+  for (size_t i = g_direct.size(); i-- > 0;) {
+    const DirectReg r = g_direct[i];
+    if (!(r.base < a + bytes && a < r.base + r.bytes)) continue;
+    // alive: the same buffer, or another live view of the registered memory
+    if (env->IsSameObject(r.ref, buf) || !env->IsSameObject(r.ref, nullptr)) continue;
+    (void)fleet_host_unregister(c, (void*)r.base);
+    env->DeleteWeakGlobalRef(r.ref);
+    g_direct.erase(g_direct.begin() + (long)i);
+  }
+}
+
 int update_rows(const std::vector<fleet_ctx*>& cs, const char* rows, size_t pitch, size_t len, int M, const double* d,
                 char* out, size_t cap, size_t* n) {
   if (cs.size() > 1) return fleet_update_rows_multi(cs.data(), (int)cs.size(), rows, pitch, len, M, d, out, cap, n, nullptr);
@@ -330,6 +374,7 @@ JNIEXPORT jbyteArray JNICALL Java_apps_cppNN_FleetUpdater_aggregateDirectNative(
     return fail(cs[0], "aggregateDirectNative (not a direct buffer of M rows)", FLEET_ERR_ARG);
   std::vector<double> d((size_t)M);
   env->GetDoubleArrayRegion(dampen, 0, M, d.data());
+  release_stale(env, cs[0], rows, base, (size_t)rowPitch * (size_t)(M - 1) + (size_t)len);
   std::vector<char> out((size_t)len + 16);
   size_t n = 0;
   const int rc = update_rows(cs, base, (size_t)rowPitch, (size_t)len, (int)M, d.data(), out.data(), out.size(), &n);
@@ -343,20 +388,34 @@ JNIEXPORT jboolean JNICALL Java_apps_cppNN_FleetUpdater_registerDirectNative(JNI
   void* p = env->GetDirectBufferAddress(buf);
   const jlong cap = env->GetDirectBufferCapacity(buf);
   if (!p || cap <= 0) return JNI_FALSE;
+  std::lock_guard<std::mutex> lk(g_direct_mu);
   const int rc = fleet_host_register(c, p, (size_t)cap);
-  if (rc != FLEET_OK) fail(c, "registerDirectNative", rc);
-  return rc == FLEET_OK ? JNI_TRUE : JNI_FALSE;
+  if (rc != FLEET_OK) {
+    fail(c, "registerDirectNative", rc);
+    return JNI_FALSE;
+  }
+  // the library released any registration overlapping this one: so do the records
+  forget_overlapping(env, (uintptr_t)p, (size_t)cap);
+  const jweak ref = env->NewWeakGlobalRef(buf);
+  if (ref) g_direct.push_back(DirectReg{(uintptr_t)p, (size_t)cap, ref});
+  return JNI_TRUE;
 }
 
-// Releases the page lock; the Java side must call it before the buffer is dropped
-// (its Cleaner frees the memory): a registration left behind still looks live to
-// the library until a later registerDirectNative covers the same memory
-// (fleet_host_register), and rows inside it would be DMA'd from the old pages.
+// Releases the page lock; the Java side should call it before the buffer is dropped
+// (its Cleaner frees the memory). A registration left behind is caught by its weak
+// reference: the next aggregateDirectNative over that memory finds the buffer
+// collected, releases the registration and stages the rows (release_stale).
 JNIEXPORT void JNICALL Java_apps_cppNN_FleetUpdater_unregisterDirectNative(JNIEnv* env, jobject, jobject buf) {
   fleet_ctx* c = ctx();
   if (!c || !buf) return;
   void* p = env->GetDirectBufferAddress(buf);
   if (!p) return;
+  std::lock_guard<std::mutex> lk(g_direct_mu);
+  for (size_t i = g_direct.size(); i-- > 0;)
+    if (g_direct[i].base == (uintptr_t)p) {
+      env->DeleteWeakGlobalRef(g_direct[i].ref);
+      g_direct.erase(g_direct.begin() + (long)i);
+    }
   const int rc = fleet_host_unregister(c, p);
   if (rc != FLEET_OK) fail(c, "unregisterDirectNative", rc);
 }
@@ -380,7 +439,7 @@ JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_fetchParamsNative(JNIEnv* en
 }
 
 // initUpdater (:161-225): srand(seed) and the rand() draws of its
-// cnn.train_class (fleet_updater_reseed: two, for the random shift that
+// cnn.train_class (fleet_updater_reseed_ex: two, for the random shift that
 // fetchParamsNative's set_random_augmentation enables; none before a fetch), E /
 // sigma / C for the sampler's mini-batch headers, and the model part (lrates, the
 // first version).
@@ -393,7 +452,7 @@ JNIEXPORT void JNICALL Java_apps_cppNN_CppNNUpdater_initUpdater(JNIEnv* env, job
   }
   {
     std::lock_guard<std::mutex> lk(g_sampler_mu);
-    fleet_updater_reseed(kSeed, fetched ? 1 : 0);
+    fleet_updater_reseed_ex(kSeed, fetched ? 1 : 0);
     g_E = E;
     g_sigma = sigma;
     g_C = C;

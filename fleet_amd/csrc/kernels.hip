@@ -56,7 +56,7 @@ __device__ __forceinline__ uint32_t needed_chars_mask(int r) {
   return r >= 3 ? 0xffffu : r == 2 ? 0x7ffu : r == 1 ? 0x3fu : 0u;
 }
 
-// Base64.cpp:196-198 -- trailing '=' for the missing bytes of a partial group
+// Base64.cpp:164-166 -- trailing '=' for the missing bytes of a partial group
 __device__ __forceinline__ uint4 pad_group(uint4 v, int r) {
   if (r == 1) {  // 4 bytes -> 6 chars + "=="
     v.y = (v.y & 0x0000ffffu) | 0x3d3d0000u;
@@ -261,7 +261,7 @@ __device__ __forceinline__ void dampen_stage(float (&r)[S], double d) {
   }
 }
 
-// out[i] = int2float(codes[i]) (Base64.cpp:116-139): fixed 9-step chains when
+// out[i] = int2float(codes[i]) (Base64.cpp:80-103): fixed 9-step chains when
 // every code of the wave ends in 0 (|value| < 1), else step multipliers from
 // the last digit. Total: no fallback needed.
 template <int S>
@@ -2414,13 +2414,13 @@ __global__ void __launch_bounds__(kKfThreads) k_kardam_finish(const float* rows,
 hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                                 int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
-                                double* norms, int* norm_parts, hipStream_t s) {
+                                double* norms, int* norm_parts, const PlanOverrides& o, hipStream_t s) {
   const int64_t groups = g_end - g_begin;
   // the update's own launch plan with the side outputs: the pipelined tiles (their
   // producers store p; k_kardam_finish does the rest), the wide tiles (side outputs
   // from the tile producers), or the stream kernel's SIMD-balanced grid
-  UpdatePlan p = plan_update(groups, plan_overrides());
-  if (p.kind == 0 && plan_overrides().grid == 0) {
+  UpdatePlan p = plan_update(groups, o);
+  if (p.kind == 0 && o.grid == 0) {
     // the stream form on the plain grid unless a grid is asked for: value-per-lane waves
     // pay the per-client wave sums for a third of the values (synth1m_256: 1747 vs
     // 1724 us, scripts/gpu_r04_a6.sh)

@@ -8,7 +8,7 @@
 //   fleet_sampler_create    initSampler (:385-479): srand(seed), the MNIST
 //                           training set (commonLib/cppNN/mnist_parser.h), the
 //                           non-IID buckets
-//   fleet_updater_reseed    initUpdater's srand(seed) (:163) and the rand()
+//   fleet_updater_reseed(_ex) initUpdater's srand(seed) (:163) and the rand()
 //                           draws of its one cnn.train_class (:216/:222) after a fetch
 //   fleet_sampler_set_hyper initUpdater's E, sigma, C (:169-171)
 //   fleet_sampler_minibatch getMiniBatch (:677-699) = uniformSample (:553-634)
@@ -217,7 +217,7 @@ void fleet_sampler_destroy(fleet_sampler* s) { delete s; }
 
 const char* fleet_sampler_last_error(const fleet_sampler* s) { return s ? s->err.c_str() : "no sampler"; }
 
-void fleet_updater_reseed(int seed, int fetched) {
+void fleet_updater_reseed_ex(int seed, int fetched) {
   std::srand((unsigned)seed);
   // cnn.train_class(train_images[0], ...) after it: the random shift of
   // set_random_augmentation(1, 1, 0, 0, edge) (fetchParamsNative :293) draws
@@ -228,6 +228,8 @@ void fleet_updater_reseed(int seed, int fetched) {
     (void)std::rand();
   }
 }
+
+void fleet_updater_reseed(int seed) { fleet_updater_reseed_ex(seed, 1); }
 
 int fleet_sampler_set_hyper(fleet_sampler* s, int E, double sigma, double C) {
   if (!s) return FLEET_ERR_ARG;

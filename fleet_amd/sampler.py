@@ -190,7 +190,7 @@ class NativeSampler:
         """initUpdater's srand(seed) and, after fetchParamsNative (fetched), its
         train_class's two rand() draws."""
         from . import lib
-        lib().fleet_updater_reseed(seed, int(bool(fetched)))
+        lib().fleet_updater_reseed_ex(seed, int(bool(fetched)))
 
     def set_hyper(self, E: int, sigma: float, C: float) -> None:
         self._check(self._L.fleet_sampler_set_hyper(self._h, int(E), float(sigma), float(C)))

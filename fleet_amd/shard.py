@@ -187,12 +187,16 @@ class ClientShardedUpdater(ShardedUpdater):
             return
         last = Mr > 0 and cb + Mr == M
         part = merged_f32[:n].double() if Mr else torch.zeros(n, dtype=torch.float64, device=merged_f32.device)
-        keep = getattr(self, "_keep", None)
-        if keep is None or keep.numel() != n:
+        # the header-slot mask, cached per (n, header positions): a later call with other
+        # header positions at the same n must not reuse the old mask
+        key = (n, tuple(int(h) for h in header_pos))
+        cached = getattr(self, "_keep", None)
+        if cached is None or cached[0] != key:
             keep = torch.zeros(n, dtype=torch.bool, device=part.device)
             if len(header_pos):
                 keep[torch.as_tensor(np.asarray(header_pos), dtype=torch.long, device=part.device)] = True
-            self._keep = keep
+            self._keep = cached = (key, keep)
+        keep = cached[1]
         acc = torch.where(keep, part if last else torch.zeros_like(part), part * (Mr / M))
         dist.all_reduce(acc, op=dist.ReduceOp.SUM, group=self.group)
         vals = values_buf if values_buf is not None else torch.empty((1, 3 * ((n + 2) // 3)), dtype=torch.float32,

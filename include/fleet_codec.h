@@ -15,9 +15,9 @@
  *     hipStream_t passed as void* (NULL = the null/default stream). Host-buffer
  *     entry points run on the context's own stream and return synchronously.
  *   - "Base64" buffers are the reference's wire format: Base64 (RFC 4648
- *     alphabet; '-' and '_' accepted as 62/63 on input, Base64.cpp:56-68) of
+ *     alphabet; '-' and '_' accepted as 62/63 on input, from_base64 at Base64.cpp:20-27) of
  *     little-endian int32 decimal fixed-point codes (Base64::float2int,
- *     Base64.cpp:84-114). Host buffers are NOT NUL-terminated.
+ *     Base64.cpp:48-78). Host buffers are NOT NUL-terminated.
  *   - Every function returns FLEET_OK (0) or a negative FLEET_ERR_* code;
  *     fleet_last_error() gives a message. The reference has no error
  *     reporting (malformed input is UB there); here it is rejected.
@@ -58,7 +58,7 @@ void fleet_destroy(fleet_ctx* ctx);
 const char* fleet_last_error(const fleet_ctx* ctx);
 int fleet_sync(fleet_ctx* ctx, void* stream);
 
-/* Base64 length of n int32/fp32 values: 4*ceil(4n/3) (Base64.cpp:166-175). */
+/* Base64 length of n int32/fp32 values: 4*ceil(4n/3) (Base64.cpp:129-136). */
 size_t fleet_b64_len(size_t n_values);
 /* Number of int32 values carried by a Base64::encode output of length len. */
 size_t fleet_b64_count(size_t len);
@@ -148,6 +148,15 @@ int fleet_update_rows_multi(fleet_ctx* const* ctxs, int n_ctx, const char* rows,
  * stale pinned pages. */
 int fleet_host_register(fleet_ctx* ctx, void* ptr, size_t bytes);
 int fleet_host_unregister(fleet_ctx* ctx, void* ptr);
+/* How the last host-buffer update on ctx (fleet_update*, its window on this context)
+ * reached HBM: FLEET_INGRESS_STAGED (copied into the context's pinned staging),
+ * FLEET_INGRESS_PINNED (one DMA straight from registered rows), or
+ * FLEET_INGRESS_NONE before any. ctx NULL: the process's most recent such update
+ * on any context (e.g. those of the JNI shim). Diagnostics and tests. */
+#define FLEET_INGRESS_NONE 0
+#define FLEET_INGRESS_STAGED 1
+#define FLEET_INGRESS_PINNED 2
+int fleet_last_ingress(fleet_ctx* ctx);
 
 /* Device-resident entry points (all buffers are device pointers) ----------
  * Uploads are stored as M rows of `pitch` bytes (pitch >= 16*ceil(len/16),
@@ -464,7 +473,11 @@ const char* fleet_sampler_last_error(const fleet_sampler* s);
  * enabled the random shift, :293), the two rand() draws of cnn.train_class's shift
  * (network.h:1840). Assumes the reference's MNIST network: no dropout layer (whose
  * training forward would draw more, layer.h:608-617) and no flips. */
-void fleet_updater_reseed(int seed, int fetched);
+void fleet_updater_reseed_ex(int seed, int fetched);
+/* the original one-argument form: fleet_updater_reseed_ex(seed, 1) (a model was
+ * fetched, the reference's server order) -- kept so callers built against it keep
+ * their meaning */
+void fleet_updater_reseed(int seed);
 /* initUpdater's E, sigma, C (:169-171), read by every later mini-batch header */
 int fleet_sampler_set_hyper(fleet_sampler* s, int E, double sigma, double C);
 /* DISTILLATION_MODE=1 with iid sampling: the trained teacher's weights

@@ -19,7 +19,7 @@
 
 /* ---------------------------------------------------------------- scalars */
 
-/* Base64.cpp:73-82 -- '-' counts as a digit; numDigits(0) == 0. */
+/* Base64.cpp:37-46 -- '-' counts as a digit; numDigits(0) == 0. */
 int fo_num_digits(int32_t number) {
   int digits = 0;
   if (number < 0) digits = 1;
@@ -36,7 +36,7 @@ int32_t fo_cvtt(float x) {
   return (int32_t)x;
 }
 
-/* Base64.cpp:84-114 with intNum == 1, precision == 9. */
+/* Base64.cpp:48-78 with intNum == 1, precision == 9. */
 int32_t fo_float2int(float x) {
   const int precision = 9;
   int digits = fo_num_digits(fo_cvtt(x));
@@ -49,7 +49,7 @@ int32_t fo_float2int(float x) {
   return (int32_t)t;
 }
 
-/* Base64.cpp:116-139 with intNum == 1, precision == 9. */
+/* Base64.cpp:80-103 with intNum == 1, precision == 9. */
 float fo_int2float(int32_t c) {
   const int precision = 9;
   int dd = abs(c % 10);
@@ -62,7 +62,7 @@ float fo_q(float x) { return fo_int2float(fo_float2int(x)); }
 
 /* ----------------------------------------------------------------- base64 */
 
-/* Base64.cpp:56-68 */
+/* Base64.cpp:20-27 */
 static const uint8_t from_b64[128] = {
     255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255,
     255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255, 255,
@@ -76,7 +76,7 @@ static const char to_b64[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwx
 
 size_t fo_b64_len(size_t n_values) { return 4 * ((4 * n_values + 2) / 3); }
 
-/* Base64.cpp:160-205 */
+/* Base64.cpp:124-169 */
 size_t fo_b64_encode(const uint8_t* buf, size_t len, char* out) {
   size_t missing = 0, ret_size = len;
   while (ret_size % 3 != 0) {
@@ -99,13 +99,13 @@ size_t fo_b64_encode(const uint8_t* buf, size_t len, char* out) {
 }
 
 static uint8_t sextet(char ch) {
-  /* `(ch <= 'z') ? from_base64[ch] : 0xff` (Base64.cpp:233-236). Bytes >= 0x80
+  /* `(ch <= 'z') ? from_base64[ch] : 0xff` (Base64.cpp:199-202). Bytes >= 0x80
    * index the table out of bounds in the reference (UB); treated as pad here. */
   unsigned char u = (unsigned char)ch;
   return u <= 'z' ? from_b64[u] : 0xff;
 }
 
-/* Base64.cpp:221-253 (the string is first padded with '=' to a multiple of 4) */
+/* Base64.cpp:185-217 (the string is first padded with '=' to a multiple of 4) */
 size_t fo_b64_decode(const char* s, size_t len, uint8_t* out) {
   size_t n = 0;
   size_t padded = (len + 3) / 4 * 4;
@@ -122,11 +122,11 @@ size_t fo_b64_decode(const char* s, size_t len, uint8_t* out) {
   return n;
 }
 
-/* Base64.cpp:145-151 */
+/* Base64.cpp:109-115 */
 size_t fo_encode_ints(const int32_t* v, size_t n, char* out) {
   return fo_b64_encode((const uint8_t*)v, n * sizeof(int32_t), out);
 }
-/* Base64.cpp:140-142 */
+/* Base64.cpp:104-106 */
 size_t fo_encode_floats(const float* v, size_t n, char* out) {
   int32_t* codes = (int32_t*)malloc(sizeof(int32_t) * (n ? n : 1));
   for (size_t i = 0; i < n; ++i) codes[i] = fo_float2int(v[i]);
@@ -134,7 +134,7 @@ size_t fo_encode_floats(const float* v, size_t n, char* out) {
   free(codes);
   return r;
 }
-/* Base64.cpp:211-219 */
+/* Base64.cpp:175-183 */
 size_t fo_decode_ints(const char* s, size_t len, int32_t* out) {
   uint8_t* bytes = (uint8_t*)malloc(len + 4);
   size_t nb = fo_b64_decode(s, len, bytes);
@@ -143,7 +143,7 @@ size_t fo_decode_ints(const char* s, size_t len, int32_t* out) {
   free(bytes);
   return n;
 }
-/* Base64.cpp:207-209 */
+/* Base64.cpp:171-173 */
 size_t fo_decode_floats(const char* s, size_t len, float* out) {
   int32_t* codes = (int32_t*)malloc(len + 4);
   size_t n = fo_decode_ints(s, len, codes);

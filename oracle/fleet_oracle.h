@@ -28,20 +28,20 @@
 extern "C" {
 #endif
 
-/* commonLib/cpp_utils/Base64.cpp:73-82 */
+/* commonLib/cpp_utils/Base64.cpp:37-46 */
 int fo_num_digits(int32_t number);
 /* x86-64 `(int) float` (cvttss2si): INT32_MIN when |x| >= 2^31 or NaN. */
 int32_t fo_cvtt(float x);
-/* Base64.cpp:84-114, intNum == 1, precision == 9 */
+/* Base64.cpp:48-78, intNum == 1, precision == 9 */
 int32_t fo_float2int(float x);
-/* Base64.cpp:116-139, intNum == 1, precision == 9 */
+/* Base64.cpp:80-103, intNum == 1, precision == 9 */
 float fo_int2float(int32_t c);
 /* Q = int2float o float2int: what the next JNI op sees after an encode. */
 float fo_q(float x);
 
-/* Base64.cpp:160-205: bytes -> text; returns text length (4*ceil(len/3)). */
+/* Base64.cpp:124-169: bytes -> text; returns text length (4*ceil(len/3)). */
 size_t fo_b64_encode(const uint8_t* buf, size_t len, char* out);
-/* Base64.cpp:211-253: text -> bytes (pad/invalid sextets drop bytes). */
+/* Base64.cpp:175-217: text -> bytes (pad/invalid sextets drop bytes). */
 size_t fo_b64_decode(const char* s, size_t len, uint8_t* out);
 size_t fo_b64_len(size_t n_values);
 

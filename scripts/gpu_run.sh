@@ -1,0 +1,73 @@
+# Parameterised GPU call: run named steps in order, each under its own time limit,
+# stopping at the first failure. Output under gpurun_out/$TAG/.
+# usage (through gpurun, from the repo root):
+#   TAG=r05b0 bash scripts/gpu_run.sh tests smoke bench strong windows:cifar10_256 profile
+# steps:
+#   tests            full pytest -m gpu
+#   smoke            __graft_entry__.smoke()
+#   bench            the default bench line (bench_default.json)
+#   strong[:W]       per-rank pipelined windows of W (default synth1m_256) at N = 1, 2, 4, 8
+#                    on one GPU (scripts/strong_probe.py), fused / update-only
+#   windows:W        W at N = 1 only: the fused step, the update alone, the encode alone
+#   profile[:W,..]   scripts/gpu_profile.sh $TAG (kernel trace + PMC passes)
+#   ab               scripts/gpu_ab_multi.sh (LIBS, WORKLOADS, REPS from the environment)
+#   kardam[:W,..]    Kardam side outputs vs the plain update (scripts/kardam_ab.py under rocprofv3)
+#   py:FILE          python3 FILE (a probe script), output in $TAG/FILE.log
+set -u
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$PWD}"
+TAG=${TAG:-run}
+O=${OUTROOT:-$PWD/gpurun_out}/$TAG; mkdir -p "$O"
+for step in "$@"; do
+  name=${step%%:*}; arg=""; [ "$name" != "$step" ] && arg=${step#*:}
+  echo "== $step"
+  case $name in
+    tests)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > "$O/tests.log" 2>&1 \
+        || { tail -30 "$O/tests.log"; exit 1; }
+      tail -1 "$O/tests.log" ;;
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { tail -20 "$O/smoke.log"; exit 1; }
+      tail -1 "$O/smoke.log" ;;
+    bench)
+      timeout -k 10 900 python3 bench.py > "$O/bench_default.json" 2> "$O/bench_default.err" || { tail -20 "$O/bench_default.err"; exit 1; }
+      cut -c1-400 "$O/bench_default.json" ;;
+    strong)
+      W=${arg:-synth1m_256}
+      for mode in fused upd; do
+        timeout -k 10 300 python3 scripts/strong_probe.py "$W" 1,2,4,8 $mode >> "$O/strong_$W.txt" 2>&1 || { tail -20 "$O/strong_$W.txt"; exit 1; }
+      done
+      cat "$O/strong_$W.txt" ;;
+    windows)
+      for mode in fused upd enc; do
+        timeout -k 10 300 python3 scripts/strong_probe.py "$arg" 1 $mode >> "$O/windows_$arg.txt" 2>&1 || { tail -20 "$O/windows_$arg.txt"; exit 1; }
+      done
+      cat "$O/windows_$arg.txt" ;;
+    profile)
+      OUTROOT=$(dirname "$O") bash scripts/gpu_profile.sh "$TAG" ${arg//,/ } || exit 1 ;;
+    ab)
+      bash scripts/gpu_ab_multi.sh > "$O/ab.txt" 2>&1 || { tail -20 "$O/ab.txt"; exit 1; }
+      cat "$O/ab.txt" ;;
+    kardam)
+      for W in ${arg:-mnist64 cifar10_256 synth1m_256}; do
+        W=${W//,/ }
+        for w in $W; do
+          timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/kardam_$w" -o run -- \
+            python3 scripts/kardam_ab.py "$w" > "$O/kardam_$w.log" 2>&1 || { tail -20 "$O/kardam_$w.log"; exit 1; }
+          echo "-- $w"
+          python3 -c "
+import csv
+for r in csv.DictReader(open('$O/kardam_$w/run_kernel_stats.csv')):
+    n = r['Name']
+    if 'k_update' in n or 'k_kardam' in n:
+        print('%-42s calls %4s avg %8.1f us' % (n.split('(')[0].replace('void fleet::', '').replace('fleet::', ''),
+                                                r['Calls'], float(r['AverageNs']) / 1e3))
+" | tee -a "$O/kardam.txt"
+        done
+      done ;;
+    py)
+      timeout -k 10 600 python3 "$arg" > "$O/$(basename "$arg").log" 2>&1 || { tail -30 "$O/$(basename "$arg").log"; exit 1; }
+      tail -40 "$O/$(basename "$arg").log" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done"

@@ -36,6 +36,8 @@ def fakejvm():
     L.fakejvm_new_array.argtypes = [C.c_int, vp, C.c_int]
     L.fakejvm_new_object_array.restype = vp
     L.fakejvm_new_object_array.argtypes = [vp, C.c_int]
+    L.fakejvm_collect.restype = None
+    L.fakejvm_collect.argtypes = [vp]
     L.fakejvm_new_direct.restype = vp
     L.fakejvm_new_direct.argtypes = [vp, C.c_long]
     L.fakejvm_new_string.restype = vp
@@ -46,6 +48,11 @@ def fakejvm():
     L.fakejvm_array_data.argtypes = [vp]
     _lib = L
     return L
+
+
+def collect(obj) -> None:
+    """The garbage collector reclaims obj: weak references to it now equal NULL."""
+    fakejvm().fakejvm_collect(obj)
 
 
 def env():

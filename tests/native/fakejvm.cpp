@@ -13,7 +13,10 @@
 //   * Get<Type>ArrayElements hands out copies (as HotSpot does) that must be
 //     released; outstanding ones are reported as leaked pins;
 //   * an optional limit on EnsureLocalCapacity / PushLocalFrame simulates a
-//     JVM that cannot grant a large frame (OutOfMemoryError pending).
+//     JVM that cannot grant a large frame (OutOfMemoryError pending);
+//   * weak global references: fakejvm_collect(obj) plays the garbage collector
+//     (a weak reference to a collected object then IsSameObject-equals NULL);
+//     live weak references are counted.
 // Built by tests/jnifake.py with g++ (no JDK exists in the image).
 #include <jni.h>
 
@@ -24,7 +27,7 @@
 
 namespace {
 
-enum Kind { BYTES = 1, INTS, FLOATS, DOUBLES, OBJECTS, DIRECT, STRING, CLASS };
+enum Kind { BYTES = 1, INTS, FLOATS, DOUBLES, OBJECTS, DIRECT, STRING, CLASS, WEAK };
 
 struct Obj {
   int kind;
@@ -34,6 +37,8 @@ struct Obj {
   std::vector<Obj*> objs;  // object array elements
   void* direct = nullptr;  // direct buffer
   jlong cap = 0;
+  bool collected = false;  // fakejvm_collect: only weak references may still name it
+  Obj* target = nullptr;   // WEAK: the referent
 };
 
 struct Frame {
@@ -43,7 +48,7 @@ struct Frame {
 
 struct State {
   std::vector<Frame> frames;
-  long overflows = 0, critical_violations = 0, pins = 0, criticals = 0, max_live = 0, exceptions = 0;
+  long overflows = 0, critical_violations = 0, pins = 0, criticals = 0, max_live = 0, exceptions = 0, weak = 0;
   long frame_limit = 1L << 30;
   int critical_depth = 0;
   bool pending = false;
@@ -230,6 +235,32 @@ jlong JNICALL GetDirectBufferCapacity(JNIEnv*, jobject b) {
   jni_call();
   return O(b)->kind == DIRECT ? O(b)->cap : -1;
 }
+// a reference resolved to its object: a weak one to its referent, NULL once collected
+Obj* resolve(jobject r) {
+  Obj* o = O(r);
+  if (o && o->kind == WEAK) o = o->target;
+  return o && o->collected ? nullptr : o;
+}
+jboolean JNICALL IsSameObject(JNIEnv*, jobject a, jobject b) {
+  jni_call();
+  return resolve(a) == resolve(b) ? JNI_TRUE : JNI_FALSE;
+}
+jweak JNICALL NewWeakGlobalRef(JNIEnv*, jobject r) {
+  jni_call();
+  Obj* t = resolve(r);
+  if (!t) return nullptr;
+  Obj* w = make(WEAK, 0, 1);
+  w->target = t;
+  g.weak++;
+  return (jweak)w;
+}
+void JNICALL DeleteWeakGlobalRef(JNIEnv*, jweak w) {
+  jni_call();
+  if (w && O(w)->kind == WEAK) {
+    delete O(w);
+    g.weak--;
+  }
+}
 
 JNINativeInterface_ make_table() {
   JNINativeInterface_ t;
@@ -267,6 +298,9 @@ JNINativeInterface_ make_table() {
   t.SetDoubleArrayRegion = (void(JNICALL*)(JNIEnv*, jdoubleArray, jsize, jsize, const jdouble*))SetRegion<jdouble>;
   t.GetPrimitiveArrayCritical = GetPrimitiveArrayCritical;
   t.ReleasePrimitiveArrayCritical = ReleasePrimitiveArrayCritical;
+  t.IsSameObject = IsSameObject;
+  t.NewWeakGlobalRef = NewWeakGlobalRef;
+  t.DeleteWeakGlobalRef = DeleteWeakGlobalRef;
   t.NewDirectByteBuffer = NewDirectByteBuffer;
   t.GetDirectBufferAddress = GetDirectBufferAddress;
   t.GetDirectBufferCapacity = GetDirectBufferCapacity;
@@ -297,6 +331,7 @@ __attribute__((visibility("default"))) long fakejvm_stat(const char* what) {
   if (!std::strcmp(what, "criticals")) return g.criticals;
   if (!std::strcmp(what, "critical_depth")) return g.critical_depth;
   if (!std::strcmp(what, "pins")) return g.pins;
+  if (!std::strcmp(what, "weak")) return g.weak;
   if (!std::strcmp(what, "live")) return live();
   if (!std::strcmp(what, "max_live")) return g.max_live;
   if (!std::strcmp(what, "pending")) return g.pending ? 1 : 0;
@@ -326,6 +361,12 @@ __attribute__((visibility("default"))) void* fakejvm_new_direct(void* p, long ca
   o->direct = p;
   o->cap = cap;
   return o;
+}
+
+// the garbage collector reclaims `obj` (the test dropped its last strong reference):
+// weak references to it now equal NULL; its memory is kept (handles stay readable)
+__attribute__((visibility("default"))) void fakejvm_collect(void* obj) {
+  if (obj) O(obj)->collected = true;
 }
 
 // a java.lang.String (modified UTF-8 = the bytes given, NUL-terminated)

@@ -119,7 +119,7 @@ struct JNINativeInterface_ {
   void* NewGlobalRef;
   void* DeleteGlobalRef;
   void(JNICALL* DeleteLocalRef)(JNIEnv*, jobject); /* 23 */
-  void* IsSameObject;
+  jboolean(JNICALL* IsSameObject)(JNIEnv*, jobject, jobject); /* 24 */
   void* NewLocalRef;
   jint(JNICALL* EnsureLocalCapacity)(JNIEnv*, jint); /* 26 */
   void* AllocObject;
@@ -321,8 +321,8 @@ struct JNINativeInterface_ {
   void(JNICALL* ReleasePrimitiveArrayCritical)(JNIEnv*, jarray, void*, jint); /* 223 */
   void* GetStringCritical;
   void* ReleaseStringCritical;
-  void* NewWeakGlobalRef;
-  void* DeleteWeakGlobalRef;
+  jweak(JNICALL* NewWeakGlobalRef)(JNIEnv*, jobject); /* 226 */
+  void(JNICALL* DeleteWeakGlobalRef)(JNIEnv*, jweak); /* 227 */
   jboolean(JNICALL* ExceptionCheck)(JNIEnv*); /* 228 */
   jobject(JNICALL* NewDirectByteBuffer)(JNIEnv*, void*, jlong); /* 229 */
   void*(JNICALL* GetDirectBufferAddress)(JNIEnv*, jobject); /* 230 */
@@ -342,6 +342,9 @@ struct JNIEnv_ {
   jint PushLocalFrame(jint capacity) { return functions->PushLocalFrame(this, capacity); }
   jobject PopLocalFrame(jobject result) { return functions->PopLocalFrame(this, result); }
   void DeleteLocalRef(jobject o) { functions->DeleteLocalRef(this, o); }
+  jboolean IsSameObject(jobject a, jobject b) { return functions->IsSameObject(this, a, b); }
+  jweak NewWeakGlobalRef(jobject o) { return functions->NewWeakGlobalRef(this, o); }
+  void DeleteWeakGlobalRef(jweak w) { functions->DeleteWeakGlobalRef(this, w); }
   jint EnsureLocalCapacity(jint capacity) { return functions->EnsureLocalCapacity(this, capacity); }
   const char* GetStringUTFChars(jstring s, jboolean* isCopy) { return functions->GetStringUTFChars(this, s, isCopy); }
   void ReleaseStringUTFChars(jstring s, const char* c) { functions->ReleaseStringUTFChars(this, s, c); }
@@ -395,6 +398,7 @@ struct JNIEnv_ {
 
 static_assert(offsetof(JNINativeInterface_, GetVersion) == 4 * sizeof(void*), "JNI table layout");
 static_assert(offsetof(JNINativeInterface_, DeleteLocalRef) == 23 * sizeof(void*), "JNI table layout");
+static_assert(offsetof(JNINativeInterface_, IsSameObject) == 24 * sizeof(void*), "JNI table layout");
 static_assert(offsetof(JNINativeInterface_, EnsureLocalCapacity) == 26 * sizeof(void*), "JNI table layout");
 static_assert(offsetof(JNINativeInterface_, GetArrayLength) == 171 * sizeof(void*), "JNI table layout");
 static_assert(offsetof(JNINativeInterface_, NewByteArray) == 176 * sizeof(void*), "JNI table layout");
@@ -402,6 +406,7 @@ static_assert(offsetof(JNINativeInterface_, GetByteArrayElements) == 184 * sizeo
 static_assert(offsetof(JNINativeInterface_, ReleaseDoubleArrayElements) == 198 * sizeof(void*), "JNI table layout");
 static_assert(offsetof(JNINativeInterface_, SetByteArrayRegion) == 208 * sizeof(void*), "JNI table layout");
 static_assert(offsetof(JNINativeInterface_, GetPrimitiveArrayCritical) == 222 * sizeof(void*), "JNI table layout");
+static_assert(offsetof(JNINativeInterface_, NewWeakGlobalRef) == 226 * sizeof(void*), "JNI table layout");
 static_assert(offsetof(JNINativeInterface_, ExceptionCheck) == 228 * sizeof(void*), "JNI table layout");
 static_assert(offsetof(JNINativeInterface_, GetDirectBufferCapacity) == 231 * sizeof(void*), "JNI table layout");
 static_assert(sizeof(JNINativeInterface_) == 234 * sizeof(void*), "JNI table size (JNI 9+)");

@@ -15,7 +15,7 @@ The same uploads then go through the pipelined step the bench times
 k_update_tiled_encode at CIFAR sizes) at the full client count, with a second
 synthetic batch as the next round's values: its merged text and merged_f32 are
 checked against the same oracle result, and the next batch's uploads it writes
-against the oracle's client encode (fo_encode_floats, Base64.cpp:140-205) of the
+against the oracle's client encode (fo_encode_floats, Base64.cpp:104-169) of the
 sampled values -- Base64 groups are independent, so the cut-down text of the
 sampled groups is the encode of the sampled values."""
 import numpy as np

@@ -262,3 +262,54 @@ def test_shim_direct_buffer_reregistration(oracle):
                                                                              J.new_doubles(d)))
     assert out == oracle.update_faithful(ups, d)
     check_rules(J)
+
+
+@pytest.mark.gpu
+def test_shim_collected_registration_is_not_used(oracle):
+    """A direct buffer the JVM collected without unregisterDirectNative:
+    a new buffer at the same address must not be DMA'd through the old page lock. The
+    shim keeps a weak reference per registration; aggregateDirectNative sees the
+    referent gone, releases the registration and stages the rows."""
+    import jnifake as J
+    L = load()
+    env = J.env()
+    M = 3
+    ups = [oracle.encode_floats(oracle.synth_upload(11, c, list(MNIST.w_sizes), list(MNIST.b_sizes)))
+           for c in range(M)]
+    Lb = len(ups[0])
+    rows = np.zeros(M * Lb, np.uint8)
+    for i, u in enumerate(ups):
+        rows[i * Lb:(i + 1) * Lb] = np.frombuffer(u, np.uint8)
+    d = [1.0, 0.5, 0.25]
+    want = oracle.update_faithful(ups, d)
+    J.begin()
+    weak0 = J.stat("weak")
+    old = J.new_direct(rows)
+    assert L.Java_apps_cppNN_FleetUpdater_registerDirectNative(env, None, old) == 1
+    assert J.stat("weak") == weak0 + 1
+    # the registered, live buffer: copy-free
+    out = J.read_bytes(L.Java_apps_cppNN_FleetUpdater_aggregateDirectNative(env, None, old, M, Lb, Lb,
+                                                                             J.new_doubles(d)))
+    assert out == want and F.lib().fleet_last_ingress(None) == 2  # FLEET_INGRESS_PINNED
+    # another live view of the same memory (a duplicate()): still copy-free
+    view = J.new_direct(rows)
+    out = J.read_bytes(L.Java_apps_cppNN_FleetUpdater_aggregateDirectNative(env, None, view, M, Lb, Lb,
+                                                                             J.new_doubles(d)))
+    assert out == want and F.lib().fleet_last_ingress(None) == 2
+    # dropped without unregisterDirectNative; a new buffer at the same address
+    J.collect(old)
+    J.collect(view)
+    new = J.new_direct(rows)
+    out = J.read_bytes(L.Java_apps_cppNN_FleetUpdater_aggregateDirectNative(env, None, new, M, Lb, Lb,
+                                                                             J.new_doubles(d)))
+    assert out == want
+    assert F.lib().fleet_last_ingress(None) == 1  # FLEET_INGRESS_STAGED: the stale lock was not used
+    assert J.stat("weak") == weak0  # the stale record's weak reference was deleted
+    # registering the new buffer works, and it is copy-free again
+    assert L.Java_apps_cppNN_FleetUpdater_registerDirectNative(env, None, new) == 1
+    out = J.read_bytes(L.Java_apps_cppNN_FleetUpdater_aggregateDirectNative(env, None, new, M, Lb, Lb,
+                                                                             J.new_doubles(d)))
+    assert out == want and F.lib().fleet_last_ingress(None) == 2
+    L.Java_apps_cppNN_FleetUpdater_unregisterDirectNative(env, None, new)
+    assert J.stat("weak") == weak0
+    check_rules(J)

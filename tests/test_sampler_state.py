@@ -293,6 +293,19 @@ def test_reseed_without_a_fetched_model_draws_nothing():
     assert got == lc.rand()
 
 
+def test_one_argument_reseed_keeps_its_meaning():
+    """fleet_updater_reseed(seed) is the original one-argument symbol: the fetched-model
+    form, fleet_updater_reseed_ex(seed, 1) (the ABI must not change under
+    the same name)."""
+    import fleet_amd
+    lc = _libc()
+    fleet_amd.lib().fleet_updater_reseed(5)
+    got = lc.rand()
+    lc.srand(5)
+    lc.rand(), lc.rand()
+    assert got == lc.rand()
+
+
 def _libc():
     lc = C.CDLL(None)
     lc.rand.restype = C.c_int
