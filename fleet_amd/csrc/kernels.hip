@@ -1212,6 +1212,195 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
                                   dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged, merged_f32, err, tk);
 }
 
+// ----------------------------------------------------------------------------
+// Woven tiles (r05): the two phases of k_update_tiled in ONE barrier interval and
+// in the same instruction stream. A block of NW waves owns 64 groups (E = 192
+// values) and walks the clients in chunks of NW: wave w produces client c0 + w's
+// p for the tile's 64 groups (one group per lane, so the dampening factor is
+// wave-uniform), while three consumer waves run the serial A = Q(A + p) of the
+// PREVIOUS chunk, one value per lane, from the other half of a double-buffered p
+// chunk. The serial steps sit between the producer's stages in the source, so
+// they share basic blocks with independent work and the scheduler fills their
+// dependent latency (k_update_tiled's phase 2 ran one dependent chain per wave
+// between two barriers: 2.95 cycles per VALU instruction against the stream
+// kernel's 2.42, profiles/r04/sq.json). One barrier per chunk instead of two; the
+// next chunk's group is loaded one chunk ahead. NW = 4: the block's fourth wave
+// only produces, and which wave that is rotates with the tile (every SIMD of a CU
+// carries the same share of serial work).
+constexpr int kWeaveTG = 64, kWeaveE = 3 * kWeaveTG;
+
+template <int NW>
+struct WeaveShared {
+  TileShared<kWeaveTG, NW, true> t;
+  float p[2][NW * kWeaveE];  // double-buffered p chunk: client j of the chunk at [j * E + value]
+};
+
+// The consumer's serial step A = Q(A + p) (the stream kernel's stage C, var_d16: branch
+// free); FIRST: the chain's first client, A = p.
+template <bool FIRST>
+__device__ __forceinline__ void weave_step(float& A, float p, const D16Table& dt, const VarEntry* vt, uint32_t& emax) {
+  if constexpr (FIRST) {
+    A = p;
+  } else {
+    const float s = A + p;
+    const uint32_t e = var_d16(f2u(s), vt);
+    emax = max(emax, e);
+    A = q_d16(s, e, &dt.st);
+  }
+}
+
+// One producer lane's item: client c (wave-uniform), group g0 + gl of the tile, its
+// 16 chars `w` already loaded -> the three p of the item, with the consumer's steps
+// of the previous chunk (CS of them, from `pc`, column `col`) woven between the stages.
+// CS = 0: produce only. FIRST: the consumed chunk is the chain's first.
+template <int NW, int CS, bool FIRST>
+__device__ __forceinline__ void weave_item(WeaveShared<NW>& sh, uint4 w, bool live, int c, int gl, int M,
+                                           const double* __restrict__ dampen, int64_t n_up, int64_t walk_end,
+                                           int64_t g0, float* __restrict__ pdst, uint32_t& badacc, float& A,
+                                           const float* __restrict__ pc, int col, uint32_t& emax) {
+  TileShared<kWeaveTG, NW, true>& t = sh.t;
+  float pp[CS > 0 ? CS : 1];
+#pragma unroll
+  for (int j = 0; j < CS; ++j) pp[j] = pc[j * kWeaveE + col];  // the consumed chunk's p: loads in flight early
+  int32_t codes[3];
+  const int64_t gp = 3 * (g0 + gl);
+  const int r = (int)min<int64_t>(3, max<int64_t>(0, n_up - gp));
+  uint32_t b;
+  if (r == 3) b = b64_decode_group_full(w, &t.tab, codes);
+  else b = b64_decode_group(w, &t.tab, codes) & needed_chars_mask(r);
+  if (live) {
+    badacc |= b;
+    if (c == M - 1)
+#pragma unroll
+      for (int e = 0; e < 3; ++e) t.last_codes[3 * gl + e] = codes[e];
+    const uint32_t hm = t.hmask[gl];
+    if (hm) {  // header slots (rare lanes): the layout check, then the chain runs on code 0 (keep_bits)
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if ((hm >> e) & 1u) {
+          atomicMin(&t.hmin[3 * gl + e], codes[e]);
+          atomicMax(&t.hmax[3 * gl + e], codes[e]);
+          codes[e] = 0;
+        }
+    }
+  }
+  if (gp + 3 > walk_end) {  // rare: slots past network::flatGrad's walk run on code 0 too
+#pragma unroll
+    for (int e = 0; e < 3; ++e)
+      if (gp + e >= walk_end) codes[e] = 0;
+  }
+  // stage A: y = Q(int2float(code))
+  float y0[3], y[3];
+  dec_stage_d16<3>(y0, codes, &t.dt);
+  if constexpr (CS > 0) weave_step<FIRST>(A, pp[0], t.dt, t.tab.var, emax);
+  q_stage_d16x<3>(y, y0, &t.dt, t.tab.var);
+  if constexpr (CS > 1) weave_step<false>(A, pp[1], t.dt, t.tab.var, emax);
+  // stage B: p = Q(f32(f64(y) * d_c)), d wave-uniform (the wave is one client)
+  dampen_stage<3>(y, dampen[__builtin_amdgcn_readfirstlane(c < M ? c : M - 1)]);
+  float p[3];
+  q_stage_d16x<3>(p, y, &t.dt, t.tab.var);
+#pragma unroll
+  for (int j = 2; j < CS; ++j) weave_step<false>(A, pp[j], t.dt, t.tab.var, emax);
+#pragma unroll
+  for (int e = 0; e < 3; ++e) pdst[3 * gl + e] = live ? p[e] : 0.0f;
+}
+
+// Tile `bid` of the woven grid (LDS state in sh).
+template <int NW>
+__device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t bid, const uint8_t* __restrict__ uploads,
+                                                   size_t pitch, int M, const double* __restrict__ dampen,
+                                                   double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end,
+                                                   const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
+                                                   float* __restrict__ merged_f32, int* __restrict__ err) {
+  static_assert(NW == 3 || NW == 4, "three consumer waves (+ one producer-only wave)");
+  constexpr int E = kWeaveE, CM = NW;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t g0 = g_begin + bid * kWeaveTG;
+  const int ng = (int)min<int64_t>(kWeaveTG, g_end - g0);
+  const int64_t walk_end = hdr_block[2];
+  // consumers: every wave but the light one (NW = 4: rotates with the tile)
+  const int light = NW == 4 ? (int)(bid & 3) : -1;
+  const bool consumer = wave != light;  // wave-uniform
+  const int col = (wave - (light >= 0 && wave > light ? 1 : 0)) * 64 + lane;  // consumer's value
+  const int nchunks = (M + CM - 1) / CM;
+  const int gl = lane;
+  const bool glive = gl < ng;
+  const uint8_t* rowbase = uploads + 16 * (g0 + (glive ? gl : 0));
+  auto load = [&](int k) -> uint4 {  // chunk k's group of this lane (client k * CM + wave)
+    const int c = k * CM + wave;
+    return *reinterpret_cast<const uint4*>(rowbase + (size_t)(c < M ? c : M - 1) * pitch);
+  };
+  uint4 nxt = load(0);  // in flight while the tables are copied
+  tile_init(sh.t, hdr_block + 4, hdr_block[1], g0, ng);
+  uint32_t badacc = 0, emax = 0;
+  float A = 0.0f;
+  // interval 0: produce chunk 0
+  {
+    const uint4 cur = nxt;
+    if (nchunks > 1) nxt = load(1);
+    const int c = wave;
+    weave_item<NW, 0, false>(sh, cur, glive && c < M, c, gl, M, dampen, n_up, walk_end, g0, sh.p[0] + wave * E, badacc,
+                             A, nullptr, col, emax);
+  }
+  __syncthreads();
+  // intervals 1 .. nchunks-1: produce chunk k, consume chunk k-1 (always CM clients)
+  for (int k = 1; k < nchunks; ++k) {
+    const uint4 cur = nxt;
+    if (k + 1 < nchunks) nxt = load(k + 1);
+    const int c = k * CM + wave;
+    float* pdst = sh.p[k & 1] + wave * E;
+    const float* pc = sh.p[(k - 1) & 1];
+    if (consumer) {
+      if (k == 1)
+        weave_item<NW, CM, true>(sh, cur, glive && c < M, c, gl, M, dampen, n_up, walk_end, g0, pdst, badacc, A, pc,
+                                 col, emax);
+      else
+        weave_item<NW, CM, false>(sh, cur, glive && c < M, c, gl, M, dampen, n_up, walk_end, g0, pdst, badacc, A, pc,
+                                  col, emax);
+    } else {
+      weave_item<NW, 0, false>(sh, cur, glive && c < M, c, gl, M, dampen, n_up, walk_end, g0, pdst, badacc, A,
+                               nullptr, col, emax);
+    }
+    __syncthreads();
+  }
+  // the last interval: consume the last chunk (cm clients)
+  if (consumer) {
+    const float* pc = sh.p[(nchunks - 1) & 1];
+    const int cm = M - (nchunks - 1) * CM;
+    int j = 0;
+    if (nchunks == 1) {
+      A = pc[col];
+      j = 1;
+    }
+    for (; j < cm; ++j) weave_step<false>(A, pc[j * E + col], sh.t.dt, sh.t.tab.var, emax);
+  }
+  if (badacc) atomicOr(err, FLEET_ERRBIT_BASE64);
+  // a running sum outside the q_gen domain (never for gradients): the whole chain again, exactly
+  const bool off = consumer && col < 3 * ng && emax >= kD16Out;
+  if (__ballot(off)) {
+    if (off) A = chain_general(uploads, pitch, M, dampen, g0 + col / 3, col % 3, &sh.t.tab);
+  }
+  __syncthreads();  // every consumer is done with the p buffers
+  float* finals = sh.p[0];
+  if (consumer) finals[col] = A;
+  __syncthreads();
+  tile_epilogue(sh.t, finals, inv_avg, n_up, walk_end, g0, ng, merged, merged_f32, err,
+                reinterpret_cast<int32_t*>(sh.p[1]));
+}
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_update_weave(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                          const double* __restrict__ dampen, double inv_avg,
+                                                          int64_t n_up, int64_t g_begin, int64_t g_end,
+                                                          const int32_t* __restrict__ hdr_block,
+                                                          uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                          int* __restrict__ err) {
+  __shared__ WeaveShared<NW> sh;
+  update_weave_block<NW>(sh, xcd_tile(blockIdx.x, gridDim.x), uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+                         hdr_block, merged, merged_f32, err);
+}
+
 
 // Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
 // Block (bx, by) encodes groups [NT*bx, NT*bx+NT) of rows [rpb*by, rpb*by+rpb):
@@ -1551,6 +1740,31 @@ __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __re
     const int64_t e = (int64_t)blockIdx.x - nU;
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                       (int)(e / ej.gx), &sh.tab, &sh.dt);
+  }
+}
+
+// The woven tiles with the next batch's client encode riding in the launch (the
+// pipelined step at CIFAR sizes): blocks [0, nU) are tiles, the rest the encode's
+// 64*NW-lane blocks on the tile's tables.
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_update_weave_encode(const uint8_t* __restrict__ uploads, size_t pitch,
+                                                                 int M, const double* __restrict__ dampen,
+                                                                 double inv_avg, int64_t n_up, int64_t g_begin,
+                                                                 int64_t g_end, const int32_t* __restrict__ hdr_block,
+                                                                 uint8_t* __restrict__ merged,
+                                                                 float* __restrict__ merged_f32, int* __restrict__ err,
+                                                                 int nU, EncodeJob ej) {
+  __shared__ WeaveShared<NW> sh;
+  if ((int)blockIdx.x < nU) {  // block-uniform
+    update_weave_block<NW>(sh, xcd_tile(blockIdx.x, nU), uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+                           hdr_block, merged, merged_f32, err);
+  } else {
+    b64_tables_init<64 * NW>(&sh.t.tab);
+    d16_table_init<64 * NW>(&sh.t.dt);
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x - nU;
+    encode_rows<true, 64 * NW>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                               (int)(e / ej.gx), &sh.t.tab, &sh.t.dt);
   }
 }
 
@@ -2020,6 +2234,12 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
       else if (v == "plain") o->grid = 1;
       else if (v == "lanes") o->grid = 2;
       else ok = false;
+    } else if (k == "tile") {
+      if (v == "auto") o->tile = 0;
+      else if (v == "classic") o->tile = 1;
+      else if (v == "weave3") o->tile = 3;
+      else if (v == "weave4") o->tile = 4;
+      else ok = false;
     } else if (k == "tile_mix") {
       if (v == "auto") o->tile_mix = 0;
       else if (v == "off") o->tile_mix = 1;
@@ -2033,7 +2253,7 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
     } else if (k == "stage_pieces") {
       ok = parse_int(v, 1, 64, &o->stage_pieces);
     } else {
-      *err = "unknown plan key '" + k + "' (update, grid, tile_mix, fused, stage_threads, stage_pieces)";
+      *err = "unknown plan key '" + k + "' (update, grid, tile, tile_mix, fused, stage_threads, stage_pieces)";
       return -1;
     }
     if (!ok) {
@@ -2141,19 +2361,26 @@ static TileSplit tile_split(int64_t groups, const PlanOverrides& o) {
 // 64-group tiles from 32 k groups (below 4 per CU they still beat 32-group tiles, whose
 // phase 2 has half the serial lanes per tile), the pipelined tiles below.
 struct UpdatePlan {
-  int kind;       // 0 stream, 1 tiled, 2 pipe
+  int kind;       // 0 stream, 1 tiled, 2 pipe, 3 woven tiles (k_update_weave<nw>)
   int nA;         // stream: blocks of group-per-lane waves (the rest a value per lane)
   int64_t blocks; // stream / tiled / pipe grid
   TileSplit t;    // tiled
+  int nw;         // woven tiles: waves per block (3 or 4)
 };
 static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o) {
-  UpdatePlan p{0, 0, 0, TileSplit{-1, 0}};
+  UpdatePlan p{0, 0, 0, TileSplit{-1, 0}, 0};
   if (o.update == 1) p.kind = 0;
   else if (o.update == 2) p.kind = 1;
   else if (o.update == 3) p.kind = 2;
   else p.kind = groups >= 256LL * 4 * 2 * 64 ? 0 : groups >= 32LL * 1024 ? 1 : 2;
+  if (p.kind == 1 && o.tile >= 3) {  // the woven tiles (one width)
+    p.kind = 3;
+    p.nw = o.tile;
+  }
   if (p.kind == 2) {
     p.blocks = (groups + 15) / 16;
+  } else if (p.kind == 3) {
+    p.blocks = (groups + kWeaveTG - 1) / kWeaveTG;
   } else if (p.kind == 1) {
     p.t = tile_split(groups, o);
     p.blocks = p.t.nW >= 0 ? p.t.nW + p.t.nN : (groups + 63) / 64;
@@ -2181,6 +2408,7 @@ std::string update_kernel_name(int64_t groups) {
   char buf[64];
   if (p.kind == 0) snprintf(buf, sizeof buf, "k_update_mixed<256, false>");
   else if (p.kind == 2) snprintf(buf, sizeof buf, "k_update_pipe<16, 1, 5, 0>");
+  else if (p.kind == 3) snprintf(buf, sizeof buf, "k_update_weave<%d>", p.nw);
   else snprintf(buf, sizeof buf, "k_update_tiled<64, false, %d, true>", p.t.nW >= 0 ? 16 : 0);  // as rocprofv3 names it
   return buf;
 }
@@ -2200,6 +2428,7 @@ std::string update_encode_kernel_name(int64_t groups) {
   if (!o.fused) return update_kernel_name(groups) + " + k_encode_f32";
   if (p.kind == 0) return "k_update_encode<256>";
   if (p.kind == 1) return "k_update_tiled_encode<64>";
+  if (p.kind == 3) return "k_update_weave_encode<" + std::to_string(p.nw) + ">";
   return "k_update_pipe<16, 1, 5, 0> (with the encode's blocks)";
 }
 
@@ -2229,6 +2458,12 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
   else if (p.kind == 1)
     launch_tiled<false>(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
                         d_err, KardamOut{}, s);
+  else if (p.kind == 3 && p.nw == 3)
+    hipLaunchKernelGGL(k_update_weave<3>, dim3((unsigned)p.blocks), dim3(192), 0, s, uploads, pitch, M, d_dampen,
+                       inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
+  else if (p.kind == 3)
+    hipLaunchKernelGGL(k_update_weave<4>, dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
+                       inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
   else
     hipLaunchKernelGGL((k_update_mixed<256, false>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M,
                        d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.nA,
@@ -2419,7 +2654,9 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   // the update's own launch plan with the side outputs: the pipelined tiles (their
   // producers store p; k_kardam_finish does the rest), the wide tiles (side outputs
   // from the tile producers), or the stream kernel's SIMD-balanced grid
-  UpdatePlan p = plan_update(groups, o);
+  PlanOverrides ok = o;
+  ok.tile = 1;  // Kardam's side outputs ride in the classic tiles (tile_kardam)
+  UpdatePlan p = plan_update(groups, ok);
   if (p.kind == 0 && o.grid == 0) {
     // the stream form on the plain grid unless a grid is asked for: value-per-lane waves
     // pay the per-client wave sums for a third of the values (synth1m_256: 1747 vs
@@ -2513,6 +2750,20 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
                                  d_err, s);
     if (e != hipSuccess) return e;
     return launch_encode_f32(values, n_up, vpitch, M, enc_out, pitch, s);
+  }
+  if (p.kind == 3) {  // the woven tiles, then the encode's blocks (64 * nw lanes each)
+    const int nt = 64 * p.nw;
+    const int64_t gx = (groups + nt - 1) / nt;
+    const int rpb = encode_rows_per_block(gx, M);
+    const int64_t nU = p.blocks, nE = gx * ((M + rpb - 1) / rpb);
+    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+    if (p.nw == 3)
+      hipLaunchKernelGGL(k_update_weave_encode<3>, dim3((unsigned)(nU + nE)), dim3(192), 0, s, uploads, pitch, M,
+                         d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)nU, ej);
+    else
+      hipLaunchKernelGGL(k_update_weave_encode<4>, dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, M,
+                         d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)nU, ej);
+    return hipGetLastError();
   }
   if (p.kind == 1) {  // the wide tiles on one width, then the encode's blocks
     const int64_t gx = blocks_for(groups, 256);

@@ -510,8 +510,8 @@ const char* fleet_update_encode_kernel(size_t len);
 /* The same plan's grid (test and profiling aid, no device needed): kind 0 stream
  * (blocks [0, n_a) a group per lane, 256 groups each, the rest a value per lane,
  * 84 groups each), 1 tiled (n_w 64-group tiles then n_n 16-group tiles; n_w = -1:
- * one width, 64-group tiles only), 2 pipelined (16-group tiles); *blocks = the
- * aggregation's grid. */
+ * one width, 64-group tiles only), 2 pipelined (16-group tiles), 3 woven tiles
+ * (64 groups each); *blocks = the aggregation's grid. */
 int fleet_update_plan_grid(size_t len, int* kind, int64_t* blocks, int64_t* n_a, int64_t* n_w, int64_t* n_n);
 
 /* Launch-plan overrides, process-wide (experiments, and tests that run every

@@ -1,7 +1,8 @@
 # Parameterised GPU call: run named steps in order, each under its own time limit,
 # stopping at the first failure. Output under gpurun_out/$TAG/.
 # usage (through gpurun, from the repo root):
-#   TAG=r05b0 bash scripts/gpu_run.sh tests smoke bench strong windows:cifar10_256 profile
+#   bash scripts/gpu_run.sh tag=r05b0 tests smoke bench strong windows:cifar10_256 profile
+#   (tag=NAME first, or TAG in the environment: the output directory)
 # steps:
 #   tests            full pytest -m gpu
 #   smoke            __graft_entry__.smoke()
@@ -13,9 +14,13 @@
 #   ab               scripts/gpu_ab_multi.sh (LIBS, WORKLOADS, REPS from the environment)
 #   kardam[:W,..]    Kardam side outputs vs the plain update (scripts/kardam_ab.py under rocprofv3)
 #   py:FILE          python3 FILE (a probe script), output in $TAG/FILE.log
+#   pytest:EXPR      pytest -m gpu -k EXPR (a subset), output in $TAG/pytest.log
+#   env:VAR=VALUE    export VAR for the steps after it (env:VAR= unsets it), e.g.
+#                    'env:FLEET_EXPERIMENTS=update=tiled;tile=weave4' (quote the ';')
 set -u
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$PWD}"
 TAG=${TAG:-run}
+case ${1:-} in tag=*) TAG=${1#tag=}; shift ;; esac
 O=${OUTROOT:-$PWD/gpurun_out}/$TAG; mkdir -p "$O"
 for step in "$@"; do
   name=${step%%:*}; arg=""; [ "$name" != "$step" ] && arg=${step#*:}
@@ -64,6 +69,14 @@ for r in csv.DictReader(open('$O/kardam_$w/run_kernel_stats.csv')):
 " | tee -a "$O/kardam.txt"
         done
       done ;;
+    env)
+      v=${arg%%=*}
+      if [ -z "${arg#*=}" ]; then unset "$v"; else export "$arg"; fi
+      echo "$v=${!v:-}" ;;
+    pytest)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$arg" \
+        >> "$O/pytest.log" 2>&1 || { tail -30 "$O/pytest.log"; exit 1; }
+      tail -1 "$O/pytest.log" ;;
     py)
       timeout -k 10 600 python3 "$arg" > "$O/$(basename "$arg").log" 2>&1 || { tail -30 "$O/$(basename "$arg").log"; exit 1; }
       tail -40 "$O/$(basename "$arg").log" ;;

@@ -92,7 +92,10 @@ def test_update_encode_rejects_overlap_and_bad_text(codec):
 @pytest.mark.parametrize("spec,kernel", [("fused=off", " + k_encode_f32"), ("update=tiled", "k_update_tiled_encode<64>"),
                                          ("update=pipe", "(with the encode's blocks)"),
                                          ("update=stream", "k_update_encode<256>"),
-                                         ("update=stream,grid=lanes", "k_update_encode<256>")])
+                                         ("update=stream,grid=lanes", "k_update_encode<256>"),
+                                         ("update=tiled,tile=weave3", "k_update_weave_encode<3>"),
+                                         ("update=tiled,tile=weave4", "k_update_weave_encode<4>"),
+                                         ("update=tiled,tile=classic", "k_update_tiled_encode<64>")])
 def test_update_encode_under_plans(codec, plan, spec, kernel):
     """The pipelined step on each launch plan, forced on sizes the planner gives
     another kernel (fused=off: the two launches back to back)."""
