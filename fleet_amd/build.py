@@ -48,7 +48,7 @@ def _run(cmd):
 
 def build_codec(force: bool = False, out: str = LIB, defines=()) -> str:
     """Build libfleetcodec.so; `out` / `defines` (-D flags) build an experiment
-    variant elsewhere (e.g. ab/ for scripts/gpu_ab_workloads.sh) from the same sources."""
+    variant elsewhere (e.g. ab/ for gpu_ab_workloads.sh (r04 tree)) from the same sources."""
     srcs = [os.path.join(CSRC, s) for s, _ in SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in ("codec_device.h", "codec_math.h", "decimal6.h", "kernels.h", "model_codec.h",
                                                    "teacher_math.h")] + [

@@ -134,6 +134,10 @@ struct fleet_ctx {
   int* h_err = nullptr;
   std::unique_ptr<WorkerPool> pool;  // staging copy threads (stage_uploads)
   int last_ingress = FLEET_INGRESS_NONE;  // how the last host-buffer update reached HBM
+  // the pipelined Kardam form's tile flags (zeroed at allocation) and its launch epoch
+  uint32_t* d_kflags = nullptr;
+  size_t d_kflags_cap = 0;
+  uint32_t kflag_epoch = 0;
 };
 
 namespace {
@@ -297,14 +301,14 @@ void parallel_for(fleet_ctx* c, int n, int threads, const std::function<void(int
 // soon as its rows are copied, so the DMA of a part overlaps the copy of the
 // next (ingress framing). col0 = 0, width = len stages whole
 // uploads; a column window is one GPU's element shard (fleet_update_multi).
-// Measured on MI355X (scripts/probe_e2e2.py, rocprofv3 memory-copy trace): 1 MiB
+// Measured on MI355X (probe_e2e2.py (r04 tree), rocprofv3 memory-copy trace): 1 MiB
 // H2D parts run at ~35 GB/s with ~9 us gaps, one 7.8 MB copy at ~53 GB/s; three
 // parts gave the shortest host-buffer update for MNIST-64 (0.27 vs 0.32 ms with
 // one part). Each part is copied by `threads` workers (the context's pool): one
 // thread's memcpy into pinned memory, not PCIe, bounded the host-buffer update
 // of large batches (synth1m_256: 56.7 -> 27.9 ms; H2D floor 25.1 ms), and 16
 // parts beat 3 there (cifar10_256, 8 threads: 9.37 -> 8.68 ms; floor 7.56 ms;
-// scripts/gpu_e2e_sweep.sh). MNIST-64: 4 threads 0.26 ms vs 1 thread 0.39 ms.
+// gpu_e2e_sweep.sh (r04 tree)). MNIST-64: 4 threads 0.26 ms vs 1 thread 0.39 ms.
 int stage_uploads(fleet_ctx* c, const char* const* uploads, size_t col0, size_t width, size_t pitch, int M,
                   size_t tail_bytes, int threads) {
   const size_t total = pitch * (size_t)M;
@@ -467,7 +471,7 @@ void fleet_destroy(fleet_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (void* p : {(void*)c->d_a, (void*)c->d_b, (void*)c->d_out, (void*)c->d_f32, (void*)c->d_dampen,
                   (void*)c->d_hdr, (void*)c->d_err, (void*)c->d_partials, (void*)c->d_dev_dampen,
-                  (void*)c->d_dev_hdr, (void*)c->d_dev_err})
+                  (void*)c->d_dev_hdr, (void*)c->d_dev_err, (void*)c->d_kflags})
     if (p) (void)hipFree(p);
   for (void* p : c->retired) (void)hipFree(p);
   for (void* p : {(void*)c->h_stage, (void*)c->h_hdr, (void*)c->h_err})
@@ -1063,10 +1067,10 @@ int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch
   // one snapshot of the launch plan for the sizing call and the launch (a concurrent
   // fleet_set_plan must not give the launch more partial slots than were sized)
   const fleet::PlanOverrides plan = fleet::plan_overrides();
-  int nw_sz = 0, parts_sz = 1;  // partial slots and norm parts per client of the launch plan (sizing call)
+  int nw_sz = 0, parts_sz = 1, flags_sz = 0;  // partial slots, norm parts per client, tile flags (sizing call)
   fleet::KardamOut kd0{lr, nullptr, nullptr, 0, nullptr, nullptr};
   (void)fleet::launch_update_kardam(nullptr, pitch, M, nullptr, 0.0, (int64_t)n, 0, (int64_t)ge, nullptr, nullptr,
-                                    nullptr, nullptr, kd0, &nw_sz, nullptr, &parts_sz, plan, s);
+                                    nullptr, nullptr, kd0, &nw_sz, nullptr, &parts_sz, &flags_sz, nullptr, 0, plan, s);
   (void)hipGetLastError();
   const size_t n_waves = (size_t)std::max(nw_sz, 1), n_parts = (size_t)std::max(parts_sz, 1);
   // scratch: [partials M x slots x 2 | norms M x parts x 2 | has_prev M]; synchronous call (host outputs)
@@ -1079,10 +1083,24 @@ int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch
   uint8_t* d_has = c->d_b + o_has;
   if (d_prev) HIP_TRY(c, hipMemcpy(d_has, has_prev, (size_t)M, hipMemcpyHostToDevice));
   fleet::KardamOut kd{lr, (const float*)d_prev, d_prev ? d_has : nullptr, vpitch, (float*)d_g_out, d_part};
-  int nw = 0, np = 1;
+  if ((size_t)flags_sz > c->d_kflags_cap) {  // new flags start at 0, which no launch's epoch is
+    if (c->d_kflags) (void)hipFree(c->d_kflags);
+    c->d_kflags = nullptr;
+    c->d_kflags_cap = 0;
+    HIP_TRY(c, hipMalloc(&c->d_kflags, sizeof(uint32_t) * (size_t)flags_sz));
+    HIP_TRY(c, hipMemsetAsync(c->d_kflags, 0, sizeof(uint32_t) * (size_t)flags_sz, s));
+    c->d_kflags_cap = (size_t)flags_sz;
+    c->kflag_epoch = 0;
+  }
+  if (++c->kflag_epoch == 0) {  // wrapped: every flag back to 0 before epoch 1 is used again
+    if (c->d_kflags_cap) HIP_TRY(c, hipMemsetAsync(c->d_kflags, 0, sizeof(uint32_t) * c->d_kflags_cap, s));
+    c->kflag_epoch = 1;
+  }
+  int nw = 0, np = 1, nf = 0;
   HIP_TRY(c, fleet::launch_update_kardam((const uint8_t*)d_uploads, pitch, M, c->d_dev_dampen, (double)1 / M,
                                          (int64_t)n, 0, (int64_t)ge, c->d_dev_hdr, (uint8_t*)d_merged,
-                                         (float*)d_merged_f32, c->d_dev_err, kd, &nw, d_norm, &np, plan, s));
+                                         (float*)d_merged_f32, c->d_dev_err, kd, &nw, d_norm, &np, &nf, c->d_kflags,
+                                         c->kflag_epoch, plan, s));
   if ((size_t)np != n_parts || (size_t)std::max(nw, 1) != n_waves)
     return fail(c, FLEET_ERR_HIP, "Kardam launch plan changed between sizing and launch");
   std::vector<double> norms(2 * (size_t)M * n_parts);

@@ -36,7 +36,9 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
 // (the pipelined form uses them as scratch p rows); g_out (nullable) = G in upload
 // coordinates (M rows of vpitch floats; may be prev itself).
 // launch_update_kardam: *n_waves = partial slots per client (sizing call: partials
-// NULL), norms = M x *norm_parts pairs of sums, added in order on the host. The plan
+// NULL), norms = M x *norm_parts pairs of sums, added in order on the host;
+// *flag_slots = the u32 tile flags the pipelined form needs (kd_flags: zeroed once at
+// allocation, kd_epoch: a value new to them, per launch). The plan
 // overrides are the caller's one snapshot, passed to the sizing call and the launch
 // alike, so a concurrent fleet_set_plan cannot change the grid between the two.
 struct PlanOverrides;
@@ -51,7 +53,8 @@ struct KardamOut {
 hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                                 int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
-                                double* norms, int* norm_parts, const PlanOverrides& o, hipStream_t s);
+                                double* norms, int* norm_parts, int* flag_slots, uint32_t* kd_flags,
+                                uint32_t kd_epoch, const PlanOverrides& o, hipStream_t s);
 // Launch-plan overrides: experiments, and the tests that run every launch variant on
 // small inputs. Process-wide; set by fleet_set_plan (spec "key=value,..." -- update=
 // auto|stream|tiled|pipe, grid=auto|plain|lanes, tile_mix=auto|off, fused=on|off,

@@ -544,18 +544,18 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // LADDER: issue priority falls as a wave gets ahead (3 -> 0 at quarters of the
   // client loop), so the waves of a SIMD keep step instead of finishing one by one in
   // age order -- the tail of a one-round grid (profiles/r04/window_traces.txt). The
-  // aggregation alone: 828 -> 786 us on synth1m_256 (scripts/gpu_r04_a6.sh); inside
+  // aggregation alone: 828 -> 786 us on synth1m_256 (r04 call a6); inside
   // k_update_encode with the encode's waves at priority 2 (see there)
   // rungs at quarters of the loop; the Kardam form's longer client steps settle later
   // (rungs at 1/2, 3/4, 7/8: 1561 -> 1517 us on synth1m_256, where they cost the fused
-  // step 1.8 % and rungs at 1/8, 1/4, 1/2 lose everywhere; scripts/gpu_r04_a18.sh)
+  // step 1.8 % and rungs at 1/8, 1/4, 1/2 lose everywhere; r04 call a18)
   const int q1 = KD ? M / 2 : M / 4, q2 = KD ? 3 * M / 4 : M / 2, q3 = KD ? 7 * M / 8 : 3 * M / 4;
   // LADDER = the first rung's priority (0: no ladder); each rung one lower, floor 0
   constexpr int P0 = LADDER, P1 = LADDER > 1 ? LADDER - 1 : 0, P2 = LADDER > 2 ? LADDER - 2 : 0;
   if constexpr (LADDER > 0) __builtin_amdgcn_s_setprio(P0);
   if constexpr (KD) {
     // Kardam: one client per trip, the next one in flight (two per trip: 1840 against
-    // 1795 us on synth1m_256, scripts/gpu_r04_a13.sh)
+    // 1795 us on synth1m_256, r04 call a13)
     for (; c < M; ++c) {
       if constexpr (LADDER > 0) {
         if (c == q1) __builtin_amdgcn_s_setprio(P1);
@@ -652,10 +652,10 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
 // instead of a sixth full wave on some. nA = gridDim.x: the plain grid.
 // KD = true adds Kardam's side outputs (kardam_lane_step; partial slots per wave).
 // Both forms run the issue-priority ladder (update_lane: synth1m_256 828 -> 786 us
-// plain, 1776 -> 1502-1546 us with Kardam's side outputs, scripts/gpu_r04_a14.sh);
+// plain, 1776 -> 1502-1546 us with Kardam's side outputs, r04 call a14);
 // its register budget asks for at least 6 waves per SIMD (73 VGPRs, no scratch;
 // unconstrained it takes 91 VGPRs: 5 waves, 1922 against 1795 us on synth1m_256; at 7
-// or 8 waves it spills 16 / 64 B a lane and runs no faster, scripts/gpu_r04_a24.sh).
+// or 8 waves it spills 16 / 64 B a lane and runs no faster, r04 call a24).
 template <int NT, bool KD>
 __global__ void __launch_bounds__(NT, KD ? 6 : 1) k_update_mixed(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                      const double* __restrict__ dampen, double inv_avg,
@@ -1462,6 +1462,165 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
   }
 }
 
+// Kardam's side outputs of the pipelined form (SURVEY.md f2; CppNNUpdater.java:463-481,
+// Kardam.java:48-106). The pipelined tiles are latency-bound -- one serial consumer
+// wave per tile (DESIGN.md §4.2) -- so Kardam's two extra Q stages stay off them:
+// their producers only store each (client, value)'s p in `rows` (k_update_pipe<...,
+// KD = true>), and finish blocks riding in the same launch turn the rows into G =
+// Q(f32(f64(p) * lr)) (into g_out when given: 0 off the flat gradient), ||G||^2 and,
+// with the worker's previous G, ||Q(G - prev)||^2. A finish block = (client c, chunk k
+// of 2 * NT groups): a lane's groups, the wave by DPP and the block's waves in LDS give
+// the chunk's two sums, in a fixed order, at parts[(c * kc + k) * 2]; the host adds a
+// client's kc chunk sums in order (a few per client: no reduce launch). rows may be
+// g_out (each lane reads its p before writing its G); prev must not overlap rows (it
+// may be g_out: a lane reads prev before writing G at the same slots).
+// The finish block of chunk k waits for the tiles over its groups: every producer wave
+// of a tile publishes the launch's epoch in its flag (flags[tile * NPW + wave]) after
+// its last pass (agent-scope release); the block's first threads spin on those flags
+// (acquire, s_sleep). Tiles are dispatched before every finish block and never wait
+// on one, so the launch drains; the epoch (new per launch, never reused) makes a
+// stale flag from an earlier launch never match, so the flags need no reset.
+struct KardamFinishJob {
+  const float* rows;  // p rows (the producers' PS output)
+  size_t rpitch;
+  float* g_out;       // nullable
+  const float* prev;  // nullable
+  size_t gpitch;
+  const uint8_t* has_prev;
+  double lr;
+  double* parts;      // M x kc pairs
+  int kc;             // chunks per client
+  uint32_t* flags;    // tiles x producer waves
+  uint32_t epoch;
+};
+template <int NT, int TG, int NPW>
+__device__ __forceinline__ void kardam_finish_block(const KardamFinishJob& kf, int64_t e, int64_t n_up, int64_t ntiles,
+                                                    const int32_t* __restrict__ hdr_block, B64Tables& tab,
+                                                    int32_t* hdr, double (*red)[NT / 64], int* __restrict__ err) {
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+  constexpr int IPL = 2, S = 3 * IPL, GROUPS = NT * IPL;
+  static_assert(GROUPS % TG == 0, "a chunk covers whole tiles");
+  constexpr int TPC = GROUPS / TG;  // tiles per chunk
+  static_assert(TPC * NPW <= NT, "one flag per thread");
+  const int kc = kf.kc;
+  const int c = (int)(e / kc), k = (int)(e % kc);
+  const bool hasp = kf.prev && kf.has_prev[c];  // block-uniform
+  const float* row = kf.rows + (size_t)c * kf.rpitch;
+  const float* prow = hasp ? kf.prev + (size_t)c * kf.gpitch : nullptr;
+  float* grow = kf.g_out ? kf.g_out + (size_t)c * kf.gpitch : nullptr;
+  const int64_t groups = (n_up + 2) / 3;
+  // the tables and the header list while the tiles work
+  b64_tables_init<NT>(&tab);
+  const int n_hdr = hdr_block[1];
+  const int64_t walk_end = hdr_block[2];
+  for (int i = threadIdx.x; i < n_hdr; i += NT) hdr[i] = hdr_block[4 + i];
+  {  // wait for the producers of the chunk's tiles
+    const int64_t t = (int64_t)k * TPC + threadIdx.x / NPW;
+    if ((int)threadIdx.x < TPC * NPW && t < ntiles) {
+      const uint32_t* f = kf.flags + t * NPW + threadIdx.x % NPW;
+      // bounded (~0.5 s): a flag that never comes (a bug, not a slow tile) fails the call
+      // instead of hanging the device
+      for (uint32_t spin = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != kf.epoch; ++spin) {
+        if (spin == (1u << 23)) {
+          atomicOr(err, FLEET_ERRBIT_ARG);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every lane reads the published p rows
+  int64_t gp[IPL];
+  bool whole[IPL], live[IPL];
+  float pv[S], qv[S];
+#pragma unroll
+  for (int h = 0; h < IPL; ++h) {
+    const int64_t g = (int64_t)k * GROUPS + h * NT + threadIdx.x;
+    live[h] = g < groups;
+    gp[h] = 3 * g;
+    whole[h] = live[h] && gp[h] + 2 < n_up;
+    pv[3 * h] = pv[3 * h + 1] = pv[3 * h + 2] = 0.0f;
+    qv[3 * h] = qv[3 * h + 1] = qv[3 * h + 2] = 0.0f;
+    if (whole[h]) {
+      const f3u t = *reinterpret_cast<const f3u*>(row + gp[h]);
+      pv[3 * h] = t.x;
+      pv[3 * h + 1] = t.y;
+      pv[3 * h + 2] = t.z;
+      if (hasp) {
+        const f3u u = *reinterpret_cast<const f3u*>(prow + gp[h]);
+        qv[3 * h] = u.x;
+        qv[3 * h + 1] = u.y;
+        qv[3 * h + 2] = u.z;
+      }
+    } else if (live[h]) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (gp[h] + q < n_up) {
+          pv[3 * h + q] = row[gp[h] + q];
+          if (hasp) qv[3 * h + q] = prow[gp[h] + q];
+        }
+    }
+  }
+  uint32_t flat = 0;
+#pragma unroll
+  for (int h = 0; h < IPL; ++h) {
+    const uint32_t hb = live[h] ? header_bits(hdr, n_hdr, gp[h]) : 7u;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      if (live[h] && gp[h] + q < n_up && gp[h] + q < walk_end && !((hb >> q) & 1u)) flat |= 1u << (3 * h + q);
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i)
+    if (!((flat >> i) & 1u)) pv[i] = 0.0f;
+  float G[S];
+  dampen_stage<S>(pv, kf.lr);  // lr is uniform
+  q_stage<S>(G, pv, &tab);
+  double sg = 0.0, sd = 0.0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    if (!((flat >> i) & 1u)) G[i] = 0.0f;
+    sg += (double)(G[i] * G[i]);
+  }
+  if (hasp) {
+    float dv[S], D[S];
+#pragma unroll
+    for (int i = 0; i < S; ++i) dv[i] = ((flat >> i) & 1u) ? G[i] - qv[i] : 0.0f;
+    q_stage<S>(D, dv, &tab);
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      if ((flat >> i) & 1u) sd += (double)(D[i] * D[i]);
+  }
+  if (grow) {
+#pragma unroll
+    for (int h = 0; h < IPL; ++h) {
+      if (whole[h]) {
+        *reinterpret_cast<f3u*>(grow + gp[h]) = f3u{G[3 * h], G[3 * h + 1], G[3 * h + 2]};
+      } else {
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          if (live[h] && gp[h] + q < n_up) grow[gp[h] + q] = G[3 * h + q];
+      }
+    }
+  }
+  sg = group_sum_f64<64>(sg);  // valid in lane 63
+  sd = group_sum_f64<64>(sd);
+  if ((threadIdx.x & 63) == 63) {
+    red[0][threadIdx.x / 64] = sg;
+    red[1][threadIdx.x / 64] = sd;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0.0, b = 0.0;
+    for (int i = 0; i < NT / 64; ++i) {
+      a += red[0][i];
+      b += red[1][i];
+    }
+    kf.parts[((size_t)c * kc + k) * 2] = a;
+    kf.parts[((size_t)c * kc + k) * 2 + 1] = b;
+  }
+}
+
 // Pipelined tile variant (E = 3*TG <= 64): producer waves compute p for passes
 // of clients into an LDS ring while wave 0 consumes them in client order (the
 // serial A = Q(A + p_c)), so the client-independent work and the serial
@@ -1486,7 +1645,8 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
                                                      const int32_t* __restrict__ hdr_block,
                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
                                                      int* __restrict__ err, int nU, EncodeJob ej,
-                                                     KardamOut kd = KardamOut{}) {
+                                                     KardamOut kd = KardamOut{},
+                                                     KardamFinishJob kf = KardamFinishJob{}) {
   constexpr int E = 3 * TG;
   static_assert(E <= 64, "one consumer wave");
   constexpr int NPW = NW - 1;                                // producer waves
@@ -1502,6 +1662,15 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   // wave index made wave-uniform (readfirstlane), so the producer/consumer
   // split below is a scalar branch and the consumer's s_setprio is its own
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  if constexpr (KD) {
+    if ((int)blockIdx.x >= nU) {  // block-uniform: Kardam's finish of one (client, chunk)
+      __shared__ double kred[2][NW];
+      static_assert(sizeof(ptile) >= sizeof(int32_t) * kMaxHeaderSlots, "the header list fits the p ring");
+      kardam_finish_block<64 * NW, TG, NPW>(kf, (int64_t)blockIdx.x - nU, n_up, nU, hdr_block, sh.tab,
+                                            reinterpret_cast<int32_t*>(ptile), kred, err);
+      return;
+    }
+  }
   if ((int)blockIdx.x >= nU) {  // block-uniform: a job riding in the launch
     b64_tables_init<64 * NW>(&sh.tab);
     __syncthreads();
@@ -1545,6 +1714,12 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       ++done;
       if (lane == 0) __hip_atomic_store(&prog[w], done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if constexpr (KD) {  // this wave's p rows are out: the finish blocks of its chunk may read them
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (lane == 0)
+        __hip_atomic_store(kf.flags + (size_t)blockIdx.x * NPW + w, kf.epoch, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
   } else {  // ---------------------------------------------------- consumer
     // the serial chain is the block's critical path: win VALU issue
@@ -1665,7 +1840,7 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   // the update waves run the issue-priority ladder (3 -> 0 as they get ahead) and the
   // encode's waves run at priority 3: the HBM-bound encode issues whenever it can, the
   // update waves that lag next. synth1m_256 step 1129-1133 -> 1119-1120 us with the
-  // encode at 2 (scripts/gpu_r04_a15.sh), 1171-1176 -> 1153-1158 us from 2 to 3 on
+  // encode at 2 (r04 call a15), 1171-1176 -> 1153-1158 us from 2 to 3 on
   // another box (gpu_r04_a16.sh); at 0 (r04 a6: 1158 us) or 1 (1138-1142 us) slower, and
   // so were update waves laddered from 2 under the encode's 3 (1134-1141 against
   // 1118-1129 us, gpu_r04_a26.sh)
@@ -2520,136 +2695,14 @@ __global__ void __launch_bounds__(NT) k_kardam_reduce(const double* __restrict__
   }
 }
 
-// Kardam's side outputs of the pipelined form (SURVEY.md f2; CppNNUpdater.java:463-481,
-// Kardam.java:48-106). The pipelined tiles are latency-bound -- one serial consumer
-// wave per tile (DESIGN.md §4.2) -- so Kardam's two extra Q stages stay off them:
-// their producers only store each (client, value)'s p in `rows` (k_update_pipe<...,
-// KD = true>), and this kernel turns the rows into G = Q(f32(f64(p) * lr)) (into g_out
-// when given: 0 off the flat gradient), ||G||^2 and, with the worker's previous G,
-// ||Q(G - prev)||^2. Block = (client c, chunk k of kKfGroups groups): a lane's groups,
-// the wave by DPP and the block's waves in LDS give the chunk's two sums, in a fixed
-// order, at parts[(c * kc + k) * 2]; the host adds a client's kc chunk sums in order
-// (a few per client: no reduce launch). rows may be g_out (each lane reads its p
-// before writing its G); prev must not overlap rows (it may be g_out: a lane reads
-// prev before writing G at the same slots).
-constexpr int kKfThreads = 256, kKfIpl = 2, kKfGroups = kKfThreads * kKfIpl;
-__global__ void __launch_bounds__(kKfThreads) k_kardam_finish(const float* rows, size_t rpitch, float* g_out,
-                                                              int64_t n_up, const int32_t* __restrict__ hdr_block,
-                                                              const float* prev, size_t gpitch,
-                                                              const uint8_t* __restrict__ has_prev, double lr,
-                                                              double* __restrict__ parts, int kc) {
-  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
-  constexpr int NT = kKfThreads, IPL = kKfIpl, S = 3 * IPL;
-  __shared__ B64Tables tab;
-  __shared__ int32_t hdr[kMaxHeaderSlots];  // the header positions: searched per group in LDS
-  __shared__ double red[2][NT / 64];
-  const int c = (int)(blockIdx.x / kc), k = (int)(blockIdx.x % kc);
-  const bool hasp = prev && has_prev[c];  // block-uniform
-  const float* row = rows + (size_t)c * rpitch;
-  const float* prow = hasp ? prev + (size_t)c * gpitch : nullptr;
-  float* grow = g_out ? g_out + (size_t)c * gpitch : nullptr;
-  const int64_t groups = (n_up + 2) / 3;
-  int64_t gp[IPL];
-  bool whole[IPL], live[IPL];
-  float pv[S], qv[S];
-  // the lane's groups first (their loads in flight while the tables are copied; slots
-  // past n_up read as 0), the flat-gradient mask after
-#pragma unroll
-  for (int h = 0; h < IPL; ++h) {
-    const int64_t g = (int64_t)k * kKfGroups + h * NT + threadIdx.x;
-    live[h] = g < groups;
-    gp[h] = 3 * g;
-    whole[h] = live[h] && gp[h] + 2 < n_up;
-    pv[3 * h] = pv[3 * h + 1] = pv[3 * h + 2] = 0.0f;
-    qv[3 * h] = qv[3 * h + 1] = qv[3 * h + 2] = 0.0f;
-    if (whole[h]) {
-      const f3u t = *reinterpret_cast<const f3u*>(row + gp[h]);
-      pv[3 * h] = t.x;
-      pv[3 * h + 1] = t.y;
-      pv[3 * h + 2] = t.z;
-      if (hasp) {
-        const f3u u = *reinterpret_cast<const f3u*>(prow + gp[h]);
-        qv[3 * h] = u.x;
-        qv[3 * h + 1] = u.y;
-        qv[3 * h + 2] = u.z;
-      }
-    } else if (live[h]) {
-#pragma unroll
-      for (int e = 0; e < 3; ++e)
-        if (gp[h] + e < n_up) {
-          pv[3 * h + e] = row[gp[h] + e];
-          if (hasp) qv[3 * h + e] = prow[gp[h] + e];
-        }
-    }
-  }
-  b64_tables_init<NT>(&tab);
-  const int n_hdr = hdr_block[1];
-  const int64_t walk_end = hdr_block[2];
-  for (int i = threadIdx.x; i < n_hdr; i += NT) hdr[i] = hdr_block[4 + i];
-  __syncthreads();
-  uint32_t flat = 0;
-#pragma unroll
-  for (int h = 0; h < IPL; ++h) {
-    const uint32_t hb = live[h] ? header_bits(hdr, n_hdr, gp[h]) : 7u;
-#pragma unroll
-    for (int e = 0; e < 3; ++e)
-      if (live[h] && gp[h] + e < n_up && gp[h] + e < walk_end && !((hb >> e) & 1u)) flat |= 1u << (3 * h + e);
-  }
-#pragma unroll
-  for (int i = 0; i < S; ++i)
-    if (!((flat >> i) & 1u)) pv[i] = 0.0f;
-  float G[S];
-  dampen_stage<S>(pv, lr);  // lr is uniform
-  q_stage<S>(G, pv, &tab);
-  double sg = 0.0, sd = 0.0;
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    if (!((flat >> i) & 1u)) G[i] = 0.0f;
-    sg += (double)(G[i] * G[i]);
-  }
-  if (hasp) {
-    float dv[S], D[S];
-#pragma unroll
-    for (int i = 0; i < S; ++i) dv[i] = ((flat >> i) & 1u) ? G[i] - qv[i] : 0.0f;
-    q_stage<S>(D, dv, &tab);
-#pragma unroll
-    for (int i = 0; i < S; ++i)
-      if ((flat >> i) & 1u) sd += (double)(D[i] * D[i]);
-  }
-  if (grow) {
-#pragma unroll
-    for (int h = 0; h < IPL; ++h) {
-      if (whole[h]) {
-        *reinterpret_cast<f3u*>(grow + gp[h]) = f3u{G[3 * h], G[3 * h + 1], G[3 * h + 2]};
-      } else {
-#pragma unroll
-        for (int e = 0; e < 3; ++e)
-          if (live[h] && gp[h] + e < n_up) grow[gp[h] + e] = G[3 * h + e];
-      }
-    }
-  }
-  sg = group_sum_f64<64>(sg);  // valid in lane 63
-  sd = group_sum_f64<64>(sd);
-  if ((threadIdx.x & 63) == 63) {
-    red[0][threadIdx.x / 64] = sg;
-    red[1][threadIdx.x / 64] = sd;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double a = 0.0, b = 0.0;
-    for (int i = 0; i < NT / 64; ++i) {
-      a += red[0][i];
-      b += red[1][i];
-    }
-    parts[((size_t)c * kc + k) * 2] = a;
-    parts[((size_t)c * kc + k) * 2 + 1] = b;
-  }
-}
+// groups per finish block of the pipelined form (k_update_pipe<16, 1, 5, 0, true>: 320 lanes x 2)
+constexpr int kKfGroups = 64 * 5 * 2;
 
 hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                                 int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
-                                double* norms, int* norm_parts, const PlanOverrides& o, hipStream_t s) {
+                                double* norms, int* norm_parts, int* flag_slots, uint32_t* kd_flags,
+                                uint32_t kd_epoch, const PlanOverrides& o, hipStream_t s) {
   const int64_t groups = g_end - g_begin;
   // the update's own launch plan with the side outputs: the pipelined tiles (their
   // producers store p; k_kardam_finish does the rest), the wide tiles (side outputs
@@ -2660,7 +2713,7 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   if (p.kind == 0 && o.grid == 0) {
     // the stream form on the plain grid unless a grid is asked for: value-per-lane waves
     // pay the per-client wave sums for a third of the values (synth1m_256: 1747 vs
-    // 1724 us, scripts/gpu_r04_a6.sh)
+    // 1724 us, r04 call a6)
     p.nA = (int)((groups + 255) / 256);
     p.blocks = p.nA;
   }
@@ -2671,9 +2724,11 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   *n_waves = p.kind == 0 ? (int)blocks * 4 : p.kind == 1 ? (int)blocks : (int)((n_up + 3) / 4);
   // norms: one pair per client (the reduce), or the finish kernel's chunk sums
   const int kc = (int)(((n_up + 2) / 3 + kKfGroups - 1) / kKfGroups);
+  *flag_slots = p.kind == 2 ? (int)blocks * 4 : 0;  // the pipelined form's tile flags (4 producer waves)
   *norm_parts = p.kind == 2 ? std::max(kc, 1) : 1;
   if (groups <= 0) return hipSuccess;
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
+  if (p.kind == 2 && !kd_flags) return hipErrorInvalidValue;
   if (p.kind == 2) {
     // p rows: the caller's G rows, unless there are none or they overlap prev (G may
     // replace prev in place: prev must stay intact until k_kardam_finish reads it)
@@ -2685,11 +2740,12 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
       kp.g_out = reinterpret_cast<float*>(kd.partials);
       kp.vpitch = (size_t)((n_up + 3) / 4 * 4);
     }
-    hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0, true>), dim3(blocks), dim3(64 * 5), 0, s, uploads, pitch, M,
-                       d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
-                       EncodeJob{}, kp);
-    hipLaunchKernelGGL(k_kardam_finish, dim3((unsigned)((int64_t)M * kc)), dim3(kKfThreads), 0, s, kp.g_out,
-                       kp.vpitch, kd.g_out, n_up, d_hdr_block, kd.prev, kd.vpitch, kd.has_prev, kd.lr, norms, kc);
+    // the tiles, then the finish blocks (one per client and chunk of kKfGroups groups)
+    const KardamFinishJob kf{kp.g_out, kp.vpitch, kd.g_out, kd.prev, kd.vpitch, kd.has_prev, kd.lr, norms, kc,
+                             kd_flags, kd_epoch};
+    hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0, true>), dim3((unsigned)(blocks + (int64_t)M * kc)), dim3(64 * 5), 0,
+                       s, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
+                       d_err, (int)blocks, EncodeJob{}, kp, kf);
     return hipGetLastError();
   }
   if (p.kind == 1)
@@ -2712,7 +2768,7 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
 
 // rows per block of the standalone client encode: about 65,536 blocks in all (a
 // lane walks its group down rpb rows, so the LDS table copy is paid once per rpb
-// rows). Measured on one box (scripts/gpu_encode_rpb.sh, two rows of loads in
+// rows). Measured on one box (gpu_encode_rpb.sh (r04 tree), two rows of loads in
 // flight): synth1m_256 encodes in 478-480 us at 4-8 rows per block, 483 at 16, 501
 // at 2 and 32, 595 at 1; the same access pattern without the codec arithmetic
 // (scripts/ubench_stream.hip, 12 B in / 16 B out per lane) runs 452-486 us.
@@ -2786,12 +2842,12 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   // the stream grid group-per-lane everywhere: the encode's blocks fill the SIMDs the
   // last round of update waves leaves idle, so the value-per-lane balancing of
   // k_update_mixed only adds instructions here (same-box A/B on synth1m_256: 1172.7 vs
-  // 1181.3 us, scripts/gpu_fused_ab.sh). 24 rows per encode block: short blocks that
+  // 1181.3 us, gpu_fused_ab.sh (r04 tree)). 24 rows per encode block: short blocks that
   // fill the slots the update's waves leave (a lane walks its group down the rows with
   // two loads in flight, so a block of hundreds of rows is a latency-bound straggler);
   // same-box A/B on synth1m_256: 1179 / 1170 us at 6 / 12 rows per block in r03; with
   // the encode's waves at priority 3 (r04) 1130 / 1097-1100 / 1084-1090 us at 6 / 12 /
-  // 24, and 48 no better (scripts/gpu_r04_a31.sh, a32.sh).
+  // 24, and 48 no better (r04 call a31, a32.sh).
   // (grid=lanes: the update's blocks a value per lane, for experiments on small windows)
   const int64_t gx = blocks_for(groups, 256);
   const bool lanes = o.grid == 2;
