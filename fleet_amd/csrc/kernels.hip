@@ -20,6 +20,16 @@
 #include "decimal6.h"
 #include "teacher_math.h"
 
+// Experiment switches of the stream kernels (r05 A/Bs; the defaults are the product):
+// FLEET_DEC_T = 1 decodes full groups on the pre-shifted tables (DecTables);
+// FLEET_STREAM_PF = 2 keeps two clients' rows in flight ahead of the one computed.
+#ifndef FLEET_DEC_T
+#define FLEET_DEC_T 0
+#endif
+#ifndef FLEET_STREAM_PF
+#define FLEET_STREAM_PF 1
+#endif
+
 namespace fleet {
 
 // Dev-only phase timestamps (scripts/ubench_tiled.hip builds with FLEET_TIMING);
@@ -463,7 +473,8 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
                                             int64_t g, int e0, bool live, int64_t g_safe,
                                             const int32_t* __restrict__ hdr_block, int32_t (&out)[S],
                                             uint32_t& bad, uint32_t& layout_bad, const KardamOut& kd = KardamOut{},
-                                            double* __restrict__ kd_part = nullptr, size_t kd_stride = 0) {
+                                            double* __restrict__ kd_part = nullptr, size_t kd_stride = 0,
+                                            const DecTables* dect = nullptr) {
   const int n_hdr = hdr_block[1];
   const int64_t walk_end = hdr_block[2];
   const int32_t* hdr = hdr_block + 4;
@@ -492,7 +503,11 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   using Row = typename std::conditional<S == 3, uint4, uint2>::type;
   auto client = [&](int c, const Row& cur) {
     if constexpr (S == 3) {
+#if FLEET_DEC_T
+      if (need == 0xffffu) bad |= b64_decode_group_full4(cur, dect, codes);
+#else
       if (need == 0xffffu) bad |= b64_decode_group_full(cur, &tab, codes);
+#endif
       else bad |= b64_decode_group(cur, &tab, codes) & need;
     } else {
       if (need == 0xffffu) bad |= b64_decode_pair_full(cur.x, cur.y, sel, &tab, codes[0]);
@@ -567,6 +582,34 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       client(c, cur);
     }
   }
+#if FLEET_STREAM_PF >= 2
+  // four clients per trip, two rows issued ahead of the pair being computed
+  if (!KD && M >= 4) {
+    Row b2, b3;
+    b1 = group_of(1);
+    for (; c + 3 < M; c += 4) {
+      FLEET_CLIENT_HOOK(c, M);
+      if constexpr (LADDER > 0) {
+        if (c == (q1 & ~3)) __builtin_amdgcn_s_setprio(P1);
+        if (c == (q2 & ~3)) __builtin_amdgcn_s_setprio(P2);
+        if (c == (q3 & ~3)) __builtin_amdgcn_s_setprio(0);
+      }
+      b2 = group_of(c + 2);
+      b3 = group_of(c + 3);
+      client(c, b0);
+      client(c + 1, b1);
+      if (c + 4 < M) b0 = group_of(c + 4);
+      if (c + 5 < M) b1 = group_of(c + 5);
+      client(c + 2, b2);
+      client(c + 3, b3);
+    }
+    // 0..3 clients left; b0 / b1 hold clients c / c + 1 when they exist
+    if (c < M) client(c, b0);
+    if (c + 1 < M) client(c + 1, b1);
+    if (c + 2 < M) client(c + 2, group_of(c + 2));
+    c = M;
+  }
+#endif
   for (; c + 1 < M; c += 2) {
     FLEET_CLIENT_HOOK(c, M);
     if constexpr (LADDER > 0) {
@@ -603,7 +646,8 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
                                                    int64_t g_begin, int64_t g_end,
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
                                                    float* __restrict__ merged_f32, int* __restrict__ err, int nA,
-                                                   const KardamOut& kd = KardamOut{}) {
+                                                   const KardamOut& kd = KardamOut{},
+                                                   const DecTables* dect = nullptr) {
   uint32_t bad = 0, layout_bad = 0;
   // Kardam: this wave's partial slot of client 0; one slot per wave of the grid
   const size_t nw = (size_t)gridDim.x * (NT / 64);
@@ -613,7 +657,7 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
     const bool live = g < g_end;
     int32_t out[3];
     update_lane<3, KD, LADDER>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out,
-                               bad, layout_bad, kd, kd_part, 2 * nw);
+                               bad, layout_bad, kd, kd_part, 2 * nw, dect);
     if (!live) return;
     if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
@@ -667,9 +711,16 @@ __global__ void __launch_bounds__(NT, KD ? 6 : 1) k_update_mixed(const uint8_t* 
   __shared__ D16Table dtab;
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
+#if FLEET_DEC_T
+  __shared__ DecTables dect;
+  dec_tables_init<NT>(&dect);
+  const DecTables* dp = &dect;
+#else
+  const DecTables* dp = nullptr;
+#endif
   __syncthreads();
   update_mixed_block<NT, KD, 3>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
-                             hdr_block, merged, merged_f32, err, nA, kd);
+                             hdr_block, merged, merged_f32, err, nA, kd, dp);
 }
 
 // Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
@@ -1836,6 +1887,13 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   __shared__ D16Table dtab;
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
+#if FLEET_DEC_T
+  __shared__ DecTables dect;
+  dec_tables_init<NT>(&dect);
+  const DecTables* dp = &dect;
+#else
+  const DecTables* dp = nullptr;
+#endif
   __syncthreads();
   // the update waves run the issue-priority ladder (3 -> 0 as they get ahead) and the
   // encode's waves run at priority 3: the HBM-bound encode issues whenever it can, the
@@ -1846,7 +1904,7 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   // 1118-1129 us, gpu_r04_a26.sh)
   if ((int)blockIdx.x < nU) {  // block-uniform
     update_mixed_block<NT, false, 3>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
-                                     hdr_block, merged, merged_f32, err, nA);
+                                     hdr_block, merged, merged_f32, err, nA, KardamOut{}, dp);
   } else {
     const int64_t e = (int64_t)blockIdx.x - nU;
     __builtin_amdgcn_s_setprio(3);

@@ -88,3 +88,13 @@ def check_side_outputs(codec, oracle, layout, M):
     has = [c % 2 == 0 for c in range(M)]
     g2, g2_dev = round_(32, g1, g1_dev, has)
     round_(33, g2, g2_dev, [True] * M, in_place=True)
+
+
+def test_kardam_pipelined_flags_across_sizes(codec, oracle, plan):
+    """The pipelined form's finish blocks wait on per-tile epoch flags held by the
+    context (k_update_pipe<..., true>): a bigger bucket grows the flags (new ones start
+    at 0, and the epoch restarts), a smaller one after it reuses the first flags with a
+    newer epoch -- every call equals the two-pass path, none waits on a stale flag."""
+    plan("update=pipe")
+    for layout, M in ((MNIST, 3), (synthetic(50_003), 2), (synthetic(3001), 5), (MNIST, 3)):
+        check_side_outputs(codec, oracle, layout, M)
