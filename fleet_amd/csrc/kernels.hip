@@ -1363,17 +1363,19 @@ __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t 
                                                    double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end,
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
                                                    float* __restrict__ merged_f32, int* __restrict__ err) {
-  static_assert(NW == 3 || NW == 4, "three consumer waves (+ one producer-only wave)");
+  static_assert(NW >= 3 && NW <= 8, "three consumer waves (+ producer-only waves)");
   constexpr int E = kWeaveE, CM = NW;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t g0 = g_begin + bid * kWeaveTG;
   const int ng = (int)min<int64_t>(kWeaveTG, g_end - g0);
   const int64_t walk_end = hdr_block[2];
-  // consumers: every wave but the light one (NW = 4: rotates with the tile)
-  const int light = NW == 4 ? (int)(bid & 3) : -1;
-  const bool consumer = wave != light;  // wave-uniform
-  const int col = (wave - (light >= 0 && wave > light ? 1 : 0)) * 64 + lane;  // consumer's value
+  // consumers: three consecutive waves from r = tile mod NW (on three different SIMDs
+  // when waves go to SIMDs round robin), so the serial work rotates over the SIMDs
+  const int r = (int)(bid % NW);
+  const int ci = (wave - r + NW) % NW;  // consumer index 0..2, or a producer-only wave
+  const bool consumer = ci < 3;          // wave-uniform
+  const int col = (consumer ? ci : 0) * 64 + lane;  // the consumer's value
   const int nchunks = (M + CM - 1) / CM;
   const int gl = lane;
   const bool glive = gl < ng;
@@ -2472,6 +2474,8 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
       else if (v == "classic") o->tile = 1;
       else if (v == "weave3") o->tile = 3;
       else if (v == "weave4") o->tile = 4;
+      else if (v == "weave6") o->tile = 6;
+      else if (v == "weave8") o->tile = 8;
       else ok = false;
     } else if (k == "tile_mix") {
       if (v == "auto") o->tile_mix = 0;
@@ -2679,6 +2683,20 @@ static void launch_tiled(const UpdatePlan& p, const uint8_t* uploads, size_t pit
                        INT32_MAX);
 }
 
+// k_update_weave<nw> (nw = 3, 4, 6, 8 waves per block)
+static void launch_weave(int nw, unsigned blocks, hipStream_t s, const uint8_t* uploads, size_t pitch, int M,
+                         const double* d_dampen, double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end,
+                         const int32_t* d_hdr_block, uint8_t* merged, float* merged_f32, int* d_err) {
+#define FLEET_WEAVE_LAUNCH(NWV)                                                                                   \
+  hipLaunchKernelGGL(k_update_weave<NWV>, dim3(blocks), dim3(64 * NWV), 0, s, uploads, pitch, M, d_dampen, inv_avg, \
+                     n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
+  if (nw == 3) FLEET_WEAVE_LAUNCH(3);
+  else if (nw == 4) FLEET_WEAVE_LAUNCH(4);
+  else if (nw == 6) FLEET_WEAVE_LAUNCH(6);
+  else FLEET_WEAVE_LAUNCH(8);
+#undef FLEET_WEAVE_LAUNCH
+}
+
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
@@ -2691,12 +2709,9 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
   else if (p.kind == 1)
     launch_tiled<false>(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
                         d_err, KardamOut{}, s);
-  else if (p.kind == 3 && p.nw == 3)
-    hipLaunchKernelGGL(k_update_weave<3>, dim3((unsigned)p.blocks), dim3(192), 0, s, uploads, pitch, M, d_dampen,
-                       inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
   else if (p.kind == 3)
-    hipLaunchKernelGGL(k_update_weave<4>, dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
-                       inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err);
+    launch_weave(p.nw, (unsigned)p.blocks, s, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block,
+                 merged, merged_f32, d_err);
   else
     hipLaunchKernelGGL((k_update_mixed<256, false>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M,
                        d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.nA,
@@ -2871,12 +2886,14 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     const int rpb = encode_rows_per_block(gx, M);
     const int64_t nU = p.blocks, nE = gx * ((M + rpb - 1) / rpb);
     const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
-    if (p.nw == 3)
-      hipLaunchKernelGGL(k_update_weave_encode<3>, dim3((unsigned)(nU + nE)), dim3(192), 0, s, uploads, pitch, M,
-                         d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)nU, ej);
-    else
-      hipLaunchKernelGGL(k_update_weave_encode<4>, dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, M,
-                         d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)nU, ej);
+#define FLEET_WEAVE_ENC_LAUNCH(NWV)                                                                             \
+  hipLaunchKernelGGL(k_update_weave_encode<NWV>, dim3((unsigned)(nU + nE)), dim3(64 * NWV), 0, s, uploads, pitch, M, \
+                     d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)nU, ej)
+    if (p.nw == 3) FLEET_WEAVE_ENC_LAUNCH(3);
+    else if (p.nw == 4) FLEET_WEAVE_ENC_LAUNCH(4);
+    else if (p.nw == 6) FLEET_WEAVE_ENC_LAUNCH(6);
+    else FLEET_WEAVE_ENC_LAUNCH(8);
+#undef FLEET_WEAVE_ENC_LAUNCH
     return hipGetLastError();
   }
   if (p.kind == 1) {  // the wide tiles on one width, then the encode's blocks

@@ -89,7 +89,8 @@ GRID_SIZES = [1, 2, 16, 17, 83, 84, 85, 255, 256, 257, 6_667, 7_654, 16_668, 32_
 
 @pytest.mark.parametrize("spec", ["", "update=stream", "update=stream,grid=plain", "update=stream,grid=lanes",
                                   "update=tiled", "update=tiled,tile_mix=off", "update=pipe",
-                                  "update=tiled,tile=weave3", "update=tiled,tile=weave4"])
+                                  "update=tiled,tile=weave3", "update=tiled,tile=weave4",
+                                  "update=tiled,tile=weave8"])
 def test_launch_grid_covers_every_group(spec):
     """The aggregation's grid (fleet_update_plan_grid) covers every group of the
     bucket exactly once and launches no block past it, under every plan: the stream

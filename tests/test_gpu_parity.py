@@ -329,7 +329,8 @@ def test_update_stream_grids(codec, oracle, plan, grid):
 
 @pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile_mix=off", "update=stream",
                                   "update=stream,grid=plain", "update=stream,grid=lanes",
-                                  "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4"])
+                                  "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4",
+                                  "update=tiled,tile=weave6", "update=tiled,tile=weave8"])
 def test_update_large_magnitudes_slow_path(codec, oracle, plan, spec):
     """Values far outside the fast path (|x| >= 1, digits != 0, >= 2^31) force
     every compaction pass and the tiled kernel's general-chain fallback (the
@@ -378,7 +379,8 @@ def test_update_two_width_tiles(codec, oracle, plan, mix):
 
 @pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile_mix=off", "update=stream",
                                   "update=stream,grid=plain", "update=stream,grid=lanes",
-                                  "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4"])
+                                  "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4",
+                                  "update=tiled,tile=weave6", "update=tiled,tile=weave8"])
 def test_update_modes(codec, oracle, plan, spec):
     """Every aggregation kernel (pipelined and two-phase tiles for small
     buckets, streaming for large ones) on ragged tiles, client counts that wrap
@@ -394,7 +396,8 @@ def test_update_modes(codec, oracle, plan, spec):
 
 @pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile_mix=off", "update=stream",
                                   "update=stream,grid=plain", "update=stream,grid=lanes",
-                                  "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4"])
+                                  "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4",
+                                  "update=tiled,tile=weave6", "update=tiled,tile=weave8"])
 @pytest.mark.parametrize("extra", [200, 201])
 def test_update_keep_slots_past_the_walk(codec, oracle, plan, spec, extra):
     """Uploads longer than their layout: mergeFlatGradient (CppNNUpdater.java:508)
