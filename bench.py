@@ -358,6 +358,9 @@ def strong_pipelined(torch, dist, codec, name, steps, warmup, rank, world):
            "groups_per_rank_max": wmax, "ms_per_step": elapsed / steps * 1e3,
            "gib_s": M * layout.n_up * 4 / (elapsed / steps) / 2**30,
            "kernel": F.update_encode_kernel(L_loc), "kernel_ms_rank0": kern_ms,
+           # what the step costs beyond rank 0's launch: the all_gather's exposed part plus
+           # the step's launch gaps and any rank imbalance (the clock is the max over ranks)
+           "exposed_ms": elapsed / steps * 1e3 - kern_ms,
            "step": "pipelined launch on the rank's column window + all_gather of the merged slices (inside; "
                    + ("issued async, overlapping the next step's launch)" if overlap else "in line)")}
     del graphs, bufs, sh, srcs, outs

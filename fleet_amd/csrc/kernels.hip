@@ -398,10 +398,38 @@ __device__ __forceinline__ double group_sum_f64(double v) {
 // coordinates for the next round's difference. `flat` bit i = value slot pos0 + i
 // is in the flat gradient (neither a header slot nor past the walk). The wave's
 // two sums go to its partial slot `part` (lane 63; k_kardam_reduce sums the waves).
+// The worker's previous G at the lane's slots (0 off the flat gradient): loaded a client
+// ahead by the stream loop, so the HBM latency of the prev rows overlaps the current
+// client's chain instead of stalling it. Returns has_prev[c] (uniform).
+template <int S>
+__device__ __forceinline__ bool kardam_prev_load(const KardamOut& kd, int c, uint32_t flat, bool live, int64_t pos0,
+                                                 int64_t n_up, float (&pv)[S]) {
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+#pragma unroll
+  for (int i = 0; i < S; ++i) pv[i] = 0.0f;
+  if (!(kd.prev && kd.has_prev[c])) return false;  // uniform
+  const float* pr = kd.prev + (size_t)c * kd.vpitch + pos0;
+  if constexpr (S == 3) {
+    if (live && pos0 + S - 1 < n_up) {  // one 12-byte access per group (rows are 4-byte aligned)
+      const f3u t = *reinterpret_cast<const f3u*>(pr);
+      pv[0] = t.x;
+      pv[1] = t.y;
+      pv[2] = t.z;
+    } else {
+#pragma unroll
+      for (int i = 0; i < S; ++i) pv[i] = ((flat >> i) & 1u) ? pr[i] : 0.0f;
+    }
+  } else {
+    pv[0] = (flat & 1u) ? pr[0] : 0.0f;
+  }
+  return true;
+}
+
 template <int S>
 __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uint32_t flat, bool live, int64_t pos0,
                                                  int64_t n_up, const KardamOut& kd, const D16Table& dtab,
-                                                 const B64Tables& tab, double* __restrict__ part) {
+                                                 const B64Tables& tab, double* __restrict__ part, bool hasp,
+                                                 const float (&pv)[S]) {
   typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
   float rg[S], G[S];
 #pragma unroll
@@ -413,22 +441,8 @@ __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uin
   for (int i = 0; i < S; ++i)
     if ((flat >> i) & 1u) sg += (double)(G[i] * G[i]);
   const bool whole = live && pos0 + S - 1 < n_up;
-  if (kd.prev && kd.has_prev[c]) {  // uniform
-    const float* pr = kd.prev + (size_t)c * kd.vpitch + pos0;
-    float pv[S], dv[S], D[S];
-    if constexpr (S == 3) {
-      if (whole) {  // one 12-byte access per group (rows are 4-byte aligned)
-        const f3u t = *reinterpret_cast<const f3u*>(pr);
-        pv[0] = t.x;
-        pv[1] = t.y;
-        pv[2] = t.z;
-      } else {
-#pragma unroll
-        for (int i = 0; i < S; ++i) pv[i] = ((flat >> i) & 1u) ? pr[i] : 0.0f;
-      }
-    } else {
-      pv[0] = (flat & 1u) ? pr[0] : 0.0f;
-    }
+  if (hasp) {  // uniform
+    float dv[S], D[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) dv[i] = ((flat >> i) & 1u) ? G[i] - pv[i] : 0.0f;
     q_stage_d16x<S>(D, dv, &dtab, tab.var);
@@ -501,6 +515,8 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   // bytes (chars 4e..4e+7); the group's three lanes together cover all 16 chars
   const uint32_t sel = b64_pair_selector(e0), need_pair = (need >> (4 * e0)) & 0xffu;
   using Row = typename std::conditional<S == 3, uint4, uint2>::type;
+  float kd_pv[S];       // KD: this client's prev values (loaded a client ahead)
+  bool kd_hasp = false;
   auto client = [&](int c, const Row& cur) {
     if constexpr (S == 3) {
 #if FLEET_DEC_T
@@ -528,7 +544,8 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       q_stage_d16x<S>(y, y0, &dtab, tab.var);
       dampen_stage<S>(y, dampen[c]);
       q_stage_d16x<S>(p, y, &dtab, tab.var);
-      kardam_lane_step<S>(p, c, flatbits, live, 3 * g + e0, n_up, kd, dtab, tab, kd_part + (size_t)c * kd_stride);
+      kardam_lane_step<S>(p, c, flatbits, live, 3 * g + e0, n_up, kd, dtab, tab, kd_part + (size_t)c * kd_stride,
+                          kd_hasp, kd_pv);
     } else {
       q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
       dampen_stage<S>(y, dampen[c]);
@@ -571,6 +588,8 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   if constexpr (KD) {
     // Kardam: one client per trip, the next one in flight (two per trip: 1840 against
     // 1795 us on synth1m_256, r04 call a13)
+    float pn[S];  // the next client's prev values, in flight with its group
+    bool hn = kardam_prev_load<S>(kd, 0, flatbits, live, 3 * g + e0, n_up, pn);
     for (; c < M; ++c) {
       if constexpr (LADDER > 0) {
         if (c == q1) __builtin_amdgcn_s_setprio(P1);
@@ -578,7 +597,13 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
         if (c == q3) __builtin_amdgcn_s_setprio(0);
       }
       const Row cur = b0;
-      if (c + 1 < M) b0 = group_of(c + 1);
+      kd_hasp = hn;
+#pragma unroll
+      for (int i = 0; i < S; ++i) kd_pv[i] = pn[i];
+      if (c + 1 < M) {
+        b0 = group_of(c + 1);
+        hn = kardam_prev_load<S>(kd, c + 1, flatbits, live, 3 * g + e0, n_up, pn);
+      }
       client(c, cur);
     }
   }
@@ -1356,14 +1381,66 @@ __device__ __forceinline__ void weave_item(WeaveShared<NW>& sh, uint4 w, bool li
   for (int e = 0; e < 3; ++e) pdst[3 * gl + e] = live ? p[e] : 0.0f;
 }
 
-// Tile `bid` of the woven grid (LDS state in sh).
+// The next batch's client encode inside the woven tiles (ENC; the pipelined step): the
+// producer-only ("light") waves, which carry no serial steps, encode the rows of the
+// tile's 64 groups -- in interval k the chunk's clients k*NW + j, row j to light wave
+// j mod (NW - 3) -- so the encode uses the issue slots the consumers' serial chains
+// leave, instead of blocks of its own after the tiles. A light wave's values for the
+// next interval are loaded one interval ahead.
 template <int NW>
+struct WeaveEnc {
+  static constexpr int NL = NW > 3 ? NW - 3 : 1;  // light waves
+  static constexpr int RPI = (NW + NL - 1) / NL;  // rows per light wave and interval (at most)
+  typedef float f3 __attribute__((ext_vector_type(3)));
+  f3 x[RPI];
+};
+template <int NW>
+__device__ __forceinline__ void weave_enc_load(WeaveEnc<NW>& we, const EncodeJob& ej, int k, int li, int M,
+                                               int64_t g, bool glive) {
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+  constexpr int NL = WeaveEnc<NW>::NL;
+  const int r = (int)min<int64_t>(3, max<int64_t>(0, ej.n - 3 * g));
+#pragma unroll
+  for (int i = 0; i < WeaveEnc<NW>::RPI; ++i) {
+    const int j = li + i * NL, row = k * NW + j;
+    we.x[i] = typename WeaveEnc<NW>::f3{0.0f, 0.0f, 0.0f};
+    if (j < NW && row < M && glive) {
+      const float* v = ej.values + (size_t)row * ej.vpitch + 3 * g;
+      if (r == 3) {
+        const f3u t = *reinterpret_cast<const f3u*>(v);
+        we.x[i] = typename WeaveEnc<NW>::f3{t.x, t.y, t.z};
+      } else {
+        we.x[i] = typename WeaveEnc<NW>::f3{v[0], r > 1 ? v[1] : 0.0f, 0.0f};
+      }
+    }
+  }
+}
+template <int NW>
+__device__ __forceinline__ void weave_enc_rows(const WeaveEnc<NW>& we, const EncodeJob& ej, int k, int li, int M,
+                                               int64_t g, bool glive, const B64Tables* tab, const D16Table* dt) {
+  constexpr int NL = WeaveEnc<NW>::NL;
+  const int r = (int)min<int64_t>(3, max<int64_t>(0, ej.n - 3 * g));
+#pragma unroll
+  for (int i = 0; i < WeaveEnc<NW>::RPI; ++i) {
+    const int j = li + i * NL, row = k * NW + j;
+    if (j < NW && row < M) {  // wave-uniform: encode_group's ballots see the whole wave
+      const float x[3] = {we.x[i].x, we.x[i].y, we.x[i].z};
+      const uint4 t = encode_group(x, r, tab, dt);
+      if (glive) store_stream16(ej.out + (size_t)row * ej.pitch + 16 * g, t);
+    }
+  }
+}
+
+// Tile `bid` of the woven grid (LDS state in sh); ej: the pipelined step's encode (ENC).
+template <int NW, bool ENC = false>
 __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t bid, const uint8_t* __restrict__ uploads,
                                                    size_t pitch, int M, const double* __restrict__ dampen,
                                                    double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end,
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
-                                                   float* __restrict__ merged_f32, int* __restrict__ err) {
+                                                   float* __restrict__ merged_f32, int* __restrict__ err,
+                                                   const EncodeJob& ej = EncodeJob{}) {
   static_assert(NW >= 3 && NW <= 8, "three consumer waves (+ producer-only waves)");
+  static_assert(!ENC || NW > 3, "the inline encode runs on the producer-only waves");
   constexpr int E = kWeaveE, CM = NW;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1385,9 +1462,22 @@ __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t 
     return *reinterpret_cast<const uint4*>(rowbase + (size_t)(c < M ? c : M - 1) * pitch);
   };
   uint4 nxt = load(0);  // in flight while the tables are copied
+  const int li = consumer ? 0 : ci - 3;  // light wave index
+  WeaveEnc<NW> we;
+  if constexpr (ENC) {
+    if (!consumer) weave_enc_load<NW>(we, ej, 0, li, M, g0 + gl, glive);
+  }
   tile_init(sh.t, hdr_block + 4, hdr_block[1], g0, ng);
   uint32_t badacc = 0, emax = 0;
   float A = 0.0f;
+  // a light wave's encode of interval k's rows, the next interval's values in flight
+  auto encode_interval = [&](int k) {
+    if constexpr (ENC) {
+      const WeaveEnc<NW> cur = we;
+      if (k + 1 < nchunks) weave_enc_load<NW>(we, ej, k + 1, li, M, g0 + gl, glive);
+      weave_enc_rows<NW>(cur, ej, k, li, M, g0 + gl, glive, &sh.t.tab, &sh.t.dt);
+    }
+  };
   // interval 0: produce chunk 0
   {
     const uint4 cur = nxt;
@@ -1395,6 +1485,7 @@ __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t 
     const int c = wave;
     weave_item<NW, 0, false>(sh, cur, glive && c < M, c, gl, M, dampen, n_up, walk_end, g0, sh.p[0] + wave * E, badacc,
                              A, nullptr, col, emax);
+    if (!consumer) encode_interval(0);
   }
   __syncthreads();
   // intervals 1 .. nchunks-1: produce chunk k, consume chunk k-1 (always CM clients)
@@ -1414,6 +1505,7 @@ __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t 
     } else {
       weave_item<NW, 0, false>(sh, cur, glive && c < M, c, gl, M, dampen, n_up, walk_end, g0, pdst, badacc, A,
                                nullptr, col, emax);
+      encode_interval(k);
     }
     __syncthreads();
   }
@@ -1571,14 +1663,17 @@ __device__ __forceinline__ void kardam_finish_block(const KardamFinishJob& kf, i
     const int64_t t = (int64_t)k * TPC + threadIdx.x / NPW;
     if ((int)threadIdx.x < TPC * NPW && t < ntiles) {
       const uint32_t* f = kf.flags + t * NPW + threadIdx.x % NPW;
-      // bounded (~0.5 s): a flag that never comes (a bug, not a slow tile) fails the call
+      // relaxed polls (an agent-scope acquire per poll would invalidate the caches the
+      // tiles are working from, for every poll of every waiting block: 160 us against
+      // 19 us for the tiles alone on mnist64, r05 call x1); ONE acquire after the barrier.
+      // Bounded (~0.5 s): a flag that never comes (a bug, not a slow tile) fails the call
       // instead of hanging the device
-      for (uint32_t spin = 0; __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != kf.epoch; ++spin) {
-        if (spin == (1u << 23)) {
+      for (uint32_t spin = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kf.epoch; ++spin) {
+        if (spin == (1u << 21)) {
           atomicOr(err, FLEET_ERRBIT_ARG);
           break;
         }
-        __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_s_sleep(8);
       }
     }
   }
@@ -1990,6 +2085,12 @@ __global__ void __launch_bounds__(64 * NW) k_update_weave_encode(const uint8_t* 
                                                                  float* __restrict__ merged_f32, int* __restrict__ err,
                                                                  int nU, EncodeJob ej) {
   __shared__ WeaveShared<NW> sh;
+  if (nU == (int)gridDim.x) {  // the encode inside the tiles (NW > 3: light waves)
+    if constexpr (NW > 3)
+      update_weave_block<NW, true>(sh, xcd_tile(blockIdx.x, nU), uploads, pitch, M, dampen, inv_avg, n_up, g_begin,
+                                   g_end, hdr_block, merged, merged_f32, err, ej);
+    return;
+  }
   if ((int)blockIdx.x < nU) {  // block-uniform
     update_weave_block<NW>(sh, xcd_tile(blockIdx.x, nU), uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                            hdr_block, merged, merged_f32, err);
@@ -2477,6 +2578,11 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
       else if (v == "weave6") o->tile = 6;
       else if (v == "weave8") o->tile = 8;
       else ok = false;
+    } else if (k == "weave_enc") {
+      if (v == "auto") o->weave_enc = 0;
+      else if (v == "inline") o->weave_enc = 1;
+      else if (v == "blocks") o->weave_enc = 2;
+      else ok = false;
     } else if (k == "tile_mix") {
       if (v == "auto") o->tile_mix = 0;
       else if (v == "off") o->tile_mix = 1;
@@ -2490,7 +2596,8 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
     } else if (k == "stage_pieces") {
       ok = parse_int(v, 1, 64, &o->stage_pieces);
     } else {
-      *err = "unknown plan key '" + k + "' (update, grid, tile, tile_mix, fused, stage_threads, stage_pieces)";
+      *err = "unknown plan key '" + k + "' (update, grid, tile, weave_enc, tile_mix, fused, stage_threads, "
+             "stage_pieces)";
       return -1;
     }
     if (!ok) {
@@ -2880,11 +2987,11 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     if (e != hipSuccess) return e;
     return launch_encode_f32(values, n_up, vpitch, M, enc_out, pitch, s);
   }
-  if (p.kind == 3) {  // the woven tiles, then the encode's blocks (64 * nw lanes each)
+  if (p.kind == 3) {  // the woven tiles, then the encode's blocks (64 * nw lanes each), or the encode inside them
     const int nt = 64 * p.nw;
     const int64_t gx = (groups + nt - 1) / nt;
     const int rpb = encode_rows_per_block(gx, M);
-    const int64_t nU = p.blocks, nE = gx * ((M + rpb - 1) / rpb);
+    const int64_t nU = p.blocks, nE = (o.weave_enc == 1 && p.nw > 3) ? 0 : gx * ((M + rpb - 1) / rpb);
     const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
 #define FLEET_WEAVE_ENC_LAUNCH(NWV)                                                                             \
   hipLaunchKernelGGL(k_update_weave_encode<NWV>, dim3((unsigned)(nU + nE)), dim3(64 * NWV), 0, s, uploads, pitch, M, \

@@ -17,6 +17,7 @@
 #   pytest:EXPR      pytest -m gpu -k EXPR (a subset), output in $TAG/pytest.log
 #   sq:W:N:MODE      SQ counters (8) + GRBM_GUI_ACTIVE + kernel trace of strong_probe.py W N MODE
 #                    (rank 0's window at N ranks; MODE fused | upd | enc), per-kernel summary
+#   sqk:W            the same counters over scripts/kardam_ab.py W (Kardam forms and the plain update)
 #   env:VAR=VALUE    export VAR for the steps after it (env:VAR= unsets it), e.g.
 #                    'env:FLEET_EXPERIMENTS=update=tiled;tile=weave4' (quote the ';')
 set -u
@@ -88,6 +89,15 @@ for r in csv.DictReader(open('$O/kardam_$w/run_kernel_stats.csv')):
       EC=$(python3 -c "import sys; sys.path.insert(0,'.'); import bench; from fleet_amd.layouts import LAYOUTS; l,m,_=bench.WORKLOADS['$W']; print(m*LAYOUTS[l].n_up/$N)")
       echo "-- $W N=$N $MODE ${FLEET_EXPERIMENTS:-default}" | tee -a "$O/sq.txt"
       python3 scripts/pmc_kernels.py "$D" "$EC" | grep -E "k_update|k_encode" | tee -a "$O/sq.txt" ;;
+    sqk)
+      W=$arg
+      D="$O/sqk_${W}${SQTAG:-}"
+      timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CU_CYCLES SQ_WAVE_CYCLES \
+        SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE --output-format csv -d "$D" -o run \
+        -- python3 scripts/kardam_ab.py "$W" > "$D.log" 2>&1 || { tail -20 "$D.log"; exit 1; }
+      EC=$(python3 -c "import sys; sys.path.insert(0,'.'); import bench; from fleet_amd.layouts import LAYOUTS; l,m,_=bench.WORKLOADS['$W']; print(m*LAYOUTS[l].n_up)")
+      echo "-- kardam $W ${FLEET_EXPERIMENTS:-default}" | tee -a "$O/sq.txt"
+      python3 scripts/pmc_kernels.py "$D" "$EC" | grep -E "k_update|k_kardam" | tee -a "$O/sq.txt" ;;
     py)
       timeout -k 10 600 python3 "$arg" > "$O/$(basename "$arg").log" 2>&1 || { tail -30 "$O/$(basename "$arg").log"; exit 1; }
       tail -40 "$O/$(basename "$arg").log" ;;
