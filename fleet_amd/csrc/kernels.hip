@@ -475,12 +475,87 @@ __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uin
   }
 }
 
+// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
+// One group (3 values) of one row: float2int (fixed chains when the wave is
+// in |x| < 1, multiplier-table chains otherwise, the general codec for values
+// outside the q_gen domain) and the 16 Base64 chars.
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab,
+                                              const D16Table* dt) {
+  int32_t codes[3];
+  // |x| < 1 for the whole wave iff the largest |x| bit pattern is (integer max,
+  // not three 6-cycle e64 compares)
+  uint32_t amax = 0;
+#pragma unroll
+  for (int e = 0; e < 3; ++e) amax = max(amax, f2u(x[e]) & 0x7fffffffu);
+  if (__ballot(amax >= 0x3f800000u) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+    // byte-table digit counts (codec_math.h d16_entry): one byte load per value;
+    // the power-of-ten slices take the compare, values outside the q_gen
+    // domain (|x| >= 1e8/1e9, inf, NaN) the general codec -- both rare, per lane
+    uint32_t ofs[3], omax = 0;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) {
+      ofs[e] = dt->d16[f2u(x[e]) >> 19];
+      omax = max(omax, ofs[e]);
+    }
+    if (__ballot(omax >= kD16Out) != 0) {
+      omax = 0;
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        if (ofs[e] == kD16Cmp) ofs[e] = d16_fix(x[e], tab->var);
+        omax = max(omax, ofs[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
+    if (__ballot(omax >= kD16Out) != 0) {
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if (ofs[e] >= kD16Out) codes[e] = enc(x[e]);
+    }
+  }
+  return pad_group(b64_encode_group(codes, tab), r);
+}
+
+// The same with the VarEntry digit counts (kernels that keep only B64Tables in LDS)
+__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
+  int32_t codes[3];
+  const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
+  if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab->var, tab->mt);
+    if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
+#pragma unroll
+      for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
+    }
+  }
+  return pad_group(b64_encode_group(codes, tab), r);
+}
+
+// A client-encode job riding in an aggregation launch (k_update_encode,
+// k_update_tiled_encode, k_update_pipe): k_encode_f32's grid, flattened x-fastest.
+struct EncodeJob {
+  const float* values;
+  int64_t n;
+  size_t vpitch;
+  uint8_t* out;
+  size_t pitch;
+  int64_t groups, gx;
+  int rows, rpb;
+};
+
+
 // One lane's share of the fused update (the stream path): the values [e0, e0 + S)
 // of group g, S = 3 (the whole group) or S = 1 (one value; three lanes of a wave
 // share a group). Returns the lane's merged codes in out[S] and its Base64 / layout
 // error bits; tables already in LDS. KD: Kardam's side outputs per client
 // (kardam_lane_step; kd_part = this wave's slot of client 0, kd_stride between clients).
-template <int S, bool KD = false, int LADDER = 0>
+template <int S, bool KD = false, int LADDER = 0, bool INLE = false>
 __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table& dtab,
                                             const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                             const double* __restrict__ dampen, double inv_avg, int64_t n_up,
@@ -488,7 +563,8 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
                                             const int32_t* __restrict__ hdr_block, int32_t (&out)[S],
                                             uint32_t& bad, uint32_t& layout_bad, const KardamOut& kd = KardamOut{},
                                             double* __restrict__ kd_part = nullptr, size_t kd_stride = 0,
-                                            const DecTables* dect = nullptr) {
+                                            const DecTables* dect = nullptr, const EncodeJob* ej = nullptr) {
+  static_assert(!INLE || (S == 3 && !KD), "the inline encode rides in the group-per-lane update");
   const int n_hdr = hdr_block[1];
   const int64_t walk_end = hdr_block[2];
   const int32_t* hdr = hdr_block + 4;
@@ -635,6 +711,29 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
     c = M;
   }
 #endif
+  // INLE: the next batch's client encode of this lane's group, row by row with the
+  // update's clients (its values loaded with the client's group, stored after it)
+  typedef float f3 __attribute__((ext_vector_type(3)));
+  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+  const int er = (int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g));
+  auto enc_load = [&](int cc) -> f3 {
+    if constexpr (INLE) {
+      if (!live) return f3{0.0f, 0.0f, 0.0f};
+      const float* v = ej->values + (size_t)cc * ej->vpitch + 3 * g;
+      if (er == 3) return *reinterpret_cast<const f3u*>(v);
+      return f3{v[0], er > 1 ? v[1] : 0.0f, 0.0f};
+    } else {
+      return f3{0.0f, 0.0f, 0.0f};
+    }
+  };
+  auto enc_store = [&](int cc, f3 xv) {
+    if constexpr (INLE) {
+      const float x[3] = {xv.x, xv.y, xv.z};
+      const uint4 t = encode_group(x, er, &tab, &dtab);
+      if (live) store_stream16(ej->out + (size_t)cc * ej->pitch + 16 * g, t);
+    }
+  };
+  f3 e0v = enc_load(0), e1v;
   for (; c + 1 < M; c += 2) {
     FLEET_CLIENT_HOOK(c, M);
     if constexpr (LADDER > 0) {
@@ -643,11 +742,20 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       if (c == (q3 & ~1)) __builtin_amdgcn_s_setprio(0);
     }
     b1 = group_of(c + 1);
+    if constexpr (INLE) e1v = enc_load(c + 1);
     client(c, b0);
-    if (c + 2 < M) b0 = group_of(c + 2);
+    if constexpr (INLE) enc_store(c, e0v);
+    if (c + 2 < M) {
+      b0 = group_of(c + 2);
+      if constexpr (INLE) e0v = enc_load(c + 2);
+    }
     client(c + 1, b1);
+    if constexpr (INLE) enc_store(c + 1, e1v);
   }
-  if (c < M) client(c, b0);
+  if (c < M) {
+    client(c, b0);
+    if constexpr (INLE) enc_store(c, e0v);
+  }
   FLEET_CLIENT_HOOK(M, M);
   if (__ballot(dmax >= kD16Out) != 0) {  // left the q_gen domain: recompute exactly (never for gradients)
     if (dmax >= kD16Out && live) {
@@ -664,7 +772,7 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
 }
 
 // Block `bid` of the SIMD-balanced stream grid (tables already in LDS).
-template <int NT, bool KD = false, int LADDER = 0>
+template <int NT, bool KD = false, int LADDER = 0, bool INLE = false>
 __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D16Table& dtab, int64_t bid,
                                                    const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                    const double* __restrict__ dampen, double inv_avg, int64_t n_up,
@@ -672,7 +780,7 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
                                                    float* __restrict__ merged_f32, int* __restrict__ err, int nA,
                                                    const KardamOut& kd = KardamOut{},
-                                                   const DecTables* dect = nullptr) {
+                                                   const DecTables* dect = nullptr, const EncodeJob* ej = nullptr) {
   uint32_t bad = 0, layout_bad = 0;
   // Kardam: this wave's partial slot of client 0; one slot per wave of the grid
   const size_t nw = (size_t)gridDim.x * (NT / 64);
@@ -681,8 +789,8 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
     const int64_t g = g_begin + bid * NT + threadIdx.x;
     const bool live = g < g_end;
     int32_t out[3];
-    update_lane<3, KD, LADDER>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block, out,
-                               bad, layout_bad, kd, kd_part, 2 * nw, dect);
+    update_lane<3, KD, LADDER, INLE>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin,
+                                     hdr_block, out, bad, layout_bad, kd, kd_part, 2 * nw, dect, ej);
     if (!live) return;
     if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
@@ -690,7 +798,7 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
     *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &tab), r);
     if (merged_f32)
       for (int e = 0; e < r; ++e) merged_f32[3 * g + e] = dec_mt(out[e], tab.mt);
-  } else {  // one value per lane, 21 groups per wave
+  } else if constexpr (!INLE) {  // one value per lane, 21 groups per wave
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t g = g_begin + (int64_t)nA * NT + ((bid - nA) * (NT / 64) + wave) * 21 + lane / 3;
     const int e = lane % 3;
@@ -747,83 +855,6 @@ __global__ void __launch_bounds__(NT, KD ? 6 : 1) k_update_mixed(const uint8_t* 
   update_mixed_block<NT, KD, 3>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                              hdr_block, merged, merged_f32, err, nA, kd, dp);
 }
-
-// Shared state of one tile of TG groups (E = 3*TG values) in LDS, for a block
-// of NW waves.
-// Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
-// One group (3 values) of one row: float2int (fixed chains when the wave is
-// in |x| < 1, multiplier-table chains otherwise, the general codec for values
-// outside the q_gen domain) and the 16 Base64 chars.
-__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab,
-                                              const D16Table* dt) {
-  int32_t codes[3];
-  // |x| < 1 for the whole wave iff the largest |x| bit pattern is (integer max,
-  // not three 6-cycle e64 compares)
-  uint32_t amax = 0;
-#pragma unroll
-  for (int e = 0; e < 3; ++e) amax = max(amax, f2u(x[e]) & 0x7fffffffu);
-  if (__ballot(amax >= 0x3f800000u) == 0) {  // wave-uniform: gradients, |x| < 1
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
-  } else {
-    // byte-table digit counts (codec_math.h d16_entry): one byte load per value;
-    // the power-of-ten slices take the compare, values outside the q_gen
-    // domain (|x| >= 1e8/1e9, inf, NaN) the general codec -- both rare, per lane
-    uint32_t ofs[3], omax = 0;
-#pragma unroll
-    for (int e = 0; e < 3; ++e) {
-      ofs[e] = dt->d16[f2u(x[e]) >> 19];
-      omax = max(omax, ofs[e]);
-    }
-    if (__ballot(omax >= kD16Out) != 0) {
-      omax = 0;
-#pragma unroll
-      for (int e = 0; e < 3; ++e) {
-        if (ofs[e] == kD16Cmp) ofs[e] = d16_fix(x[e], tab->var);
-        omax = max(omax, ofs[e]);
-      }
-    }
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
-    if (__ballot(omax >= kD16Out) != 0) {
-#pragma unroll
-      for (int e = 0; e < 3; ++e)
-        if (ofs[e] >= kD16Out) codes[e] = enc(x[e]);
-    }
-  }
-  return pad_group(b64_encode_group(codes, tab), r);
-}
-
-// The same with the VarEntry digit counts (kernels that keep only B64Tables in LDS)
-__device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const B64Tables* tab) {
-  int32_t codes[3];
-  const bool fast = q_ok(x[0]) && q_ok(x[1]) && q_ok(x[2]);
-  if (__ballot(!fast) == 0) {  // wave-uniform: gradients, |x| < 1
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_fast(x[e]);
-  } else {
-#pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_mt(x[e], tab->var, tab->mt);
-    if (!(q_gen_ok(x[0]) && q_gen_ok(x[1]) && q_gen_ok(x[2]))) {  // |x| >= 1e8/1e9, inf, NaN
-#pragma unroll
-      for (int e = 0; e < 3; ++e) codes[e] = enc(x[e]);
-    }
-  }
-  return pad_group(b64_encode_group(codes, tab), r);
-}
-
-// A client-encode job riding in an aggregation launch (k_update_encode,
-// k_update_tiled_encode, k_update_pipe): k_encode_f32's grid, flattened x-fastest.
-struct EncodeJob {
-  const float* values;
-  int64_t n;
-  size_t vpitch;
-  uint8_t* out;
-  size_t pitch;
-  int64_t groups, gx;
-  int rows, rpb;
-};
-
 
 // D16: the tile also holds the byte-table digit counts (D16Table, 9 KB), and the
 // epilogue assembles its merged codes in the tile's p buffer instead of outcodes.
@@ -1972,7 +2003,7 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
 // aggregation's blocks first (they fit the chip in one round) and streams the
 // encode's blocks through the wave slots and issue cycles they leave. Each
 // block's results are those of the separate kernels.
-template <int NT>
+template <int NT, bool INLE = false>
 __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                       const double* __restrict__ dampen, double inv_avg,
                                                       int64_t n_up, int64_t g_begin, int64_t g_end,
@@ -1999,6 +2030,11 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   // another box (gpu_r04_a16.sh); at 0 (r04 a6: 1158 us) or 1 (1138-1142 us) slower, and
   // so were update waves laddered from 2 under the encode's 3 (1134-1141 against
   // 1118-1129 us, gpu_r04_a26.sh)
+  if constexpr (INLE) {  // every block an update block; each lane also encodes its group's next-batch rows
+    update_mixed_block<NT, false, 3, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin,
+                                           g_end, hdr_block, merged, merged_f32, err, nA, KardamOut{}, dp, &ej);
+    return;
+  }
   if ((int)blockIdx.x < nU) {  // block-uniform
     update_mixed_block<NT, false, 3>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                                      hdr_block, merged, merged_f32, err, nA, KardamOut{}, dp);
@@ -2028,6 +2064,10 @@ template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_
                                               double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
                                               uint8_t* __restrict__, float* __restrict__, int* __restrict__, int, int,
                                               EncodeJob);
+template __global__ void k_update_encode<256, true>(const uint8_t* __restrict__, size_t, int,
+                                                    const double* __restrict__, double, int64_t, int64_t, int64_t,
+                                                    const int32_t* __restrict__, uint8_t* __restrict__,
+                                                    float* __restrict__, int* __restrict__, int, int, EncodeJob);
 #else
 extern template __global__ void k_update_mixed<256, false>(const uint8_t* __restrict__, size_t, int,
                                                            const double* __restrict__, double, int64_t, int64_t,
@@ -2041,6 +2081,11 @@ extern template __global__ void k_update_encode<256>(const uint8_t* __restrict__
                                                      const double* __restrict__, double, int64_t, int64_t, int64_t,
                                                      const int32_t* __restrict__, uint8_t* __restrict__,
                                                      float* __restrict__, int* __restrict__, int, int, EncodeJob);
+extern template __global__ void k_update_encode<256, true>(const uint8_t* __restrict__, size_t, int,
+                                                           const double* __restrict__, double, int64_t, int64_t,
+                                                           int64_t, const int32_t* __restrict__, uint8_t* __restrict__,
+                                                           float* __restrict__, int* __restrict__, int, int,
+                                                           EncodeJob);
 #endif
 
 #ifndef FLEET_STREAM_TU
@@ -2578,6 +2623,11 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
       else if (v == "weave6") o->tile = 6;
       else if (v == "weave8") o->tile = 8;
       else ok = false;
+    } else if (k == "stream_enc") {
+      if (v == "auto") o->stream_enc = 0;
+      else if (v == "inline") o->stream_enc = 1;
+      else if (v == "blocks") o->stream_enc = 2;
+      else ok = false;
     } else if (k == "weave_enc") {
       if (v == "auto") o->weave_enc = 0;
       else if (v == "inline") o->weave_enc = 1;
@@ -2596,7 +2646,7 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
     } else if (k == "stage_pieces") {
       ok = parse_int(v, 1, 64, &o->stage_pieces);
     } else {
-      *err = "unknown plan key '" + k + "' (update, grid, tile, weave_enc, tile_mix, fused, stage_threads, "
+      *err = "unknown plan key '" + k + "' (update, grid, tile, weave_enc, stream_enc, tile_mix, fused, stage_threads, "
              "stage_pieces)";
       return -1;
     }
@@ -3037,6 +3087,11 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   const int rpb = std::min(M, 24);
   const int64_t nE = gx * ((M + rpb - 1) / rpb);
   const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+  if (o.stream_enc == 1 && !lanes) {  // the encode inside the update lanes: one block per 256 groups
+    hipLaunchKernelGGL((k_update_encode<256, true>), dim3((unsigned)gx), dim3(256), 0, s, uploads, pitch, M, d_dampen,
+                       inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)gx, (int)gx, ej);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nUf + nE)), dim3(256), 0, s, uploads, pitch, M, d_dampen,
                      inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf, nUf, ej);
   return hipGetLastError();

@@ -93,6 +93,7 @@ def test_update_encode_rejects_overlap_and_bad_text(codec):
                                          ("update=pipe", "(with the encode's blocks)"),
                                          ("update=stream", "k_update_encode<256>"),
                                          ("update=stream,grid=lanes", "k_update_encode<256>"),
+                                         ("update=stream,stream_enc=inline", "k_update_encode<256>"),
                                          ("update=tiled,tile=weave3", "k_update_weave_encode<3>"),
                                          ("update=tiled,tile=weave4", "k_update_weave_encode<4>"),
                                          ("update=tiled,tile=weave8", "k_update_weave_encode<8>"),
