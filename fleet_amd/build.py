@@ -67,6 +67,9 @@ def build_codec(force: bool = False, out: str = LIB, defines=()) -> str:
         sched = os.environ.get("FLEET_STREAM_SCHED", "max-ilp")
         extra = ["-mllvm", f"-amdgpu-sched-strategy={sched}"] if (
             src.endswith("stream_kernels.hip") and sched != "default") else []
+        main_sched = os.environ.get("FLEET_MAIN_SCHED", "")  # experiments: the main unit's scheduler
+        if main_sched and src.endswith("/kernels.hip"):
+            extra = ["-mllvm", f"-amdgpu-sched-strategy={main_sched}"]
         _run([HIPCC, *lang, *COMMON, *extra, *[f"-D{d}" for d in defines], "-c", src, "-o", obj])
         return obj
 
