@@ -486,6 +486,13 @@ namespace {
 std::atomic<int> g_last_ingress{FLEET_INGRESS_NONE};  // the process's most recent one
 }
 
+#ifdef FLEET_TRACE
+// dev builds only (-DFLEET_TRACE): where the tile kernels write their phase trace
+extern "C" __attribute__((visibility("default"))) int fleet_dev_trace(void* d_buf) {
+  return fleet::set_trace_buffer(d_buf) == hipSuccess ? FLEET_OK : FLEET_ERR_HIP;
+}
+#endif
+
 int fleet_last_ingress(fleet_ctx* c) {
   if (!c) return g_last_ingress.load();
   std::lock_guard<std::mutex> lk(c->mu);

@@ -116,4 +116,7 @@ hipError_t launch_layout_parse(const uint8_t* up, int64_t n, int cap, int32_t* o
 hipError_t launch_synth(uint64_t seed, int client0, int64_t elem0, int rows, int64_t n_up, float* out, size_t vpitch,
                         const int32_t* d_hpos, const float* d_hval, int n_hdr, hipStream_t s);
 hipError_t launch_digest(int fn, unsigned long long* out, hipStream_t s);
+#ifdef FLEET_TRACE
+hipError_t set_trace_buffer(void* p);  // dev builds: the tile kernels' phase trace (FLEET_WTRACE)
+#endif
 }  // namespace fleet

@@ -49,6 +49,21 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
   do {                     \
   } while (0)
 #endif
+// Dev-only per-wave phase trace of the tile kernels (FLEET_TRACE builds: scripts/tile_trace.py):
+// the shader clock at phase boundaries of tiles 0..63, chunk k < 64, wave w < 8, slot s < 4;
+// stored by lane 0 with vector stores. Compiled out of the library.
+#ifdef FLEET_TRACE
+static __device__ unsigned long long* g_fleet_trace;
+#define FLEET_WTRACE(tile, k, slot)                                                                        \
+  do {                                                                                                     \
+    if (g_fleet_trace && (tile) < 64 && (k) < 64 && (threadIdx.x & 63) == 0)                               \
+      g_fleet_trace[((((tile) * 64 + (k)) * 8 + (threadIdx.x >> 6)) * 4) + (slot)] = clock64();          \
+  } while (0)
+#else
+#define FLEET_WTRACE(tile, k, slot) \
+  do {                              \
+  } while (0)
+#endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
 // (scripts/ubench_window.hip defines it); compiled out of the library.
 #ifndef FLEET_CLIENT_HOOK
@@ -689,7 +704,7 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   }
 #if FLEET_STREAM_PF >= 2
   // four clients per trip, two rows issued ahead of the pair being computed
-  if (!KD && M >= 4) {
+  if (!KD && !INLE && M >= 4) {
     Row b2, b3;
     b1 = group_of(1);
     for (; c + 3 < M; c += 4) {
@@ -1225,6 +1240,7 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
   for (int c0 = 0; c0 < M; c0 += CM) {
     const int cm = min(CM, M - c0);
     const int nitems = cm * TG;
+    FLEET_WTRACE(bid, c0 / CM, 0);
 #if FLEET_TILE_PF
     {
       const TileItems<TG, 2> it = nit;
@@ -1239,7 +1255,9 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
       if (base == 0) FLEET_TSTAMP(2);
     }
 #endif
+    FLEET_WTRACE(bid, c0 / CM, 1);
     __syncthreads();
+    FLEET_WTRACE(bid, c0 / CM, 2);
     FLEET_TSTAMP(3);
     // phase 2: serial accumulation, one value per thread
     if (tid < E) {
@@ -1271,6 +1289,7 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
         }
       }
     }
+    FLEET_WTRACE(bid, c0 / CM, 3);
     __syncthreads();
   }
   FLEET_TSTAMP(4);
@@ -1539,6 +1558,7 @@ __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t 
   __syncthreads();
   // intervals 1 .. nchunks-1: produce chunk k, consume chunk k-1 (always CM clients)
   for (int k = 1; k < nchunks; ++k) {
+    FLEET_WTRACE(bid, k, 0);
     const uint4 cur = nxt;
     if (k + 1 < nchunks) nxt = load(k + 1);
     const int c = k * CM + wave;
@@ -1556,7 +1576,9 @@ __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t 
                                nullptr, col, emax);
       encode_interval(k);
     }
+    FLEET_WTRACE(bid, k, 1);
     __syncthreads();
+    FLEET_WTRACE(bid, k, 2);
   }
   // the last interval: consume the last chunk (cm clients)
   if (consumer) {
@@ -2697,6 +2719,13 @@ void plan_env_init() {
   });
 }
 }  // namespace
+
+#ifdef FLEET_TRACE
+hipError_t set_trace_buffer(void* p) {
+  unsigned long long* q = static_cast<unsigned long long*>(p);
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_fleet_trace), &q, sizeof(q));
+}
+#endif
 
 PlanOverrides plan_overrides() {
   plan_env_init();

@@ -18,6 +18,8 @@
 #   sq:W:N:MODE      SQ counters (8) + GRBM_GUI_ACTIVE + kernel trace of strong_probe.py W N MODE
 #                    (rank 0's window at N ranks; MODE fused | upd | enc), per-kernel summary
 #   sqk:W            the same counters over scripts/kardam_ab.py W (Kardam forms and the plain update)
+#   trace:W:N:MODE   per-wave phase trace of the tile kernels (scripts/tile_trace.py; needs
+#                    FLEET_CODEC_LIB=ab/trace.so, a FLEET_TRACE build)
 #   env:VAR=VALUE    export VAR for the steps after it (env:VAR= unsets it), e.g.
 #                    'env:FLEET_EXPERIMENTS=update=tiled;tile=weave4' (quote the ';')
 set -u
@@ -98,6 +100,11 @@ for r in csv.DictReader(open('$O/kardam_$w/run_kernel_stats.csv')):
       EC=$(python3 -c "import sys; sys.path.insert(0,'.'); import bench; from fleet_amd.layouts import LAYOUTS; l,m,_=bench.WORKLOADS['$W']; print(m*LAYOUTS[l].n_up)")
       echo "-- kardam $W ${FLEET_EXPERIMENTS:-default}" | tee -a "$O/sq.txt"
       python3 scripts/pmc_kernels.py "$D" "$EC" | grep -E "k_update|k_kardam" | tee -a "$O/sq.txt" ;;
+    trace)
+      IFS=: read -r W N MODE <<< "$arg"
+      echo "-- ${FLEET_EXPERIMENTS:-default}" >> "$O/trace.txt"
+      timeout -k 10 300 python3 scripts/tile_trace.py "$W" "$N" "$MODE" >> "$O/trace.txt" 2>&1 || { tail -20 "$O/trace.txt"; exit 1; }
+      tail -14 "$O/trace.txt" ;;
     py)
       timeout -k 10 600 python3 "$arg" > "$O/$(basename "$arg").log" 2>&1 || { tail -30 "$O/$(basename "$arg").log"; exit 1; }
       tail -40 "$O/$(basename "$arg").log" ;;
