@@ -26,7 +26,7 @@
 #include "../../include/fleet_codec.h"
 #include "kernels.h"
 
-static_assert(FLEET_MAX_HEADERS == fleet::kMaxHeaderSlots, "k_kardam_finish sizes its LDS header list by it");
+static_assert(FLEET_MAX_HEADERS == fleet::kMaxHeaderSlots, "the kernels size their LDS header lists by it");
 #include "model_codec.h"
 #include "codec_device.h"
 

@@ -32,8 +32,8 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
 // pipelined tiles): per client c and flat value (upload positions that are neither header slots nor past the walk)
 //   G = Q(f32(f64(p) lr))            the decoded Kardam.setGrad text (p = stage B)
 //   D = Q(G - prev[c])               the decoded g.subtract(prev) text (has_prev[c])
-// partials[(c * n_waves + w) * 2 + {0, 1}] = per-wave sums of (double)(G*G), (double)(D*D)
-// (the pipelined form uses them as scratch p rows); g_out (nullable) = G in upload
+// partials[(c * n_waves + w) * 2 + {0, 1}] = per-wave (or per-tile) sums of (double)(G*G),
+// (double)(D*D); g_out (nullable) = G in upload
 // coordinates (M rows of vpitch floats; may be prev itself).
 // launch_update_kardam: *n_waves = partial slots per client (sizing call: partials
 // NULL), norms = M x *norm_parts pairs of sums, added in order on the host;

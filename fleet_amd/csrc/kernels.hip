@@ -59,9 +59,24 @@ static __device__ unsigned long long* g_fleet_trace;
     if (g_fleet_trace && (tile) < 64 && (k) < 64 && (threadIdx.x & 63) == 0)                               \
       g_fleet_trace[((((tile) * 64 + (k)) * 8 + (threadIdx.x >> 6)) * 4) + (slot)] = clock64();          \
   } while (0)
+// per block (dispatch order blockIdx.x < 65536): the constant 100 MHz clock at its start and
+// end and its hardware id (XCC, SE, CU): residency and rounds of a launch
+#define FLEET_BTRACE(slot)                                                                                  \
+  do {                                                                                                      \
+    if (g_fleet_trace && blockIdx.x < 65536 && threadIdx.x == 0) {                                         \
+      unsigned long long* bt_ = g_fleet_trace + 64 * 64 * 8 * 4 + (size_t)blockIdx.x * 4;                 \
+      bt_[slot] = wall_clock64();                                                                           \
+      if ((slot) == 0)                                                                                      \
+        bt_[2] = ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)) << 32) |  \
+                 (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));          \
+    }                                                                                                       \
+  } while (0)
 #else
 #define FLEET_WTRACE(tile, k, slot) \
   do {                              \
+  } while (0)
+#define FLEET_BTRACE(slot) \
+  do {                     \
   } while (0)
 #endif
 // Dev-only per-wave progress trace of the stream kernels' client loop
@@ -1035,21 +1050,18 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const T
     const double a = group_sum_f64<TG>(sg[h]), b = group_sum_f64<TG>(sd[h]);
     if (it.cvalid[h] && (threadIdx.x & (TG - 1)) == TG - 1) {  // the group's last lane: its client's tile sum
       const size_t slot = ((size_t)(it.c_base + it.cl[h]) * tk.ntiles + tk.tile) * 2;
-      kd.partials[slot] = a;
-      kd.partials[slot + 1] = b;
+      // sc1: the pipelined form's reduce blocks read them in the same launch
+      __hip_atomic_store(kd.partials + slot, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(kd.partials + slot + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
 
-// PS: also store every live item's p in the rows p_out (client c at c * p_pitch, upload
-// coordinates; 0 in header slots and past the walk) -- Kardam's pipelined form
-// (k_update_pipe<..., KD = true> + k_kardam_finish).
-template <int TG, int IPT, int NW, bool KD = false, bool D16 = false, bool PS = false>
+template <int TG, int IPT, int NW, bool KD = false, bool D16 = false>
 __device__ __forceinline__ void tile_compute(TileShared<TG, NW, D16>& sh, const TileItems<TG, IPT>& it, int M,
                                              const double* __restrict__ dampen, int64_t n_up, int64_t walk_end,
                                              int64_t g0, float* __restrict__ pdst, uint32_t& badacc,
-                                             const TileKd& tk = TileKd{}, float* __restrict__ p_out = nullptr,
-                                             size_t p_pitch = 0) {
+                                             const TileKd& tk = TileKd{}) {
   constexpr int E = 3 * TG, S = 3 * IPT;
   int32_t codes[S];
 #pragma unroll
@@ -1114,24 +1126,6 @@ __device__ __forceinline__ void tile_compute(TileShared<TG, NW, D16>& sh, const 
 #pragma unroll
       for (int e = 0; e < 3; ++e) pdst[it.cc[h] * E + 3 * it.gl[h] + e] = p[3 * h + e];
   if constexpr (KD) tile_kardam<TG, IPT, NW>(sh, it, p, n_up, g0, tk);
-  if constexpr (PS) {
-    typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
-#pragma unroll
-    for (int h = 0; h < IPT; ++h) {
-      if (!it.live[h]) continue;
-      const int64_t gp = 3 * (g0 + it.gl[h]);
-      const uint32_t hm = sh.hmask[it.gl[h]];
-      float v[3];
-#pragma unroll
-      for (int e = 0; e < 3; ++e) v[e] = (((hm >> e) & 1u) || gp + e >= walk_end) ? 0.0f : p[3 * h + e];
-      float* dst = p_out + (size_t)(it.c_base + it.cc[h]) * p_pitch + gp;
-      // sc1 (agent-scope relaxed) stores: the finish blocks of the same launch read them
-      // from other CUs and XCDs (kardam_finish_block) without an L2 writeback per wave
-#pragma unroll
-      for (int e = 0; e < 3; ++e)
-        if (gp + e < n_up) __hip_atomic_store(dst + e, v[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
 }
 
 template <int TG, int IPT, int NW, bool KD = false, bool D16 = false>
@@ -1341,6 +1335,7 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
                 "the narrow tiles' state fits the wide tiles' LDS");
   __shared__ TileShared<TG, 4, D16> sh;
   __shared__ float ptile[tiled_chunk_clients<TG, D16>() * 3 * TG];
+  FLEET_BTRACE(0);
   const TileKd tk{kd, (int64_t)blockIdx.x, (int64_t)gridDim.x, (int64_t)hdr_block[2]};
   if constexpr (TG2 > 0) {
     if ((int)blockIdx.x >= nW) {  // block-uniform: a narrow tile after the wide rounds
@@ -1348,12 +1343,14 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
       update_tiled_block<TG2, KD, D16>(reinterpret_cast<TileShared<TG2, 4, D16>&>(sh), ptile,
                                        xcd_tile(b, nN), uploads, pitch, M, dampen, inv_avg, n_up,
                                        g_begin + (int64_t)nW * TG, g_end, hdr_block, merged, merged_f32, err, tk);
+      FLEET_BTRACE(1);
       return;
     }
   }
   const int64_t nw = TG2 > 0 ? (int64_t)nW : (int64_t)gridDim.x;
   update_tiled_block<TG, KD, D16>(sh, ptile, xcd_tile(blockIdx.x, nw), uploads, pitch, M,
                                   dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged, merged_f32, err, tk);
+  FLEET_BTRACE(1);
 }
 
 // ----------------------------------------------------------------------------
@@ -1613,8 +1610,10 @@ __global__ void __launch_bounds__(64 * NW) k_update_weave(const uint8_t* __restr
                                                           uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
                                                           int* __restrict__ err) {
   __shared__ WeaveShared<NW> sh;
+  FLEET_BTRACE(0);
   update_weave_block<NW>(sh, xcd_tile(blockIdx.x, gridDim.x), uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                          hdr_block, merged, merged_f32, err);
+  FLEET_BTRACE(1);
 }
 
 
@@ -1679,165 +1678,62 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
 }
 
 // Kardam's side outputs of the pipelined form (CppNNUpdater.java:463-481,
-// Kardam.java:48-106). The pipelined tiles are latency-bound -- one serial consumer
-// wave per tile -- so Kardam's two extra Q stages stay off them:
-// their producers only store each (client, value)'s p in `rows` (k_update_pipe<...,
-// KD = true>), and finish blocks riding in the same launch turn the rows into G =
-// Q(f32(f64(p) * lr)) (into g_out when given: 0 off the flat gradient), ||G||^2 and,
-// with the worker's previous G, ||Q(G - prev)||^2. A finish block = (client c, chunk k
-// of 2 * NT groups): a lane's groups, the wave by DPP and the block's waves in LDS give
-// the chunk's two sums, in a fixed order, at parts[(c * kc + k) * 2]; the host adds a
-// client's kc chunk sums in order (a few per client: no reduce launch). rows may be
-// g_out (each lane reads its p before writing its G); prev must not overlap rows (it
-// may be g_out: a lane reads prev before writing G at the same slots).
-// The finish block of chunk k waits for the tiles over its groups: every producer wave
-// of a tile publishes the launch's epoch in its flag (flags[tile * NPW + wave]) after
-// its last pass (agent-scope release); the block's first threads spin on those flags
-// (acquire, s_sleep). Tiles are dispatched before every finish block and never wait
-// on one, so the launch drains; the epoch (new per launch, never reused) makes a
-// stale flag from an earlier launch never match, so the flags need no reset.
-struct KardamFinishJob {
-  const float* rows;  // p rows (the producers' PS output)
-  size_t rpitch;
-  float* g_out;       // nullable
-  const float* prev;  // nullable
-  size_t gpitch;
-  const uint8_t* has_prev;
-  double lr;
-  double* parts;      // M x kc pairs
-  int kc;             // chunks per client
-  uint32_t* flags;    // tiles x producer waves
+// Kardam.java:48-106): the tiles' producer waves compute them with p (tile_kardam: G =
+// Q(f32(f64(p) * lr)) into g_out, ||G||^2 and ||Q(G - prev)||^2 summed over the tile's
+// groups per client, one partial slot per (client, tile)), and M reduce blocks riding
+// in the same launch add a client's tile partials in a fixed order -- no second launch
+// (a dependent launch costs >= 4.5 us at MNIST size, a quarter of the update).
+// Hand-off: a producer wave's partial stores are sc1 (agent-scope relaxed atomics) and
+// drained (vmcnt 0) before it publishes the launch's epoch in its flag
+// (flags[tile * NPW + wave]); a reduce block polls every flag with relaxed sc1 loads,
+// then reads the partials with sc1 loads (no agent-scope release / acquire: their L2
+// writeback and invalidate per wave cost more than the whole reduce). Tiles are
+// dispatched before every reduce block and never wait on one, so the launch drains;
+// the epoch (new per launch, never reused) makes a stale flag never match, so the
+// flags need no reset.
+struct KardamReduceJob {
+  double* norms;    // M pairs
+  uint32_t* flags;  // tiles x producer waves
   uint32_t epoch;
 };
-template <int NT, int TG, int NPW>
-__device__ __forceinline__ void kardam_finish_block(const KardamFinishJob& kf, int64_t e, int64_t n_up, int64_t ntiles,
-                                                    const int32_t* __restrict__ hdr_block, B64Tables& tab,
-                                                    int32_t* hdr, double (*red)[NT / 64], int* __restrict__ err) {
-  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
-  constexpr int IPL = 2, S = 3 * IPL, GROUPS = NT * IPL;
-  static_assert(GROUPS % TG == 0, "a chunk covers whole tiles");
-  constexpr int TPC = GROUPS / TG;  // tiles per chunk
-  static_assert(TPC * NPW <= NT, "one flag per thread");
-  const int kc = kf.kc;
-  const int c = (int)(e / kc), k = (int)(e % kc);
-  const bool hasp = kf.prev && kf.has_prev[c];  // block-uniform
-  const float* row = kf.rows + (size_t)c * kf.rpitch;
-  const float* prow = hasp ? kf.prev + (size_t)c * kf.gpitch : nullptr;
-  float* grow = kf.g_out ? kf.g_out + (size_t)c * kf.gpitch : nullptr;
-  const int64_t groups = (n_up + 2) / 3;
-  // the tables and the header list while the tiles work
-  b64_tables_init<NT>(&tab);
-  const int n_hdr = hdr_block[1];
-  const int64_t walk_end = hdr_block[2];
-  for (int i = threadIdx.x; i < n_hdr; i += NT) hdr[i] = hdr_block[4 + i];
-  {  // wait for the producers of the chunk's tiles
-    const int64_t t = (int64_t)k * TPC + threadIdx.x / NPW;
-    if ((int)threadIdx.x < TPC * NPW && t < ntiles) {
-      const uint32_t* f = kf.flags + t * NPW + threadIdx.x % NPW;
-      // relaxed polls (an agent-scope acquire per poll would invalidate the caches the
-      // tiles are working from, for every poll of every waiting block: 160 us against
-      // 19 us for the tiles alone on mnist64, r05 call x1); ONE acquire after the barrier.
-      // Bounded (~0.5 s): a flag that never comes (a bug, not a slow tile) fails the call
-      // instead of hanging the device
-      for (uint32_t spin = 0; __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kf.epoch; ++spin) {
-        if (spin == (1u << 21)) {
-          atomicOr(err, FLEET_ERRBIT_ARG);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(8);
+template <int NT, int NPW>
+__device__ __forceinline__ void kardam_reduce_block(const KardamReduceJob& kr, int c, int64_t ntiles,
+                                                    const double* partials, double (*red)[NT / 64],
+                                                    int* __restrict__ err) {
+  // every tile's producers done (bounded ~0.5 s: a flag that never comes fails the call)
+  for (int64_t f = threadIdx.x; f < ntiles * NPW; f += NT) {
+    for (uint32_t spin = 0; __hip_atomic_load(kr.flags + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kr.epoch;
+         ++spin) {
+      if (spin == (1u << 21)) {
+        atomicOr(err, FLEET_ERRBIT_ARG);
+        break;
       }
+      __builtin_amdgcn_s_sleep(8);
     }
   }
   __syncthreads();
-  // the p rows are read with sc1 loads (agent-scope relaxed atomics) below: no acquire
-  // fence, whose cache invalidation every waiting block would pay
-  auto ld = [](const float* q) { return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-  int64_t gp[IPL];
-  bool whole[IPL], live[IPL];
-  float pv[S], qv[S];
-#pragma unroll
-  for (int h = 0; h < IPL; ++h) {
-    const int64_t g = (int64_t)k * GROUPS + h * NT + threadIdx.x;
-    live[h] = g < groups;
-    gp[h] = 3 * g;
-    whole[h] = live[h] && gp[h] + 2 < n_up;
-    pv[3 * h] = pv[3 * h + 1] = pv[3 * h + 2] = 0.0f;
-    qv[3 * h] = qv[3 * h + 1] = qv[3 * h + 2] = 0.0f;
-    if (whole[h]) {
-      pv[3 * h] = ld(row + gp[h]);
-      pv[3 * h + 1] = ld(row + gp[h] + 1);
-      pv[3 * h + 2] = ld(row + gp[h] + 2);
-      if (hasp) {  // written by an earlier launch: plain loads
-        const f3u u = *reinterpret_cast<const f3u*>(prow + gp[h]);
-        qv[3 * h] = u.x;
-        qv[3 * h + 1] = u.y;
-        qv[3 * h + 2] = u.z;
-      }
-    } else if (live[h]) {
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        if (gp[h] + q < n_up) {
-          pv[3 * h + q] = ld(row + gp[h] + q);
-          if (hasp) qv[3 * h + q] = prow[gp[h] + q];
-        }
-    }
+  // the client's tile partials in a fixed order: lane t of the block adds tiles t, t + NT, ...
+  const double* p = partials + (size_t)c * ntiles * 2;
+  double a = 0.0, b = 0.0;
+  for (int64_t t = threadIdx.x; t < ntiles; t += NT) {
+    a += __hip_atomic_load(p + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b += __hip_atomic_load(p + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  uint32_t flat = 0;
-#pragma unroll
-  for (int h = 0; h < IPL; ++h) {
-    const uint32_t hb = live[h] ? header_bits(hdr, n_hdr, gp[h]) : 7u;
-#pragma unroll
-    for (int q = 0; q < 3; ++q)
-      if (live[h] && gp[h] + q < n_up && gp[h] + q < walk_end && !((hb >> q) & 1u)) flat |= 1u << (3 * h + q);
-  }
-#pragma unroll
-  for (int i = 0; i < S; ++i)
-    if (!((flat >> i) & 1u)) pv[i] = 0.0f;
-  float G[S];
-  dampen_stage<S>(pv, kf.lr);  // lr is uniform
-  q_stage<S>(G, pv, &tab);
-  double sg = 0.0, sd = 0.0;
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    if (!((flat >> i) & 1u)) G[i] = 0.0f;
-    sg += (double)(G[i] * G[i]);
-  }
-  if (hasp) {
-    float dv[S], D[S];
-#pragma unroll
-    for (int i = 0; i < S; ++i) dv[i] = ((flat >> i) & 1u) ? G[i] - qv[i] : 0.0f;
-    q_stage<S>(D, dv, &tab);
-#pragma unroll
-    for (int i = 0; i < S; ++i)
-      if ((flat >> i) & 1u) sd += (double)(D[i] * D[i]);
-  }
-  if (grow) {
-#pragma unroll
-    for (int h = 0; h < IPL; ++h) {
-      if (whole[h]) {
-        *reinterpret_cast<f3u*>(grow + gp[h]) = f3u{G[3 * h], G[3 * h + 1], G[3 * h + 2]};
-      } else {
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          if (live[h] && gp[h] + q < n_up) grow[gp[h] + q] = G[3 * h + q];
-      }
-    }
-  }
-  sg = group_sum_f64<64>(sg);  // valid in lane 63
-  sd = group_sum_f64<64>(sd);
+  a = group_sum_f64<64>(a);  // valid in lane 63
+  b = group_sum_f64<64>(b);
   if ((threadIdx.x & 63) == 63) {
-    red[0][threadIdx.x / 64] = sg;
-    red[1][threadIdx.x / 64] = sd;
+    red[0][threadIdx.x / 64] = a;
+    red[1][threadIdx.x / 64] = b;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    double a = 0.0, b = 0.0;
+    double sa = 0.0, sb = 0.0;
     for (int i = 0; i < NT / 64; ++i) {
-      a += red[0][i];
-      b += red[1][i];
+      sa += red[0][i];
+      sb += red[1][i];
     }
-    kf.parts[((size_t)c * kc + k) * 2] = a;
-    kf.parts[((size_t)c * kc + k) * 2 + 1] = b;
+    kr.norms[2 * c] = sa;
+    kr.norms[2 * c + 1] = sb;
   }
 }
 
@@ -1850,9 +1746,9 @@ __device__ __forceinline__ void kardam_finish_block(const KardamFinishJob& kf, i
 //           a pass is ready after one wave's work -- the consumer starts
 //           early -- while the NW-1 producer waves work on successive passes
 //           in parallel.
-// Blocks [nU, ...): the next batch's client encode (ej; the pipelined step).
-// KD = true: the producers also store every item's p in Kardam's G rows (kd.g_out or
-// scratch), which k_kardam_finish turns into G, D and the norms (launch_update_kardam).
+// Blocks [nU, ...): the next batch's client encode (ej; the pipelined step), or with
+// KD = true Kardam's reduce blocks: the producers compute Kardam's side outputs with p
+// (tile_kardam) and one block per client adds its tile partials (kardam_reduce_block).
 // Hand-off through LDS: a producer wave publishes its count of finished passes
 // with a workgroup release after its p writes; the consumer acquires it before
 // reading a pass, and publishes "passes consumed" so producers never overwrite
@@ -1866,7 +1762,7 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
                                                      int* __restrict__ err, int nU, EncodeJob ej,
                                                      KardamOut kd = KardamOut{},
-                                                     KardamFinishJob kf = KardamFinishJob{}) {
+                                                     KardamReduceJob kr = KardamReduceJob{}) {
   constexpr int E = 3 * TG;
   static_assert(E <= 64, "one consumer wave");
   constexpr int NPW = NW - 1;                                // producer waves
@@ -1883,11 +1779,9 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   // split below is a scalar branch and the consumer's s_setprio is its own
   const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
   if constexpr (KD) {
-    if ((int)blockIdx.x >= nU) {  // block-uniform: Kardam's finish of one (client, chunk)
+    if ((int)blockIdx.x >= nU) {  // block-uniform: Kardam's reduce of one client's tile partials
       __shared__ double kred[2][NW];
-      static_assert(sizeof(ptile) >= sizeof(int32_t) * kMaxHeaderSlots, "the header list fits the p ring");
-      kardam_finish_block<64 * NW, TG, NPW>(kf, (int64_t)blockIdx.x - nU, n_up, nU, hdr_block, sh.tab,
-                                            reinterpret_cast<int32_t*>(ptile), kred, err);
+      kardam_reduce_block<64 * NW, NPW>(kr, (int)blockIdx.x - nU, nU, kd.partials, kred, err);
       return;
     }
   }
@@ -1928,19 +1822,18 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
         while (__hip_atomic_load(&consumed, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < pass - RING + 1)
           __builtin_amdgcn_s_sleep(1);
       }
-      tile_compute<TG, IPT, NW, false, false, KD>(sh, cur, M, dampen, n_up, hdr_block[2], g0,
-                                                  ptile + (pass % RING) * CPP * E, badacc, TileKd{}, kd.g_out,
-                                                  kd.vpitch);
+      tile_compute<TG, IPT, NW, KD>(sh, cur, M, dampen, n_up, hdr_block[2], g0, ptile + (pass % RING) * CPP * E,
+                                    badacc, TileKd{kd, (int64_t)blockIdx.x, (int64_t)nU, (int64_t)hdr_block[2]});
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       ++done;
       if (lane == 0) __hip_atomic_store(&prog[w], done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if constexpr (KD) {  // this wave's p rows are out: the finish blocks of its chunk may read them
+    if constexpr (KD) {  // this wave's Kardam partials are out: the reduce blocks may read them
       // the sc1 stores drained (vmcnt 0), then the flag: no agent-scope release (an L2
       // writeback per wave; 82 us against 19 us for the tiles alone on mnist64, r05 call x2)
       __builtin_amdgcn_s_waitcnt(0);
       if (lane == 0)
-        __hip_atomic_store(kf.flags + (size_t)blockIdx.x * NPW + w, kf.epoch, __ATOMIC_RELAXED,
+        __hip_atomic_store(kr.flags + (size_t)blockIdx.x * NPW + w, kr.epoch, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
   } else {  // ---------------------------------------------------- consumer
@@ -2148,9 +2041,11 @@ __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __re
                                                              int nU, EncodeJob ej) {
   __shared__ TileShared<TG, 4, true> sh;
   __shared__ float ptile[tiled_chunk_clients<TG, true>() * 3 * TG];
+  FLEET_BTRACE(0);
   if ((int)blockIdx.x < nU) {  // block-uniform
     update_tiled_block<TG, false, true>(sh, ptile, xcd_tile(blockIdx.x, nU), uploads, pitch, M, dampen, inv_avg, n_up,
                                         g_begin, g_end, hdr_block, merged, merged_f32, err);
+    FLEET_BTRACE(1);
   } else {
     b64_tables_init(&sh.tab);
     d16_table_init(&sh.dt);
@@ -2158,6 +2053,7 @@ __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __re
     const int64_t e = (int64_t)blockIdx.x - nU;
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                       (int)(e / ej.gx), &sh.tab, &sh.dt);
+    FLEET_BTRACE(1);
   }
 }
 
@@ -2975,18 +2871,15 @@ __global__ void __launch_bounds__(NT) k_kardam_reduce(const double* __restrict__
   }
 }
 
-// groups per finish block of the pipelined form (k_update_pipe<16, 1, 5, 0, true>: 320 lanes x 2)
-constexpr int kKfGroups = 64 * 5 * 2;
-
 hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                                 int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
                                 double* norms, int* norm_parts, int* flag_slots, uint32_t* kd_flags,
                                 uint32_t kd_epoch, const PlanOverrides& o, hipStream_t s) {
   const int64_t groups = g_end - g_begin;
-  // the update's own launch plan with the side outputs: the pipelined tiles (their
-  // producers store p; k_kardam_finish does the rest), the wide tiles (side outputs
-  // from the tile producers), or the stream kernel's SIMD-balanced grid
+  // the update's own launch plan with the side outputs: the pipelined tiles (side outputs
+  // from the producers, the reduce blocks in the same launch), the wide tiles (side
+  // outputs from the tile producers), or the stream kernel's SIMD-balanced grid
   PlanOverrides ok = o;
   ok.tile = 1;  // Kardam's side outputs ride in the classic tiles (tile_kardam)
   UpdatePlan p = plan_update(groups, ok);
@@ -2998,34 +2891,18 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
     p.blocks = p.nA;
   }
   const unsigned blocks = (unsigned)p.blocks;
-  // partial slots per client: a wave of the stream grid or a tile; the pipelined form
-  // uses the slots' bytes as its p rows (4 floats a slot) unless they can go straight
-  // into the caller's G rows
-  *n_waves = p.kind == 0 ? (int)blocks * 4 : p.kind == 1 ? (int)blocks : (int)((n_up + 3) / 4);
-  // norms: one pair per client (the reduce), or the finish kernel's chunk sums
-  const int kc = (int)(((n_up + 2) / 3 + kKfGroups - 1) / kKfGroups);
+  // partial slots per client: a wave of the stream grid or a tile
+  *n_waves = p.kind == 0 ? (int)blocks * 4 : (int)blocks;
   *flag_slots = p.kind == 2 ? (int)blocks * 4 : 0;  // the pipelined form's tile flags (4 producer waves)
-  *norm_parts = p.kind == 2 ? std::max(kc, 1) : 1;
+  *norm_parts = 1;                                   // one pair per client
   if (groups <= 0) return hipSuccess;
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
   if (p.kind == 2 && !kd_flags) return hipErrorInvalidValue;
-  if (p.kind == 2) {
-    // p rows: the caller's G rows, unless there are none or they overlap prev (G may
-    // replace prev in place: prev must stay intact until k_kardam_finish reads it)
-    const uintptr_t span = (uintptr_t)M * kd.vpitch * sizeof(float);
-    const uintptr_t go = reinterpret_cast<uintptr_t>(kd.g_out), pv = reinterpret_cast<uintptr_t>(kd.prev);
-    const bool overlap = kd.g_out && kd.prev && go < pv + span && pv < go + span;
-    KardamOut kp = kd;
-    if (!kd.g_out || overlap) {
-      kp.g_out = reinterpret_cast<float*>(kd.partials);
-      kp.vpitch = (size_t)((n_up + 3) / 4 * 4);
-    }
-    // the tiles, then the finish blocks (one per client and chunk of kKfGroups groups)
-    const KardamFinishJob kf{kp.g_out, kp.vpitch, kd.g_out, kd.prev, kd.vpitch, kd.has_prev, kd.lr, norms, kc,
-                             kd_flags, kd_epoch};
-    hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0, true>), dim3((unsigned)(blocks + (int64_t)M * kc)), dim3(64 * 5), 0,
-                       s, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
-                       d_err, (int)blocks, EncodeJob{}, kp, kf);
+  if (p.kind == 2) {  // the tiles, then one reduce block per client
+    const KardamReduceJob kr{norms, kd_flags, kd_epoch};
+    hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0, true>), dim3((unsigned)(blocks + (unsigned)M)), dim3(64 * 5), 0, s,
+                       uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
+                       d_err, (int)blocks, EncodeJob{}, kd, kr);
     return hipGetLastError();
   }
   if (p.kind == 1)

@@ -35,7 +35,8 @@ def main():
     L_loc = F.b64_len(sh.n_local)
     nxt = torch.zeros_like(sh.text)
     sh.encode()
-    trace = torch.zeros(64 * 64 * 8 * 4, dtype=torch.int64, device="cuda")
+    NW = 64 * 64 * 8 * 4
+    trace = torch.zeros(NW + 65536 * 4, dtype=torch.int64, device="cuda")
 
     def run():
         if mode == "fused":
@@ -51,7 +52,9 @@ def main():
         run()
     torch.cuda.synchronize()
     codec.check()
-    t = trace.cpu().numpy().reshape(64, 64, 8, 4).astype(np.float64)
+    full = trace.cpu().numpy()
+    t = full[:NW].reshape(64, 64, 8, 4).astype(np.float64)
+    bt = full[NW:].reshape(65536, 4)
     kern = F.update_kernel(L_loc) if mode == "upd" else F.update_encode_kernel(L_loc)
     print(f"{name} N={N} {mode} kernel={kern} groups/rank={sh.groups}", flush=True)
     waves = [w for w in range(8) if t[:, :, w, 0].any()]
@@ -78,8 +81,35 @@ def main():
     # whole tile: first stamp to last
     first = np.where(t[:, :, :, 0] > 0, t[:, :, :, 0], np.inf).min(axis=(1, 2))
     last = t.max(axis=(1, 2, 3))
+    residency(bt)
     print(f"tile span (cycles): mean {np.mean(last - first):.0f}, min {np.min(last - first):.0f}, "
           f"max {np.max(last - first):.0f}; per chunk {np.mean(last - first) / max(1, len(chunks)):.0f}")
+
+
+def residency(bt):
+    """Block start / end (100 MHz clock) of every traced block: rounds of the launch."""
+    used = bt[:, 0] > 0
+    if not used.any():
+        return
+    st, en = bt[used, 0].astype(np.float64), bt[used, 1].astype(np.float64)
+    t0 = st.min()
+    st, en = (st - t0) / 100.0, (en - t0) / 100.0  # us
+    n = used.sum()
+    hw = bt[used, 2]
+    xcc = (hw >> 32) & 0xF
+    cu = (hw >> 8) & 0xF
+    se = (hw >> 13) & 0x7
+    first = st < 2.0
+    print(f"blocks {n}: started in the first 2 us {first.sum()}, start max {st.max():.1f} us, end max {en.max():.1f} us, "
+          f"block span mean {np.mean(en - st):.1f} us")
+    key = xcc * 64 + se * 16 + cu
+    _, counts = np.unique(key[first], return_counts=True)
+    print(f"first-round blocks per CU: min {counts.min()} max {counts.max()} mean {counts.mean():.2f} "
+          f"({len(counts)} CUs)")
+    for lo, hi in ((0, 2), (2, 50), (50, 150), (150, 400), (400, 1e9)):
+        m = (st >= lo) & (st < hi)
+        if m.any():
+            print(f"  start in [{lo}, {hi}) us: {m.sum()} blocks, their end mean {en[m].mean():.1f} us")
 
 
 if __name__ == "__main__":
