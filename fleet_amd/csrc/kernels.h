@@ -59,7 +59,7 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
 // small inputs. Process-wide; set by fleet_set_plan (spec "key=value,..." -- update=
 // auto|stream|tiled|pipe, grid=auto|plain|lanes, tile_mix=auto|off, fused=on|off,
 // stage_threads=N, stage_pieces=N, tile=auto|classic|weave3|4|6|8,
-// weave_enc=auto|inline|blocks, stream_enc=auto|inline|blocks) or, once at first
+// weave_enc=auto|inline|blocks, stream_enc=auto|inline|blocks, tile_enc_rows=N) or, once at first
 // use, from FLEET_EXPERIMENTS (the
 // same spec). The default (empty spec) is the measured plan.
 struct PlanOverrides {
@@ -68,6 +68,7 @@ struct PlanOverrides {
   int tile = 0;           // tiles: 0 auto, 1 classic (two phases), 3/4/6/8 woven (k_update_weave<nw>)
   int weave_enc = 0;      // woven fused step: 0 auto, 1 encode inside the tiles (light waves), 2 encode blocks
   int stream_enc = 0;     // stream fused step: 0 auto, 1 encode inside the update lanes, 2 encode blocks
+  int tile_enc_rows = 0;  // tiled fused step: rows per encode block (0 auto: 24)
   int tile_mix = 0;       // 0 auto (two widths when a partial round of tiles remains), 1 one width
   int fused = 1;          // 0: the pipelined step as two launches (update, then encode)
   int stage_threads = 0;  // host staging copy threads (0 auto)

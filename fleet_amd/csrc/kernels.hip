@@ -2562,6 +2562,8 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
       else if (v == "weave6") o->tile = 6;
       else if (v == "weave8") o->tile = 8;
       else ok = false;
+    } else if (k == "tile_enc_rows") {
+      ok = parse_int(v, 1, 4096, &o->tile_enc_rows);
     } else if (k == "stream_enc") {
       if (v == "auto") o->stream_enc = 0;
       else if (v == "inline") o->stream_enc = 1;
@@ -2585,7 +2587,8 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
     } else if (k == "stage_pieces") {
       ok = parse_int(v, 1, 64, &o->stage_pieces);
     } else {
-      *err = "unknown plan key '" + k + "' (update, grid, tile, weave_enc, stream_enc, tile_mix, fused, stage_threads, "
+      *err = "unknown plan key '" + k + "' (update, grid, tile, weave_enc, stream_enc, tile_enc_rows, tile_mix, fused, "
+             "stage_threads, "
              "stage_pieces)";
       return -1;
     }
@@ -2981,8 +2984,12 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     return hipGetLastError();
   }
   if (p.kind == 1) {  // the wide tiles on one width, then the encode's blocks
+    // 24 rows per encode block, as in k_update_encode: each block copies the tile's
+    // 14 KB of tables into LDS, so the standalone encode's ~65,536 blocks (2 rows each at
+    // CIFAR sizes) spent the step on table copies -- the encode ran mostly after the
+    // tiles, 230 us of it on cifar10_256 against 157 us alone (r05 residency trace)
     const int64_t gx = blocks_for(groups, 256);
-    const int rpb = encode_rows_per_block(gx, M);
+    const int rpb = std::min(M, o.tile_enc_rows > 0 ? o.tile_enc_rows : 24);
     const int64_t nU = (groups + 63) / 64, nE = gx * ((M + rpb - 1) / rpb);
     const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
     hipLaunchKernelGGL((k_update_tiled_encode<64>), dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, M,

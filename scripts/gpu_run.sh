@@ -103,7 +103,9 @@ for r in csv.DictReader(open('$O/kardam_$w/run_kernel_stats.csv')):
     trace)
       IFS=: read -r W N MODE <<< "$arg"
       echo "-- ${FLEET_EXPERIMENTS:-default}" >> "$O/trace.txt"
-      timeout -k 10 300 python3 scripts/tile_trace.py "$W" "$N" "$MODE" >> "$O/trace.txt" 2>&1 || { tail -20 "$O/trace.txt"; exit 1; }
+      PL=$(echo "${FLEET_EXPERIMENTS:-default}" | tr ';=,' '___')
+      TRACE_OUT="$O/bt_${W}_n${N}_${MODE}_${PL}.npy" timeout -k 10 300 python3 scripts/tile_trace.py "$W" "$N" "$MODE" \
+        >> "$O/trace.txt" 2>&1 || { tail -20 "$O/trace.txt"; exit 1; }
       tail -14 "$O/trace.txt" ;;
     py)
       timeout -k 10 600 python3 "$arg" > "$O/$(basename "$arg").log" 2>&1 || { tail -30 "$O/$(basename "$arg").log"; exit 1; }

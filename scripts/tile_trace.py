@@ -55,6 +55,8 @@ def main():
     full = trace.cpu().numpy()
     t = full[:NW].reshape(64, 64, 8, 4).astype(np.float64)
     bt = full[NW:].reshape(65536, 4)
+    if os.environ.get("TRACE_OUT"):  # the raw block trace for offline analysis
+        np.save(os.environ["TRACE_OUT"], bt[bt[:, 0] > 0])
     kern = F.update_kernel(L_loc) if mode == "upd" else F.update_encode_kernel(L_loc)
     print(f"{name} N={N} {mode} kernel={kern} groups/rank={sh.groups}", flush=True)
     waves = [w for w in range(8) if t[:, :, w, 0].any()]
