@@ -33,6 +33,10 @@
 #ifndef FLEET_TILE_PF
 #define FLEET_TILE_PF 0
 #endif
+// FLEET_TILE_LADDER = 0: the classic / woven tiles without the progress priority ladder.
+#ifndef FLEET_TILE_LADDER
+#define FLEET_TILE_LADDER 1
+#endif
 
 namespace fleet {
 
@@ -1231,10 +1235,25 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
   TileItems<TG, 2> nit;
   tile_load<TG, 2>(nit, uploads, pitch, g0, ng, 0, min(CM, M) * TG, tid, 256);
 #endif
+  // Issue-priority ladder over the client loop (3 -> 0 at quarters of it), as in the
+  // stream kernel: a CU's tiles are all resident at once and the oldest win issue
+  // arbitration, so without it they finished one by one -- on cifar10_256 the tiles of
+  // one CU ended 118 us apart on a 245 us mean span, the last ones running alone in a
+  // latency-bound tail (r05 residency trace, scripts/bt_analyze.py). A tile that gets
+  // ahead yields, the lagging ones catch up.
+  const int nch = (M + CM - 1) / CM;
+  const int r1 = nch / 4, r2 = nch / 2, r3 = 3 * nch / 4;
+  if (FLEET_TILE_LADDER) __builtin_amdgcn_s_setprio(3);
   for (int c0 = 0; c0 < M; c0 += CM) {
     const int cm = min(CM, M - c0);
     const int nitems = cm * TG;
     FLEET_WTRACE(bid, c0 / CM, 0);
+    if (FLEET_TILE_LADDER) {
+      const int k = c0 / CM;
+      if (k == r1) __builtin_amdgcn_s_setprio(2);
+      if (k == r2) __builtin_amdgcn_s_setprio(1);
+      if (k == r3) __builtin_amdgcn_s_setprio(0);
+    }
 #if FLEET_TILE_PF
     {
       const TileItems<TG, 2> it = nit;
@@ -1553,9 +1572,17 @@ __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t 
     if (!consumer) encode_interval(0);
   }
   __syncthreads();
-  // intervals 1 .. nchunks-1: produce chunk k, consume chunk k-1 (always CM clients)
+  // intervals 1 .. nchunks-1: produce chunk k, consume chunk k-1 (always CM clients);
+  // the progress priority ladder of the classic tiles (update_tiled_block)
+  const int r1 = nchunks / 4, r2 = nchunks / 2, r3 = 3 * nchunks / 4;
+  if (FLEET_TILE_LADDER) __builtin_amdgcn_s_setprio(3);
   for (int k = 1; k < nchunks; ++k) {
     FLEET_WTRACE(bid, k, 0);
+    if (FLEET_TILE_LADDER) {
+      if (k == r1) __builtin_amdgcn_s_setprio(2);
+      if (k == r2) __builtin_amdgcn_s_setprio(1);
+      if (k == r3) __builtin_amdgcn_s_setprio(0);
+    }
     const uint4 cur = nxt;
     if (k + 1 < nchunks) nxt = load(k + 1);
     const int c = k * CM + wave;
