@@ -205,13 +205,13 @@ def update_kernel(length: int) -> str:
 
 def update_plan_grid(length: int) -> dict:
     """The aggregation's launch grid for uploads of `length` bytes (fleet_update_plan_grid):
-    kind ("stream" / "tiled" / "pipe" / "weave"), blocks, and n_a / n_w / n_n (see fleet_codec.h)."""
+    kind ("stream" / "tiled" / "pipe" / "weave" / "flat"), blocks, and n_a / n_w / n_n (see fleet_codec.h)."""
     k = C.c_int()
     b, a, w, n = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
     rc = lib().fleet_update_plan_grid(length, C.byref(k), C.byref(b), C.byref(a), C.byref(w), C.byref(n))
     if rc != 0:
         raise FleetError(f"fleet_update_plan_grid: {rc}")
-    return {"kind": ("stream", "tiled", "pipe", "weave")[k.value], "blocks": b.value, "n_a": a.value, "n_w": w.value,
+    return {"kind": ("stream", "tiled", "pipe", "weave", "flat")[k.value], "blocks": b.value, "n_a": a.value, "n_w": w.value,
             "n_n": n.value}
 
 

@@ -57,10 +57,13 @@ __device__ unsigned long long g_fleet_timing[16384 * 8];
 // the shader clock at phase boundaries of tiles 0..63, chunk k < 64, wave w < 8, slot s < 4;
 // stored by lane 0 with vector stores. Compiled out of the library.
 #ifdef FLEET_TRACE
+#ifndef FLEET_TRACE_WAVES  // 0: block start / end only (fewer SGPRs: the kernel keeps its residency)
+#define FLEET_TRACE_WAVES 1
+#endif
 static __device__ unsigned long long* g_fleet_trace;
 #define FLEET_WTRACE(tile, k, slot)                                                                        \
   do {                                                                                                     \
-    if (g_fleet_trace && (tile) < 64 && (k) < 64 && (threadIdx.x & 63) == 0)                               \
+    if (FLEET_TRACE_WAVES && g_fleet_trace && (tile) < 64 && (k) < 64 && (threadIdx.x & 63) == 0)          \
       g_fleet_trace[((((tile) * 64 + (k)) * 8 + (threadIdx.x >> 6)) * 4) + (slot)] = clock64();          \
   } while (0)
 // per block (dispatch order blockIdx.x < 65536): the constant 100 MHz clock at its start and
@@ -1373,6 +1376,196 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
 }
 
 // ----------------------------------------------------------------------------
+// Flat tiles (r05): k_update_tiled's two phases with the tile width W a runtime
+// value (16, 32 or 64 groups), so one launch deals the groups out as ONE round over
+// the CUs' block slots: whole rounds of 64-group tiles, then the rest in tiles of the
+// width that leaves the most loaded CU the least work. cifar10_256 (104,623 groups,
+// 256 CUs, 7 slots per CU): 1,536 64-group tiles + 198 32-group tiles, at most
+// 6 x 64 + 32 = 416 groups on a CU, where the one-width grid put 7 x 64 = 448 on most
+// CUs and the compile-time two-width grid (two inlined tile bodies: 106 SGPRs, 6
+// blocks per CU) ran its 16-group tiles as a second round -- either way the kernel
+// took as long as its most loaded CU (317-320 us against a 252 us first round, r05
+// residency traces). One tile body (85 SGPRs, 23 KB of LDS): 7 blocks per CU.
+// A tile's (client, group) items are client-major over its W groups, 512 per pass
+// (two per thread): 512 / W whole clients per pass, so phase 2 is k_update_tiled's.
+constexpr int kFlatTG = 64;     // the widest flat tile (E = 192 values, one per phase-2 thread)
+constexpr int kFlatPass = 512;  // items per pass
+constexpr int kFlatSlots = 7;   // blocks per CU (LDS 23 KB, 85 SGPRs; r05 residency traces)
+
+// scalarMultiply(getDampen) for a lane's own client (dampen_stage with a per-lane d: a
+// narrow tile's wave spans 64 / W clients): the binary32 multiply when every lane's d is
+// a binary32 value (wave-uniform branch), the f64 product otherwise; both exact.
+__device__ __forceinline__ void dampen_lane3(float (&r)[3], double d) {
+  const uint64_t b = __builtin_bit_cast(uint64_t, d);
+  const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+  const uint32_t ex = (hi >> 20) & 0x7ffu;
+  const bool f32ok = (lo & 0x1fffffffu) == 0 && ex - 897u < 254u;
+  if (__ballot(!f32ok) == 0) {
+    const float df = u2f((hi & 0x80000000u) | ((ex - 896u) << 23) | ((hi & 0xfffffu) << 3) | (lo >> 29));
+#pragma unroll
+    for (int i = 0; i < 3; ++i) r[i] = r[i] * df;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) r[i] = (float)((double)r[i] * d);
+  }
+}
+
+// One pass's items of a thread: items tid and tid + 256 of the pass (client c, group gl)
+struct FlatItems {
+  uint4 w[2];
+  int c[2], gl[2];
+  bool live[2];
+};
+
+// p of the thread's two items -> pbuf[item * 3 + e]: tile_compute's stages
+// (CppNNUpdater.java:463-464). W64: a wave's items are one client (wave-uniform d).
+__device__ __forceinline__ void flat_compute(TileShared<kFlatTG, 4, true>& sh, const FlatItems& it, int M,
+                                             const double* __restrict__ dampen, int64_t n_up, int64_t walk_end,
+                                             int64_t g0, int ng, bool W64, float* __restrict__ pbuf, int tid,
+                                             uint32_t& badacc) {
+  int32_t codes[6];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int r = (int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * (g0 + it.gl[h])));
+    uint32_t b;
+    if (r == 3) b = b64_decode_group_full(it.w[h], &sh.tab, codes + 3 * h);
+    else b = b64_decode_group(it.w[h], &sh.tab, codes + 3 * h) & needed_chars_mask(r);
+    if (it.live[h]) {
+      badacc |= b;
+      if (it.c[h] == M - 1)
+        for (int e = 0; e < 3; ++e) sh.last_codes[3 * it.gl[h] + e] = codes[3 * h + e];
+      const uint32_t hm = sh.hmask[it.gl[h]];
+      if (hm) {  // header slots (rare lanes): the layout check, then the chain runs on code 0 (keep_bits)
+        for (int e = 0; e < 3; ++e)
+          if ((hm >> e) & 1u) {
+            atomicMin(&sh.hmin[3 * it.gl[h] + e], codes[3 * h + e]);
+            atomicMax(&sh.hmax[3 * it.gl[h] + e], codes[3 * h + e]);
+            codes[3 * h + e] = 0;
+          }
+      }
+    }
+  }
+  if (3 * (g0 + ng) > walk_end) {  // block-uniform, rare: slots past the walk run on code 0 too
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int e = 0; e < 3; ++e)
+        if (3 * (g0 + it.gl[h]) + e >= walk_end) codes[3 * h + e] = 0;
+  }
+  float y0[6], y[6], r[6], p[6];
+  dec_stage_d16<6>(y0, codes, &sh.dt);
+  q_stage_d16x<6>(y, y0, &sh.dt, sh.tab.var);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float t[3] = {y[3 * h], y[3 * h + 1], y[3 * h + 2]};
+    if (W64) dampen_stage<3>(t, dampen[__builtin_amdgcn_readfirstlane(it.c[h])]);  // block-uniform branch
+    else dampen_lane3(t, dampen[it.c[h]]);
+#pragma unroll
+    for (int e = 0; e < 3; ++e) r[3 * h + e] = t[e];
+  }
+  q_stage_d16x<6>(p, r, &sh.dt, sh.tab.var);
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    if (it.live[h])
+#pragma unroll
+      for (int e = 0; e < 3; ++e) pbuf[(tid + 256 * h) * 3 + e] = p[3 * h + e];
+}
+
+// Flat tile: groups [g0, g0 + ng) on the item mapping of width W = 1 << lw (ng <= W <=
+// kFlatTG), pbuf = kFlatPass * 3 floats; `tile` its index (dev traces only).
+__device__ __forceinline__ void update_flat_block(TileShared<kFlatTG, 4, true>& sh, float* pbuf, int64_t tile,
+                                                  int64_t g0, int ng, int lw, const uint8_t* __restrict__ uploads,
+                                                  size_t pitch, int M, const double* __restrict__ dampen,
+                                                  double inv_avg, int64_t n_up, const int32_t* __restrict__ hdr_block,
+                                                  uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                  int* __restrict__ err) {
+  static_assert(3 * kFlatTG <= 256 && 2 * 3 * kFlatTG <= 3 * kFlatPass, "phase 2 / epilogue fit the block / pbuf");
+  const int tid = threadIdx.x;
+  const int W = 1 << lw, E = 3 * W;
+  const int cpp = kFlatPass >> lw;  // whole clients per pass
+  const int64_t walk_end = hdr_block[2];
+  tile_init(sh, hdr_block + 4, hdr_block[1], g0, ng);
+  float A = 0.f;  // phase-2 value: element tid of the tile (tid < E)
+  uint32_t off_domain = 0, badacc = 0;
+  // the thread's items: (client offset, group) fixed across passes (W divides 256)
+  int icl[2], igl[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    icl[h] = (tid + 256 * h) >> lw;
+    igl[h] = (tid + 256 * h) & (W - 1);
+  }
+  // the issue-priority ladder of update_tiled_block (3 -> 0 at quarters of the passes)
+  const int npass = (M + cpp - 1) / cpp;
+  const int r1 = npass / 4, r2 = npass / 2, r3 = 3 * npass / 4;
+  if (FLEET_TILE_LADDER) __builtin_amdgcn_s_setprio(3);
+  for (int k = 0; k < npass; ++k) {
+    if (FLEET_TILE_LADDER) {
+      if (k == r1) __builtin_amdgcn_s_setprio(2);
+      if (k == r2) __builtin_amdgcn_s_setprio(1);
+      if (k == r3) __builtin_amdgcn_s_setprio(0);
+    }
+    const int c0 = k * cpp, cm = min(cpp, M - c0);
+    FLEET_WTRACE(tile, k, 0);
+    FlatItems it;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      it.live[h] = icl[h] < cm && igl[h] < ng;
+      it.c[h] = c0 + (icl[h] < cm ? icl[h] : 0);
+      it.gl[h] = it.live[h] ? igl[h] : 0;
+      it.w[h] = *reinterpret_cast<const uint4*>(uploads + (size_t)it.c[h] * pitch + 16 * (g0 + it.gl[h]));
+    }
+    if (__ballot(it.live[0]) != 0)  // wave-uniform: only a last pass or a ragged tile has dead waves
+      flat_compute(sh, it, M, dampen, n_up, walk_end, g0, ng, lw == 6, pbuf, tid, badacc);
+    FLEET_WTRACE(tile, k, 1);
+    __syncthreads();
+    FLEET_WTRACE(tile, k, 2);
+    // phase 2: serial accumulation, one value per thread (k_update_tiled's stage C)
+    if (tid < E) {
+      int j = 0;
+      if (c0 == 0) {
+        A = pbuf[tid];
+        j = 1;
+      }
+#pragma unroll 2
+      for (; j < cm; ++j) {
+        const float s = A + pbuf[j * E + tid];
+        const uint32_t e = var_d16(f2u(s), sh.tab.var);
+        off_domain |= (uint32_t)(e >= kD16Out);
+        A = q_d16(s, e, &sh.dt.st);
+      }
+    }
+    FLEET_WTRACE(tile, k, 3);
+    __syncthreads();
+  }
+  if (badacc) atomicOr(err, FLEET_ERRBIT_BASE64);
+  if (tid >= 3 * ng) off_domain = 0;  // columns past the last group hold no values
+  if (__ballot(off_domain != 0)) {    // wave-uniform, never for gradients
+    if (off_domain) A = chain_general(uploads, pitch, M, dampen, g0 + tid / 3, tid % 3, &sh.tab);
+  }
+  if (tid < E) pbuf[tid] = A;
+  __syncthreads();
+  tile_epilogue(sh, pbuf, inv_avg, n_up, walk_end, g0, ng, merged, merged_f32, err,
+                reinterpret_cast<int32_t*>(pbuf + 3 * kFlatTG));
+}
+
+// The grid of k_update_flat: blocks [0, nW) are 64-group tiles, [nW, nU) tiles of
+// 1 << lw2 groups (the last one ragged), each run in XCD-aware order (xcd_tile).
+struct FlatGrid {
+  int nW, nU, lw2;
+};
+__device__ __forceinline__ void flat_tile_range(int64_t b, const FlatGrid& fg, int64_t g_begin, int64_t g_end,
+                                                int64_t* g0, int* ng, int* lw) {
+  if (b < fg.nW) {
+    *g0 = g_begin + 64 * xcd_tile(b, fg.nW);
+    *lw = 6;
+  } else {
+    *g0 = g_begin + 64 * (int64_t)fg.nW + (xcd_tile(b - fg.nW, fg.nU - fg.nW) << fg.lw2);
+    *lw = fg.lw2;
+  }
+  *ng = (int)min<int64_t>(1 << *lw, g_end - *g0);
+}
+
+// ----------------------------------------------------------------------------
 // Woven tiles (r05): the two phases of k_update_tiled in ONE barrier interval and
 // in the same instruction stream. A block of NW waves owns 64 groups (E = 192
 // values) and walks the clients in chunks of NW: wave w produces client c0 + w's
@@ -2084,6 +2277,36 @@ __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __re
   }
 }
 
+// The flat tiles (update_flat_block) on blocks [0, fg.nU); with fg.nU < gridDim.x the
+// client encode's blocks follow (the fused step), on the tile's tables as in
+// k_update_tiled_encode.
+__global__ void __launch_bounds__(256) k_update_flat(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                     const double* __restrict__ dampen, double inv_avg, int64_t n_up,
+                                                     int64_t g_begin, int64_t g_end,
+                                                     const int32_t* __restrict__ hdr_block,
+                                                     uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                     int* __restrict__ err, FlatGrid fg, EncodeJob ej) {
+  __shared__ TileShared<kFlatTG, 4, true> sh;
+  __shared__ float pbuf[3 * kFlatPass];
+  FLEET_BTRACE(0);
+  if ((int)blockIdx.x < fg.nU) {  // block-uniform
+    int64_t g0;
+    int ng, lw;
+    flat_tile_range(blockIdx.x, fg, g_begin, g_end, &g0, &ng, &lw);
+    if (ng > 0)
+      update_flat_block(sh, pbuf, blockIdx.x, g0, ng, lw, uploads, pitch, M, dampen, inv_avg, n_up, hdr_block, merged,
+                        merged_f32, err);
+  } else {
+    b64_tables_init(&sh.tab);
+    d16_table_init(&sh.dt);
+    __syncthreads();
+    const int64_t e = (int64_t)blockIdx.x - fg.nU;
+    encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                      (int)(e / ej.gx), &sh.tab, &sh.dt);
+  }
+  FLEET_BTRACE(1);
+}
+
 // The woven tiles with the next batch's client encode riding in the launch (the
 // pipelined step at CIFAR sizes): blocks [0, nU) are tiles, the rest the encode's
 // 64*NW-lane blocks on the tile's tables.
@@ -2584,10 +2807,17 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
     } else if (k == "tile") {
       if (v == "auto") o->tile = 0;
       else if (v == "classic") o->tile = 1;
+      else if (v == "flat") o->tile = 2;
       else if (v == "weave3") o->tile = 3;
       else if (v == "weave4") o->tile = 4;
       else if (v == "weave6") o->tile = 6;
       else if (v == "weave8") o->tile = 8;
+      else ok = false;
+    } else if (k == "flat_w2") {
+      if (v == "auto") o->flat_w2 = 0;
+      else if (v == "16") o->flat_w2 = 16;
+      else if (v == "32") o->flat_w2 = 32;
+      else if (v == "64") o->flat_w2 = 64;
       else ok = false;
     } else if (k == "tile_enc_rows") {
       ok = parse_int(v, 1, 4096, &o->tile_enc_rows);
@@ -2614,7 +2844,7 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
     } else if (k == "stage_pieces") {
       ok = parse_int(v, 1, 64, &o->stage_pieces);
     } else {
-      *err = "unknown plan key '" + k + "' (update, grid, tile, weave_enc, stream_enc, tile_enc_rows, tile_mix, fused, "
+      *err = "unknown plan key '" + k + "' (update, grid, tile, flat_w2, weave_enc, stream_enc, tile_enc_rows, tile_mix, fused, "
              "stage_threads, "
              "stage_pieces)";
       return -1;
@@ -2720,6 +2950,34 @@ static TileSplit tile_split(int64_t groups, const PlanOverrides& o) {
   return t;
 }
 
+// k_update_flat's grid for `groups` groups: r whole rounds of 64-group tiles over the
+// CUs, the rest in tiles of w2 = 64, 32 or 16 groups dealt round robin after them. Picks
+// the w2 that leaves the most loaded CU the fewest groups (r * 64 + ceil(n2 / CUs) * w2)
+// with every tile resident at once (r + ceil(n2 / CUs) <= kFlatSlots), the wider on a tie
+// (a narrow tile's phase 2 has fewer serial lanes); more than one round of 64-group
+// tiles when the groups do not fit one.
+static FlatGrid flat_grid(int64_t groups, const PlanOverrides& o) {
+  const int64_t cus = device_simds() / 4;
+  const int64_t r = groups / (64 * cus);
+  const int64_t rest = groups - r * 64 * cus;
+  int best = -1;
+  int64_t best_load = INT64_MAX;
+  for (int lw2 = 6; lw2 >= 4; --lw2) {
+    const int w2 = 1 << lw2;
+    if (o.flat_w2 && o.flat_w2 != w2) continue;
+    const int64_t n2 = (rest + w2 - 1) / w2, per_cu = (n2 + cus - 1) / cus;
+    if (r + per_cu > kFlatSlots && !(o.flat_w2 == w2)) continue;
+    const int64_t load = r * 64 + per_cu * w2;
+    if (load < best_load) {
+      best_load = load;
+      best = lw2;
+    }
+  }
+  if (best < 0) best = 6;  // more than a round: 64-group tiles throughout
+  const int64_t n2 = (rest + (1 << best) - 1) >> best;
+  return FlatGrid{(int)(r * cus), (int)(r * cus + n2), best};
+}
+
 // The aggregation's launch plan for a bucket (or window) of `groups` 3-value groups.
 //   pipe   -- k_update_pipe<16, 1, 5, 0>: 16-group tiles, 4 producer waves + one
 //             consumer wave (MNIST-size buckets: the serial chain is the critical path);
@@ -2731,14 +2989,15 @@ static TileSplit tile_split(int64_t groups, const PlanOverrides& o) {
 // 64-group tiles from 32 k groups (below 4 per CU they still beat 32-group tiles, whose
 // phase 2 has half the serial lanes per tile), the pipelined tiles below.
 struct UpdatePlan {
-  int kind;       // 0 stream, 1 tiled, 2 pipe, 3 woven tiles (k_update_weave<nw>)
+  int kind;       // 0 stream, 1 tiled, 2 pipe, 3 woven tiles (k_update_weave<nw>), 4 flat tiles
   int nA;         // stream: blocks of group-per-lane waves (the rest a value per lane)
   int64_t blocks; // stream / tiled / pipe grid
   TileSplit t;    // tiled
   int nw;         // woven tiles: waves per block (3 or 4)
+  FlatGrid fg;    // flat tiles
 };
 static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o) {
-  UpdatePlan p{0, 0, 0, TileSplit{-1, 0}, 0};
+  UpdatePlan p{0, 0, 0, TileSplit{-1, 0}, 0, FlatGrid{0, 0, 6}};
   if (o.update == 1) p.kind = 0;
   else if (o.update == 2) p.kind = 1;
   else if (o.update == 3) p.kind = 2;
@@ -2747,8 +3006,12 @@ static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o) {
     p.kind = 3;
     p.nw = o.tile;
   }
+  if (p.kind == 1 && o.tile == 2) p.kind = 4;
   if (p.kind == 2) {
     p.blocks = (groups + 15) / 16;
+  } else if (p.kind == 4) {
+    p.fg = flat_grid(groups, o);
+    p.blocks = p.fg.nU;
   } else if (p.kind == 3) {
     p.blocks = (groups + kWeaveTG - 1) / kWeaveTG;
   } else if (p.kind == 1) {
@@ -2779,6 +3042,7 @@ std::string update_kernel_name(int64_t groups) {
   if (p.kind == 0) snprintf(buf, sizeof buf, "k_update_mixed<256, false>");
   else if (p.kind == 2) snprintf(buf, sizeof buf, "k_update_pipe<16, 1, 5, 0>");
   else if (p.kind == 3) snprintf(buf, sizeof buf, "k_update_weave<%d>", p.nw);
+  else if (p.kind == 4) snprintf(buf, sizeof buf, "k_update_flat");
   else snprintf(buf, sizeof buf, "k_update_tiled<64, false, %d, true>", p.t.nW >= 0 ? 16 : 0);  // as rocprofv3 names it
   return buf;
 }
@@ -2790,6 +3054,11 @@ void update_plan_grid(int64_t groups, int* kind, int64_t* blocks, int64_t* n_a, 
   *n_a = p.nA;
   *n_w = p.t.nW;
   *n_n = p.t.nN;
+  if (p.kind == 4) {  // flat: n_w 64-group tiles, n_n tiles of 1 << n_a groups
+    *n_a = p.fg.lw2;
+    *n_w = p.fg.nW;
+    *n_n = p.fg.nU - p.fg.nW;
+  }
 }
 
 std::string update_encode_kernel_name(int64_t groups) {
@@ -2799,6 +3068,7 @@ std::string update_encode_kernel_name(int64_t groups) {
   if (p.kind == 0) return "k_update_encode<256>";
   if (p.kind == 1) return "k_update_tiled_encode<64>";
   if (p.kind == 3) return "k_update_weave_encode<" + std::to_string(p.nw) + ">";
+  if (p.kind == 4) return "k_update_flat";
   return "k_update_pipe<16, 1, 5, 0> (with the encode's blocks)";
 }
 
@@ -2845,6 +3115,9 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
   else if (p.kind == 3)
     launch_weave(p.nw, (unsigned)p.blocks, s, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block,
                  merged, merged_f32, d_err);
+  else if (p.kind == 4)
+    hipLaunchKernelGGL(k_update_flat, dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg,
+                       n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.fg, EncodeJob{});
   else
     hipLaunchKernelGGL((k_update_mixed<256, false>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M,
                        d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.nA,
@@ -3008,6 +3281,15 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     else if (p.nw == 6) FLEET_WEAVE_ENC_LAUNCH(6);
     else FLEET_WEAVE_ENC_LAUNCH(8);
 #undef FLEET_WEAVE_ENC_LAUNCH
+    return hipGetLastError();
+  }
+  if (p.kind == 4) {  // the flat tiles' round, then the encode's blocks (24 rows each, as below)
+    const int64_t gx = blocks_for(groups, 256);
+    const int rpb = std::min(M, o.tile_enc_rows > 0 ? o.tile_enc_rows : 24);
+    const int64_t nU = p.blocks, nE = gx * ((M + rpb - 1) / rpb);
+    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+    hipLaunchKernelGGL(k_update_flat, dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg,
+                       n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, p.fg, ej);
     return hipGetLastError();
   }
   if (p.kind == 1) {  // the wide tiles on one width, then the encode's blocks

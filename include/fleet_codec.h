@@ -502,8 +502,8 @@ int fleet_sampler_last_indices(fleet_sampler* s, int32_t* out, size_t cap, size_
 
 /* Name of the aggregation kernel fleet_update / fleet_update_device launch for
  * an upload of `len` Base64 bytes (or a group window of that many bytes), as
- * rocprofv3 names it: "k_update_mixed<256>", "k_update_tiled<64, false, TG2, true>"
- * or "k_update_pipe<16, 1, 5, 0>"; and what fleet_update_encode_device launches
+ * rocprofv3 names it: "k_update_mixed<256>", "k_update_tiled<64, false, TG2, true>",
+ * "k_update_flat" or "k_update_pipe<16, 1, 5, 0>"; and what fleet_update_encode_device launches
  * (profiling aid; thread-local storage, valid until the thread's next call). */
 const char* fleet_update_kernel(size_t len);
 const char* fleet_update_encode_kernel(size_t len);
@@ -511,14 +511,18 @@ const char* fleet_update_encode_kernel(size_t len);
  * (blocks [0, n_a) a group per lane, 256 groups each, the rest a value per lane,
  * 84 groups each), 1 tiled (n_w 64-group tiles then n_n 16-group tiles; n_w = -1:
  * one width, 64-group tiles only), 2 pipelined (16-group tiles), 3 woven tiles
- * (64 groups each); *blocks = the aggregation's grid. */
+ * (64 groups each), 4 flat tiles (n_w 64-group tiles, then n_n tiles of 1 << n_a
+ * groups, the last one ragged); *blocks = the aggregation's grid. */
 int fleet_update_plan_grid(size_t len, int* kind, int64_t* blocks, int64_t* n_a, int64_t* n_w, int64_t* n_n);
 
 /* Launch-plan overrides, process-wide (experiments, and tests that run every
  * launch variant on small inputs; results are identical under every plan). spec =
  * comma-separated key=value items: update=auto|stream|tiled|pipe, grid=auto|plain|
- * lanes (the stream grid), tile_mix=auto|off, fused=on|off (the pipelined step as
- * one launch or two), stage_threads=1..64, stage_pieces=1..64 (host staging); ""
+ * lanes (the stream grid), tile=auto|classic|flat|weave3|weave4|weave6|weave8 and
+ * flat_w2=auto|16|32|64 (the tiles' form; the flat grid's narrow width), tile_mix=auto|off,
+ * tile_enc_rows=N, weave_enc=auto|inline|blocks, stream_enc=auto|inline|blocks,
+ * fused=on|off (the pipelined step as one launch or two), stage_threads=1..64,
+ * stage_pieces=1..64 (host staging); ""
  * restores the measured default. An unknown key or value rejects the whole spec
  * (FLEET_ERR_ARG, the reason in err) and leaves the plan unchanged. The environment
  * variable FLEET_EXPERIMENTS, read once at first use, takes the same spec; no other

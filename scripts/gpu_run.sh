@@ -20,6 +20,8 @@
 #   sqk:W            the same counters over scripts/kardam_ab.py W (Kardam forms and the plain update)
 #   trace:W:N:MODE   per-wave phase trace of the tile kernels (scripts/tile_trace.py; needs
 #                    FLEET_CODEC_LIB=ab/trace.so, a FLEET_TRACE build)
+#   plans:W:N:MODE:P1|P2|..  same-process A/B of launch plans (scripts/plan_ab.py; '-' = default,
+#                    ';' between a plan's keys)
 #   env:VAR=VALUE    export VAR for the steps after it (env:VAR= unsets it), e.g.
 #                    'env:FLEET_EXPERIMENTS=update=tiled;tile=weave4' (quote the ';')
 set -u
@@ -107,6 +109,12 @@ for r in csv.DictReader(open('$O/kardam_$w/run_kernel_stats.csv')):
       TRACE_OUT="$O/bt_${W}_n${N}_${MODE}_${PL}.npy" timeout -k 10 300 python3 scripts/tile_trace.py "$W" "$N" "$MODE" \
         >> "$O/trace.txt" 2>&1 || { tail -20 "$O/trace.txt"; exit 1; }
       tail -14 "$O/trace.txt" ;;
+    plans)
+      IFS=: read -r W N MODE PL <<< "$arg"
+      IFS='|' read -r -a PA <<< "$PL"
+      timeout -k 10 600 python3 scripts/plan_ab.py "$W" "$N" "$MODE" "${PA[@]}" 2>&1 | grep -v amdgpu.ids >> "$O/plans.txt" \
+        || { tail -20 "$O/plans.txt"; exit 1; }
+      tail -$((${#PA[@]} + 1)) "$O/plans.txt" ;;
     py)
       timeout -k 10 600 python3 "$arg" > "$O/$(basename "$arg").log" 2>&1 || { tail -30 "$O/$(basename "$arg").log"; exit 1; }
       tail -40 "$O/$(basename "$arg").log" ;;

@@ -5,6 +5,7 @@ chunk by chunk, wave by wave (kernels.hip FLEET_WTRACE). Prints, per wave role, 
 cycles of each phase and of the barrier waits, so the tile's idle time shows where it is.
 
 usage: FLEET_CODEC_LIB=ab/trace.so python3 scripts/tile_trace.py WORKLOAD [N] [upd|fused]
+(ab/btrace.so, FLEET_TRACE_WAVES=0: block start / end only, at the product build's SGPR count)
 (N: rank 0's window of the workload split over N ranks, as strong_probe.py)"""
 import ctypes as C
 import os
@@ -60,6 +61,9 @@ def main():
     kern = F.update_kernel(L_loc) if mode == "upd" else F.update_encode_kernel(L_loc)
     print(f"{name} N={N} {mode} kernel={kern} groups/rank={sh.groups}", flush=True)
     waves = [w for w in range(8) if t[:, :, w, 0].any()]
+    if not waves:  # a block-only trace build (FLEET_TRACE_WAVES=0): residency alone
+        residency(bt)
+        return
     chunks = [k for k in range(64) if t[:, k, waves[0], 0].any()]
     print(f"traced tiles 64, chunks {len(chunks)} (k {chunks[0]}..{chunks[-1]}), waves {waves}")
     classic = t[:, :, :, 3].any()

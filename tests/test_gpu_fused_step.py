@@ -100,7 +100,9 @@ def test_update_encode_rejects_overlap_and_bad_text(codec):
                                          ("update=tiled,tile=weave4,weave_enc=inline", "k_update_weave_encode<4>"),
                                          ("update=tiled,tile=weave6,weave_enc=inline", "k_update_weave_encode<6>"),
                                          ("update=tiled,tile=weave8,weave_enc=inline", "k_update_weave_encode<8>"),
-                                         ("update=tiled,tile=classic", "k_update_tiled_encode<64>")])
+                                         ("update=tiled,tile=classic", "k_update_tiled_encode<64>"),
+                                         ("update=tiled,tile=flat", "k_update_flat"),
+                                         ("update=tiled,tile=flat,flat_w2=16", "k_update_flat")])
 def test_update_encode_under_plans(codec, plan, spec, kernel):
     """The pipelined step on each launch plan, forced on sizes the planner gives
     another kernel (fused=off: the two launches back to back)."""
