@@ -588,7 +588,15 @@ struct EncodeJob {
   size_t pitch;
   int64_t groups, gx;
   int rows, rpb;
+  int prio = 0;  // the encode blocks' issue priority (the tiles' fused step)
 };
+
+// s_setprio takes an immediate
+__device__ __forceinline__ void encode_prio(int p) {
+  if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p >= 3) __builtin_amdgcn_s_setprio(3);
+}
 
 
 // One lane's share of the fused update (the stream path): the values [e0, e0 + S)
@@ -2270,6 +2278,7 @@ __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __re
     b64_tables_init(&sh.tab);
     d16_table_init(&sh.dt);
     __syncthreads();
+    encode_prio(ej.prio);
     const int64_t e = (int64_t)blockIdx.x - nU;
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                       (int)(e / ej.gx), &sh.tab, &sh.dt);
@@ -2279,7 +2288,9 @@ __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __re
 
 // The flat tiles (update_flat_block) on blocks [0, fg.nU); with fg.nU < gridDim.x the
 // client encode's blocks follow (the fused step), on the tile's tables as in
-// k_update_tiled_encode.
+// k_update_tiled_encode. (The encode inside the tiles -- the fourth wave encoding the
+// tile's columns during phase 2 -- made it the critical path: 449 against 390 us on
+// cifar10_256, r05.)
 __global__ void __launch_bounds__(256) k_update_flat(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                      const double* __restrict__ dampen, double inv_avg, int64_t n_up,
                                                      int64_t g_begin, int64_t g_end,
@@ -2300,6 +2311,7 @@ __global__ void __launch_bounds__(256) k_update_flat(const uint8_t* __restrict__
     b64_tables_init(&sh.tab);
     d16_table_init(&sh.dt);
     __syncthreads();
+    encode_prio(ej.prio);
     const int64_t e = (int64_t)blockIdx.x - fg.nU;
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                       (int)(e / ej.gx), &sh.tab, &sh.dt);
@@ -2813,6 +2825,9 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
       else if (v == "weave6") o->tile = 6;
       else if (v == "weave8") o->tile = 8;
       else ok = false;
+    } else if (k == "tile_enc_prio") {
+      if (v == "auto") o->tile_enc_prio = -1;
+      else ok = parse_int(v, 0, 3, &o->tile_enc_prio);
     } else if (k == "flat_w2") {
       if (v == "auto") o->flat_w2 = 0;
       else if (v == "16") o->flat_w2 = 16;
@@ -2844,7 +2859,7 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
     } else if (k == "stage_pieces") {
       ok = parse_int(v, 1, 64, &o->stage_pieces);
     } else {
-      *err = "unknown plan key '" + k + "' (update, grid, tile, flat_w2, weave_enc, stream_enc, tile_enc_rows, tile_mix, fused, "
+      *err = "unknown plan key '" + k + "' (update, grid, tile, flat_w2, tile_enc_prio, weave_enc, stream_enc, tile_enc_rows, tile_mix, fused, "
              "stage_threads, "
              "stage_pieces)";
       return -1;
@@ -2996,7 +3011,7 @@ struct UpdatePlan {
   int nw;         // woven tiles: waves per block (3 or 4)
   FlatGrid fg;    // flat tiles
 };
-static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o) {
+static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o, bool fused = false) {
   UpdatePlan p{0, 0, 0, TileSplit{-1, 0}, 0, FlatGrid{0, 0, 6}};
   if (o.update == 1) p.kind = 0;
   else if (o.update == 2) p.kind = 1;
@@ -3006,7 +3021,11 @@ static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o) {
     p.kind = 3;
     p.nw = o.tile;
   }
-  if (p.kind == 1 && o.tile == 2) p.kind = 4;
+  // the flat tiles for the update alone; the fused step keeps the one-width 64-group tiles,
+  // whose free block slots start the encode's blocks beside them (same-process A/B, r05:
+  // the update alone 276 -> 261 us on cifar10_256, 241 -> 227 on the N = 4 window, 1133 ->
+  // 1099 on cifar100_1024; the fused step 380 against 392 on cifar10_256)
+  if (p.kind == 1 && (o.tile == 2 || (o.tile == 0 && !fused))) p.kind = 4;
   if (p.kind == 2) {
     p.blocks = (groups + 15) / 16;
   } else if (p.kind == 4) {
@@ -3063,7 +3082,7 @@ void update_plan_grid(int64_t groups, int* kind, int64_t* blocks, int64_t* n_a, 
 
 std::string update_encode_kernel_name(int64_t groups) {
   const PlanOverrides o = plan_overrides();
-  const UpdatePlan p = plan_update(groups, o);
+  const UpdatePlan p = plan_update(groups, o, true);
   if (!o.fused) return update_kernel_name(groups) + " + k_encode_f32";
   if (p.kind == 0) return "k_update_encode<256>";
   if (p.kind == 1) return "k_update_tiled_encode<64>";
@@ -3116,8 +3135,8 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
     launch_weave(p.nw, (unsigned)p.blocks, s, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block,
                  merged, merged_f32, d_err);
   else if (p.kind == 4)
-    hipLaunchKernelGGL(k_update_flat, dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg,
-                       n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.fg, EncodeJob{});
+    hipLaunchKernelGGL(k_update_flat, dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
+                       inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.fg, EncodeJob{});
   else
     hipLaunchKernelGGL((k_update_mixed<256, false>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M,
                        d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.nA,
@@ -3174,6 +3193,12 @@ __global__ void __launch_bounds__(NT) k_kardam_reduce(const double* __restrict__
   }
 }
 
+// waves per block of the Kardam pipelined form (one consumer, the rest producers)
+#ifndef FLEET_KD_NW
+#define FLEET_KD_NW 5
+#endif
+constexpr int kKdPipeNW = FLEET_KD_NW;
+
 hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                                 int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
@@ -3196,14 +3221,15 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   const unsigned blocks = (unsigned)p.blocks;
   // partial slots per client: a wave of the stream grid or a tile
   *n_waves = p.kind == 0 ? (int)blocks * 4 : (int)blocks;
-  *flag_slots = p.kind == 2 ? (int)blocks * 4 : 0;  // the pipelined form's tile flags (4 producer waves)
+  *flag_slots = p.kind == 2 ? (int)blocks * (kKdPipeNW - 1) : 0;  // the pipelined form's tile flags (per producer wave)
   *norm_parts = 1;                                   // one pair per client
   if (groups <= 0) return hipSuccess;
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
   if (p.kind == 2 && !kd_flags) return hipErrorInvalidValue;
   if (p.kind == 2) {  // the tiles, then one reduce block per client
     const KardamReduceJob kr{norms, kd_flags, kd_epoch};
-    hipLaunchKernelGGL((k_update_pipe<16, 1, 5, 0, true>), dim3((unsigned)(blocks + (unsigned)M)), dim3(64 * 5), 0, s,
+    hipLaunchKernelGGL((k_update_pipe<16, 1, kKdPipeNW, 0, true>), dim3((unsigned)(blocks + (unsigned)M)),
+                       dim3(64 * kKdPipeNW), 0, s,
                        uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
                        d_err, (int)blocks, EncodeJob{}, kd, kr);
     return hipGetLastError();
@@ -3260,7 +3286,11 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
                                 int* d_err, const float* values, size_t vpitch, uint8_t* enc_out, hipStream_t s) {
   const int64_t groups = (n_up + 2) / 3;
   const PlanOverrides o = plan_overrides();
-  const UpdatePlan p = plan_update(groups, o);
+  const UpdatePlan p = plan_update(groups, o, true);
+  // the tiles' encode blocks at issue priority 3 beside the tiles' ladder (3 -> 0) from
+  // 64 k groups, 0 below: cifar10_256 394 -> 380 us, the N = 4 window 319 -> 311,
+  // cifar100_1024 1622 -> 1593, the N = 8 window 174.5 -> 178.5 (r05 same-process A/B)
+  const int tprio = o.tile_enc_prio >= 0 ? o.tile_enc_prio : groups >= 65536 ? 3 : 0;
   if (groups == 0 || !o.fused) {
     hipError_t e = launch_update(uploads, pitch, M, d_dampen, inv_avg, n_up, 0, groups, d_hdr_block, merged, merged_f32,
                                  d_err, s);
@@ -3287,9 +3317,9 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     const int64_t gx = blocks_for(groups, 256);
     const int rpb = std::min(M, o.tile_enc_rows > 0 ? o.tile_enc_rows : 24);
     const int64_t nU = p.blocks, nE = gx * ((M + rpb - 1) / rpb);
-    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
-    hipLaunchKernelGGL(k_update_flat, dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg,
-                       n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, p.fg, ej);
+    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb, tprio};
+    hipLaunchKernelGGL(k_update_flat, dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, M, d_dampen,
+                       inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, p.fg, ej);
     return hipGetLastError();
   }
   if (p.kind == 1) {  // the wide tiles on one width, then the encode's blocks
@@ -3300,7 +3330,7 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     const int64_t gx = blocks_for(groups, 256);
     const int rpb = std::min(M, o.tile_enc_rows > 0 ? o.tile_enc_rows : 24);
     const int64_t nU = (groups + 63) / 64, nE = gx * ((M + rpb - 1) / rpb);
-    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb, tprio};
     hipLaunchKernelGGL((k_update_tiled_encode<64>), dim3((unsigned)(nU + nE)), dim3(256), 0, s, uploads, pitch, M,
                        d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)nU, ej);
     return hipGetLastError();

@@ -519,7 +519,8 @@ int fleet_update_plan_grid(size_t len, int* kind, int64_t* blocks, int64_t* n_a,
  * launch variant on small inputs; results are identical under every plan). spec =
  * comma-separated key=value items: update=auto|stream|tiled|pipe, grid=auto|plain|
  * lanes (the stream grid), tile=auto|classic|flat|weave3|weave4|weave6|weave8 and
- * flat_w2=auto|16|32|64 (the tiles' form; the flat grid's narrow width), tile_mix=auto|off,
+ * flat_w2=auto|16|32|64, tile_enc_prio=auto|0..3 (the tiles' form; the flat grid's
+ * narrow width; the tiles' fused encode blocks' issue priority), tile_mix=auto|off,
  * tile_enc_rows=N, weave_enc=auto|inline|blocks, stream_enc=auto|inline|blocks,
  * fused=on|off (the pipelined step as one launch or two), stage_threads=1..64,
  * stage_pieces=1..64 (host staging); ""

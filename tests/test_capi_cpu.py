@@ -88,7 +88,8 @@ GRID_SIZES = [1, 2, 16, 17, 83, 84, 85, 255, 256, 257, 6_667, 7_654, 16_668, 32_
 
 
 @pytest.mark.parametrize("spec", ["", "update=stream", "update=stream,grid=plain", "update=stream,grid=lanes",
-                                  "update=tiled", "update=tiled,tile_mix=off", "update=pipe",
+                                  "update=tiled", "update=tiled,tile=classic", "update=tiled,tile=classic,tile_mix=off",
+                                  "update=pipe",
                                   "update=tiled,tile=weave3", "update=tiled,tile=weave4",
                                   "update=tiled,tile=weave8", "update=tiled,tile=flat",
                                   "update=tiled,tile=flat,flat_w2=16",
@@ -132,8 +133,9 @@ def test_launch_grid_covers_every_group(spec):
             else:
                 assert b == -(-groups // 16), (groups, g)
             if spec.startswith("update="):
-                want = ("weave" if "tile=weave" in spec else "flat" if "tile=flat" in spec
-                        else spec.split(",")[0].split("=")[1])
+                want = spec.split(",")[0].split("=")[1]
+                if want == "tiled" and "tile=classic" not in spec:  # the update alone: flat tiles unless asked
+                    want = "weave" if "tile=weave" in spec else "flat"
                 assert g["kind"] == want, (spec, g)
     finally:
         F.set_plan("")

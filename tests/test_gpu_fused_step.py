@@ -102,7 +102,9 @@ def test_update_encode_rejects_overlap_and_bad_text(codec):
                                          ("update=tiled,tile=weave8,weave_enc=inline", "k_update_weave_encode<8>"),
                                          ("update=tiled,tile=classic", "k_update_tiled_encode<64>"),
                                          ("update=tiled,tile=flat", "k_update_flat"),
-                                         ("update=tiled,tile=flat,flat_w2=16", "k_update_flat")])
+                                         ("update=tiled,tile=flat,flat_w2=16", "k_update_flat"),
+                                         ("update=tiled,tile=flat,tile_enc_prio=3", "k_update_flat"),
+                                         ("update=tiled,tile_enc_prio=2", "k_update_tiled_encode<64>")])
 def test_update_encode_under_plans(codec, plan, spec, kernel):
     """The pipelined step on each launch plan, forced on sizes the planner gives
     another kernel (fused=off: the two launches back to back)."""
@@ -124,5 +126,5 @@ def test_plan_overrides_are_validated():
         assert F.plan() == ""
     with F.plan_override("update=tiled; grid=plain"):
         assert F.plan() == "update=tiled,grid=plain"
-        assert F.update_kernel(F.b64_len(LAYOUTS["mnist"].n_up)).startswith("k_update_tiled<64")
+        assert F.update_kernel(F.b64_len(LAYOUTS["mnist"].n_up)) == "k_update_flat"
     assert F.plan() == ""

@@ -327,7 +327,7 @@ def test_update_stream_grids(codec, oracle, plan, grid):
         assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
-@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile_mix=off", "update=stream",
+@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile=classic,tile_mix=off", "update=stream",
                                   "update=stream,grid=plain", "update=stream,grid=lanes",
                                   "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4",
                                   "update=tiled,tile=weave6", "update=tiled,tile=weave8", "update=tiled,tile=flat",
@@ -360,7 +360,7 @@ def test_update_two_width_tiles(codec, oracle, plan, mix):
     16-group tiles; tile_mix=off the one-width grid): 16,668 groups = one round of
     256 wide tiles + 284 groups, the last narrow tile ragged; large magnitudes force
     the in-stage fallbacks and the general-chain recompute in both tile widths."""
-    plan(f"update=tiled,tile_mix={mix}")
+    plan(f"update=tiled,tile=classic,tile_mix={mix}")
     lay = synthetic(50_003)
     hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
     rng = np.random.default_rng(11)
@@ -409,7 +409,7 @@ def test_update_flat_tiles(codec, oracle, plan, w2):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
-@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile_mix=off", "update=stream",
+@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile=classic,tile_mix=off", "update=stream",
                                   "update=stream,grid=plain", "update=stream,grid=lanes",
                                   "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4",
                                   "update=tiled,tile=weave6", "update=tiled,tile=weave8", "update=tiled,tile=flat",
@@ -427,7 +427,7 @@ def test_update_modes(codec, oracle, plan, spec):
         assert codec.update(ups, d) == oracle.update_fused(ups, d, hm), (lay.name, M)
 
 
-@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile_mix=off", "update=stream",
+@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile=classic,tile_mix=off", "update=stream",
                                   "update=stream,grid=plain", "update=stream,grid=lanes",
                                   "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4",
                                   "update=tiled,tile=weave6", "update=tiled,tile=weave8", "update=tiled,tile=flat",
