@@ -113,52 +113,6 @@ __device__ __forceinline__ void d16_table_init(D16Table* t) {
   }
 }
 
-// Pre-shifted decode tables (r05): t[i][ch] = sextet(ch) << (18 - 6i) for the four
-// chars of a quad, or bit 31 alone for a char outside the alphabet. A quad's 24 bits
-// are then the OR of four lookups (v_or3 + v_or, no shifts), and bit 31 of the OR of
-// the group's four quads flags an invalid char -- the perms below never select a
-// quad's top byte, so the flag stays out of the codes.
-struct DecTables {
-  uint32_t t[4][256];
-};
-static_assert(sizeof(DecTables) % 16 == 0, "copied as uint4");
-FLEET_HDC DecTables make_dec_tables() {
-  DecTables d{};
-  for (int i = 0; i < 4; ++i)
-    for (int ch = 0; ch < 256; ++ch) {
-      const uint8_t v = b64_from_value(ch);
-      d.t[i][ch] = v == 0xff ? 0x80000000u : (uint32_t)v << (18 - 6 * i);
-    }
-  return d;
-}
-static __constant__ DecTables g_dec_tables = make_dec_tables();
-template <int NT = 256>
-__device__ __forceinline__ void dec_tables_init(DecTables* t) {
-  constexpr int n16 = (int)(sizeof(DecTables) / 16);
-  const uint4* src = reinterpret_cast<const uint4*>(&g_dec_tables);
-  uint4* dst = reinterpret_cast<uint4*>(t);
-#pragma unroll
-  for (int i0 = 0; i0 < n16; i0 += NT) {
-    const int i = i0 + (int)threadIdx.x;
-    if (i < n16) dst[i] = src[i];
-  }
-}
-// b64_decode_group_full on the pre-shifted tables: nonzero iff a char is invalid
-__device__ __forceinline__ uint32_t b64_decode_group_full4(uint4 w, const DecTables* d, int32_t codes[3]) {
-  const uint32_t words[4] = {w.x, w.y, w.z, w.w};
-  uint32_t V[4];
-#pragma unroll
-  for (int qd = 0; qd < 4; ++qd) {
-    const uint32_t a = d->t[0][words[qd] & 0xff], b = d->t[1][(words[qd] >> 8) & 0xff];
-    const uint32_t c = d->t[2][(words[qd] >> 16) & 0xff], e = d->t[3][words[qd] >> 24];
-    V[qd] = a | b | c | e;
-  }
-  codes[0] = (int32_t)__builtin_amdgcn_perm(V[1], V[0], 0x06000102u);
-  codes[1] = (int32_t)__builtin_amdgcn_perm(V[2], V[1], 0x05060001u);
-  codes[2] = (int32_t)__builtin_amdgcn_perm(V[3], V[2], 0x04050600u);
-  return (V[0] | V[1] | V[2] | V[3]) >> 31;
-}
-
 // One 16-char group -> 12 bytes -> 3 little-endian int32 codes.
 // Returns a 16-bit mask of chars that are not in the alphabet (bit i = char i).
 __device__ __forceinline__ uint32_t b64_decode_group(uint4 w, const B64Tables* t, int32_t codes[3]) {

@@ -21,18 +21,6 @@
 #include "teacher_math.h"
 
 // Experiment switches of the stream kernels (r05 A/Bs; the defaults are the product):
-// FLEET_DEC_T = 1 decodes full groups on the pre-shifted tables (DecTables);
-// FLEET_STREAM_PF = 2 keeps two clients' rows in flight ahead of the one computed.
-#ifndef FLEET_DEC_T
-#define FLEET_DEC_T 0
-#endif
-#ifndef FLEET_STREAM_PF
-#define FLEET_STREAM_PF 1
-#endif
-// FLEET_TILE_PF = 1: the classic tiles load the next chunk's groups before the serial phase.
-#ifndef FLEET_TILE_PF
-#define FLEET_TILE_PF 0
-#endif
 // FLEET_TILE_LADDER = 0: the classic / woven tiles without the progress priority ladder.
 #ifndef FLEET_TILE_LADDER
 #define FLEET_TILE_LADDER 1
@@ -612,7 +600,7 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
                                             const int32_t* __restrict__ hdr_block, int32_t (&out)[S],
                                             uint32_t& bad, uint32_t& layout_bad, const KardamOut& kd = KardamOut{},
                                             double* __restrict__ kd_part = nullptr, size_t kd_stride = 0,
-                                            const DecTables* dect = nullptr, const EncodeJob* ej = nullptr) {
+                                            const EncodeJob* ej = nullptr) {
   static_assert(!INLE || (S == 3 && !KD), "the inline encode rides in the group-per-lane update");
   const int n_hdr = hdr_block[1];
   const int64_t walk_end = hdr_block[2];
@@ -644,11 +632,7 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   bool kd_hasp = false;
   auto client = [&](int c, const Row& cur) {
     if constexpr (S == 3) {
-#if FLEET_DEC_T
-      if (need == 0xffffu) bad |= b64_decode_group_full4(cur, dect, codes);
-#else
       if (need == 0xffffu) bad |= b64_decode_group_full(cur, &tab, codes);
-#endif
       else bad |= b64_decode_group(cur, &tab, codes) & need;
     } else {
       if (need == 0xffffu) bad |= b64_decode_pair_full(cur.x, cur.y, sel, &tab, codes[0]);
@@ -732,34 +716,6 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       client(c, cur);
     }
   }
-#if FLEET_STREAM_PF >= 2
-  // four clients per trip, two rows issued ahead of the pair being computed
-  if (!KD && !INLE && M >= 4) {
-    Row b2, b3;
-    b1 = group_of(1);
-    for (; c + 3 < M; c += 4) {
-      FLEET_CLIENT_HOOK(c, M);
-      if constexpr (LADDER > 0) {
-        if (c == (q1 & ~3)) __builtin_amdgcn_s_setprio(P1);
-        if (c == (q2 & ~3)) __builtin_amdgcn_s_setprio(P2);
-        if (c == (q3 & ~3)) __builtin_amdgcn_s_setprio(0);
-      }
-      b2 = group_of(c + 2);
-      b3 = group_of(c + 3);
-      client(c, b0);
-      client(c + 1, b1);
-      if (c + 4 < M) b0 = group_of(c + 4);
-      if (c + 5 < M) b1 = group_of(c + 5);
-      client(c + 2, b2);
-      client(c + 3, b3);
-    }
-    // 0..3 clients left; b0 / b1 hold clients c / c + 1 when they exist
-    if (c < M) client(c, b0);
-    if (c + 1 < M) client(c + 1, b1);
-    if (c + 2 < M) client(c + 2, group_of(c + 2));
-    c = M;
-  }
-#endif
   // INLE: the next batch's client encode of this lane's group, row by row with the
   // update's clients (its values loaded with the client's group, stored after it)
   typedef float f3 __attribute__((ext_vector_type(3)));
@@ -829,7 +785,7 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
                                                    float* __restrict__ merged_f32, int* __restrict__ err, int nA,
                                                    const KardamOut& kd = KardamOut{},
-                                                   const DecTables* dect = nullptr, const EncodeJob* ej = nullptr) {
+                                                   const EncodeJob* ej = nullptr) {
   uint32_t bad = 0, layout_bad = 0;
   // Kardam: this wave's partial slot of client 0; one slot per wave of the grid
   const size_t nw = (size_t)gridDim.x * (NT / 64);
@@ -839,7 +795,7 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
     const bool live = g < g_end;
     int32_t out[3];
     update_lane<3, KD, LADDER, INLE>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin,
-                                     hdr_block, out, bad, layout_bad, kd, kd_part, 2 * nw, dect, ej);
+                                     hdr_block, out, bad, layout_bad, kd, kd_part, 2 * nw, ej);
     if (!live) return;
     if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
@@ -893,16 +849,9 @@ __global__ void __launch_bounds__(NT, KD ? 6 : 1) k_update_mixed(const uint8_t* 
   __shared__ D16Table dtab;
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
-#if FLEET_DEC_T
-  __shared__ DecTables dect;
-  dec_tables_init<NT>(&dect);
-  const DecTables* dp = &dect;
-#else
-  const DecTables* dp = nullptr;
-#endif
   __syncthreads();
   update_mixed_block<NT, KD, 3>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
-                             hdr_block, merged, merged_f32, err, nA, kd, dp);
+                             hdr_block, merged, merged_f32, err, nA, kd);
 }
 
 // D16: the tile also holds the byte-table digit counts (D16Table, 9 KB), and the
@@ -1239,13 +1188,6 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
   uint32_t off_domain = 0;
   float amax = 0.f;  // narrow tiles: max |A + p| (q_lat is exact below 1e8 for any sign)
   uint32_t badacc = 0;
-#if FLEET_TILE_PF
-  // one pass per chunk (CM * TG <= 512 items): the next chunk's groups are loaded before
-  // this chunk's serial phase, so their HBM latency overlaps it
-  static_assert(CM * TG <= 512, "one pass per chunk");
-  TileItems<TG, 2> nit;
-  tile_load<TG, 2>(nit, uploads, pitch, g0, ng, 0, min(CM, M) * TG, tid, 256);
-#endif
   // Issue-priority ladder over the client loop (3 -> 0 at quarters of it), as in the
   // stream kernel: a CU's tiles are all resident at once and the oldest win issue
   // arbitration, so without it they finished one by one -- on cifar10_256 the tiles of
@@ -1265,20 +1207,11 @@ __device__ __forceinline__ void update_tiled_block(TileShared<TG, 4, D16>& sh, f
       if (k == r2) __builtin_amdgcn_s_setprio(1);
       if (k == r3) __builtin_amdgcn_s_setprio(0);
     }
-#if FLEET_TILE_PF
-    {
-      const TileItems<TG, 2> it = nit;
-      tile_compute<TG, 2, 4, KD, D16>(sh, it, M, dampen, n_up, hdr_block[2], g0, ptile, badacc, tk);
-      FLEET_TSTAMP(2);
-    }
-    if (c0 + CM < M) tile_load<TG, 2>(nit, uploads, pitch, g0, ng, c0 + CM, min(CM, M - c0 - CM) * TG, tid, 256);
-#else
     for (int base = 0; base < nitems; base += 512) {
       tile_produce<TG, 2, 4, KD>(sh, uploads, pitch, M, dampen, n_up, hdr_block[2], g0, ng, c0, nitems, base + tid,
                                  256, ptile, badacc, tk);
       if (base == 0) FLEET_TSTAMP(2);
     }
-#endif
     FLEET_WTRACE(bid, c0 / CM, 1);
     __syncthreads();
     FLEET_WTRACE(bid, c0 / CM, 2);
@@ -2179,13 +2112,6 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   __shared__ D16Table dtab;
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
-#if FLEET_DEC_T
-  __shared__ DecTables dect;
-  dec_tables_init<NT>(&dect);
-  const DecTables* dp = &dect;
-#else
-  const DecTables* dp = nullptr;
-#endif
   __syncthreads();
   // the update waves run the issue-priority ladder (3 -> 0 as they get ahead) and the
   // encode's waves run at priority 3: the HBM-bound encode issues whenever it can, the
@@ -2196,12 +2122,12 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   // 1118-1129 us, gpu_r04_a26.sh)
   if constexpr (INLE) {  // every block an update block; each lane also encodes its group's next-batch rows
     update_mixed_block<NT, false, 3, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin,
-                                           g_end, hdr_block, merged, merged_f32, err, nA, KardamOut{}, dp, &ej);
+                                           g_end, hdr_block, merged, merged_f32, err, nA, KardamOut{}, &ej);
     return;
   }
   if ((int)blockIdx.x < nU) {  // block-uniform
     update_mixed_block<NT, false, 3>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
-                                     hdr_block, merged, merged_f32, err, nA, KardamOut{}, dp);
+                                     hdr_block, merged, merged_f32, err, nA, KardamOut{});
   } else {
     const int64_t e = (int64_t)blockIdx.x - nU;
     __builtin_amdgcn_s_setprio(3);
