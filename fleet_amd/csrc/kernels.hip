@@ -1329,9 +1329,13 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
 // residency traces). One tile body (85 SGPRs, 23 KB of LDS): 7 blocks per CU.
 // A tile's (client, group) items are client-major over its W groups, 512 per pass
 // (two per thread): 512 / W whole clients per pass, so phase 2 is k_update_tiled's.
-constexpr int kFlatTG = 64;     // the widest flat tile (E = 192 values, one per phase-2 thread)
+// the widest flat tile (E = 192 values, one per phase-2 thread). 85-group tiles (six whole
+// clients per pass, a fourth phase-2 wave, 23.4 KB of LDS: 6 blocks per CU) were slower
+// everywhere: cifar10_256 update 275.5 against 268.4 us, the N = 4 window 250.3 against
+// 230.6 (r05, profiles/r05/ab_flat_width85.txt)
+constexpr int kFlatTG = 64;
 constexpr int kFlatPass = 512;  // items per pass
-constexpr int kFlatSlots = 7;   // blocks per CU (LDS 23 KB, 85 SGPRs; r05 residency traces)
+constexpr int kFlatSlots = 7;   // blocks per CU (LDS 22.6 KB, 91 SGPRs; r05 residency traces)
 
 // scalarMultiply(getDampen) for a lane's own client (dampen_stage with a per-lane d: a
 // narrow tile's wave spans 64 / W clients): the binary32 multiply when every lane's d is
@@ -1412,28 +1416,29 @@ __device__ __forceinline__ void flat_compute(TileShared<kFlatTG, 4, true>& sh, c
       for (int e = 0; e < 3; ++e) pbuf[(tid + 256 * h) * 3 + e] = p[3 * h + e];
 }
 
-// Flat tile: groups [g0, g0 + ng) on the item mapping of width W = 1 << lw (ng <= W <=
-// kFlatTG), pbuf = kFlatPass * 3 floats; `tile` its index (dev traces only).
+// Flat tile: groups [g0, g0 + ng) on the item mapping of width W (ng <= W <= kFlatTG;
+// a pass holds 512 / W whole clients), pbuf = kFlatPass * 3 floats; `tile` its index
+// (dev traces only).
 __device__ __forceinline__ void update_flat_block(TileShared<kFlatTG, 4, true>& sh, float* pbuf, int64_t tile,
-                                                  int64_t g0, int ng, int lw, const uint8_t* __restrict__ uploads,
+                                                  int64_t g0, int ng, int W, const uint8_t* __restrict__ uploads,
                                                   size_t pitch, int M, const double* __restrict__ dampen,
                                                   double inv_avg, int64_t n_up, const int32_t* __restrict__ hdr_block,
                                                   uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
                                                   int* __restrict__ err) {
   static_assert(3 * kFlatTG <= 256 && 2 * 3 * kFlatTG <= 3 * kFlatPass, "phase 2 / epilogue fit the block / pbuf");
   const int tid = threadIdx.x;
-  const int W = 1 << lw, E = 3 * W;
-  const int cpp = kFlatPass >> lw;  // whole clients per pass
+  const int E = 3 * W;
+  const int cpp = kFlatPass / W;  // whole clients per pass (items past cpp * W idle)
   const int64_t walk_end = hdr_block[2];
   tile_init(sh, hdr_block + 4, hdr_block[1], g0, ng);
   float A = 0.f;  // phase-2 value: element tid of the tile (tid < E)
   uint32_t off_domain = 0, badacc = 0;
-  // the thread's items: (client offset, group) fixed across passes (W divides 256)
+  // the thread's items: (client offset, group), the same in every pass
   int icl[2], igl[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    icl[h] = (tid + 256 * h) >> lw;
-    igl[h] = (tid + 256 * h) & (W - 1);
+    icl[h] = (tid + 256 * h) / W;
+    igl[h] = (tid + 256 * h) % W;
   }
   // the issue-priority ladder of update_tiled_block (3 -> 0 at quarters of the passes)
   const int npass = (M + cpp - 1) / cpp;
@@ -1456,7 +1461,7 @@ __device__ __forceinline__ void update_flat_block(TileShared<kFlatTG, 4, true>& 
       it.w[h] = *reinterpret_cast<const uint4*>(uploads + (size_t)it.c[h] * pitch + 16 * (g0 + it.gl[h]));
     }
     if (__ballot(it.live[0]) != 0)  // wave-uniform: only a last pass or a ragged tile has dead waves
-      flat_compute(sh, it, M, dampen, n_up, walk_end, g0, ng, lw == 6, pbuf, tid, badacc);
+      flat_compute(sh, it, M, dampen, n_up, walk_end, g0, ng, W == 64, pbuf, tid, badacc);
     FLEET_WTRACE(tile, k, 1);
     __syncthreads();
     FLEET_WTRACE(tile, k, 2);
@@ -1489,21 +1494,21 @@ __device__ __forceinline__ void update_flat_block(TileShared<kFlatTG, 4, true>& 
                 reinterpret_cast<int32_t*>(pbuf + 3 * kFlatTG));
 }
 
-// The grid of k_update_flat: blocks [0, nW) are 64-group tiles, [nW, nU) tiles of
-// 1 << lw2 groups (the last one ragged), each run in XCD-aware order (xcd_tile).
+// The grid of k_update_flat: blocks [0, nW) are tiles of w1 groups, [nW, nU) tiles of
+// w2 groups (the last one ragged), each run in XCD-aware order (xcd_tile).
 struct FlatGrid {
-  int nW, nU, lw2;
+  int nW, nU, w1, w2;
 };
 __device__ __forceinline__ void flat_tile_range(int64_t b, const FlatGrid& fg, int64_t g_begin, int64_t g_end,
-                                                int64_t* g0, int* ng, int* lw) {
+                                                int64_t* g0, int* ng, int* w) {
   if (b < fg.nW) {
-    *g0 = g_begin + 64 * xcd_tile(b, fg.nW);
-    *lw = 6;
+    *g0 = g_begin + fg.w1 * xcd_tile(b, fg.nW);
+    *w = fg.w1;
   } else {
-    *g0 = g_begin + 64 * (int64_t)fg.nW + (xcd_tile(b - fg.nW, fg.nU - fg.nW) << fg.lw2);
-    *lw = fg.lw2;
+    *g0 = g_begin + fg.w1 * (int64_t)fg.nW + fg.w2 * xcd_tile(b - fg.nW, fg.nU - fg.nW);
+    *w = fg.w2;
   }
-  *ng = (int)min<int64_t>(1 << *lw, g_end - *g0);
+  *ng = (int)min<int64_t>(*w, g_end - *g0);
 }
 
 // ----------------------------------------------------------------------------
@@ -2228,10 +2233,10 @@ __global__ void __launch_bounds__(256) k_update_flat(const uint8_t* __restrict__
   FLEET_BTRACE(0);
   if ((int)blockIdx.x < fg.nU) {  // block-uniform
     int64_t g0;
-    int ng, lw;
-    flat_tile_range(blockIdx.x, fg, g_begin, g_end, &g0, &ng, &lw);
+    int ng, w;
+    flat_tile_range(blockIdx.x, fg, g_begin, g_end, &g0, &ng, &w);
     if (ng > 0)
-      update_flat_block(sh, pbuf, blockIdx.x, g0, ng, lw, uploads, pitch, M, dampen, inv_avg, n_up, hdr_block, merged,
+      update_flat_block(sh, pbuf, blockIdx.x, g0, ng, w, uploads, pitch, M, dampen, inv_avg, n_up, hdr_block, merged,
                         merged_f32, err);
   } else {
     b64_tables_init(&sh.tab);
@@ -2756,10 +2761,7 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
       else ok = parse_int(v, 0, 3, &o->tile_enc_prio);
     } else if (k == "flat_w2") {
       if (v == "auto") o->flat_w2 = 0;
-      else if (v == "16") o->flat_w2 = 16;
-      else if (v == "32") o->flat_w2 = 32;
-      else if (v == "64") o->flat_w2 = 64;
-      else ok = false;
+      else ok = parse_int(v, 1, kFlatTG, &o->flat_w2);
     } else if (k == "tile_enc_rows") {
       ok = parse_int(v, 1, 4096, &o->tile_enc_rows);
     } else if (k == "stream_enc") {
@@ -2891,32 +2893,32 @@ static TileSplit tile_split(int64_t groups, const PlanOverrides& o) {
   return t;
 }
 
-// k_update_flat's grid for `groups` groups: r whole rounds of 64-group tiles over the
-// CUs, the rest in tiles of w2 = 64, 32 or 16 groups dealt round robin after them. Picks
-// the w2 that leaves the most loaded CU the fewest groups (r * 64 + ceil(n2 / CUs) * w2)
-// with every tile resident at once (r + ceil(n2 / CUs) <= kFlatSlots), the wider on a tie
-// (a narrow tile's phase 2 has fewer serial lanes); more than one round of 64-group
-// tiles when the groups do not fit one.
+// k_update_flat's grid for `groups` groups: r whole rounds of kFlatTG-group tiles over the
+// CUs, the rest in tiles of w2 = kFlatTG, 1/2 or 1/4 of it dealt round robin after them.
+// Picks the w2 that leaves the most loaded CU the fewest groups (r * kFlatTG +
+// ceil(n2 / CUs) * w2) with every tile resident at once (r + ceil(n2 / CUs) <= kFlatSlots),
+// the wider on a tie; more than one round of the widest tiles when the groups do not fit
+// one. (On the N = 8 window, 2.7 tiles per CU, the 16-group tiles' extra serial chains
+// also hide latency: the update 156-159 us on one width, 143 us with them; r05.)
 static FlatGrid flat_grid(int64_t groups, const PlanOverrides& o) {
-  const int64_t cus = device_simds() / 4;
-  const int64_t r = groups / (64 * cus);
-  const int64_t rest = groups - r * 64 * cus;
+  const int64_t cus = device_simds() / 4, w1 = kFlatTG;
+  const int64_t r = groups / (w1 * cus);
+  const int64_t rest = groups - r * w1 * cus;
   int best = -1;
   int64_t best_load = INT64_MAX;
-  for (int lw2 = 6; lw2 >= 4; --lw2) {
-    const int w2 = 1 << lw2;
-    if (o.flat_w2 && o.flat_w2 != w2) continue;
+  for (int k = 0; k < 3; ++k) {
+    const int w2 = o.flat_w2 ? o.flat_w2 : kFlatTG >> k;  // a forced width: that one, even past a round
     const int64_t n2 = (rest + w2 - 1) / w2, per_cu = (n2 + cus - 1) / cus;
-    if (r + per_cu > kFlatSlots && !(o.flat_w2 == w2)) continue;
-    const int64_t load = r * 64 + per_cu * w2;
+    if (r + per_cu > kFlatSlots && !o.flat_w2) continue;
+    const int64_t load = r * w1 + per_cu * w2;
     if (load < best_load) {
       best_load = load;
-      best = lw2;
+      best = w2;
     }
   }
-  if (best < 0) best = 6;  // more than a round: 64-group tiles throughout
-  const int64_t n2 = (rest + (1 << best) - 1) >> best;
-  return FlatGrid{(int)(r * cus), (int)(r * cus + n2), best};
+  if (best < 0) best = kFlatTG;  // more than a round: the widest tiles throughout
+  const int64_t n2 = (rest + best - 1) / best;
+  return FlatGrid{(int)(r * cus), (int)(r * cus + n2), kFlatTG, best};
 }
 
 // The aggregation's launch plan for a bucket (or window) of `groups` 3-value groups.
@@ -2938,7 +2940,7 @@ struct UpdatePlan {
   FlatGrid fg;    // flat tiles
 };
 static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o, bool fused = false) {
-  UpdatePlan p{0, 0, 0, TileSplit{-1, 0}, 0, FlatGrid{0, 0, 6}};
+  UpdatePlan p{0, 0, 0, TileSplit{-1, 0}, 0, FlatGrid{0, 0, kFlatTG, kFlatTG}};
   if (o.update == 1) p.kind = 0;
   else if (o.update == 2) p.kind = 1;
   else if (o.update == 3) p.kind = 2;
@@ -2947,11 +2949,12 @@ static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o, bool fused
     p.kind = 3;
     p.nw = o.tile;
   }
-  // the flat tiles for the update alone; the fused step keeps the one-width 64-group tiles,
-  // whose free block slots start the encode's blocks beside them (same-process A/B, r05:
-  // the update alone 276 -> 261 us on cifar10_256, 241 -> 227 on the N = 4 window, 1133 ->
-  // 1099 on cifar100_1024; the fused step 380 against 392 on cifar10_256)
-  if (p.kind == 1 && (o.tile == 2 || (o.tile == 0 && !fused))) p.kind = 4;
+  // the flat tiles for the update alone; the fused step keeps the one-width 64-group tiles
+  // from 64 k groups, whose free block slots start the encode's blocks beside them
+  // (same-process A/B, r05: the update alone 276 -> 261 us on cifar10_256, 241 -> 227 on
+  // the N = 4 window, 1133 -> 1099 on cifar100_1024; the fused step 380 against 392 on
+  // cifar10_256, but 170.6 against 181.4 us on the N = 8 window)
+  if (p.kind == 1 && (o.tile == 2 || (o.tile == 0 && (!fused || groups < 65536)))) p.kind = 4;
   if (p.kind == 2) {
     p.blocks = (groups + 15) / 16;
   } else if (p.kind == 4) {
@@ -2999,8 +3002,8 @@ void update_plan_grid(int64_t groups, int* kind, int64_t* blocks, int64_t* n_a, 
   *n_a = p.nA;
   *n_w = p.t.nW;
   *n_n = p.t.nN;
-  if (p.kind == 4) {  // flat: n_w 64-group tiles, n_n tiles of 1 << n_a groups
-    *n_a = p.fg.lw2;
+  if (p.kind == 4) {  // flat: n_w tiles of kFlatTG groups, n_n tiles of n_a groups
+    *n_a = p.fg.w2;
     *n_w = p.fg.nW;
     *n_n = p.fg.nU - p.fg.nW;
   }

@@ -511,7 +511,7 @@ const char* fleet_update_encode_kernel(size_t len);
  * (blocks [0, n_a) a group per lane, 256 groups each, the rest a value per lane,
  * 84 groups each), 1 tiled (n_w 64-group tiles then n_n 16-group tiles; n_w = -1:
  * one width, 64-group tiles only), 2 pipelined (16-group tiles), 3 woven tiles
- * (64 groups each), 4 flat tiles (n_w 64-group tiles, then n_n tiles of 1 << n_a
+ * (64 groups each), 4 flat tiles (n_w 64-group tiles, then n_n tiles of n_a
  * groups, the last one ragged); *blocks = the aggregation's grid. */
 int fleet_update_plan_grid(size_t len, int* kind, int64_t* blocks, int64_t* n_a, int64_t* n_w, int64_t* n_n);
 
@@ -519,7 +519,7 @@ int fleet_update_plan_grid(size_t len, int* kind, int64_t* blocks, int64_t* n_a,
  * launch variant on small inputs; results are identical under every plan). spec =
  * comma-separated key=value items: update=auto|stream|tiled|pipe, grid=auto|plain|
  * lanes (the stream grid), tile=auto|classic|flat|weave3|weave4|weave6|weave8 and
- * flat_w2=auto|16|32|64, tile_enc_prio=auto|0..3 (the tiles' form; the flat grid's
+ * flat_w2=auto|1..64, tile_enc_prio=auto|0..3 (the tiles' form; the flat grid's
  * narrow width; the tiles' fused encode blocks' issue priority), tile_mix=auto|off,
  * tile_enc_rows=N, weave_enc=auto|inline|blocks, stream_enc=auto|inline|blocks,
  * fused=on|off (the pipelined step as one launch or two), stage_threads=1..64,
