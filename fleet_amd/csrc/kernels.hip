@@ -941,14 +941,17 @@ struct TileKd {
 // Per item (one client, one group): the text Kardam.setGrad stores, G =
 // Q(f32(f64(p) * lr)), written to g_out; ||G||^2 and, with the worker's previous
 // G, ||Q(G - prev)||^2 over the flat gradient's slots (getNorm: float products
-// summed in double). A client's TG groups of the tile are TG consecutive lanes of
-// one wave (items are client-major and waves start at multiples of 64), so the
-// lane group's sum is the (client, tile) partial: one write, no atomics, a fixed
-// order (k_kardam_reduce then sums the tiles in order).
-template <int TG, int IPT, int NW, bool D16>
-__device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const TileItems<TG, IPT>& it,
-                                            const float (&p)[3 * IPT], int64_t n_up, int64_t g0, const TileKd& tk) {
-  static_assert(64 % TG == 0 && TG >= 16, "a client's groups in one lane group of 16, 32 or 64");
+// summed in double). A client's W groups of the tile are W consecutive lanes of
+// one wave (items are client-major, W in {16, 32, 64} and waves start at multiples of
+// 64), so the lane group's sum is the (client, tile) partial: one write, no atomics,
+// a fixed order (k_kardam_reduce then sums the tiles in order). Item h: client c[h]
+// and group gl[h] (live[h]: a real item), partial slot client cp[h] (cvalid[h]: that
+// client exists -- dead groups of a live client still write their lane group's zeros).
+template <int IPT, int NW, int TGS, bool D16>
+__device__ __forceinline__ void kardam_items(TileShared<TGS, NW, D16>& sh, const int (&c)[IPT], const int (&gl)[IPT],
+                                             const bool (&live)[IPT], const int (&cp)[IPT], const bool (&cvalid)[IPT],
+                                             const float (&p)[3 * IPT], int W, int64_t n_up, int64_t g0,
+                                             const TileKd& tk) {
   constexpr int S = 3 * IPT;
   const KardamOut& kd = tk.kd;
   float rg[S], G[S];
@@ -965,17 +968,16 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const T
   uint32_t flat = 0, hasps = 0;
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
-    const int c = it.c_base + it.cc[h];
-    const int64_t gp = 3 * (g0 + it.gl[h]);
-    const uint32_t hm = it.live[h] ? sh.hmask[it.gl[h]] : 7u;
-    const bool hasp = kd.prev && it.live[h] && kd.has_prev[c];
+    const int64_t gp = 3 * (g0 + gl[h]);
+    const uint32_t hm = live[h] ? sh.hmask[gl[h]] : 7u;
+    const bool hasp = kd.prev && live[h] && kd.has_prev[c[h]];
     hasps |= (uint32_t)hasp << h;
     sg[h] = 0.0;
     // prev / G rows: one 12-byte access per whole group (rows are 4-byte aligned)
-    const bool whole = it.live[h] && gp + 2 < n_up;
+    const bool whole = live[h] && gp + 2 < n_up;
     float pv[3] = {0.0f, 0.0f, 0.0f};
     if (hasp && whole) {
-      const f3u t = *reinterpret_cast<const f3u*>(kd.prev + (size_t)c * kd.vpitch + gp);
+      const f3u t = *reinterpret_cast<const f3u*>(kd.prev + (size_t)c[h] * kd.vpitch + gp);
       pv[0] = t.x;
       pv[1] = t.y;
       pv[2] = t.z;
@@ -984,22 +986,22 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const T
 #pragma unroll
     for (int e = 0; e < 3; ++e) {
       const int64_t pos = gp + e;
-      const bool f = it.live[h] && !((hm >> e) & 1u) && pos < n_up && pos < tk.walk_end;
+      const bool f = live[h] && !((hm >> e) & 1u) && pos < n_up && pos < tk.walk_end;
       flat |= (uint32_t)f << (3 * h + e);
       const float g = G[3 * h + e];
       if (f) sg[h] += (double)(g * g);
-      if (hasp && !whole && f) pv[e] = kd.prev[(size_t)c * kd.vpitch + pos];
+      if (hasp && !whole && f) pv[e] = kd.prev[(size_t)c[h] * kd.vpitch + pos];
       dv[3 * h + e] = (f && hasp) ? g - pv[e] : 0.0f;
       gv[e] = f ? g : 0.0f;
     }
     if (kd.g_out) {
-      float* go = kd.g_out + (size_t)c * kd.vpitch + gp;
+      float* go = kd.g_out + (size_t)c[h] * kd.vpitch + gp;
       if (whole) {
         *reinterpret_cast<f3u*>(go) = f3u{gv[0], gv[1], gv[2]};
       } else {
 #pragma unroll
         for (int e = 0; e < 3; ++e)
-          if (it.live[h] && gp + e < n_up) go[e] = gv[e];
+          if (live[h] && gp + e < n_up) go[e] = gv[e];
       }
     }
   }
@@ -1011,14 +1013,38 @@ __device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const T
 #pragma unroll
     for (int e = 0; e < 3; ++e)
       if (((flat >> (3 * h + e)) & 1u) && ((hasps >> h) & 1u)) sd[h] += (double)(D[3 * h + e] * D[3 * h + e]);
-    const double a = group_sum_f64<TG>(sg[h]), b = group_sum_f64<TG>(sd[h]);
-    if (it.cvalid[h] && (threadIdx.x & (TG - 1)) == TG - 1) {  // the group's last lane: its client's tile sum
-      const size_t slot = ((size_t)(it.c_base + it.cl[h]) * tk.ntiles + tk.tile) * 2;
+    double a, b;  // W is block-uniform: one branch per item
+    if (W == 64) {
+      a = group_sum_f64<64>(sg[h]);
+      b = group_sum_f64<64>(sd[h]);
+    } else if (W == 32) {
+      a = group_sum_f64<32>(sg[h]);
+      b = group_sum_f64<32>(sd[h]);
+    } else {
+      a = group_sum_f64<16>(sg[h]);
+      b = group_sum_f64<16>(sd[h]);
+    }
+    if (cvalid[h] && (threadIdx.x & (W - 1)) == W - 1) {  // the group's last lane: its client's tile sum
+      const size_t slot = ((size_t)cp[h] * tk.ntiles + tk.tile) * 2;
       // sc1: the pipelined form's reduce blocks read them in the same launch
       __hip_atomic_store(kd.partials + slot, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(kd.partials + slot + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+}
+
+// kardam_items over a tile producer's TileItems (the classic and pipelined tiles)
+template <int TG, int IPT, int NW, bool D16>
+__device__ __forceinline__ void tile_kardam(TileShared<TG, NW, D16>& sh, const TileItems<TG, IPT>& it,
+                                            const float (&p)[3 * IPT], int64_t n_up, int64_t g0, const TileKd& tk) {
+  static_assert(64 % TG == 0 && TG >= 16, "a client's groups in one lane group of 16, 32 or 64");
+  int c[IPT], cp[IPT];
+#pragma unroll
+  for (int h = 0; h < IPT; ++h) {
+    c[h] = it.c_base + it.cc[h];
+    cp[h] = it.c_base + it.cl[h];
+  }
+  kardam_items<IPT, NW>(sh, c, it.gl, it.live, cp, it.cvalid, p, TG, n_up, g0, tk);
 }
 
 template <int TG, int IPT, int NW, bool KD = false, bool D16 = false>
@@ -1360,14 +1386,18 @@ struct FlatItems {
   uint4 w[2];
   int c[2], gl[2];
   bool live[2];
+  bool cvalid[2];  // the item's client exists (its group may be past the tile's last)
 };
 
 // p of the thread's two items -> pbuf[item * 3 + e]: tile_compute's stages
-// (CppNNUpdater.java:463-464). W64: a wave's items are one client (wave-uniform d).
+// (CppNNUpdater.java:463-464). W = 64: a wave's items are one client (wave-uniform d).
+// KD: Kardam's side outputs with p (kardam_items; W in {16, 32, 64}).
+template <bool KD = false>
 __device__ __forceinline__ void flat_compute(TileShared<kFlatTG, 4, true>& sh, const FlatItems& it, int M,
                                              const double* __restrict__ dampen, int64_t n_up, int64_t walk_end,
-                                             int64_t g0, int ng, bool W64, float* __restrict__ pbuf, int tid,
-                                             uint32_t& badacc) {
+                                             int64_t g0, int ng, int W, float* __restrict__ pbuf, int tid,
+                                             uint32_t& badacc, const TileKd& tk) {
+  const bool W64 = W == 64;
   int32_t codes[6];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -1414,17 +1444,19 @@ __device__ __forceinline__ void flat_compute(TileShared<kFlatTG, 4, true>& sh, c
     if (it.live[h])
 #pragma unroll
       for (int e = 0; e < 3; ++e) pbuf[(tid + 256 * h) * 3 + e] = p[3 * h + e];
+  if constexpr (KD) kardam_items<2, 4>(sh, it.c, it.gl, it.live, it.c, it.cvalid, p, W, n_up, g0, tk);
 }
 
 // Flat tile: groups [g0, g0 + ng) on the item mapping of width W (ng <= W <= kFlatTG;
 // a pass holds 512 / W whole clients), pbuf = kFlatPass * 3 floats; `tile` its index
-// (dev traces only).
+// (Kardam's partial slot; dev traces). KD: Kardam's side outputs (flat_compute).
+template <bool KD = false>
 __device__ __forceinline__ void update_flat_block(TileShared<kFlatTG, 4, true>& sh, float* pbuf, int64_t tile,
                                                   int64_t g0, int ng, int W, const uint8_t* __restrict__ uploads,
                                                   size_t pitch, int M, const double* __restrict__ dampen,
                                                   double inv_avg, int64_t n_up, const int32_t* __restrict__ hdr_block,
                                                   uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                  int* __restrict__ err) {
+                                                  int* __restrict__ err, const TileKd& tk = TileKd{}) {
   static_assert(3 * kFlatTG <= 256 && 2 * 3 * kFlatTG <= 3 * kFlatPass, "phase 2 / epilogue fit the block / pbuf");
   const int tid = threadIdx.x;
   const int E = 3 * W;
@@ -1456,12 +1488,13 @@ __device__ __forceinline__ void update_flat_block(TileShared<kFlatTG, 4, true>& 
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       it.live[h] = icl[h] < cm && igl[h] < ng;
+      it.cvalid[h] = icl[h] < cm;
       it.c[h] = c0 + (icl[h] < cm ? icl[h] : 0);
       it.gl[h] = it.live[h] ? igl[h] : 0;
       it.w[h] = *reinterpret_cast<const uint4*>(uploads + (size_t)it.c[h] * pitch + 16 * (g0 + it.gl[h]));
     }
     if (__ballot(it.live[0]) != 0)  // wave-uniform: only a last pass or a ragged tile has dead waves
-      flat_compute(sh, it, M, dampen, n_up, walk_end, g0, ng, W == 64, pbuf, tid, badacc);
+      flat_compute<KD>(sh, it, M, dampen, n_up, walk_end, g0, ng, W, pbuf, tid, badacc, tk);
     FLEET_WTRACE(tile, k, 1);
     __syncthreads();
     FLEET_WTRACE(tile, k, 2);
@@ -2222,12 +2255,13 @@ __global__ void __launch_bounds__(256) k_update_tiled_encode(const uint8_t* __re
 // k_update_tiled_encode. (The encode inside the tiles -- the fourth wave encoding the
 // tile's columns during phase 2 -- made it the critical path: 449 against 390 us on
 // cifar10_256, r05.)
-__global__ void __launch_bounds__(256) k_update_flat(const uint8_t* __restrict__ uploads, size_t pitch, int M,
-                                                     const double* __restrict__ dampen, double inv_avg, int64_t n_up,
-                                                     int64_t g_begin, int64_t g_end,
-                                                     const int32_t* __restrict__ hdr_block,
-                                                     uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                     int* __restrict__ err, FlatGrid fg, EncodeJob ej) {
+template <bool KD>
+__device__ __forceinline__ void flat_kernel(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                            const double* __restrict__ dampen, double inv_avg, int64_t n_up,
+                                            int64_t g_begin, int64_t g_end, const int32_t* __restrict__ hdr_block,
+                                            uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                            int* __restrict__ err, const FlatGrid& fg, const EncodeJob& ej,
+                                            const KardamOut& kd) {
   __shared__ TileShared<kFlatTG, 4, true> sh;
   __shared__ float pbuf[3 * kFlatPass];
   FLEET_BTRACE(0);
@@ -2235,10 +2269,12 @@ __global__ void __launch_bounds__(256) k_update_flat(const uint8_t* __restrict__
     int64_t g0;
     int ng, w;
     flat_tile_range(blockIdx.x, fg, g_begin, g_end, &g0, &ng, &w);
-    if (ng > 0)
-      update_flat_block(sh, pbuf, blockIdx.x, g0, ng, w, uploads, pitch, M, dampen, inv_avg, n_up, hdr_block, merged,
-                        merged_f32, err);
-  } else {
+    // every tile writes its partial slots (Kardam), an empty one too
+    if (KD || ng > 0)
+      update_flat_block<KD>(sh, pbuf, blockIdx.x, g0, max(ng, 0), w, uploads, pitch, M, dampen, inv_avg, n_up,
+                            hdr_block, merged, merged_f32, err,
+                            TileKd{kd, (int64_t)blockIdx.x, (int64_t)fg.nU, (int64_t)hdr_block[2]});
+  } else if constexpr (!KD) {
     b64_tables_init(&sh.tab);
     d16_table_init(&sh.dt);
     __syncthreads();
@@ -2248,6 +2284,27 @@ __global__ void __launch_bounds__(256) k_update_flat(const uint8_t* __restrict__
                       (int)(e / ej.gx), &sh.tab, &sh.dt);
   }
   FLEET_BTRACE(1);
+}
+
+__global__ void __launch_bounds__(256) k_update_flat(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                     const double* __restrict__ dampen, double inv_avg, int64_t n_up,
+                                                     int64_t g_begin, int64_t g_end,
+                                                     const int32_t* __restrict__ hdr_block,
+                                                     uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                     int* __restrict__ err, FlatGrid fg, EncodeJob ej) {
+  flat_kernel<false>(uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged, merged_f32, err, fg,
+                     ej, KardamOut{});
+}
+
+// The flat tiles with Kardam's side outputs (their partials summed by k_kardam_reduce)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(84), amdgpu_num_vgpr(72))) k_update_flat_kd(const uint8_t* __restrict__ uploads, size_t pitch, int M,
+                                                        const double* __restrict__ dampen, double inv_avg,
+                                                        int64_t n_up, int64_t g_begin, int64_t g_end,
+                                                        const int32_t* __restrict__ hdr_block,
+                                                        uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
+                                                        int* __restrict__ err, FlatGrid fg, KardamOut kd) {
+  flat_kernel<true>(uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged, merged_f32, err, fg,
+                    EncodeJob{}, kd);
 }
 
 // The woven tiles with the next batch's client encode riding in the launch (the
@@ -3138,7 +3195,10 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   // from the producers, the reduce blocks in the same launch), the wide tiles (side
   // outputs from the tile producers), or the stream kernel's SIMD-balanced grid
   PlanOverrides ok = o;
-  ok.tile = 1;  // Kardam's side outputs ride in the classic tiles (tile_kardam)
+  // Kardam's side outputs ride in the flat tiles (kardam_items: narrow widths 16 / 32 /
+  // 64 only) or, when asked for, the classic tiles; not in the woven ones
+  const bool flat_ok = o.flat_w2 == 0 || o.flat_w2 == 16 || o.flat_w2 == 32 || o.flat_w2 == 64;
+  ok.tile = (o.tile == 1 || !flat_ok) ? 1 : 2;
   UpdatePlan p = plan_update(groups, ok);
   if (p.kind == 0 && o.grid == 0) {
     // the stream form on the plain grid unless a grid is asked for: value-per-lane waves
@@ -3163,7 +3223,10 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
                        d_err, (int)blocks, EncodeJob{}, kd, kr);
     return hipGetLastError();
   }
-  if (p.kind == 1)
+  if (p.kind == 4)
+    hipLaunchKernelGGL(k_update_flat_kd, dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
+                       g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.fg, kd);
+  else if (p.kind == 1)
     launch_tiled<true>(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
                        d_err, kd, s);
   else
