@@ -57,7 +57,7 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
                                 uint32_t kd_epoch, const PlanOverrides& o, hipStream_t s);
 // Launch-plan overrides: experiments, and the tests that run every launch variant on
 // small inputs. Process-wide; set by fleet_set_plan (spec "key=value,..." -- update=
-// auto|stream|tiled|pipe, grid=auto|plain|lanes, tile_mix=auto|off, fused=on|off,
+// auto|stream|tiled|pipe, grid=auto|plain|lanes|balanced, tile_mix=auto|off, fused=on|off,
 // stage_threads=N, stage_pieces=N, tile=auto|classic|flat|weave3|4|6|8, flat_w2=auto|N,
 // tile_enc_prio=auto|0..3,
 // weave_enc=auto|inline|blocks, stream_enc=auto|inline|blocks, tile_enc_rows=N) or, once at first

@@ -2803,6 +2803,7 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
       if (v == "auto") o->grid = 0;
       else if (v == "plain") o->grid = 1;
       else if (v == "lanes") o->grid = 2;
+      else if (v == "balanced") o->grid = 3;
       else ok = false;
     } else if (k == "tile") {
       if (v == "auto") o->tile = 0;
@@ -3347,8 +3348,19 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   // 24, and 48 no better (r04 call a31, a32.sh).
   // (grid=lanes: the update's blocks a value per lane, for experiments on small windows)
   const int64_t gx = blocks_for(groups, 256);
+  // (grid=balanced: the update alone's SIMD-balanced split, whole rounds of group-per-lane
+  // waves and the rest a value per lane, under the encode's blocks too)
   const bool lanes = o.grid == 2;
-  const int nAf = lanes ? 0 : (int)gx, nUf = lanes ? (int)((groups + 83) / 84) : (int)gx;
+  int nAf = lanes ? 0 : (int)gx, nUf = lanes ? (int)((groups + 83) / 84) : (int)gx;
+  if (o.grid == 3) {
+    PlanOverrides ob = o;
+    ob.grid = 0;
+    const UpdatePlan pb = plan_update(groups, ob);
+    if (pb.kind == 0) {
+      nAf = pb.nA;
+      nUf = (int)pb.blocks;
+    }
+  }
   const int rpb = std::min(M, 24);
   const int64_t nE = gx * ((M + rpb - 1) / rpb);
   const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};

@@ -517,7 +517,7 @@ int fleet_update_plan_grid(size_t len, int* kind, int64_t* blocks, int64_t* n_a,
 
 /* Launch-plan overrides, process-wide (experiments, and tests that run every
  * launch variant on small inputs; results are identical under every plan). spec =
- * comma-separated key=value items: update=auto|stream|tiled|pipe, grid=auto|plain|
+ * comma-separated key=value items: update=auto|stream|tiled|pipe, grid=auto|plain|balanced|
  * lanes (the stream grid), tile=auto|classic|flat|weave3|weave4|weave6|weave8 and
  * flat_w2=auto|1..64, tile_enc_prio=auto|0..3 (the tiles' form; the flat grid's
  * narrow width; the tiles' fused encode blocks' issue priority), tile_mix=auto|off,

@@ -13,9 +13,14 @@ import os
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# the newest round that committed a headline line together with its kernel trace
-PROF = sorted(os.path.dirname(p) for p in glob.glob(os.path.join(ROOT, "profiles", "r*", "bench_default.json"))
-              if os.path.exists(os.path.join(os.path.dirname(p), "synth1m_256_kernel_stats.csv")))[-1]
+
+
+def _newest_round():
+    """The newest round that committed a headline line together with its kernel trace
+    (None where the CSVs do not travel, e.g. a GPU box's snapshot)."""
+    rounds = sorted(os.path.dirname(p) for p in glob.glob(os.path.join(ROOT, "profiles", "r*", "bench_default.json"))
+                    if os.path.exists(os.path.join(os.path.dirname(p), "synth1m_256_kernel_stats.csv")))
+    return rounds[-1] if rounds else None
 
 
 def _kernel_avg_ns(stats_csv, kernel):
@@ -32,6 +37,9 @@ def _kernel_avg_ns(stats_csv, kernel):
 
 @pytest.mark.parametrize("line", ["bench_default.json"])
 def test_headline_roofline_matches_profile(line):
+    PROF = _newest_round()
+    if PROF is None:
+        pytest.skip("no committed profile round with its kernel trace here")
     path = os.path.join(PROF, line)
     d = json.loads(open(path).read().strip().splitlines()[-1])
     assert d["config"]["workload"] == "synth1m_256"
