@@ -3351,8 +3351,9 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   // Below four waves of group-per-lane update per SIMD (the N = 2 strong window: 2.7) the
   // update alone's SIMD-balanced split -- whole rounds of group-per-lane waves, the rest a
   // value per lane -- also under the encode's blocks (grid=balanced): synth1m_256's N = 2
-  // window 635.3 -> 604.3 us, while the full width (5.3 waves per SIMD) loses with it,
-  // 1106.6 -> 1159.8 us (r05 same-process A/B, profiles/r05/ab_fused_balanced.txt)
+  // window 635.3 -> 604.3 us, configs[4]'s N = 8 window 11.09 -> 10.05 ms, while the full
+  // width (5.3 waves per SIMD) loses with it, 1106.6 -> 1159.8 us; one group-per-lane round
+  // fewer loses at N = 2 (624.0 us) (r05 same-process A/B, profiles/r05/ab_fused_balanced.txt)
   const bool lanes = o.grid == 2;
   int nAf = lanes ? 0 : (int)gx, nUf = lanes ? (int)((groups + 83) / 84) : (int)gx;
   if (o.grid == 3 || (o.grid == 0 && groups < 4LL * 64 * device_simds())) {
