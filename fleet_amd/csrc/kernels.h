@@ -71,7 +71,7 @@ struct PlanOverrides {
   int tile_enc_prio = -1; // tiled / flat fused step: the encode blocks' issue priority (-1 auto)
   int weave_enc = 0;      // woven fused step: 0 auto, 1 encode inside the tiles (light waves), 2 encode blocks
   int stream_enc = 0;     // stream fused step: 0 auto, 1 encode inside the update lanes, 2 encode blocks
-  int tile_enc_rows = 0;  // tiled fused step: rows per encode block (0 auto: 24)
+  int tile_enc_rows = 0;  // fused steps (tiles and stream): rows per encode block (0 auto: 24)
   int tile_mix = 0;       // 0 auto (two widths when a partial round of tiles remains), 1 one width
   int fused = 1;          // 0: the pipelined step as two launches (update, then encode)
   int stage_threads = 0;  // host staging copy threads (0 auto)
