@@ -1360,9 +1360,6 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
 // everywhere: cifar10_256 update 275.5 against 268.4 us, the N = 4 window 250.3 against
 // 230.6 (r05, profiles/r05/ab_flat_width85.txt)
 constexpr int kFlatTG = 64;
-#ifndef FLEET_FLAT_P2COST
-#define FLEET_FLAT_P2COST 0
-#endif
 constexpr int kFlatPass = 512;  // items per pass
 constexpr int kFlatSlots = 7;   // blocks per CU (LDS 22.6 KB, 91 SGPRs; r05 residency traces)
 
@@ -1511,15 +1508,9 @@ __device__ __forceinline__ void update_flat_block(TileShared<kFlatTG, 4, true>& 
 #pragma unroll 2
       for (; j < cm; ++j) {
         const float s = A + pbuf[j * E + tid];
-#if FLEET_FLAT_P2COST == 1  // dev timing only (wrong results): phase 2 without the Q
-        A = s;
-#elif FLEET_FLAT_P2COST == 2  // dev timing only (wrong results): phase 2 without the digit-count lookup
-        A = q_d16(s, 16u * (f2u(s) & 7u), &sh.dt.st);
-#else
         const uint32_t e = var_d16(f2u(s), sh.tab.var);
         off_domain |= (uint32_t)(e >= kD16Out);
         A = q_d16(s, e, &sh.dt.st);
-#endif
       }
     }
     FLEET_WTRACE(tile, k, 3);
