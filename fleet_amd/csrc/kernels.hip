@@ -2958,13 +2958,15 @@ static TileSplit tile_split(int64_t groups, const PlanOverrides& o) {
 // the wider on a tie; more than one round of the widest tiles when the groups do not fit
 // one. (On the N = 8 window, 2.7 tiles per CU, the 16-group tiles' extra serial chains
 // also hide latency: the update 156-159 us on one width, 143 us with them; r05.)
-static FlatGrid flat_grid(int64_t groups, const PlanOverrides& o) {
+static FlatGrid flat_grid(int64_t groups, const PlanOverrides& o, bool fused) {
   const int64_t cus = device_simds() / 4, w1 = kFlatTG;
   const int64_t r = groups / (w1 * cus);
   const int64_t rest = groups - r * w1 * cus;
   int best = -1;
   int64_t best_load = INT64_MAX;
-  for (int k = 0; k < 3; ++k) {
+  // the fused step: no quarter-width tiles (their extra blocks take the slots the encode's
+  // blocks would start in; the N = 8 window 175.4 -> 173.1 us with half-width ones, r05)
+  for (int k = 0; k < (fused ? 2 : 3); ++k) {
     const int w2 = o.flat_w2 ? o.flat_w2 : kFlatTG >> k;  // a forced width: that one, even past a round
     const int64_t n2 = (rest + w2 - 1) / w2, per_cu = (n2 + cus - 1) / cus;
     if (r + per_cu > kFlatSlots && !o.flat_w2) continue;
@@ -3016,7 +3018,7 @@ static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o, bool fused
   if (p.kind == 2) {
     p.blocks = (groups + 15) / 16;
   } else if (p.kind == 4) {
-    p.fg = flat_grid(groups, o);
+    p.fg = flat_grid(groups, o, fused);
     p.blocks = p.fg.nU;
   } else if (p.kind == 3) {
     p.blocks = (groups + kWeaveTG - 1) / kWeaveTG;
