@@ -1344,24 +1344,25 @@ __global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict_
 
 // ----------------------------------------------------------------------------
 // Flat tiles (r05): k_update_tiled's two phases with the tile width W a runtime
-// value (16, 32 or 64 groups), so one launch deals the groups out as ONE round over
-// the CUs' block slots: whole rounds of 64-group tiles, then the rest in tiles of the
-// width that leaves the most loaded CU the least work. cifar10_256 (104,623 groups,
-// 256 CUs, 7 slots per CU): 1,536 64-group tiles + 198 32-group tiles, at most
-// 6 x 64 + 32 = 416 groups on a CU, where the one-width grid put 7 x 64 = 448 on most
-// CUs and the compile-time two-width grid (two inlined tile bodies: 106 SGPRs, 6
-// blocks per CU) ran its 16-group tiles as a second round -- either way the kernel
-// took as long as its most loaded CU (317-320 us against a 252 us first round, r05
-// residency traces). One tile body (85 SGPRs, 23 KB of LDS): 7 blocks per CU.
-// A tile's (client, group) items are client-major over its W groups, 512 per pass
-// (two per thread): 512 / W whole clients per pass, so phase 2 is k_update_tiled's.
-// the widest flat tile (E = 192 values, one per phase-2 thread). 85-group tiles (six whole
-// clients per pass, a fourth phase-2 wave, 23.4 KB of LDS: 6 blocks per CU) were slower
-// everywhere: cifar10_256 update 275.5 against 268.4 us, the N = 4 window 250.3 against
-// 230.6 (r05, profiles/r05/ab_flat_width85.txt)
+// value (up to 64 groups; the planner uses 64, 32 and 16), so one launch deals the
+// groups out as ONE round over the CUs' block slots: whole rounds of 64-group tiles,
+// then the rest in tiles of the width that leaves the most loaded CU the least work.
+// cifar10_256 (104,623 groups, 256 CUs, 7 slots per CU): 1,536 64-group tiles + 198
+// 32-group tiles, at most 6 x 64 + 32 = 416 groups on a CU, where the one-width grid
+// put 7 x 64 = 448 on most CUs and the compile-time two-width grid (two inlined tile
+// bodies: 106 SGPRs, 6 blocks per CU) ran its 16-group tiles as a second round --
+// either way the kernel took as long as its most loaded CU (317-320 us against a
+// 252 us first round, r05 residency traces). One tile body (92 SGPRs, 22.6 KB of
+// LDS): 7 blocks per CU. A tile's (client, group) items are client-major over its W
+// groups, 512 per pass (two per thread): floor(512 / W) whole clients per pass, so
+// phase 2 is k_update_tiled's.
+// The widest flat tile: E = 192 values, one per phase-2 thread. 85-group tiles (six
+// whole clients per pass, a fourth phase-2 wave, 23.4 KB of LDS: 6 blocks per CU) were
+// slower everywhere: cifar10_256 update 275.5 against 268.4 us, the N = 4 window 250.3
+// against 230.6 (r05, profiles/r05/ab_flat_width85.txt).
 constexpr int kFlatTG = 64;
 constexpr int kFlatPass = 512;  // items per pass
-constexpr int kFlatSlots = 7;   // blocks per CU (LDS 22.6 KB, 91 SGPRs; r05 residency traces)
+constexpr int kFlatSlots = 7;   // blocks per CU (LDS 22.6 KB, 92 SGPRs; r05 residency traces)
 
 // scalarMultiply(getDampen) for a lane's own client (dampen_stage with a per-lane d: a
 // narrow tile's wave spans 64 / W clients): the binary32 multiply when every lane's d is

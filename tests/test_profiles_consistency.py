@@ -9,6 +9,7 @@ import csv
 import glob
 import json
 import os
+import re
 
 import pytest
 
@@ -23,14 +24,18 @@ def _newest_round():
     return rounds[-1] if rounds else None
 
 
+def _canon(name):
+    """A kernel name without spaces and with default trailing template arguments dropped
+    (rocprofv3 spells k_update_encode<256, false> where the bench says k_update_encode<256>)."""
+    return re.sub(r"(,false)?(,0)?(,256)?>$", ">", re.sub(r"\s+", "", name))
+
+
 def _kernel_avg_ns(stats_csv, kernel):
-    # rocprofv3 spells the template argument and the full signature; match on the
-    # kernel's name with its template arguments
-    name, _, targs = kernel.partition("<")
+    # rocprofv3 spells the full signature: compare the name with its template arguments
     with open(stats_csv, newline="") as f:
         for row in csv.DictReader(f):
-            n = row["Name"]
-            if f"fleet::{name}<{targs}" in n if targs else f"fleet::{name}(" in n:
+            n = row["Name"].split("(")[0].replace("void ", "").replace("fleet::", "")
+            if _canon(n) == _canon(kernel):
                 return float(row["AverageNs"])
     raise KeyError(kernel)
 
