@@ -3049,7 +3049,7 @@ std::string update_kernel_name(int64_t groups) {
   const UpdatePlan p = plan_update(groups, plan_overrides());
   char buf[64];
   if (p.kind == 0) snprintf(buf, sizeof buf, "k_update_mixed<256, false>");
-  else if (p.kind == 2) snprintf(buf, sizeof buf, "k_update_pipe<16, 1, 5, 0>");
+  else if (p.kind == 2) snprintf(buf, sizeof buf, "k_update_pipe<16, 1, 5, 0, false>");
   else if (p.kind == 3) snprintf(buf, sizeof buf, "k_update_weave<%d>", p.nw);
   else if (p.kind == 4) snprintf(buf, sizeof buf, "k_update_flat");
   else snprintf(buf, sizeof buf, "k_update_tiled<64, false, %d, true>", p.t.nW >= 0 ? 16 : 0);  // as rocprofv3 names it
@@ -3074,11 +3074,11 @@ std::string update_encode_kernel_name(int64_t groups) {
   const PlanOverrides o = plan_overrides();
   const UpdatePlan p = plan_update(groups, o, true);
   if (!o.fused) return update_kernel_name(groups) + " + k_encode_f32";
-  if (p.kind == 0) return "k_update_encode<256>";
+  if (p.kind == 0) return o.stream_enc == 1 && o.grid != 2 ? "k_update_encode<256, true>" : "k_update_encode<256, false>";
   if (p.kind == 1) return "k_update_tiled_encode<64>";
   if (p.kind == 3) return "k_update_weave_encode<" + std::to_string(p.nw) + ">";
   if (p.kind == 4) return "k_update_flat";
-  return "k_update_pipe<16, 1, 5, 0> (with the encode's blocks)";
+  return "k_update_pipe<16, 1, 5, 0, false> (with the encode's blocks)";
 }
 
 // k_update_tiled on the plan's grid; KD: with Kardam's side outputs.

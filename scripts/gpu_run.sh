@@ -14,6 +14,7 @@
 #   ab               scripts/gpu_ab_multi.sh (LIBS, WORKLOADS, REPS from the environment)
 #   kardam[:W,..]    Kardam side outputs vs the plain update (scripts/kardam_ab.py under rocprofv3)
 #   py:FILE          python3 FILE (a probe script), output in $TAG/FILE.log
+#   pyargs:FILE|A|B  python3 FILE A B (arguments split at '|'), appended to $TAG/FILE.log
 #   pytest:EXPR      pytest -m gpu -k EXPR (a subset), output in $TAG/pytest.log
 #   sq:W:N:MODE      SQ counters (8) + GRBM_GUI_ACTIVE + kernel trace of strong_probe.py W N MODE
 #                    (rank 0's window at N ranks; MODE fused | upd | enc), per-kernel summary
@@ -115,6 +116,11 @@ for r in csv.DictReader(open('$O/kardam_$w/run_kernel_stats.csv')):
       timeout -k 10 600 python3 scripts/plan_ab.py "$W" "$N" "$MODE" "${PA[@]}" 2>&1 | grep -v amdgpu.ids >> "$O/plans.txt" \
         || { tail -20 "$O/plans.txt"; exit 1; }
       tail -$((${#PA[@]} + 1)) "$O/plans.txt" ;;
+    pyargs)
+      IFS='|' read -r -a PA <<< "$arg"
+      timeout -k 10 600 python3 "${PA[@]}" 2>&1 | grep -v amdgpu.ids >> "$O/$(basename "${PA[0]}").log" \
+        || { tail -30 "$O/$(basename "${PA[0]}").log"; exit 1; }
+      tail -12 "$O/$(basename "${PA[0]}").log" ;;
     py)
       timeout -k 10 600 python3 "$arg" > "$O/$(basename "$arg").log" 2>&1 || { tail -30 "$O/$(basename "$arg").log"; exit 1; }
       tail -40 "$O/$(basename "$arg").log" ;;
