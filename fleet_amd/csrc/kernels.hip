@@ -2966,13 +2966,15 @@ static FlatGrid flat_grid(int64_t groups, const PlanOverrides& o, bool fused) {
   int best = -1;
   int64_t best_load = INT64_MAX;
   // the fused step: no quarter-width tiles (their extra blocks take the slots the encode's
-  // blocks would start in; the N = 8 window 175.4 -> 173.1 us with half-width ones, r05)
+  // blocks would start in) and half-width ones on a tie (the N = 8 window, 192 groups per
+  // CU either way: 175.4 us with quarter-width, 173.1 / 176.6 with half-width against
+  // 182.3 with full-width narrow tiles; r05 same-process A/Bs)
   for (int k = 0; k < (fused ? 2 : 3); ++k) {
     const int w2 = o.flat_w2 ? o.flat_w2 : kFlatTG >> k;  // a forced width: that one, even past a round
     const int64_t n2 = (rest + w2 - 1) / w2, per_cu = (n2 + cus - 1) / cus;
     if (r + per_cu > kFlatSlots && !o.flat_w2) continue;
     const int64_t load = r * w1 + per_cu * w2;
-    if (load < best_load) {
+    if (load < best_load || (fused && load == best_load)) {  // the fused step: the narrower on a tie
       best_load = load;
       best = w2;
     }
