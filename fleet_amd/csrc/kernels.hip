@@ -3007,7 +3007,14 @@ static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o, bool fused
   if (o.update == 1) p.kind = 0;
   else if (o.update == 2) p.kind = 1;
   else if (o.update == 3) p.kind = 2;
-  else p.kind = groups >= 256LL * 4 * 2 * 64 ? 0 : groups >= 32LL * 1024 ? 1 : 2;
+  else {
+    // the tiles from 32 k groups; the update alone (auto tiles) from 24 k, where its woven
+    // tiles already beat the pipelined ones (cifar10_256's N = 4 window, 26 k groups: 100.8
+    // against 141.3 us; 20.9 k: 106.9 / 109.4; 18.4 k and below the pipelined tiles win;
+    // r05, profiles/r05/ab_weave_vs_pipe.txt)
+    const int64_t tile_min = (!fused && o.tile == 0) ? 24LL * 1024 : 32LL * 1024;
+    p.kind = groups >= 256LL * 4 * 2 * 64 ? 0 : groups >= tile_min ? 1 : 2;
+  }
   if (p.kind == 1 && o.tile >= 3) {  // the woven tiles (one width)
     p.kind = 3;
     p.nw = o.tile;
@@ -3017,6 +3024,15 @@ static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o, bool fused
   // (same-process A/B, r05: the update alone 276 -> 261 us on cifar10_256, 241 -> 227 on
   // the N = 4 window, 1133 -> 1099 on cifar100_1024; the fused step 380 against 392 on
   // cifar10_256, but 170.6 against 181.4 us on the N = 8 window)
+  // the update alone up to three 64-group tiles per CU (the N = 8 window: 2.7, latency-
+  // bound): the woven 8-wave tiles, whose serial steps run between the producers' stages,
+  // one round of them at most (synth1m_256's N = 8 window 125.3 against 143.8 us for the
+  // flat tiles, cifar10_256's N = 3 122.2 against 146.2; at 3.2 and 3.6 tiles per CU they
+  // lose, 190-194 against 161-165 us; r05 same-process A/B, profiles/r05/ab_weave_small.txt)
+  if (p.kind == 1 && o.tile == 0 && !fused && groups <= 3LL * 64 * (device_simds() / 4)) {
+    p.kind = 3;
+    p.nw = 8;
+  }
   if (p.kind == 1 && (o.tile == 2 || (o.tile == 0 && (!fused || groups < 65536)))) p.kind = 4;
   if (p.kind == 2) {
     p.blocks = (groups + 15) / 16;

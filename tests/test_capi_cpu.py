@@ -134,8 +134,10 @@ def test_launch_grid_covers_every_group(spec):
                 assert b == -(-groups // 16), (groups, g)
             if spec.startswith("update="):
                 want = spec.split(",")[0].split("=")[1]
-                if want == "tiled" and "tile=classic" not in spec:  # the update alone: flat tiles unless asked
-                    want = "weave" if "tile=weave" in spec else "flat"
+                if want == "tiled" and "tile=classic" not in spec:  # the update alone: flat tiles unless asked,
+                    # the woven 8-wave tiles up to three per CU (256 CUs without a device)
+                    want = ("weave" if "tile=weave" in spec or ("tile=" not in spec and groups <= 3 * 64 * 256)
+                            else "flat")
                 assert g["kind"] == want, (spec, g)
     finally:
         F.set_plan("")

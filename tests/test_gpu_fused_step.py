@@ -126,5 +126,5 @@ def test_plan_overrides_are_validated():
         assert F.plan() == ""
     with F.plan_override("update=tiled; grid=plain"):
         assert F.plan() == "update=tiled,grid=plain"
-        assert F.update_kernel(F.b64_len(LAYOUTS["mnist"].n_up)) == "k_update_flat"
+        assert F.update_kernel(F.b64_len(LAYOUTS["mnist"].n_up)) == "k_update_weave<8>"
     assert F.plan() == ""
