@@ -2169,7 +2169,7 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
                                      hdr_block, merged, merged_f32, err, nA, KardamOut{});
   } else {
     const int64_t e = (int64_t)blockIdx.x - nU;
-    __builtin_amdgcn_s_setprio(3);
+    encode_prio(ej.prio);
     encode_rows<true>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                      (int)(e / ej.gx), &tab, &dtab);
   }
@@ -3377,7 +3377,8 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   // fewer loses at N = 2 (624.0 us) (r05 same-process A/B, profiles/r05/ab_fused_balanced.txt)
   const bool lanes = o.grid == 2;
   int nAf = lanes ? 0 : (int)gx, nUf = lanes ? (int)((groups + 83) / 84) : (int)gx;
-  if (o.grid == 3 || (o.grid == 0 && groups < 4LL * 64 * device_simds())) {
+  const bool balanced = o.grid == 3 || (o.grid == 0 && groups < 4LL * 64 * device_simds());
+  if (balanced) {
     PlanOverrides ob = o;
     ob.grid = 0;
     const UpdatePlan pb = plan_update(groups, ob);
@@ -3388,7 +3389,12 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   }
   const int rpb = std::min(M, o.tile_enc_rows > 0 ? o.tile_enc_rows : 24);
   const int64_t nE = gx * ((M + rpb - 1) / rpb);
-  const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+  // the encode's waves at priority 3 over the full width (r04, see k_update_encode), at 0
+  // under the balanced split of a small window: there the update waves, 2.7 per SIMD, are
+  // the critical path (the N = 2 window 588.9 -> 572.5 us, while the full width loses at 2,
+  // 1083.7 -> 1108.4; r05 same-process A/B, profiles/r05/ab_stream_encode_prio.txt)
+  const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb,
+                     o.tile_enc_prio >= 0 ? o.tile_enc_prio : balanced ? 0 : 3};
   if (o.stream_enc == 1 && !lanes) {  // the encode inside the update lanes: one block per 256 groups
     hipLaunchKernelGGL((k_update_encode<256, true>), dim3((unsigned)gx), dim3(256), 0, s, uploads, pitch, M, d_dampen,
                        inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)gx, (int)gx, ej);

@@ -378,6 +378,28 @@ def test_update_two_width_tiles(codec, oracle, plan, mix):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
+@pytest.mark.parametrize("n,kernel", [(90_001, "k_update_weave<8>"), (160_003, "k_update_flat")])
+def test_update_default_small_windows(codec, oracle, plan, n, kernel):
+    """The default plan's update alone on windows the woven 8-wave tiles take (24 k groups
+    up to three 64-group tiles per CU) and just past them (the flat tiles), with large
+    magnitudes in a few slots (in-stage fallbacks, the general-chain recompute) and a
+    ragged last group."""
+    plan("")
+    lay = synthetic(n)
+    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
+    rng = np.random.default_rng(n)
+    M = 5
+    ups = []
+    for c in range(M):
+        v = oracle.synth_upload(21, c, list(lay.w_sizes), list(lay.b_sizes))
+        big = (rng.random(len(v)) < 0.01) & (hm == 0)
+        v[big] = (np.exp(rng.uniform(0, 21, big.sum())) * rng.choice([-1, 1], big.sum())).astype(np.float32)
+        ups.append(oracle.encode_floats(v))
+    d = [1.0, 0.5, 1 / 3, 2.0, 0.1]
+    assert F.update_kernel(len(ups[0])) == kernel
+    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
+
+
 @pytest.mark.parametrize("w2", ["auto", "16", "21", "32", "64"])
 def test_update_flat_tiles(codec, oracle, plan, w2):
     """k_update_flat's one-round grid: whole rounds of 64-group tiles, then tiles of
