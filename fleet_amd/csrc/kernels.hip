@@ -2333,6 +2333,7 @@ __global__ void __launch_bounds__(64 * NW) k_update_weave_encode(const uint8_t* 
     b64_tables_init<64 * NW>(&sh.t.tab);
     d16_table_init<64 * NW>(&sh.t.dt);
     __syncthreads();
+    encode_prio(ej.prio);
     const int64_t e = (int64_t)blockIdx.x - nU;
     encode_rows<true, 64 * NW>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                                (int)(e / ej.gx), &sh.t.tab, &sh.t.dt);
@@ -3314,9 +3315,12 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   if (p.kind == 3) {  // the woven tiles, then the encode's blocks (64 * nw lanes each), or the encode inside them
     const int nt = 64 * p.nw;
     const int64_t gx = (groups + nt - 1) / nt;
-    const int rpb = encode_rows_per_block(gx, M);
+    // 24 rows per encode block as in the other fused forms (the standalone encode's rule
+    // gave these blocks one or two rows each, every block copying the tables for them)
+    const int rpb = std::min(M, o.tile_enc_rows > 0 ? o.tile_enc_rows : 24);
     const int64_t nU = p.blocks, nE = (o.weave_enc == 1 && p.nw > 3) ? 0 : gx * ((M + rpb - 1) / rpb);
-    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb};
+    const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb,
+                       o.tile_enc_prio >= 0 ? o.tile_enc_prio : 0};
 #define FLEET_WEAVE_ENC_LAUNCH(NWV)                                                                             \
   hipLaunchKernelGGL(k_update_weave_encode<NWV>, dim3((unsigned)(nU + nE)), dim3(64 * NWV), 0, s, uploads, pitch, M, \
                      d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)nU, ej)
