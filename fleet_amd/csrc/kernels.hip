@@ -3034,6 +3034,15 @@ static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o, bool fused
     p.kind = 3;
     p.nw = 8;
   }
+  // the fused step on small windows: the woven tiles with the encode's blocks after them
+  // from 14 k to 40 k groups (8 waves up to 32 k, 6 above), the pipelined tiles below
+  // (cifar10_256's N = 5 window 134.7 -> 107.5 us, cifar100_1024's N = 4 672.4 -> 463.0,
+  // cifar10_256's N = 3 160.2 -> 147.6 against the flat tiles; 13 k groups: 90.0 pipelined
+  // against 94.1; r05 same-process A/B, profiles/r05/ab_weave_fused.txt)
+  if (fused && o.update == 0 && o.tile == 0 && groups >= 14LL * 1024 && groups < 40LL * 1024) {
+    p.kind = 3;
+    p.nw = groups < 32LL * 1024 ? 8 : 6;
+  }
   if (p.kind == 1 && (o.tile == 2 || (o.tile == 0 && (!fused || groups < 65536)))) p.kind = 4;
   if (p.kind == 2) {
     p.blocks = (groups + 15) / 16;

@@ -2,8 +2,10 @@
 batch and the client encode of the next in one launch must give exactly what
 fleet_update_device and fleet_encode_device give as two calls -- the merged text,
 merged_f32 and the next batch's uploads, byte for byte -- on the stream grid (the
-fused kernel k_update_encode), on the wide tiles (k_update_tiled_encode) and on
-the pipelined tiles (k_update_pipe with the encode's blocks appended). The two
+fused kernel k_update_encode), on the wide tiles (k_update_tiled_encode), the flat
+and woven tiles of small windows (k_update_flat, k_update_weave_encode<8 | 6>: 62,001
+and 104,003 values, 20.7 k and 34.7 k groups) and on the pipelined tiles (k_update_pipe
+with the encode's blocks appended). The two
 separate calls are themselves checked against the oracle elsewhere
 (test_gpu_parity.py, test_gpu_full_size.py)."""
 import numpy as np
@@ -29,7 +31,8 @@ def _batch(codec, torch, lay, M, seed, n_values=None):
 @pytest.mark.parametrize("lay_name,M,n_values", [("synth1m", 6, None), ("synth1m", 1, None),
                                                   ("cifar10", 5, None), ("cifar100", 4, None), ("mnist", 3, None),
                                                   ("mnist", 64, None), ("synth1m", 3, 1_000_003), ("synth1m", 2, 150_001),
-                                                  ("synth1m", 2, 100)])
+                                                  ("synth1m", 2, 100), ("synth1m", 4, 62_001), ("synth1m", 3, 104_003),
+                                                  ("synth1m", 3, 131_075)])
 def test_update_encode_equals_two_calls(codec, lay_name, M, n_values, pad=0):
     torch = pytest.importorskip("torch")
     lay = LAYOUTS[lay_name]
