@@ -275,6 +275,44 @@ __device__ __forceinline__ void q_stage_d16x(float (&out)[S], const float (&x)[S
   }
 }
 
+// q_stage_d16x with the digit offsets from the VarEntry compare (var_d16, as
+// q_stage_v16): branch-free up to the exact fallback for values outside the q_gen
+// domain (a drop-in where every stage output is used).
+template <int S>
+__device__ __forceinline__ void q_stage_v16x(float (&out)[S], const float (&x)[S], const D16Table* dt,
+                                             const VarEntry* vt) {
+  uint32_t e[S], emax = 0;
+#pragma unroll
+  for (int i = 0; i < S; ++i) {
+    e[i] = var_d16(f2u(x[i]), vt);
+    emax = max(emax, e[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < S; ++i) out[i] = q_d16(x[i], e[i], &dt->st);
+  if (__ballot(emax >= kD16Out) != 0) {
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      if (e[i] >= kD16Out) out[i] = q(x[i]);
+  }
+}
+
+#ifndef FLEET_KD_STAGE
+#define FLEET_KD_STAGE 0
+#endif
+// Kardam's G and D stages: the byte table (0) or the VarEntry compare (1)
+template <int S>
+__device__ __forceinline__ void q_stage_kd(float (&out)[S], const float (&x)[S], const D16Table* dt,
+                                           const VarEntry* vt) {
+  if constexpr (FLEET_KD_STAGE & 1) q_stage_v16x<S>(out, x, dt, vt);
+  else q_stage_d16x<S>(out, x, dt, vt);
+}
+template <int S>
+__device__ __forceinline__ void q_stage_kdab(float (&out)[S], const float (&x)[S], const D16Table* dt,
+                                             const VarEntry* vt) {
+  if constexpr (FLEET_KD_STAGE & 2) q_stage_v16x<S>(out, x, dt, vt);
+  else q_stage_d16x<S>(out, x, dt, vt);
+}
+
 // scalarMultiply(getDampen) (cppNN_backend.cpp:753-777): (float)((double)y * d).
 // When d is a binary32 value (1, 1/2, ... -- staleness 0 gives 1 under every
 // getDampen policy) the double product of two binary32 values is exact and one
@@ -420,6 +458,33 @@ __device__ __forceinline__ double group_sum_f64(double v) {
   return v;
 }
 
+// Two sums at once (Kardam's squared norms): the sums of a and of b over each aligned
+// group of TG lanes (32 or 64), a's valid in lane TG/2 - 1 of the group, b's in lane
+// TG - 1. One gfx950 half swap (v_permlane32_swap / v_permlane16_swap: the upper half
+// of a's group against the lower half of b's) and one add fold the pair into one
+// register -- a's group halves summed in the group's lower half, b's in the upper --,
+// then one group_sum_f64 of half the width: 3 + 15 instructions for TG = 64 against
+// 36 for two group_sum_f64<64>. Every lane of the wave active.
+template <int TG>
+__device__ __forceinline__ double pair_sum_f64(double a, double b) {
+  static_assert(TG == 32 || TG == 64, "half swaps of 32 or 16 lanes");
+  const uint64_t ab = __builtin_bit_cast(uint64_t, a), bb = __builtin_bit_cast(uint64_t, b);
+  const uint32_t alo = (uint32_t)ab, ahi = (uint32_t)(ab >> 32), blo = (uint32_t)bb, bhi = (uint32_t)(bb >> 32);
+  double x, y;
+  if constexpr (TG == 64) {
+    const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+    x = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+    y = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  } else {
+    const auto lo = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+    x = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+    y = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  }
+  return group_sum_f64<TG / 2>(x + y);
+}
+
 // Kardam's bookkeeping of one client step in a stream lane (KD = true; SURVEY.md f2,
 // CppNNUpdater.java:463-481, Kardam.java:48-106): G = Q(f32(f64(p) * lr)) -- the
 // picked gradient scalarMultiply(getLrate()) --, its squared norm and that of
@@ -454,27 +519,34 @@ __device__ __forceinline__ bool kardam_prev_load(const KardamOut& kd, int c, uin
   return true;
 }
 
-template <int S>
+// FULL: every lane of the wave has all S slots in the flat gradient (flat = 2^S - 1,
+// a whole group in range): no per-slot selects (the common wave, taken by a uniform
+// branch hoisted out of the client loop).
+template <int S, bool FULL = false>
 __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uint32_t flat, bool live, int64_t pos0,
                                                  int64_t n_up, const KardamOut& kd, const D16Table& dtab,
                                                  const B64Tables& tab, double* __restrict__ part, bool hasp,
                                                  const float (&pv)[S]) {
   typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
+  if constexpr (FULL) {
+    flat = (1u << S) - 1u;
+    live = true;
+  }
   float rg[S], G[S];
 #pragma unroll
   for (int i = 0; i < S; ++i) rg[i] = p[i];
   dampen_stage<S>(rg, kd.lr);  // lr is uniform
-  q_stage_d16x<S>(G, rg, &dtab, tab.var);
+  q_stage_kd<S>(G, rg, &dtab, tab.var);
   double sg = 0.0, sd = 0.0;
 #pragma unroll
   for (int i = 0; i < S; ++i)
     if ((flat >> i) & 1u) sg += (double)(G[i] * G[i]);
-  const bool whole = live && pos0 + S - 1 < n_up;
+  const bool whole = FULL || (live && pos0 + S - 1 < n_up);
   if (hasp) {  // uniform
     float dv[S], D[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) dv[i] = ((flat >> i) & 1u) ? G[i] - pv[i] : 0.0f;
-    q_stage_d16x<S>(D, dv, &dtab, tab.var);
+    q_stage_kd<S>(D, dv, &dtab, tab.var);
 #pragma unroll
     for (int i = 0; i < S; ++i)
       if ((flat >> i) & 1u) sd += (double)(D[i] * D[i]);
@@ -493,15 +565,12 @@ __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uin
           if (live && pos0 + i < n_up) go[i] = gv[i];
       }
     } else {
-      if (live && pos0 < n_up) go[0] = gv[0];
+      if (FULL || (live && pos0 < n_up)) go[0] = gv[0];
     }
   }
-  sg = group_sum_f64<64>(sg);  // DPP lane moves: every lane of the wave is here
-  sd = group_sum_f64<64>(sd);
-  if ((threadIdx.x & 63) == 63) {
-    part[0] = sg;
-    part[1] = sd;
-  }
+  // every lane of the wave is here: the two sums in lanes 31 and 63
+  const double s = pair_sum_f64<64>(sg, sd);
+  if ((threadIdx.x & 31) == 31) part[(threadIdx.x >> 5) & 1] = s;
 }
 
 // Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
@@ -617,6 +686,8 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       if (live && pos < n_up && pos < walk_end && !((hbits >> i) & 1u)) flatbits |= 1u << i;
     }
   }
+  // every lane's slots all in the flat gradient (most waves): kardam_lane_step's FULL form
+  const bool kd_full = KD && __ballot(flatbits != (1u << S) - 1u) == 0;
   // waves holding header slots (layout check) or keep slots (keep_bits: their chains run
   // on code 0 up to the last client, whose codes the merged output keeps): wave-uniform
   const bool wave_keep = __ballot(keep_bits<S>(hbits, live, 3 * g + e0, walk_end) != 0) != 0;
@@ -650,11 +721,15 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
     float y0[S], y[S], p[S];
     dec_stage_d16<S>(y0, codes, &dtab);
     if constexpr (KD) {  // stages A and B feed the side outputs: the exact in-stage fallback
-      q_stage_d16x<S>(y, y0, &dtab, tab.var);
+      q_stage_kdab<S>(y, y0, &dtab, tab.var);
       dampen_stage<S>(y, dampen[c]);
-      q_stage_d16x<S>(p, y, &dtab, tab.var);
-      kardam_lane_step<S>(p, c, flatbits, live, 3 * g + e0, n_up, kd, dtab, tab, kd_part + (size_t)c * kd_stride,
-                          kd_hasp, kd_pv);
+      q_stage_kdab<S>(p, y, &dtab, tab.var);
+      if (kd_full)
+        kardam_lane_step<S, true>(p, c, flatbits, live, 3 * g + e0, n_up, kd, dtab, tab,
+                                  kd_part + (size_t)c * kd_stride, kd_hasp, kd_pv);
+      else
+        kardam_lane_step<S>(p, c, flatbits, live, 3 * g + e0, n_up, kd, dtab, tab, kd_part + (size_t)c * kd_stride,
+                            kd_hasp, kd_pv);
     } else {
       q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
       dampen_stage<S>(y, dampen[c]);
@@ -943,8 +1018,8 @@ struct TileKd {
 // G, ||Q(G - prev)||^2 over the flat gradient's slots (getNorm: float products
 // summed in double). A client's W groups of the tile are W consecutive lanes of
 // one wave (items are client-major, W in {16, 32, 64} and waves start at multiples of
-// 64), so the lane group's sum is the (client, tile) partial: one write, no atomics,
-// a fixed order (k_kardam_reduce then sums the tiles in order). Item h: client c[h]
+// 64), so the lane group's sums are the (client, tile) partial: one write per sum, no
+// atomics, a fixed order (k_kardam_reduce then sums the tiles in order). Item h: client c[h]
 // and group gl[h] (live[h]: a real item), partial slot client cp[h] (cvalid[h]: that
 // client exists -- dead groups of a live client still write their lane group's zeros).
 template <int IPT, int NW, int TGS, bool D16>
@@ -958,7 +1033,7 @@ __device__ __forceinline__ void kardam_items(TileShared<TGS, NW, D16>& sh, const
 #pragma unroll
   for (int i = 0; i < S; ++i) rg[i] = p[i];
   dampen_stage<S>(rg, kd.lr);  // (float)((double)p * lr), lr uniform
-  if constexpr (D16) q_stage_d16x<S>(G, rg, &sh.dt, sh.tab.var);  // exact (in-stage fallback)
+  if constexpr (D16) q_stage_kd<S>(G, rg, &sh.dt, sh.tab.var);  // exact (in-stage fallback)
   else q_stage<S>(G, rg, &sh.tab);
   // per item: the flat slots, ||G||^2, prev and G - prev, the G row out; then one D stage
   // for all the lane's items (one ballot / fix-up pass, not one per item)
@@ -1005,7 +1080,7 @@ __device__ __forceinline__ void kardam_items(TileShared<TGS, NW, D16>& sh, const
       }
     }
   }
-  if constexpr (D16) q_stage_d16x<S>(D, dv, &sh.dt, sh.tab.var);
+  if constexpr (D16) q_stage_kd<S>(D, dv, &sh.dt, sh.tab.var);
   else q_stage<S>(D, dv, &sh.tab);
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
@@ -1013,22 +1088,23 @@ __device__ __forceinline__ void kardam_items(TileShared<TGS, NW, D16>& sh, const
 #pragma unroll
     for (int e = 0; e < 3; ++e)
       if (((flat >> (3 * h + e)) & 1u) && ((hasps >> h) & 1u)) sd[h] += (double)(D[3 * h + e] * D[3 * h + e]);
-    double a, b;  // W is block-uniform: one branch per item
-    if (W == 64) {
-      a = group_sum_f64<64>(sg[h]);
-      b = group_sum_f64<64>(sd[h]);
-    } else if (W == 32) {
-      a = group_sum_f64<32>(sg[h]);
-      b = group_sum_f64<32>(sd[h]);
+    // the client's tile sums (W is block-uniform: one branch per item): 16-lane groups
+    // both in the group's last lane, wider ones sg in the middle lane, sd in the last
+    const int l = threadIdx.x & (W - 1);
+    const size_t slot = ((size_t)cp[h] * tk.ntiles + tk.tile) * 2;
+    // sc1: the pipelined form's reduce blocks read them in the same launch
+    if (W == 16) {
+      const double a = group_sum_f64<16>(sg[h]), b = group_sum_f64<16>(sd[h]);
+      if (cvalid[h] && l == W - 1) {
+        __hip_atomic_store(kd.partials + slot, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(kd.partials + slot + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     } else {
-      a = group_sum_f64<16>(sg[h]);
-      b = group_sum_f64<16>(sd[h]);
-    }
-    if (cvalid[h] && (threadIdx.x & (W - 1)) == W - 1) {  // the group's last lane: its client's tile sum
-      const size_t slot = ((size_t)cp[h] * tk.ntiles + tk.tile) * 2;
-      // sc1: the pipelined form's reduce blocks read them in the same launch
-      __hip_atomic_store(kd.partials + slot, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(kd.partials + slot + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      double s;
+      if (W == 64) s = pair_sum_f64<64>(sg[h], sd[h]);
+      else s = pair_sum_f64<32>(sg[h], sd[h]);
+      if (cvalid[h] && (l == W - 1 || l == W / 2 - 1))
+        __hip_atomic_store(kd.partials + slot + (l == W - 1), s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
