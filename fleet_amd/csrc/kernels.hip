@@ -275,44 +275,6 @@ __device__ __forceinline__ void q_stage_d16x(float (&out)[S], const float (&x)[S
   }
 }
 
-// q_stage_d16x with the digit offsets from the VarEntry compare (var_d16, as
-// q_stage_v16): branch-free up to the exact fallback for values outside the q_gen
-// domain (a drop-in where every stage output is used).
-template <int S>
-__device__ __forceinline__ void q_stage_v16x(float (&out)[S], const float (&x)[S], const D16Table* dt,
-                                             const VarEntry* vt) {
-  uint32_t e[S], emax = 0;
-#pragma unroll
-  for (int i = 0; i < S; ++i) {
-    e[i] = var_d16(f2u(x[i]), vt);
-    emax = max(emax, e[i]);
-  }
-#pragma unroll
-  for (int i = 0; i < S; ++i) out[i] = q_d16(x[i], e[i], &dt->st);
-  if (__ballot(emax >= kD16Out) != 0) {
-#pragma unroll
-    for (int i = 0; i < S; ++i)
-      if (e[i] >= kD16Out) out[i] = q(x[i]);
-  }
-}
-
-#ifndef FLEET_KD_STAGE
-#define FLEET_KD_STAGE 0
-#endif
-// Kardam's G and D stages: the byte table (0) or the VarEntry compare (1)
-template <int S>
-__device__ __forceinline__ void q_stage_kd(float (&out)[S], const float (&x)[S], const D16Table* dt,
-                                           const VarEntry* vt) {
-  if constexpr (FLEET_KD_STAGE & 1) q_stage_v16x<S>(out, x, dt, vt);
-  else q_stage_d16x<S>(out, x, dt, vt);
-}
-template <int S>
-__device__ __forceinline__ void q_stage_kdab(float (&out)[S], const float (&x)[S], const D16Table* dt,
-                                             const VarEntry* vt) {
-  if constexpr (FLEET_KD_STAGE & 2) q_stage_v16x<S>(out, x, dt, vt);
-  else q_stage_d16x<S>(out, x, dt, vt);
-}
-
 // scalarMultiply(getDampen) (cppNN_backend.cpp:753-777): (float)((double)y * d).
 // When d is a binary32 value (1, 1/2, ... -- staleness 0 gives 1 under every
 // getDampen policy) the double product of two binary32 values is exact and one
@@ -536,7 +498,7 @@ __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uin
 #pragma unroll
   for (int i = 0; i < S; ++i) rg[i] = p[i];
   dampen_stage<S>(rg, kd.lr);  // lr is uniform
-  q_stage_kd<S>(G, rg, &dtab, tab.var);
+  q_stage_d16x<S>(G, rg, &dtab, tab.var);
   double sg = 0.0, sd = 0.0;
 #pragma unroll
   for (int i = 0; i < S; ++i)
@@ -546,7 +508,7 @@ __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uin
     float dv[S], D[S];
 #pragma unroll
     for (int i = 0; i < S; ++i) dv[i] = ((flat >> i) & 1u) ? G[i] - pv[i] : 0.0f;
-    q_stage_kd<S>(D, dv, &dtab, tab.var);
+    q_stage_d16x<S>(D, dv, &dtab, tab.var);
 #pragma unroll
     for (int i = 0; i < S; ++i)
       if ((flat >> i) & 1u) sd += (double)(D[i] * D[i]);
@@ -721,9 +683,9 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
     float y0[S], y[S], p[S];
     dec_stage_d16<S>(y0, codes, &dtab);
     if constexpr (KD) {  // stages A and B feed the side outputs: the exact in-stage fallback
-      q_stage_kdab<S>(y, y0, &dtab, tab.var);
+      q_stage_d16x<S>(y, y0, &dtab, tab.var);
       dampen_stage<S>(y, dampen[c]);
-      q_stage_kdab<S>(p, y, &dtab, tab.var);
+      q_stage_d16x<S>(p, y, &dtab, tab.var);
       if (kd_full)
         kardam_lane_step<S, true>(p, c, flatbits, live, 3 * g + e0, n_up, kd, dtab, tab,
                                   kd_part + (size_t)c * kd_stride, kd_hasp, kd_pv);
@@ -1033,7 +995,7 @@ __device__ __forceinline__ void kardam_items(TileShared<TGS, NW, D16>& sh, const
 #pragma unroll
   for (int i = 0; i < S; ++i) rg[i] = p[i];
   dampen_stage<S>(rg, kd.lr);  // (float)((double)p * lr), lr uniform
-  if constexpr (D16) q_stage_kd<S>(G, rg, &sh.dt, sh.tab.var);  // exact (in-stage fallback)
+  if constexpr (D16) q_stage_d16x<S>(G, rg, &sh.dt, sh.tab.var);  // exact (in-stage fallback)
   else q_stage<S>(G, rg, &sh.tab);
   // per item: the flat slots, ||G||^2, prev and G - prev, the G row out; then one D stage
   // for all the lane's items (one ballot / fix-up pass, not one per item)
@@ -1080,7 +1042,7 @@ __device__ __forceinline__ void kardam_items(TileShared<TGS, NW, D16>& sh, const
       }
     }
   }
-  if constexpr (D16) q_stage_kd<S>(D, dv, &sh.dt, sh.tab.var);
+  if constexpr (D16) q_stage_d16x<S>(D, dv, &sh.dt, sh.tab.var);
   else q_stage<S>(D, dv, &sh.tab);
 #pragma unroll
   for (int h = 0; h < IPT; ++h) {
