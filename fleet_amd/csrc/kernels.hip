@@ -421,7 +421,7 @@ __device__ __forceinline__ double group_sum_f64(double v) {
 }
 
 // Two sums at once (Kardam's squared norms): the sums of a and of b over each aligned
-// group of TG lanes (32 or 64), a's valid in lane TG/2 - 1 of the group, b's in lane
+// group of TG lanes (16, 32 or 64), a's valid in lane TG/2 - 1 of the group, b's in lane
 // TG - 1. One gfx950 half swap (v_permlane32_swap / v_permlane16_swap: the upper half
 // of a's group against the lower half of b's) and one add fold the pair into one
 // register -- a's group halves summed in the group's lower half, b's in the upper --,
@@ -429,22 +429,34 @@ __device__ __forceinline__ double group_sum_f64(double v) {
 // 36 for two group_sum_f64<64>. Every lane of the wave active.
 template <int TG>
 __device__ __forceinline__ double pair_sum_f64(double a, double b) {
-  static_assert(TG == 32 || TG == 64, "half swaps of 32 or 16 lanes");
-  const uint64_t ab = __builtin_bit_cast(uint64_t, a), bb = __builtin_bit_cast(uint64_t, b);
-  const uint32_t alo = (uint32_t)ab, ahi = (uint32_t)(ab >> 32), blo = (uint32_t)bb, bhi = (uint32_t)(bb >> 32);
-  double x, y;
-  if constexpr (TG == 64) {
-    const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
-    const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
-    x = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
-    y = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  static_assert(TG == 16 || TG == 32 || TG == 64, "half swaps of 32 or 16 lanes, a row mirror");
+  if constexpr (TG == 16) {
+    // a 16-lane row: each lane keeps a (lanes 0-7 of the row) or b (8-15) and takes its
+    // mirror lane's other value (row_mirror: lane i reads 15 - i, the other half), then
+    // the half's three DPP steps: 16 instructions against 24 for two group_sum_f64<16>
+    const bool up = (threadIdx.x & 8) != 0;
+    double v = (up ? b : a) + dpp_move_f64<0x140, 0xf>(up ? a : b);
+    v += dpp_move_f64<0x141, 0xf>(v);  // row_half_mirror
+    v += dpp_move_f64<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v += dpp_move_f64<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    return v;
   } else {
-    const auto lo = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
-    const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
-    x = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
-    y = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+    const uint64_t ab = __builtin_bit_cast(uint64_t, a), bb = __builtin_bit_cast(uint64_t, b);
+    const uint32_t alo = (uint32_t)ab, ahi = (uint32_t)(ab >> 32), blo = (uint32_t)bb, bhi = (uint32_t)(bb >> 32);
+    double x, y;
+    if constexpr (TG == 64) {
+      const auto lo = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+      const auto hi = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+      x = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+      y = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+    } else {
+      const auto lo = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+      const auto hi = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+      x = __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]);
+      y = __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+    }
+    return group_sum_f64<TG / 2>(x + y);
   }
-  return group_sum_f64<TG / 2>(x + y);
 }
 
 // Kardam's bookkeeping of one client step in a stream lane (KD = true; SURVEY.md f2,
@@ -453,7 +465,7 @@ __device__ __forceinline__ double pair_sum_f64(double a, double b) {
 // Q(G - prev) (getNorm: float products summed in double), G stored in upload
 // coordinates for the next round's difference. `flat` bit i = value slot pos0 + i
 // is in the flat gradient (neither a header slot nor past the walk). The wave's
-// two sums go to its partial slot `part` (lane 63; k_kardam_reduce sums the waves).
+// two sums go to its partial slot `part` (lanes 31 and 63; k_kardam_reduce sums the waves).
 // The worker's previous G at the lane's slots (0 off the flat gradient): loaded a client
 // ahead by the stream loop, so the HBM latency of the prev rows overlaps the current
 // client's chain instead of stalling it. Returns has_prev[c] (uniform).
@@ -1050,24 +1062,17 @@ __device__ __forceinline__ void kardam_items(TileShared<TGS, NW, D16>& sh, const
 #pragma unroll
     for (int e = 0; e < 3; ++e)
       if (((flat >> (3 * h + e)) & 1u) && ((hasps >> h) & 1u)) sd[h] += (double)(D[3 * h + e] * D[3 * h + e]);
-    // the client's tile sums (W is block-uniform: one branch per item): 16-lane groups
-    // both in the group's last lane, wider ones sg in the middle lane, sd in the last
+    // the client's tile sums (W is block-uniform: one branch per item): sg in the lane
+    // group's middle lane, sd in its last
     const int l = threadIdx.x & (W - 1);
     const size_t slot = ((size_t)cp[h] * tk.ntiles + tk.tile) * 2;
     // sc1: the pipelined form's reduce blocks read them in the same launch
-    if (W == 16) {
-      const double a = group_sum_f64<16>(sg[h]), b = group_sum_f64<16>(sd[h]);
-      if (cvalid[h] && l == W - 1) {
-        __hip_atomic_store(kd.partials + slot, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(kd.partials + slot + 1, b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    } else {
-      double s;
-      if (W == 64) s = pair_sum_f64<64>(sg[h], sd[h]);
-      else s = pair_sum_f64<32>(sg[h], sd[h]);
-      if (cvalid[h] && (l == W - 1 || l == W / 2 - 1))
-        __hip_atomic_store(kd.partials + slot + (l == W - 1), s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    double s;
+    if (W == 64) s = pair_sum_f64<64>(sg[h], sd[h]);
+    else if (W == 32) s = pair_sum_f64<32>(sg[h], sd[h]);
+    else s = pair_sum_f64<16>(sg[h], sd[h]);
+    if (cvalid[h] && (l == W - 1 || l == W / 2 - 1))
+      __hip_atomic_store(kd.partials + slot + (l == W - 1), s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
