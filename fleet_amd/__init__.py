@@ -125,6 +125,7 @@ def lib() -> C.CDLL:
         "fleet_model_version": (i32, [vp, vp, vp, i32, vp, sz, vp, vp]),
         "fleet_model_params_device": (i32, [vp, vp, sz, vp, sz, i32, vp, vp]),
         "fleet_minibatch_len": (sz, [i32, i32, i32, i32]),
+        "fleet_test_kardam_skew": (i32, [vp, C.c_uint]),
         "fleet_kardam_grads": (i32, [vp, vp, vp, i32, vp, C.c_double, vp, vp, sz, szp, vp, vp]),
         "fleet_descent_window_device": (i32, [vp, vp, vp, vp, sz, sz, vp, vp, i32, vp, vp, i32, C.c_float, vp]),
         "fleet_minibatch_device": (i32, [vp, vp, sz, i32, vp, vp, i32, vp, i32, vp, vp, vp]),
@@ -512,6 +513,11 @@ class Codec:
             _stream(stream))
         self._check(rc)
         return ng, nd
+
+    def test_kardam_skew(self, skew: int) -> None:
+        """Test hook: the pipelined Kardam form's reduce blocks wait for a later epoch than
+        the tiles publish (skew != 0), so the call fails on their bounded wait."""
+        self._check(self._L.fleet_test_kardam_skew(self._h, int(skew)))
 
     def encode_device(self, values_f32, n: int, out_u8, stream=None):
         """values_f32: float32 CUDA tensor [M, vpitch]; out_u8: uint8 [M, pitch]."""

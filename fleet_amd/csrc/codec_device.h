@@ -113,6 +113,29 @@ __device__ __forceinline__ void d16_table_init(D16Table* t) {
   }
 }
 
+// The stream kernels' extra table: int2float's step count by byte sum (codec_math.h
+// ld16_entry), 4 KB beside their D16Table (the tiles, LDS-bound, keep the division).
+struct alignas(16) LastDigitTable {
+  uint8_t ld16[4096];
+};
+FLEET_HDC LastDigitTable make_last_digit_table() {
+  LastDigitTable t{};
+  for (uint32_t i = 0; i < 4096; ++i) t.ld16[i] = ld16_entry(i);
+  return t;
+}
+static __constant__ LastDigitTable g_ld16_table = make_last_digit_table();
+template <int NT = 256>
+__device__ __forceinline__ void ld16_table_init(LastDigitTable* t) {
+  constexpr int n16 = (int)(sizeof(LastDigitTable) / 16);
+  const uint4* src = reinterpret_cast<const uint4*>(&g_ld16_table);
+  uint4* dst = reinterpret_cast<uint4*>(t);
+#pragma unroll
+  for (int i0 = 0; i0 < n16; i0 += NT) {
+    const int i = i0 + (int)threadIdx.x;
+    if (i < n16) dst[i] = src[i];
+  }
+}
+
 // One 16-char group -> 12 bytes -> 3 little-endian int32 codes.
 // Returns a 16-bit mask of chars that are not in the alphabet (bit i = char i).
 __device__ __forceinline__ uint32_t b64_decode_group(uint4 w, const B64Tables* t, int32_t codes[3]) {
@@ -135,6 +158,20 @@ __device__ __forceinline__ uint32_t b64_decode_group(uint4 w, const B64Tables* t
   return bad;
 }
 
+// (a << k) | b as ONE v_lshl_or_b32: written out, the two-level shift-or of four sextets
+// is re-associated by the compiler into four instructions (two shifts, v_lshl_or,
+// v_or3); three v_lshl_or are the minimum
+template <int K>
+__device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(K), "v"(b));
+  return r;
+}
+// the 24 bits of one quad's sextets s0..s3 (big-endian)
+__device__ __forceinline__ uint32_t quad24(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3) {
+  return lshl_or<12>(lshl_or<6>(s0, s1), lshl_or<6>(s2, s3));
+}
+
 // Same decode for a full group (all 16 chars carry data): returns nonzero if any
 // char is outside the alphabet. Sextets compose by shift-or; no per-char mask:
 // valid entries are 0..63 and the invalid marker 0xff has bit 6 set, so the OR of
@@ -150,7 +187,7 @@ __device__ __forceinline__ uint32_t b64_decode_group_full(uint4 w, const B64Tabl
     const uint32_t s2 = t->from[(words[qd] >> 16) & 0xff];
     const uint32_t s3 = t->from[words[qd] >> 24];
     anyf |= s0 | s1 | s2 | s3;
-    V[qd] = (((((s0 << 6) | s1) << 6) | s2) << 6) | s3;  // flag bits only land above bit 23
+    V[qd] = quad24(s0, s1, s2, s3);  // (an invalid char's garbage: the call fails on anyf)
   }
   codes[0] = (int32_t)__builtin_amdgcn_perm(V[1], V[0], 0x06000102u);
   codes[1] = (int32_t)__builtin_amdgcn_perm(V[2], V[1], 0x05060001u);
@@ -176,7 +213,7 @@ __device__ __forceinline__ uint32_t b64_decode_pair_full(uint32_t w0, uint32_t w
     const uint32_t s2 = t->from[(words[qd] >> 16) & 0xff];
     const uint32_t s3 = t->from[words[qd] >> 24];
     anyf |= s0 | s1 | s2 | s3;
-    V[qd] = (((((s0 << 6) | s1) << 6) | s2) << 6) | s3;
+    V[qd] = quad24(s0, s1, s2, s3);
   }
   code = (int32_t)__builtin_amdgcn_perm(V[1], V[0], sel);
   return anyf & 0x40u;
@@ -215,7 +252,7 @@ __device__ __forceinline__ uint4 b64_encode_group(const int32_t codes[3], const 
     uint32_t b = t->to[(V[qd] >> 12) & 63];
     uint32_t c = t->to[(V[qd] >> 6) & 63];
     uint32_t d = t->to[V[qd] & 63];
-    out[qd] = a | (b << 8) | (c << 16) | (d << 24);
+    out[qd] = lshl_or<16>(lshl_or<8>(d, c), lshl_or<8>(b, a));  // three instructions (the OR form takes four)
   }
   return make_uint4(out[0], out[1], out[2], out[3]);
 }

@@ -555,6 +555,30 @@ FLEET_HDC StepTables make_step_tables() {
   }
   return t;
 }
+// 16 * (|c| % 10) for every int32 c without a division (the stream kernels' int2float
+// step count): 256 = 1 (mod 5) and 2^32 = 1 (mod 5), so with S the sum of the four
+// bytes of c's bit pattern u, |c| = u = S (mod 5) for c >= 0 and |c| = 2^32 - u = 1 - S
+// (mod 5) for c < 0, while |c| = u (mod 2). One table byte per (S, sign, u & 1):
+// index S + 1024 * sign + 2048 * (u & 1), 4 KB. On gfx950 the index is v_alignbit
+// (rotl 11 puts bit 0 at 11 and the sign at 10), v_and and v_sad_u8 (the byte sum
+// plus those two bits) -- three instructions for the six of the mulhi remainder.
+// Checked for every int32 by tests/native/check_math.cpp d16 and GPU digest fn 23.
+FLEET_HDC uint8_t ld16_entry(uint32_t i) {
+  const uint32_t S = i & 1023u, neg = (i >> 10) & 1u, odd = (i >> 11) & 1u;
+  if (S > 1020u) return 0;
+  const uint32_t m5 = neg ? (1026u - S) % 5u : S % 5u;  // 1 - S + 5 * 205 >= 6 > 0
+  const uint32_t r = (m5 & 1u) == odd ? m5 : m5 + 5u;
+  return (uint8_t)(r << 4);
+}
+FLEET_HD uint32_t ld16_index(int32_t c) {
+  const uint32_t u = (uint32_t)c;
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_sad_u8(u, 0u, __builtin_amdgcn_alignbit(u, u, 21) & 0xc00u);
+#else
+  return (u & 255u) + ((u >> 8) & 255u) + ((u >> 16) & 255u) + (u >> 24) + ((u >> 31) << 10) + ((u & 1u) << 11);
+#endif
+}
+
 // int2float(c) given r16 = 16 * (|c| % 10): the /10 chain's multipliers at r16
 FLEET_HD float dec_d16(int32_t c, uint32_t r16, const StepTables* st) {
   typedef float f4 __attribute__((ext_vector_type(4)));

@@ -138,6 +138,7 @@ struct fleet_ctx {
   uint32_t* d_kflags = nullptr;
   size_t d_kflags_cap = 0;
   uint32_t kflag_epoch = 0;
+  uint32_t kflag_test_skew = 0;       // fleet_test_kardam_skew: reduce blocks wait for a later epoch
 };
 
 namespace {
@@ -248,6 +249,7 @@ int read_err(fleet_ctx* c, hipStream_t s, int* d_errbuf = nullptr) {
   if (e & 1) return fail(c, FLEET_ERR_BASE64, "input is not Base64::encode output (alphabet/padding)");
   if (e & 2) return fail(c, FLEET_ERR_LAYOUT, "uploads disagree on the gradient layout header slots");
   if (e & 4) return fail(c, FLEET_ERR_ARG, "sample index outside the dataset");
+  if (e & 8) return fail(c, FLEET_ERR_HIP, "a cross-block hand-off timed out (Kardam reduce blocks)");
   return FLEET_OK;
 }
 
@@ -1107,12 +1109,22 @@ int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch
   HIP_TRY(c, fleet::launch_update_kardam((const uint8_t*)d_uploads, pitch, M, c->d_dev_dampen, (double)1 / M,
                                          (int64_t)n, 0, (int64_t)ge, c->d_dev_hdr, (uint8_t*)d_merged,
                                          (float*)d_merged_f32, c->d_dev_err, kd, &nw, d_norm, &np, &nf, c->d_kflags,
-                                         c->kflag_epoch, plan, s));
+                                         c->kflag_epoch, plan, s, c->kflag_test_skew));
   if ((size_t)np != n_parts || (size_t)std::max(nw, 1) != n_waves)
     return fail(c, FLEET_ERR_HIP, "Kardam launch plan changed between sizing and launch");
   std::vector<double> norms(2 * (size_t)M * n_parts);
   HIP_TRY(c, hipMemcpyAsync(norms.data(), d_norm, sizeof(double) * norms.size(), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_err, c->d_dev_err, sizeof(int), hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
+  // the pipelined form's reduce blocks wait on the tiles' flags with a bound: a flag that
+  // never came leaves FLEET_ERRBIT_SYNC, and the norms are not to be trusted. The call is
+  // synchronous, so it fails now (the bit is cleared; other sticky bits stay for fleet_check)
+  if (*c->h_err & FLEET_ERRBIT_SYNC) {
+    *c->h_err &= ~FLEET_ERRBIT_SYNC;
+    HIP_TRY(c, hipMemcpyAsync(c->d_dev_err, c->h_err, sizeof(int), hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    return fail(c, FLEET_ERR_HIP, "Kardam reduce blocks timed out waiting for the tiles' flags");
+  }
   for (int i = 0; i < M; ++i) {
     double a = 0.0, b = 0.0;  // the client's chunk sums, in order
     for (size_t k = 0; k < n_parts; ++k) {
@@ -1122,6 +1134,13 @@ int fleet_update_kardam_device(fleet_ctx* c, const void* d_uploads, size_t pitch
     norm_g[i] = std::sqrt(a);
     norm_diff[i] = (d_prev && has_prev[i]) ? std::sqrt(b) : std::nan("");
   }
+  return FLEET_OK;
+}
+
+int fleet_test_kardam_skew(fleet_ctx* c, unsigned skew) {
+  if (!c) return FLEET_ERR_ARG;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->kflag_test_skew = skew;
   return FLEET_OK;
 }
 
@@ -1779,7 +1798,7 @@ const char* fleet_plan(void) {
 
 int fleet_selftest_digest(fleet_ctx* c, int fn, uint64_t* out) {
   if (!c || !out) return FLEET_ERR_ARG;
-  if (fn < 0 || fn > 22) return fail(c, FLEET_ERR_ARG, "no self-test function %d", fn);
+  if (fn < 0 || fn > 23) return fail(c, FLEET_ERR_ARG, "no self-test function %d", fn);
   std::lock_guard<std::mutex> lk(c->mu);
   DEVICE_SCOPE(c);
   unsigned long long* d = nullptr;

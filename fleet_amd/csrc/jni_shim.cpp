@@ -390,12 +390,15 @@ JNIEXPORT jboolean JNICALL Java_apps_cppNN_FleetUpdater_registerDirectNative(JNI
   if (!p || cap <= 0) return JNI_FALSE;
   std::lock_guard<std::mutex> lk(g_direct_mu);
   const int rc = fleet_host_register(c, p, (size_t)cap);
+  // the library released any registration overlapping this one before it tried to page-
+  // lock the range (p and cap are valid here, so that happened whether or not the lock
+  // succeeded): drop their records either way, or a later release would unregister
+  // memory the library no longer holds
+  forget_overlapping(env, (uintptr_t)p, (size_t)cap);
   if (rc != FLEET_OK) {
     fail(c, "registerDirectNative", rc);
     return JNI_FALSE;
   }
-  // the library released any registration overlapping this one: so do the records
-  forget_overlapping(env, (uintptr_t)p, (size_t)cap);
   const jweak ref = env->NewWeakGlobalRef(buf);
   if (ref) g_direct.push_back(DirectReg{(uintptr_t)p, (size_t)cap, ref});
   return JNI_TRUE;

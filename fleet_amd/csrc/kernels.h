@@ -9,6 +9,7 @@
 #define FLEET_ERRBIT_BASE64 1
 #define FLEET_ERRBIT_LAYOUT 2
 #define FLEET_ERRBIT_ARG 4
+#define FLEET_ERRBIT_SYNC 8  // a cross-block hand-off timed out (Kardam reduce blocks)
 
 namespace fleet {
 
@@ -54,13 +55,14 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
                                 int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
                                 double* norms, int* norm_parts, int* flag_slots, uint32_t* kd_flags,
-                                uint32_t kd_epoch, const PlanOverrides& o, hipStream_t s);
+                                uint32_t kd_epoch, const PlanOverrides& o, hipStream_t s,
+                                uint32_t kd_wait_skew = 0);
 // Launch-plan overrides: experiments, and the tests that run every launch variant on
 // small inputs. Process-wide; set by fleet_set_plan (spec "key=value,..." -- update=
 // auto|stream|tiled|pipe, grid=auto|plain|lanes|balanced, tile_mix=auto|off, fused=on|off,
 // stage_threads=N, stage_pieces=N, tile=auto|classic|flat|weave3|4|6|8, flat_w2=auto|N,
 // tile_enc_prio=auto|0..3,
-// weave_enc=auto|inline|blocks, stream_enc=auto|inline|blocks, tile_enc_rows=N) or, once at first
+// weave_enc=auto|inline|blocks, tile_enc_rows=N) or, once at first
 // use, from FLEET_EXPERIMENTS (the
 // same spec). The default (empty spec) is the measured plan.
 struct PlanOverrides {
@@ -70,7 +72,6 @@ struct PlanOverrides {
   int flat_w2 = 0;        // flat tiles: width of the tiles after the whole 64-group rounds (0 auto)
   int tile_enc_prio = -1; // tiled / flat fused step: the encode blocks' issue priority (-1 auto)
   int weave_enc = 0;      // woven fused step: 0 auto, 1 encode inside the tiles (light waves), 2 encode blocks
-  int stream_enc = 0;     // stream fused step: 0 auto, 1 encode inside the update lanes, 2 encode blocks
   int tile_enc_rows = 0;  // fused steps (tiles and stream): rows per encode block (0 auto: 24)
   int tile_mix = 0;       // 0 auto (two widths when a partial round of tiles remains), 1 one width
   int fused = 1;          // 0: the pipelined step as two launches (update, then encode)

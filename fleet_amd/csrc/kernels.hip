@@ -246,6 +246,16 @@ __device__ __forceinline__ void dec_stage_d16(float (&out)[S], const int32_t (&c
   }
 }
 
+// dec_stage_d16 with the step count from the byte-sum table (codec_math.h ld16_entry):
+// three VALU instructions and one LDS byte read for the six of the mulhi remainder
+// (the stream kernels, which have the LDS for its 4 KB)
+template <int S>
+__device__ __forceinline__ void dec_stage_ld16(float (&out)[S], const int32_t (&codes)[S], const D16Table* dt,
+                                               const uint8_t* ld16) {
+#pragma unroll
+  for (int i = 0; i < S; ++i) out[i] = dec_d16(codes[i], ld16[ld16_index(codes[i])], &dt->st);
+}
+
 // q_stage_d16 with the exact in-stage fallback (the general codec per lane for
 // values outside the q_gen domain): a drop-in for q_stage where every stage
 // output is used (Kardam's side outputs).
@@ -581,7 +591,9 @@ __device__ __forceinline__ uint4 encode_group(const float (&x)[3], int r, const 
       }
     }
 #pragma unroll
-    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e] < kD16Out ? ofs[e] : 0u, &dt->st);
+    // offsets >= kD16Out read the tables' identity rows (garbage codes, never a fault;
+    // replaced below), so no select is spent on the common path
+    for (int e = 0; e < 3; ++e) codes[e] = enc_d16(x[e], ofs[e], &dt->st);
     if (__ballot(omax >= kD16Out) != 0) {
 #pragma unroll
       for (int e = 0; e < 3; ++e)
@@ -630,12 +642,16 @@ __device__ __forceinline__ void encode_prio(int p) {
 }
 
 
+// Buffer resource word 3 for raw byte-addressed dword loads on gfx9-family parts (gfx950).
+constexpr int kBufferDword3 = 0x00020000;
+
 // One lane's share of the fused update (the stream path): the values [e0, e0 + S)
 // of group g, S = 3 (the whole group) or S = 1 (one value; three lanes of a wave
 // share a group). Returns the lane's merged codes in out[S] and its Base64 / layout
 // error bits; tables already in LDS. KD: Kardam's side outputs per client
 // (kardam_lane_step; kd_part = this wave's slot of client 0, kd_stride between clients).
-template <int S, bool KD = false, int LADDER = 0, bool INLE = false>
+// LD: the kernel holds the byte-sum step-count table in LDS (ld16; dec_stage_ld16).
+template <int S, bool KD = false, int LADDER = 0, bool LD = false>
 __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table& dtab,
                                             const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                             const double* __restrict__ dampen, double inv_avg, int64_t n_up,
@@ -643,12 +659,15 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
                                             const int32_t* __restrict__ hdr_block, int32_t (&out)[S],
                                             uint32_t& bad, uint32_t& layout_bad, const KardamOut& kd = KardamOut{},
                                             double* __restrict__ kd_part = nullptr, size_t kd_stride = 0,
-                                            const EncodeJob* ej = nullptr) {
-  static_assert(!INLE || (S == 3 && !KD), "the inline encode rides in the group-per-lane update");
+                                            const uint8_t* __restrict__ ld16 = nullptr) {
   const int n_hdr = hdr_block[1];
   const int64_t walk_end = hdr_block[2];
   const int32_t* hdr = hdr_block + 4;
-  const uint8_t* rowp = uploads + 16 * (live ? g : g_safe);
+  // the lane's byte offset in a row as 32 bits (a row is one client's text, < 2^31 bytes:
+  // checked by the launchers), so each row's load is a buffer load at this offset from the
+  // uniform row address (scalar registers, advanced by SALU) -- no 64-bit VALU address
+  // arithmetic per client
+  const uint32_t lane_off = (uint32_t)(16 * (live ? g : g_safe)) + (S == 3 ? 0u : 4u * (uint32_t)e0);
   const uint32_t need = needed_chars_mask((int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g)));
   const uint32_t hbits = live ? (header_bits(hdr, n_hdr, 3 * g) >> e0) & ((1u << S) - 1u) : 0u;
   // Kardam: the lane's value slots in the flat gradient
@@ -693,7 +712,8 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       }
     }
     float y0[S], y[S], p[S];
-    dec_stage_d16<S>(y0, codes, &dtab);
+    if constexpr (LD) dec_stage_ld16<S>(y0, codes, &dtab, ld16);
+    else dec_stage_d16<S>(y0, codes, &dtab);
     if constexpr (KD) {  // stages A and B feed the side outputs: the exact in-stage fallback
       q_stage_d16x<S>(y, y0, &dtab, tab.var);
       dampen_stage<S>(y, dampen[c]);
@@ -720,11 +740,16 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
     }
   };
   auto group_of = [&](int c) {
+    // row c as a buffer resource built by SALU from the wave-uniform row address
+    const __amdgpu_buffer_rsrc_t row = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(uploads + (size_t)c * pitch), (short)0, 0x7fffffff, kBufferDword3);
     if constexpr (S == 3) {
-      return *reinterpret_cast<const uint4*>(rowp + (size_t)c * pitch);
+      typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+      const u4v v = __builtin_amdgcn_raw_buffer_load_b128(row, lane_off, 0, 0);
+      return make_uint4(v.x, v.y, v.z, v.w);
     } else {  // two dwords at 4e (4-byte aligned only)
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(rowp + (size_t)c * pitch + 4 * e0);
-      return make_uint2(w[0], w[1]);
+      return make_uint2(__builtin_amdgcn_raw_buffer_load_b32(row, lane_off, 0, 0),
+                        __builtin_amdgcn_raw_buffer_load_b32(row, lane_off + 4u, 0, 0));
     }
   };
   // two clients per trip, the next client's group always in flight, in alternating
@@ -765,29 +790,6 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       client(c, cur);
     }
   }
-  // INLE: the next batch's client encode of this lane's group, row by row with the
-  // update's clients (its values loaded with the client's group, stored after it)
-  typedef float f3 __attribute__((ext_vector_type(3)));
-  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
-  const int er = (int)min<int64_t>(3, max<int64_t>(0, n_up - 3 * g));
-  auto enc_load = [&](int cc) -> f3 {
-    if constexpr (INLE) {
-      if (!live) return f3{0.0f, 0.0f, 0.0f};
-      const float* v = ej->values + (size_t)cc * ej->vpitch + 3 * g;
-      if (er == 3) return *reinterpret_cast<const f3u*>(v);
-      return f3{v[0], er > 1 ? v[1] : 0.0f, 0.0f};
-    } else {
-      return f3{0.0f, 0.0f, 0.0f};
-    }
-  };
-  auto enc_store = [&](int cc, f3 xv) {
-    if constexpr (INLE) {
-      const float x[3] = {xv.x, xv.y, xv.z};
-      const uint4 t = encode_group(x, er, &tab, &dtab);
-      if (live) store_stream16(ej->out + (size_t)cc * ej->pitch + 16 * g, t);
-    }
-  };
-  f3 e0v = enc_load(0), e1v;
   for (; c + 1 < M; c += 2) {
     FLEET_CLIENT_HOOK(c, M);
     if constexpr (LADDER > 0) {
@@ -796,20 +798,11 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       if (c == (q3 & ~1)) __builtin_amdgcn_s_setprio(0);
     }
     b1 = group_of(c + 1);
-    if constexpr (INLE) e1v = enc_load(c + 1);
     client(c, b0);
-    if constexpr (INLE) enc_store(c, e0v);
-    if (c + 2 < M) {
-      b0 = group_of(c + 2);
-      if constexpr (INLE) e0v = enc_load(c + 2);
-    }
+    if (c + 2 < M) b0 = group_of(c + 2);
     client(c + 1, b1);
-    if constexpr (INLE) enc_store(c + 1, e1v);
   }
-  if (c < M) {
-    client(c, b0);
-    if constexpr (INLE) enc_store(c, e0v);
-  }
+  if (c < M) client(c, b0);
   FLEET_CLIENT_HOOK(M, M);
   if (__ballot(dmax >= kD16Out) != 0) {  // left the q_gen domain: recompute exactly (never for gradients)
     if (dmax >= kD16Out && live) {
@@ -826,7 +819,7 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
 }
 
 // Block `bid` of the SIMD-balanced stream grid (tables already in LDS).
-template <int NT, bool KD = false, int LADDER = 0, bool INLE = false>
+template <int NT, bool KD = false, int LADDER = 0, bool LD = false>
 __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D16Table& dtab, int64_t bid,
                                                    const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                    const double* __restrict__ dampen, double inv_avg, int64_t n_up,
@@ -834,7 +827,7 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
                                                    float* __restrict__ merged_f32, int* __restrict__ err, int nA,
                                                    const KardamOut& kd = KardamOut{},
-                                                   const EncodeJob* ej = nullptr) {
+                                                   const uint8_t* __restrict__ ld16 = nullptr) {
   uint32_t bad = 0, layout_bad = 0;
   // Kardam: this wave's partial slot of client 0; one slot per wave of the grid
   const size_t nw = (size_t)gridDim.x * (NT / 64);
@@ -843,8 +836,8 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
     const int64_t g = g_begin + bid * NT + threadIdx.x;
     const bool live = g < g_end;
     int32_t out[3];
-    update_lane<3, KD, LADDER, INLE>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin,
-                                     hdr_block, out, bad, layout_bad, kd, kd_part, 2 * nw, ej);
+    update_lane<3, KD, LADDER, LD>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, 0, live, g_begin, hdr_block,
+                                   out, bad, layout_bad, kd, kd_part, 2 * nw, ld16);
     if (!live) return;
     if (bad) atomicOr(err, FLEET_ERRBIT_BASE64);
     if (layout_bad) atomicOr(err, FLEET_ERRBIT_LAYOUT);
@@ -852,14 +845,14 @@ __device__ __forceinline__ void update_mixed_block(const B64Tables& tab, const D
     *reinterpret_cast<uint4*>(merged + 16 * g) = pad_group(b64_encode_group(out, &tab), r);
     if (merged_f32)
       for (int e = 0; e < r; ++e) merged_f32[3 * g + e] = dec_mt(out[e], tab.mt);
-  } else if constexpr (!INLE) {  // one value per lane, 21 groups per wave
+  } else {  // one value per lane, 21 groups per wave
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t g = g_begin + (int64_t)nA * NT + ((bid - nA) * (NT / 64) + wave) * 21 + lane / 3;
     const int e = lane % 3;
     const bool live = lane < 63 && g < g_end;
     int32_t out[1];
-    update_lane<1, KD, LADDER>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, e, live, g_begin, hdr_block, out,
-                               bad, layout_bad, kd, kd_part, 2 * nw);
+    update_lane<1, KD, LADDER, LD>(tab, dtab, uploads, pitch, M, dampen, inv_avg, n_up, g, e, live, g_begin, hdr_block,
+                                   out, bad, layout_bad, kd, kd_part, 2 * nw, ld16);
     const int base = lane - e;  // the group's three lanes (lane 63 reads its own)
     const int32_t o0 = __shfl(out[0], base), o1 = __shfl(out[0], base + 1), o2 = __shfl(out[0], base + 2);
     if (!live) return;
@@ -896,11 +889,13 @@ __global__ void __launch_bounds__(NT, KD ? 6 : 1) k_update_mixed(const uint8_t* 
                                                      int* __restrict__ err, int nA, KardamOut kd) {
   __shared__ B64Tables tab;
   __shared__ D16Table dtab;
+  __shared__ LastDigitTable ldt;
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
+  ld16_table_init<NT>(&ldt);
   __syncthreads();
-  update_mixed_block<NT, KD, 3>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
-                             hdr_block, merged, merged_f32, err, nA, kd);
+  update_mixed_block<NT, KD, 3, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
+                                      hdr_block, merged, merged_f32, err, nA, kd, ldt.ld16);
 }
 
 // D16: the tile also holds the byte-table digit counts (D16Table, 9 KB), and the
@@ -1938,22 +1933,29 @@ struct KardamReduceJob {
   double* norms;    // M pairs
   uint32_t* flags;  // tiles x producer waves
   uint32_t epoch;
+  uint32_t wait_skew = 0;  // test hook (fleet_test_kardam_skew): the reduce waits for epoch + skew
 };
 template <int NT, int NPW>
 __device__ __forceinline__ void kardam_reduce_block(const KardamReduceJob& kr, int c, int64_t ntiles,
                                                     const double* partials, double (*red)[NT / 64],
                                                     int* __restrict__ err) {
-  // every tile's producers done (bounded ~0.5 s: a flag that never comes fails the call)
-  for (int64_t f = threadIdx.x; f < ntiles * NPW; f += NT) {
-    for (uint32_t spin = 0; __hip_atomic_load(kr.flags + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kr.epoch;
+  // every tile's producers done (bounded ~0.5 s: a flag that never comes sets
+  // FLEET_ERRBIT_SYNC, which fleet_update_kardam_device reads after its sync and fails
+  // the call; the thread stops waiting at its first missing flag)
+  const uint32_t want = kr.epoch + kr.wait_skew;
+  bool late = false;
+  for (int64_t f = threadIdx.x; f < ntiles * NPW && !late; f += NT) {
+    for (uint32_t spin = 0; __hip_atomic_load(kr.flags + f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want;
          ++spin) {
       if (spin == (1u << 21)) {
-        atomicOr(err, FLEET_ERRBIT_ARG);
+        atomicOr(err, FLEET_ERRBIT_SYNC);
+        late = true;
         break;
       }
       __builtin_amdgcn_s_sleep(8);
     }
   }
+  // (the barrier also keeps the compiler from hoisting the partial loads above the polls)
   __syncthreads();
   // the client's tile partials in a fixed order: lane t of the block adds tiles t, t + NT, ...
   const double* p = partials + (size_t)c * ntiles * 2;
@@ -2073,7 +2075,12 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
     }
     if constexpr (KD) {  // this wave's Kardam partials are out: the reduce blocks may read them
       // the sc1 stores drained (vmcnt 0), then the flag: no agent-scope release (an L2
-      // writeback per wave; 82 us against 19 us for the tiles alone on mnist64, r05 call x2)
+      // writeback per wave; 82 us against 19 us for the tiles alone on mnist64, r05 call x2).
+      // Hardware order: the partials are agent-scope (sc1) atomic stores, complete at the
+      // agent's coherence point once vmcnt reaches 0, and the flag store issues after that.
+      // Compiler order: the waitcnt intrinsic is not a memory operation, so an empty asm
+      // with a memory clobber keeps every partial store above it (no fence instruction).
+      asm volatile("" ::: "memory");
       __builtin_amdgcn_s_waitcnt(0);
       if (lane == 0)
         __hip_atomic_store(kr.flags + (size_t)blockIdx.x * NPW + w, kr.epoch, __ATOMIC_RELAXED,
@@ -2182,7 +2189,7 @@ __global__ void __launch_bounds__(256) k_encode_f32(const float* __restrict__ va
 // aggregation's blocks first (they fit the chip in one round) and streams the
 // encode's blocks through the wave slots and issue cycles they leave. Each
 // block's results are those of the separate kernels.
-template <int NT, bool INLE = false>
+template <int NT>
 __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                       const double* __restrict__ dampen, double inv_avg,
                                                       int64_t n_up, int64_t g_begin, int64_t g_end,
@@ -2192,8 +2199,10 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   static_assert(NT == 256, "the encode blocks are 256 lanes");
   __shared__ B64Tables tab;
   __shared__ D16Table dtab;
+  __shared__ LastDigitTable ldt;
   b64_tables_init<NT>(&tab);
   d16_table_init<NT>(&dtab);
+  if ((int)blockIdx.x < nU) ld16_table_init<NT>(&ldt);  // block-uniform: the update blocks read it
   __syncthreads();
   // the update waves run the issue-priority ladder (3 -> 0 as they get ahead) and the
   // encode's waves run at priority 3: the HBM-bound encode issues whenever it can, the
@@ -2202,14 +2211,9 @@ __global__ void __launch_bounds__(NT) k_update_encode(const uint8_t* __restrict_
   // another box (gpu_r04_a16.sh); at 0 (r04 a6: 1158 us) or 1 (1138-1142 us) slower, and
   // so were update waves laddered from 2 under the encode's 3 (1134-1141 against
   // 1118-1129 us, gpu_r04_a26.sh)
-  if constexpr (INLE) {  // every block an update block; each lane also encodes its group's next-batch rows
-    update_mixed_block<NT, false, 3, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin,
-                                           g_end, hdr_block, merged, merged_f32, err, nA, KardamOut{}, &ej);
-    return;
-  }
   if ((int)blockIdx.x < nU) {  // block-uniform
-    update_mixed_block<NT, false, 3>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
-                                     hdr_block, merged, merged_f32, err, nA, KardamOut{});
+    update_mixed_block<NT, false, 3, true>(tab, dtab, blockIdx.x, uploads, pitch, M, dampen, inv_avg, n_up, g_begin,
+                                           g_end, hdr_block, merged, merged_f32, err, nA, KardamOut{}, ldt.ld16);
   } else {
     const int64_t e = (int64_t)blockIdx.x - nU;
     encode_prio(ej.prio);
@@ -2236,10 +2240,6 @@ template __global__ void k_update_encode<256>(const uint8_t* __restrict__, size_
                                               double, int64_t, int64_t, int64_t, const int32_t* __restrict__,
                                               uint8_t* __restrict__, float* __restrict__, int* __restrict__, int, int,
                                               EncodeJob);
-template __global__ void k_update_encode<256, true>(const uint8_t* __restrict__, size_t, int,
-                                                    const double* __restrict__, double, int64_t, int64_t, int64_t,
-                                                    const int32_t* __restrict__, uint8_t* __restrict__,
-                                                    float* __restrict__, int* __restrict__, int, int, EncodeJob);
 #else
 extern template __global__ void k_update_mixed<256, false>(const uint8_t* __restrict__, size_t, int,
                                                            const double* __restrict__, double, int64_t, int64_t,
@@ -2253,11 +2253,6 @@ extern template __global__ void k_update_encode<256>(const uint8_t* __restrict__
                                                      const double* __restrict__, double, int64_t, int64_t, int64_t,
                                                      const int32_t* __restrict__, uint8_t* __restrict__,
                                                      float* __restrict__, int* __restrict__, int, int, EncodeJob);
-extern template __global__ void k_update_encode<256, true>(const uint8_t* __restrict__, size_t, int,
-                                                           const double* __restrict__, double, int64_t, int64_t,
-                                                           int64_t, const int32_t* __restrict__, uint8_t* __restrict__,
-                                                           float* __restrict__, int* __restrict__, int, int,
-                                                           EncodeJob);
 #endif
 
 #ifndef FLEET_STREAM_TU
@@ -2313,11 +2308,19 @@ __device__ __forceinline__ void flat_kernel(const uint8_t* __restrict__ uploads,
     int64_t g0;
     int ng, w;
     flat_tile_range(blockIdx.x, fg, g_begin, g_end, &g0, &ng, &w);
-    // every tile writes its partial slots (Kardam), an empty one too
-    if (KD || ng > 0)
-      update_flat_block<KD>(sh, pbuf, blockIdx.x, g0, max(ng, 0), w, uploads, pitch, M, dampen, inv_avg, n_up,
-                            hdr_block, merged, merged_f32, err,
+    if (ng > 0) {
+      update_flat_block<KD>(sh, pbuf, blockIdx.x, g0, ng, w, uploads, pitch, M, dampen, inv_avg, n_up, hdr_block,
+                            merged, merged_f32, err,
                             TileKd{kd, (int64_t)blockIdx.x, (int64_t)fg.nU, (int64_t)hdr_block[2]});
+    } else if constexpr (KD) {
+      // an empty tile (flat_grid makes none today) still owns its (client, tile) partial
+      // slots, which k_kardam_reduce sums: zero them explicitly
+      for (int c = threadIdx.x; c < M; c += blockDim.x) {
+        double* slot = kd.partials + ((size_t)c * fg.nU + blockIdx.x) * 2;
+        slot[0] = 0.0;
+        slot[1] = 0.0;
+      }
+    }
   } else if constexpr (!KD) {
     b64_tables_init(&sh.tab);
     d16_table_init(&sh.dt);
@@ -2867,11 +2870,6 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
       else ok = parse_int(v, 1, kFlatTG, &o->flat_w2);
     } else if (k == "tile_enc_rows") {
       ok = parse_int(v, 1, 4096, &o->tile_enc_rows);
-    } else if (k == "stream_enc") {
-      if (v == "auto") o->stream_enc = 0;
-      else if (v == "inline") o->stream_enc = 1;
-      else if (v == "blocks") o->stream_enc = 2;
-      else ok = false;
     } else if (k == "weave_enc") {
       if (v == "auto") o->weave_enc = 0;
       else if (v == "inline") o->weave_enc = 1;
@@ -2890,7 +2888,7 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
     } else if (k == "stage_pieces") {
       ok = parse_int(v, 1, 64, &o->stage_pieces);
     } else {
-      *err = "unknown plan key '" + k + "' (update, grid, tile, flat_w2, tile_enc_prio, weave_enc, stream_enc, tile_enc_rows, tile_mix, fused, "
+      *err = "unknown plan key '" + k + "' (update, grid, tile, flat_w2, tile_enc_prio, weave_enc, tile_enc_rows, tile_mix, fused, "
              "stage_threads, "
              "stage_pieces)";
       return -1;
@@ -2953,6 +2951,11 @@ std::string plan_spec() {
 }
 
 static inline unsigned blocks_for(int64_t n, int t) { return (unsigned)((n + t - 1) / t); }
+
+// The stream kernels address a lane's group by a 32-bit byte offset in its row (buffer
+// loads from the row's uniform address): one client's text below 2 GiB (a Java byte[]
+// holds less anyway).
+static inline bool row_fits(int64_t n_up) { return 16 * ((n_up + 2) / 3) + 16 < (1LL << 31); }
 
 // SIMDs of the current device (4 per CU), cached per device (a process may drive
 // several GPUs, one launching thread each; concurrent first calls store the same value)
@@ -3145,7 +3148,7 @@ std::string update_encode_kernel_name(int64_t groups) {
   const PlanOverrides o = plan_overrides();
   const UpdatePlan p = plan_update(groups, o, true);
   if (!o.fused) return update_kernel_name(groups) + " + k_encode_f32";
-  if (p.kind == 0) return o.stream_enc == 1 && o.grid != 2 ? "k_update_encode<256, true>" : "k_update_encode<256, false>";
+  if (p.kind == 0) return "k_update_encode<256>";
   if (p.kind == 1) return "k_update_tiled_encode<64>";
   if (p.kind == 3) return "k_update_weave_encode<" + std::to_string(p.nw) + ">";
   if (p.kind == 4) return "k_update_flat";
@@ -3183,6 +3186,7 @@ static void launch_weave(int nw, unsigned blocks, hipStream_t s, const uint8_t* 
 hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                          int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                          uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
+  if (!row_fits(n_up)) return hipErrorInvalidValue;
   if (g_end <= g_begin) return hipSuccess;
   const UpdatePlan p = plan_update(g_end - g_begin, plan_overrides());
   if (p.kind == 2)
@@ -3264,7 +3268,8 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
                                 int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
                                 uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, int* n_waves,
                                 double* norms, int* norm_parts, int* flag_slots, uint32_t* kd_flags,
-                                uint32_t kd_epoch, const PlanOverrides& o, hipStream_t s) {
+                                uint32_t kd_epoch, const PlanOverrides& o, hipStream_t s, uint32_t kd_wait_skew) {
+  if (!row_fits(n_up)) return hipErrorInvalidValue;
   const int64_t groups = g_end - g_begin;
   // the update's own launch plan with the side outputs: the pipelined tiles (side outputs
   // from the producers, the reduce blocks in the same launch), the wide tiles (side
@@ -3291,7 +3296,7 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   if (!kd.partials) return hipErrorInvalidValue;  // sizing call: *n_waves only
   if (p.kind == 2 && !kd_flags) return hipErrorInvalidValue;
   if (p.kind == 2) {  // the tiles, then one reduce block per client
-    const KardamReduceJob kr{norms, kd_flags, kd_epoch};
+    const KardamReduceJob kr{norms, kd_flags, kd_epoch, kd_wait_skew};
     hipLaunchKernelGGL((k_update_pipe<16, 1, kKdPipeNW, 0, true>), dim3((unsigned)(blocks + (unsigned)M)),
                        dim3(64 * kKdPipeNW), 0, s,
                        uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
@@ -3351,6 +3356,7 @@ hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int 
 hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, const double* d_dampen, double inv_avg,
                                 int64_t n_up, const int32_t* d_hdr_block, uint8_t* merged, float* merged_f32,
                                 int* d_err, const float* values, size_t vpitch, uint8_t* enc_out, hipStream_t s) {
+  if (!row_fits(n_up)) return hipErrorInvalidValue;
   const int64_t groups = (n_up + 2) / 3;
   const PlanOverrides o = plan_overrides();
   const UpdatePlan p = plan_update(groups, o, true);
@@ -3451,11 +3457,6 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
   // 1083.7 -> 1108.4; r05 same-process A/B, profiles/r05/ab_stream_encode_prio.txt)
   const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb,
                      o.tile_enc_prio >= 0 ? o.tile_enc_prio : balanced ? 0 : 3};
-  if (o.stream_enc == 1 && !lanes) {  // the encode inside the update lanes: one block per 256 groups
-    hipLaunchKernelGGL((k_update_encode<256, true>), dim3((unsigned)gx), dim3(256), 0, s, uploads, pitch, M, d_dampen,
-                       inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)gx, (int)gx, ej);
-    return hipGetLastError();
-  }
   hipLaunchKernelGGL((k_update_encode<256>), dim3((unsigned)(nUf + nE)), dim3(256), 0, s, uploads, pitch, M, d_dampen,
                      inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, nAf, nUf, ej);
   return hipGetLastError();
@@ -3558,12 +3559,14 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
   __shared__ B64Tables tab;
   __shared__ XlTable xl;
   __shared__ D16Table dtab;
+  __shared__ LastDigitTable ldt;
   {
     constexpr DigitEntry init[32] = FLEET_DIGIT_TABLE;
     if (threadIdx.x < 32) dig[threadIdx.x] = init[threadIdx.x];
     b64_tables_init(&tab);
     xl_table_init(&xl);
     d16_table_init(&dtab);
+    ld16_table_init(&ldt);
     __syncthreads();
   }
   const VarEntry* var = tab.var;
@@ -3626,6 +3629,7 @@ __global__ void __launch_bounds__(256) k_digest(int fn, unsigned long long* __re
                use = q_gen_ok(x);
                const uint32_t e = var_d16(u, var);
                o = use ? (e < kD16Out ? f2u(q_d16(x, e, &dtab.st)) : 0xdeadbeefu) : 0u; break; }
+      case 23: o = f2u(dec_d16((int32_t)u, ldt.ld16[ld16_index((int32_t)u)], &dtab.st)); break;  // stream int2float (as fn 0)
       case 22: { const float x = u2f(u);                              // strtof("%.6g") of the model-version copy
                use = (u & 0x7f800000u) != 0x7f800000u;
                o = use ? f2u(g6_roundtrip(x)) : 0u; break; }

@@ -523,7 +523,7 @@ int fleet_update_plan_grid(size_t len, int* kind, int64_t* blocks, int64_t* n_a,
  * lanes (the stream grid), tile=auto|classic|flat|weave3|weave4|weave6|weave8 and
  * flat_w2=auto|1..64, tile_enc_prio=auto|0..3 (the tiles' form; the flat grid's
  * narrow width; the tiles' fused encode blocks' issue priority), tile_mix=auto|off,
- * tile_enc_rows=N, weave_enc=auto|inline|blocks, stream_enc=auto|inline|blocks,
+ * tile_enc_rows=N, weave_enc=auto|inline|blocks,
  * fused=on|off (the pipelined step as one launch or two), stage_threads=1..64,
  * stage_pieces=1..64 (host staging); ""
  * restores the measured default. An unknown key or value rejects the whole spec
@@ -533,6 +533,12 @@ int fleet_update_plan_grid(size_t len, int* kind, int64_t* blocks, int64_t* n_a,
  * default; thread-local storage). */
 int fleet_set_plan(const char* spec, char* err, size_t cap);
 const char* fleet_plan(void);
+
+/* Test hook (no reference counterpart): the pipelined Kardam form's reduce blocks of
+ * this context wait for the launch's epoch + skew, which no tile publishes when skew
+ * != 0, so their bounded wait times out and fleet_update_kardam_device returns
+ * FLEET_ERR_HIP. skew = 0 restores the normal hand-off. */
+int fleet_test_kardam_skew(fleet_ctx* ctx, unsigned skew);
 
 #ifdef __cplusplus
 }

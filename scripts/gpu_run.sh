@@ -25,7 +25,7 @@
 #                    ';' between a plan's keys)
 #   env:VAR=VALUE    export VAR for the steps after it (env:VAR= unsets it), e.g.
 #                    'env:FLEET_EXPERIMENTS=update=tiled;tile=weave4' (quote the ';')
-set -u
+set -u -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$PWD}"
 TAG=${TAG:-run}
 case ${1:-} in tag=*) TAG=${1#tag=}; shift ;; esac

@@ -1,7 +1,9 @@
 #!/bin/bash
 # Dev tool: run a GPU script on a frozen copy of the tree (.snap/, sent with the tree)
 # so that the working tree can change while gpurun waits for a box. Retries only
-# when gpurun ran nothing (no box free / transient preparation failure).
+# when gpurun ran nothing (no box free / transient preparation failure). The copy is
+# removed when the call ends, so no later call (the driver's round-end runs included)
+# ships it or a stale library inside it.
 # usage: scripts/snap_run.sh SCRIPT TIMEOUT LOG
 set -u
 script=$1; tmo=$2; log=$3
@@ -9,6 +11,7 @@ cd /root/repo
 rm -rf .snap && mkdir .snap
 tar --exclude ./.git --exclude ./.snap --exclude ./gpurun_out --exclude './ab/*.objs' --exclude '__pycache__' --exclude '*.pyc' \
   -cf - . | tar -xf - -C .snap
+trap 'rm -rf /root/repo/.snap' EXIT
 cmd="export OUTROOT=\$GRAFT_REPO_ROOT/gpurun_out; cd .snap && export GRAFT_REPO_ROOT=\$PWD && bash $script"
 for i in $(seq 1 12); do
   /usr/local/graft/bin/gpurun --timeout "$tmo" -- "$cmd" > "$log" 2>&1

@@ -116,6 +116,7 @@ int main(int argc, char** argv) {
       const int32_t c = (int32_t)(uint32_t)i;
       const uint32_t a = c < 0 ? 0u - (uint32_t)c : (uint32_t)c;
       if (!same(dec_d16(c, last_digit_u(a) << 4, &g_st), fo_int2float(c))) g_bad++;
+      if (ld16_entry(ld16_index(c)) != last_digit_u(a) << 4) g_bad++;  // the stream kernels' byte-sum form
     });
     long cmp_slices = 0;
     for (uint32_t i = 0; i < 8192; ++i) cmp_slices += dt[i] == kD16Cmp;
@@ -275,8 +276,9 @@ int main(int argc, char** argv) {
     if (last_digit_u(a) != a % 10u) g_bad++;
     if (!same(dec_mt_r(c, last_digit_u(a), mt), fo_int2float(c))) g_bad++;
     if (!same(dec_d16(c, last_digit_u(a) << 4, &g_st), fo_int2float(c))) g_bad++;
+    if (ld16_entry(ld16_index(c)) != (a % 10u) << 4) g_bad++;  // the stream kernels' byte-sum step count
   });
-  report("dec_mt/dec_d16/last_digit_u", b0);
+  report("dec_mt/dec_d16/last_digit_u/ld16", b0);
 
   b0 = g_bad;  // dec_gen (+ packed) vs int2float, every code
   par_for(0, 1ull << 32, s, [](uint64_t i) {

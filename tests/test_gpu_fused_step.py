@@ -94,9 +94,8 @@ def test_update_encode_rejects_overlap_and_bad_text(codec):
 
 @pytest.mark.parametrize("spec,kernel", [("fused=off", " + k_encode_f32"), ("update=tiled", "k_update_tiled_encode<64>"),
                                          ("update=pipe", "k_update_pipe<16, 1, 5, 0, false> (with the encode's blocks)"),
-                                         ("update=stream", "k_update_encode<256, false>"),
-                                         ("update=stream,grid=lanes", "k_update_encode<256, false>"),
-                                         ("update=stream,stream_enc=inline", "k_update_encode<256, true>"),
+                                         ("update=stream", "k_update_encode<256>"),
+                                         ("update=stream,grid=lanes", "k_update_encode<256>"),
                                          ("update=tiled,tile=weave3", "k_update_weave_encode<3>"),
                                          ("update=tiled,tile=weave4", "k_update_weave_encode<4>"),
                                          ("update=tiled,tile=weave8", "k_update_weave_encode<8>"),

@@ -101,3 +101,35 @@ def test_kardam_pipelined_flags_across_sizes(codec, oracle, plan):
     plan("update=pipe")
     for layout, M in ((MNIST, 3), (synthetic(50_003), 2), (synthetic(3001), 5), (MNIST, 3)):
         check_side_outputs(codec, oracle, layout, M)
+
+
+def test_kardam_pipelined_timeout_fails_the_call(codec, oracle, plan):
+    """A tile flag that never arrives (the reduce blocks made to wait for a later
+    epoch by the test hook) fails fleet_update_kardam_device itself instead of
+    returning norms summed from unfinished tiles; the next call, with the
+    normal hand-off, is exact again and the context's error word is clean."""
+    plan("update=pipe")
+    layout, M = MNIST, 2
+    L = F.b64_len(layout.n_up)
+    pitch = 16 * ((L + 15) // 16)
+    ups = [oracle.encode_floats(oracle.synth_upload(41, c, list(layout.w_sizes), list(layout.b_sizes)))
+           for c in range(M)]
+    host = np.zeros((M, pitch), np.uint8)
+    for c, u in enumerate(ups):
+        host[c, :L] = np.frombuffer(u, np.uint8)
+    t = torch.from_numpy(host).cuda()
+    merged = torch.zeros(pitch, dtype=torch.uint8, device="cuda")
+    d = [1.0, 0.5]
+    codec.test_kardam_skew(1)
+    try:
+        with pytest.raises(F.FleetError):
+            codec.update_kardam_device(t, L, d, layout.header_positions(), 0.05, merged)
+    finally:
+        codec.test_kardam_skew(0)
+    codec.check()
+    ng, _ = codec.update_kardam_device(t, L, d, layout.header_positions(), 0.05, merged)
+    codec.check()
+    torch.cuda.synchronize()
+    assert merged.cpu().numpy()[:L].tobytes() == codec.update(ups, d)
+    _, eng, _ = codec.kardam_grads(ups, d, 0.05, None)
+    np.testing.assert_allclose(ng, eng, rtol=1e-12, atol=0)
