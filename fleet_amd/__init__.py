@@ -225,7 +225,8 @@ def update_encode_kernel(length: int) -> str:
 
 def set_plan(spec: str = "") -> None:
     """Launch-plan overrides (fleet_set_plan; process-wide): "update=auto|stream|tiled|pipe",
-    "grid=auto|plain|lanes", "tile_mix=auto|off", "fused=on|off", "stage_threads=N",
+    "grid=auto|plain|balanced|lanes", "tile=auto|classic|flat|weave6|weave8", "flat_w2=auto|N",
+    "tile_enc_prio=auto|0..3", "tile_enc_rows=N", "fused=on|off", "stage_threads=N",
     "stage_pieces=N", comma-separated; "" restores the measured default. Results are
     identical under every plan; an invalid spec raises and changes nothing."""
     err = C.create_string_buffer(256)

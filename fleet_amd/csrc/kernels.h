@@ -59,21 +59,19 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
                                 uint32_t kd_wait_skew = 0);
 // Launch-plan overrides: experiments, and the tests that run every launch variant on
 // small inputs. Process-wide; set by fleet_set_plan (spec "key=value,..." -- update=
-// auto|stream|tiled|pipe, grid=auto|plain|lanes|balanced, tile_mix=auto|off, fused=on|off,
-// stage_threads=N, stage_pieces=N, tile=auto|classic|flat|weave3|4|6|8, flat_w2=auto|N,
+// auto|stream|tiled|pipe, grid=auto|plain|lanes|balanced, fused=on|off,
+// stage_threads=N, stage_pieces=N, tile=auto|classic|flat|weave6|8, flat_w2=auto|N,
 // tile_enc_prio=auto|0..3,
-// weave_enc=auto|inline|blocks, tile_enc_rows=N) or, once at first
+// tile_enc_rows=N) or, once at first
 // use, from FLEET_EXPERIMENTS (the
 // same spec). The default (empty spec) is the measured plan.
 struct PlanOverrides {
   int update = 0;         // 0 auto, 1 stream grid, 2 64-group tiles, 3 16-group pipelined tiles
   int grid = 0;           // stream grid: 0 auto, 1 a group per lane everywhere, 2 a value per lane everywhere
-  int tile = 0;           // tiles: 0 auto (flat alone, classic fused), 1 classic, 2 flat, 3/4/6/8 woven
+  int tile = 0;           // tiles: 0 auto (flat alone, classic fused), 1 classic, 2 flat, 6/8 woven
   int flat_w2 = 0;        // flat tiles: width of the tiles after the whole 64-group rounds (0 auto)
   int tile_enc_prio = -1; // tiled / flat fused step: the encode blocks' issue priority (-1 auto)
-  int weave_enc = 0;      // woven fused step: 0 auto, 1 encode inside the tiles (light waves), 2 encode blocks
   int tile_enc_rows = 0;  // fused steps (tiles and stream): rows per encode block (0 auto: 24)
-  int tile_mix = 0;       // 0 auto (two widths when a partial round of tiles remains), 1 one width
   int fused = 1;          // 0: the pipelined step as two launches (update, then encode)
   int stage_threads = 0;  // host staging copy threads (0 auto)
   int stage_pieces = 0;   // host staging H2D parts (0 auto)

@@ -1339,47 +1339,6 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t nb) {
   return x * q + (x < r ? x : r) + i;
 }
 
-// KD = true: Kardam's side outputs from the tile producers (tile_kardam).
-//
-// TG2 > 0: a two-width grid. Every tile of a launch is resident at once at CIFAR
-// sizes (cifar10_256: 1,635 tiles of 64 groups for 1,792 block slots), so the
-// kernel takes as long as its most loaded CU: 7 tiles where the average is 6.4.
-// Blocks [0, nW) are whole rounds of TG-wide tiles (nW a multiple of the CU
-// count: the same number on every CU), the groups after them go to TG2-wide
-// tiles (a quarter or half of a wide tile's work) spread over the CUs, so the
-// last partial round costs its share of the work instead of a whole tile.
-// D16: the tiles on the byte-table digit counts (TileShared<..., true>).
-template <int TG, bool KD = false, int TG2 = 0, bool D16 = false>
-__global__ void __launch_bounds__(256) k_update_tiled(const uint8_t* __restrict__ uploads, size_t pitch, int M,
-                                                      const double* __restrict__ dampen, double inv_avg,
-                                                      int64_t n_up, int64_t g_begin, int64_t g_end,
-                                                      const int32_t* __restrict__ hdr_block,
-                                                      uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                                      int* __restrict__ err, KardamOut kd = KardamOut{},
-                                                      int nW = INT32_MAX) {
-  static_assert(TG2 == 0 || (TG2 < TG && sizeof(TileShared<TG2, 4, D16>) <= sizeof(TileShared<TG, 4, D16>) &&
-                             tiled_chunk_clients<TG2, D16>() * 3 * TG2 <= tiled_chunk_clients<TG, D16>() * 3 * TG),
-                "the narrow tiles' state fits the wide tiles' LDS");
-  __shared__ TileShared<TG, 4, D16> sh;
-  __shared__ float ptile[tiled_chunk_clients<TG, D16>() * 3 * TG];
-  FLEET_BTRACE(0);
-  const TileKd tk{kd, (int64_t)blockIdx.x, (int64_t)gridDim.x, (int64_t)hdr_block[2]};
-  if constexpr (TG2 > 0) {
-    if ((int)blockIdx.x >= nW) {  // block-uniform: a narrow tile after the wide rounds
-      const int64_t nN = (int64_t)gridDim.x - nW, b = (int64_t)blockIdx.x - nW;
-      update_tiled_block<TG2, KD, D16>(reinterpret_cast<TileShared<TG2, 4, D16>&>(sh), ptile,
-                                       xcd_tile(b, nN), uploads, pitch, M, dampen, inv_avg, n_up,
-                                       g_begin + (int64_t)nW * TG, g_end, hdr_block, merged, merged_f32, err, tk);
-      FLEET_BTRACE(1);
-      return;
-    }
-  }
-  const int64_t nw = TG2 > 0 ? (int64_t)nW : (int64_t)gridDim.x;
-  update_tiled_block<TG, KD, D16>(sh, ptile, xcd_tile(blockIdx.x, nw), uploads, pitch, M,
-                                  dampen, inv_avg, n_up, g_begin, g_end, hdr_block, merged, merged_f32, err, tk);
-  FLEET_BTRACE(1);
-}
-
 // ----------------------------------------------------------------------------
 // Flat tiles (r05): k_update_tiled's two phases with the tile width W a runtime
 // value (up to 64 groups; the planner uses 64, 32 and 16), so one launch deals the
@@ -1676,66 +1635,14 @@ __device__ __forceinline__ void weave_item(WeaveShared<NW>& sh, uint4 w, bool li
   for (int e = 0; e < 3; ++e) pdst[3 * gl + e] = live ? p[e] : 0.0f;
 }
 
-// The next batch's client encode inside the woven tiles (ENC; the pipelined step): the
-// producer-only ("light") waves, which carry no serial steps, encode the rows of the
-// tile's 64 groups -- in interval k the chunk's clients k*NW + j, row j to light wave
-// j mod (NW - 3) -- so the encode uses the issue slots the consumers' serial chains
-// leave, instead of blocks of its own after the tiles. A light wave's values for the
-// next interval are loaded one interval ahead.
+// Tile `bid` of the woven grid (LDS state in sh).
 template <int NW>
-struct WeaveEnc {
-  static constexpr int NL = NW > 3 ? NW - 3 : 1;  // light waves
-  static constexpr int RPI = (NW + NL - 1) / NL;  // rows per light wave and interval (at most)
-  typedef float f3 __attribute__((ext_vector_type(3)));
-  f3 x[RPI];
-};
-template <int NW>
-__device__ __forceinline__ void weave_enc_load(WeaveEnc<NW>& we, const EncodeJob& ej, int k, int li, int M,
-                                               int64_t g, bool glive) {
-  typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
-  constexpr int NL = WeaveEnc<NW>::NL;
-  const int r = (int)min<int64_t>(3, max<int64_t>(0, ej.n - 3 * g));
-#pragma unroll
-  for (int i = 0; i < WeaveEnc<NW>::RPI; ++i) {
-    const int j = li + i * NL, row = k * NW + j;
-    we.x[i] = typename WeaveEnc<NW>::f3{0.0f, 0.0f, 0.0f};
-    if (j < NW && row < M && glive) {
-      const float* v = ej.values + (size_t)row * ej.vpitch + 3 * g;
-      if (r == 3) {
-        const f3u t = *reinterpret_cast<const f3u*>(v);
-        we.x[i] = typename WeaveEnc<NW>::f3{t.x, t.y, t.z};
-      } else {
-        we.x[i] = typename WeaveEnc<NW>::f3{v[0], r > 1 ? v[1] : 0.0f, 0.0f};
-      }
-    }
-  }
-}
-template <int NW>
-__device__ __forceinline__ void weave_enc_rows(const WeaveEnc<NW>& we, const EncodeJob& ej, int k, int li, int M,
-                                               int64_t g, bool glive, const B64Tables* tab, const D16Table* dt) {
-  constexpr int NL = WeaveEnc<NW>::NL;
-  const int r = (int)min<int64_t>(3, max<int64_t>(0, ej.n - 3 * g));
-#pragma unroll
-  for (int i = 0; i < WeaveEnc<NW>::RPI; ++i) {
-    const int j = li + i * NL, row = k * NW + j;
-    if (j < NW && row < M) {  // wave-uniform: encode_group's ballots see the whole wave
-      const float x[3] = {we.x[i].x, we.x[i].y, we.x[i].z};
-      const uint4 t = encode_group(x, r, tab, dt);
-      if (glive) store_stream16(ej.out + (size_t)row * ej.pitch + 16 * g, t);
-    }
-  }
-}
-
-// Tile `bid` of the woven grid (LDS state in sh); ej: the pipelined step's encode (ENC).
-template <int NW, bool ENC = false>
 __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t bid, const uint8_t* __restrict__ uploads,
                                                    size_t pitch, int M, const double* __restrict__ dampen,
                                                    double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end,
                                                    const int32_t* __restrict__ hdr_block, uint8_t* __restrict__ merged,
-                                                   float* __restrict__ merged_f32, int* __restrict__ err,
-                                                   const EncodeJob& ej = EncodeJob{}) {
-  static_assert(NW >= 3 && NW <= 8, "three consumer waves (+ producer-only waves)");
-  static_assert(!ENC || NW > 3, "the inline encode runs on the producer-only waves");
+                                                   float* __restrict__ merged_f32, int* __restrict__ err) {
+  static_assert(NW == 6 || NW == 8, "three consumer waves + producer-only waves (the planned widths)");
   constexpr int E = kWeaveE, CM = NW;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1757,22 +1664,9 @@ __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t 
     return *reinterpret_cast<const uint4*>(rowbase + (size_t)(c < M ? c : M - 1) * pitch);
   };
   uint4 nxt = load(0);  // in flight while the tables are copied
-  const int li = consumer ? 0 : ci - 3;  // light wave index
-  WeaveEnc<NW> we;
-  if constexpr (ENC) {
-    if (!consumer) weave_enc_load<NW>(we, ej, 0, li, M, g0 + gl, glive);
-  }
   tile_init(sh.t, hdr_block + 4, hdr_block[1], g0, ng);
   uint32_t badacc = 0, emax = 0;
   float A = 0.0f;
-  // a light wave's encode of interval k's rows, the next interval's values in flight
-  auto encode_interval = [&](int k) {
-    if constexpr (ENC) {
-      const WeaveEnc<NW> cur = we;
-      if (k + 1 < nchunks) weave_enc_load<NW>(we, ej, k + 1, li, M, g0 + gl, glive);
-      weave_enc_rows<NW>(cur, ej, k, li, M, g0 + gl, glive, &sh.t.tab, &sh.t.dt);
-    }
-  };
   // interval 0: produce chunk 0
   {
     const uint4 cur = nxt;
@@ -1780,7 +1674,6 @@ __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t 
     const int c = wave;
     weave_item<NW, 0, false>(sh, cur, glive && c < M, c, gl, M, dampen, n_up, walk_end, g0, sh.p[0] + wave * E, badacc,
                              A, nullptr, col, emax);
-    if (!consumer) encode_interval(0);
   }
   __syncthreads();
   // intervals 1 .. nchunks-1: produce chunk k, consume chunk k-1 (always CM clients);
@@ -1809,7 +1702,6 @@ __device__ __forceinline__ void update_weave_block(WeaveShared<NW>& sh, int64_t 
     } else {
       weave_item<NW, 0, false>(sh, cur, glive && c < M, c, gl, M, dampen, n_up, walk_end, g0, pdst, badacc, A,
                                nullptr, col, emax);
-      encode_interval(k);
     }
     FLEET_WTRACE(bid, k, 1);
     __syncthreads();
@@ -2366,12 +2258,6 @@ __global__ void __launch_bounds__(64 * NW) k_update_weave_encode(const uint8_t* 
                                                                  float* __restrict__ merged_f32, int* __restrict__ err,
                                                                  int nU, EncodeJob ej) {
   __shared__ WeaveShared<NW> sh;
-  if (nU == (int)gridDim.x) {  // the encode inside the tiles (NW > 3: light waves)
-    if constexpr (NW > 3)
-      update_weave_block<NW, true>(sh, xcd_tile(blockIdx.x, nU), uploads, pitch, M, dampen, inv_avg, n_up, g_begin,
-                                   g_end, hdr_block, merged, merged_f32, err, ej);
-    return;
-  }
   if ((int)blockIdx.x < nU) {  // block-uniform
     update_weave_block<NW>(sh, xcd_tile(blockIdx.x, nU), uploads, pitch, M, dampen, inv_avg, n_up, g_begin, g_end,
                            hdr_block, merged, merged_f32, err);
@@ -2857,8 +2743,6 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
       if (v == "auto") o->tile = 0;
       else if (v == "classic") o->tile = 1;
       else if (v == "flat") o->tile = 2;
-      else if (v == "weave3") o->tile = 3;
-      else if (v == "weave4") o->tile = 4;
       else if (v == "weave6") o->tile = 6;
       else if (v == "weave8") o->tile = 8;
       else ok = false;
@@ -2870,15 +2754,6 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
       else ok = parse_int(v, 1, kFlatTG, &o->flat_w2);
     } else if (k == "tile_enc_rows") {
       ok = parse_int(v, 1, 4096, &o->tile_enc_rows);
-    } else if (k == "weave_enc") {
-      if (v == "auto") o->weave_enc = 0;
-      else if (v == "inline") o->weave_enc = 1;
-      else if (v == "blocks") o->weave_enc = 2;
-      else ok = false;
-    } else if (k == "tile_mix") {
-      if (v == "auto") o->tile_mix = 0;
-      else if (v == "off") o->tile_mix = 1;
-      else ok = false;
     } else if (k == "fused") {
       if (v == "on") o->fused = 1;
       else if (v == "off") o->fused = 0;
@@ -2888,7 +2763,7 @@ int parse_plan(const char* spec, PlanOverrides* o, std::string* norm, std::strin
     } else if (k == "stage_pieces") {
       ok = parse_int(v, 1, 64, &o->stage_pieces);
     } else {
-      *err = "unknown plan key '" + k + "' (update, grid, tile, flat_w2, tile_enc_prio, weave_enc, tile_enc_rows, tile_mix, fused, "
+      *err = "unknown plan key '" + k + "' (update, grid, tile, flat_w2, tile_enc_prio, tile_enc_rows, fused, "
              "stage_threads, "
              "stage_pieces)";
       return -1;
@@ -2981,24 +2856,6 @@ static int device_simds() {
   return v;
 }
 
-// The two-width split of k_update_tiled's 64-group grid over `groups` groups: nW
-// wide tiles (whole rounds over the CUs: the same count on every CU) and nN 16-group
-// tiles for the rest; nW = -1 (one width) when there is no whole round or no partial one.
-struct TileSplit {
-  int nW;
-  int64_t nN;
-};
-static TileSplit tile_split(int64_t groups, const PlanOverrides& o) {
-  TileSplit t{-1, 0};
-  if (o.tile_mix == 1) return t;
-  const int cus = device_simds() / 4;
-  const int64_t tiles = (groups + 63) / 64, rounds = tiles / cus;
-  if (rounds < 1 || tiles % cus == 0) return t;
-  t.nW = (int)(rounds * cus);
-  t.nN = (groups - (int64_t)t.nW * 64 + 15) / 16;
-  return t;
-}
-
 // k_update_flat's grid for `groups` groups: r whole rounds of kFlatTG-group tiles over the
 // CUs, the rest in tiles of w2 = kFlatTG, 1/2 or 1/4 of it dealt round robin after them.
 // Picks the w2 that leaves the most loaded CU the fewest groups (r * kFlatTG +
@@ -3045,12 +2902,11 @@ struct UpdatePlan {
   int kind;       // 0 stream, 1 tiled, 2 pipe, 3 woven tiles (k_update_weave<nw>), 4 flat tiles
   int nA;         // stream: blocks of group-per-lane waves (the rest a value per lane)
   int64_t blocks; // stream / tiled / pipe grid
-  TileSplit t;    // tiled
   int nw;         // woven tiles: waves per block (3 or 4)
   FlatGrid fg;    // flat tiles
 };
 static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o, bool fused = false) {
-  UpdatePlan p{0, 0, 0, TileSplit{-1, 0}, 0, FlatGrid{0, 0, kFlatTG, kFlatTG}};
+  UpdatePlan p{0, 0, 0, 0, FlatGrid{0, 0, kFlatTG, kFlatTG}};
   if (o.update == 1) p.kind = 0;
   else if (o.update == 2) p.kind = 1;
   else if (o.update == 3) p.kind = 2;
@@ -3097,9 +2953,8 @@ static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o, bool fused
     p.blocks = p.fg.nU;
   } else if (p.kind == 3) {
     p.blocks = (groups + kWeaveTG - 1) / kWeaveTG;
-  } else if (p.kind == 1) {
-    p.t = tile_split(groups, o);
-    p.blocks = p.t.nW >= 0 ? p.t.nW + p.t.nN : (groups + 63) / 64;
+  } else if (p.kind == 1) {  // one width (the fused step's tiles; the update alone under tile=classic)
+    p.blocks = (groups + 63) / 64;
   } else {
     const int64_t plain = (groups + 255) / 256;
     if (o.grid == 1) {
@@ -3126,7 +2981,7 @@ std::string update_kernel_name(int64_t groups) {
   else if (p.kind == 2) snprintf(buf, sizeof buf, "k_update_pipe<16, 1, 5, 0, false>");
   else if (p.kind == 3) snprintf(buf, sizeof buf, "k_update_weave<%d>", p.nw);
   else if (p.kind == 4) snprintf(buf, sizeof buf, "k_update_flat");
-  else snprintf(buf, sizeof buf, "k_update_tiled<64, false, %d, true>", p.t.nW >= 0 ? 16 : 0);  // as rocprofv3 names it
+  else snprintf(buf, sizeof buf, "k_update_tiled_encode<64>");  // its tiles alone, no encode blocks
   return buf;
 }
 
@@ -3135,8 +2990,8 @@ void update_plan_grid(int64_t groups, int* kind, int64_t* blocks, int64_t* n_a, 
   *kind = p.kind;
   *blocks = p.blocks;
   *n_a = p.nA;
-  *n_w = p.t.nW;
-  *n_n = p.t.nN;
+  *n_w = -1;  // one width: blocks = ceil(groups / 64)
+  *n_n = 0;
   if (p.kind == 4) {  // flat: n_w tiles of kFlatTG groups, n_n tiles of n_a groups
     *n_a = p.fg.w2;
     *n_w = p.fg.nW;
@@ -3155,30 +3010,23 @@ std::string update_encode_kernel_name(int64_t groups) {
   return "k_update_pipe<16, 1, 5, 0, false> (with the encode's blocks)";
 }
 
-// k_update_tiled on the plan's grid; KD: with Kardam's side outputs.
-template <bool KD>
+// The classic one-width tiles alone (tile=classic for the update without the encode):
+// k_update_tiled_encode<64> with no encode blocks
 static void launch_tiled(const UpdatePlan& p, const uint8_t* uploads, size_t pitch, int M, const double* d_dampen,
                          double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end, const int32_t* d_hdr_block,
-                         uint8_t* merged, float* merged_f32, int* d_err, const KardamOut& kd, hipStream_t s) {
-  if (p.t.nW >= 0)
-    hipLaunchKernelGGL((k_update_tiled<64, KD, 16, true>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch,
-                       M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd, p.t.nW);
-  else
-    hipLaunchKernelGGL((k_update_tiled<64, KD, 0, true>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch,
-                       M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, kd,
-                       INT32_MAX);
+                         uint8_t* merged, float* merged_f32, int* d_err, hipStream_t s) {
+  hipLaunchKernelGGL((k_update_tiled_encode<64>), dim3((unsigned)p.blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
+                     inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, (int)p.blocks, EncodeJob{});
 }
 
-// k_update_weave<nw> (nw = 3, 4, 6, 8 waves per block)
+// k_update_weave<nw> (nw = 6 or 8 waves per block)
 static void launch_weave(int nw, unsigned blocks, hipStream_t s, const uint8_t* uploads, size_t pitch, int M,
                          const double* d_dampen, double inv_avg, int64_t n_up, int64_t g_begin, int64_t g_end,
                          const int32_t* d_hdr_block, uint8_t* merged, float* merged_f32, int* d_err) {
 #define FLEET_WEAVE_LAUNCH(NWV)                                                                                   \
   hipLaunchKernelGGL(k_update_weave<NWV>, dim3(blocks), dim3(64 * NWV), 0, s, uploads, pitch, M, d_dampen, inv_avg, \
                      n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err)
-  if (nw == 3) FLEET_WEAVE_LAUNCH(3);
-  else if (nw == 4) FLEET_WEAVE_LAUNCH(4);
-  else if (nw == 6) FLEET_WEAVE_LAUNCH(6);
+  if (nw == 6) FLEET_WEAVE_LAUNCH(6);
   else FLEET_WEAVE_LAUNCH(8);
 #undef FLEET_WEAVE_LAUNCH
 }
@@ -3194,8 +3042,8 @@ hipError_t launch_update(const uint8_t* uploads, size_t pitch, int M, const doub
                        d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, INT32_MAX,
                        EncodeJob{});
   else if (p.kind == 1)
-    launch_tiled<false>(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
-                        d_err, KardamOut{}, s);
+    launch_tiled(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err,
+                 s);
   else if (p.kind == 3)
     launch_weave(p.nw, (unsigned)p.blocks, s, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block,
                  merged, merged_f32, d_err);
@@ -3275,10 +3123,12 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   // from the producers, the reduce blocks in the same launch), the wide tiles (side
   // outputs from the tile producers), or the stream kernel's SIMD-balanced grid
   PlanOverrides ok = o;
-  // Kardam's side outputs ride in the flat tiles (kardam_items: narrow widths 16 / 32 /
-  // 64 only) or, when asked for, the classic tiles; not in the woven ones
+  // Kardam's side outputs ride in the flat tiles at every tile size (kardam_items: narrow
+  // widths 16 / 32 / 64 only, so another forced width is ignored here), never in the
+  // classic or woven ones
   const bool flat_ok = o.flat_w2 == 0 || o.flat_w2 == 16 || o.flat_w2 == 32 || o.flat_w2 == 64;
-  ok.tile = (o.tile == 1 || !flat_ok) ? 1 : 2;
+  ok.tile = 2;
+  if (!flat_ok) ok.flat_w2 = 0;
   UpdatePlan p = plan_update(groups, ok);
   if (p.kind == 0 && o.grid == 0) {
     // the stream form on the plain grid unless a grid is asked for: value-per-lane waves
@@ -3306,9 +3156,6 @@ hipError_t launch_update_kardam(const uint8_t* uploads, size_t pitch, int M, con
   if (p.kind == 4)
     hipLaunchKernelGGL(k_update_flat_kd, dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen, inv_avg, n_up,
                        g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.fg, kd);
-  else if (p.kind == 1)
-    launch_tiled<true>(p, uploads, pitch, M, d_dampen, inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32,
-                       d_err, kd, s);
   else
     hipLaunchKernelGGL((k_update_mixed<256, true>), dim3(blocks), dim3(256), 0, s, uploads, pitch, M, d_dampen,
                        inv_avg, n_up, g_begin, g_end, d_hdr_block, merged, merged_f32, d_err, p.nA, kd);
@@ -3370,21 +3217,19 @@ hipError_t launch_update_encode(const uint8_t* uploads, size_t pitch, int M, con
     if (e != hipSuccess) return e;
     return launch_encode_f32(values, n_up, vpitch, M, enc_out, pitch, s);
   }
-  if (p.kind == 3) {  // the woven tiles, then the encode's blocks (64 * nw lanes each), or the encode inside them
+  if (p.kind == 3) {  // the woven tiles, then the encode's blocks (64 * nw lanes each)
     const int nt = 64 * p.nw;
     const int64_t gx = (groups + nt - 1) / nt;
     // 24 rows per encode block as in the other fused forms (the standalone encode's rule
     // gave these blocks one or two rows each, every block copying the tables for them)
     const int rpb = std::min(M, o.tile_enc_rows > 0 ? o.tile_enc_rows : 24);
-    const int64_t nU = p.blocks, nE = (o.weave_enc == 1 && p.nw > 3) ? 0 : gx * ((M + rpb - 1) / rpb);
+    const int64_t nU = p.blocks, nE = gx * ((M + rpb - 1) / rpb);
     const EncodeJob ej{values, n_up, vpitch, enc_out, pitch, groups, gx, M, rpb,
                        o.tile_enc_prio >= 0 ? o.tile_enc_prio : 0};
 #define FLEET_WEAVE_ENC_LAUNCH(NWV)                                                                             \
   hipLaunchKernelGGL(k_update_weave_encode<NWV>, dim3((unsigned)(nU + nE)), dim3(64 * NWV), 0, s, uploads, pitch, M, \
                      d_dampen, inv_avg, n_up, (int64_t)0, groups, d_hdr_block, merged, merged_f32, d_err, (int)nU, ej)
-    if (p.nw == 3) FLEET_WEAVE_ENC_LAUNCH(3);
-    else if (p.nw == 4) FLEET_WEAVE_ENC_LAUNCH(4);
-    else if (p.nw == 6) FLEET_WEAVE_ENC_LAUNCH(6);
+    if (p.nw == 6) FLEET_WEAVE_ENC_LAUNCH(6);
     else FLEET_WEAVE_ENC_LAUNCH(8);
 #undef FLEET_WEAVE_ENC_LAUNCH
     return hipGetLastError();

@@ -520,10 +520,10 @@ int fleet_update_plan_grid(size_t len, int* kind, int64_t* blocks, int64_t* n_a,
 /* Launch-plan overrides, process-wide (experiments, and tests that run every
  * launch variant on small inputs; results are identical under every plan). spec =
  * comma-separated key=value items: update=auto|stream|tiled|pipe, grid=auto|plain|balanced|
- * lanes (the stream grid), tile=auto|classic|flat|weave3|weave4|weave6|weave8 and
+ * lanes (the stream grid; lanes = every group a value per lane, the balanced grid's tail
+ * form, for tests on small inputs), tile=auto|classic|flat|weave6|weave8 and
  * flat_w2=auto|1..64, tile_enc_prio=auto|0..3 (the tiles' form; the flat grid's
- * narrow width; the tiles' fused encode blocks' issue priority), tile_mix=auto|off,
- * tile_enc_rows=N, weave_enc=auto|inline|blocks,
+ * narrow width; the tiles' fused encode blocks' issue priority), tile_enc_rows=N,
  * fused=on|off (the pipelined step as one launch or two), stage_threads=1..64,
  * stage_pieces=1..64 (host staging); ""
  * restores the measured default. An unknown key or value rejects the whole spec

@@ -1,7 +1,8 @@
 # A/B/C...: several builds of the C-ABI (LIBS = space-separated label=path.so[,VAR=VALUE...]) on WORKLOADS,
 # alternating per repetition on one box; one line per run with the aggregation kernel, the
 # standalone encode, the pipelined step's kernel and the step time (bench events)
-set -u
+set -u -o pipefail
+mkdir -p gpurun_out
 WL=${WORKLOADS:-synth1m_256}
 for rep in $(seq ${REPS:-2}); do
   for w in $WL; do

@@ -24,7 +24,7 @@
 #   plans:W:N:MODE:P1|P2|..  same-process A/B of launch plans (scripts/plan_ab.py; '-' = default,
 #                    ';' between a plan's keys)
 #   env:VAR=VALUE    export VAR for the steps after it (env:VAR= unsets it), e.g.
-#                    'env:FLEET_EXPERIMENTS=update=tiled;tile=weave4' (quote the ';')
+#                    'env:FLEET_EXPERIMENTS=update=tiled;tile=weave6' (quote the ';')
 set -u -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$PWD}"
 TAG=${TAG:-run}

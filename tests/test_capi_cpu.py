@@ -70,7 +70,8 @@ def test_plan_overrides_validated_on_host():
     reaches the launch path (kernels.hip reads no other)."""
     import os
     F.set_plan("")
-    for bad in ("update=fast", "k_update=stream", "grid", "stage_pieces=0", "fused=1", "update=stream,tile_mix=no"):
+    for bad in ("update=fast", "k_update=stream", "grid", "stage_pieces=0", "fused=1", "update=stream,tile_mix=off",
+                "update=tiled,tile=weave3", "update=stream,stream_enc=inline", "update=tiled,weave_enc=inline"):
         with pytest.raises(F.FleetError):
             F.set_plan(bad)
         assert F.plan() == ""
@@ -88,10 +89,8 @@ GRID_SIZES = [1, 2, 16, 17, 83, 84, 85, 255, 256, 257, 6_667, 7_654, 16_668, 32_
 
 
 @pytest.mark.parametrize("spec", ["", "update=stream", "update=stream,grid=plain", "update=stream,grid=lanes",
-                                  "update=tiled", "update=tiled,tile=classic", "update=tiled,tile=classic,tile_mix=off",
-                                  "update=pipe",
-                                  "update=tiled,tile=weave3", "update=tiled,tile=weave4",
-                                  "update=tiled,tile=weave8", "update=tiled,tile=flat",
+                                  "update=tiled", "update=tiled,tile=classic", "update=pipe",
+                                  "update=tiled,tile=weave6", "update=tiled,tile=weave8", "update=tiled,tile=flat",
                                   "update=tiled,tile=flat,flat_w2=16",
                                   "update=tiled,tile=flat,flat_w2=64", "update=tiled,tile=flat,flat_w2=21"])
 def test_launch_grid_covers_every_group(spec):
@@ -113,13 +112,8 @@ def test_launch_grid_covers_every_group(spec):
                 else:
                     rest = groups - covered_a
                     assert b - g["n_a"] == -(-rest // 84), (groups, g)
-            elif g["kind"] == "tiled":
-                if g["n_w"] >= 0:
-                    cov = 64 * g["n_w"] + 16 * g["n_n"]
-                    assert b == g["n_w"] + g["n_n"] and cov >= groups and cov - 16 < groups, (groups, g)
-                    assert 64 * g["n_w"] < groups, (groups, g)
-                else:
-                    assert b == -(-groups // 64), (groups, g)
+            elif g["kind"] == "tiled":  # one width (tile=classic: the fused step's tiles alone)
+                assert g["n_w"] < 0 and b == -(-groups // 64), (groups, g)
             elif g["kind"] == "weave":
                 assert b == -(-groups // 64), (groups, g)
             elif g["kind"] == "flat":  # n_w 64-group tiles, then n_n tiles of 2^n_a groups, the last ragged

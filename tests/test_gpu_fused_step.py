@@ -96,12 +96,8 @@ def test_update_encode_rejects_overlap_and_bad_text(codec):
                                          ("update=pipe", "k_update_pipe<16, 1, 5, 0, false> (with the encode's blocks)"),
                                          ("update=stream", "k_update_encode<256>"),
                                          ("update=stream,grid=lanes", "k_update_encode<256>"),
-                                         ("update=tiled,tile=weave3", "k_update_weave_encode<3>"),
-                                         ("update=tiled,tile=weave4", "k_update_weave_encode<4>"),
+                                         ("update=tiled,tile=weave6", "k_update_weave_encode<6>"),
                                          ("update=tiled,tile=weave8", "k_update_weave_encode<8>"),
-                                         ("update=tiled,tile=weave4,weave_enc=inline", "k_update_weave_encode<4>"),
-                                         ("update=tiled,tile=weave6,weave_enc=inline", "k_update_weave_encode<6>"),
-                                         ("update=tiled,tile=weave8,weave_enc=inline", "k_update_weave_encode<8>"),
                                          ("update=tiled,tile=classic", "k_update_tiled_encode<64>"),
                                          ("update=tiled,tile=flat", "k_update_flat"),
                                          ("update=tiled,tile=flat,flat_w2=16", "k_update_flat"),
@@ -122,7 +118,7 @@ def test_plan_overrides_are_validated():
     F.set_plan("")
     assert F.plan() == ""
     for bad in ("update=fast", "k_update=stream", "grid", "stage_threads=0", "stage_threads=65", "fused=1",
-                "update=stream,tile_mix=maybe"):
+                "update=stream,tile_mix=off", "update=tiled,tile=weave4"):
         with pytest.raises(F.FleetError):
             F.set_plan(bad)
         assert F.plan() == ""

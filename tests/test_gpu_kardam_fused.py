@@ -34,13 +34,12 @@ def test_kardam_side_outputs(codec, oracle, layout, M):
 
 @pytest.mark.parametrize("spec", ["update=stream,grid=plain", "update=stream,grid=lanes", "update=stream",
                                   "update=tiled", "update=tiled,flat_w2=16", "update=tiled,flat_w2=32",
-                                  "update=tiled,flat_w2=21", "update=tiled,tile=classic",
-                                  "update=tiled,tile=classic,tile_mix=off", "update=pipe"])
+                                  "update=tiled,flat_w2=21", "update=tiled,tile=classic", "update=pipe"])
 def test_kardam_side_outputs_under_plans(codec, oracle, plan, spec):
     """Every launch plan's Kardam form on ragged sizes: the stream kernel's group-per-
     lane and value-per-lane blocks (k_update_mixed<256, true>), the flat tiles with each
-    narrow width (k_update_flat_kd; a width other than 16 / 32 / 64 falls back to the
-    classic tiles), both classic tile grids, the pipelined tiles."""
+    narrow width (k_update_flat_kd; a width other than 16 / 32 / 64, or tile=classic,
+    keeps the flat tiles at their planned widths), the pipelined tiles."""
     plan(spec)
     for layout, M in ((synthetic(3001), 4), (synthetic(50_003), 3), (MNIST, 5)):
         check_side_outputs(codec, oracle, layout, M)

@@ -327,10 +327,9 @@ def test_update_stream_grids(codec, oracle, plan, grid):
         assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
 
 
-@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile=classic,tile_mix=off", "update=stream",
-                                  "update=stream,grid=plain", "update=stream,grid=lanes",
-                                  "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4",
-                                  "update=tiled,tile=weave6", "update=tiled,tile=weave8", "update=tiled,tile=flat",
+@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=stream", "update=stream,grid=plain",
+                                  "update=stream,grid=lanes", "update=tiled,tile=classic", "update=tiled,tile=weave6",
+                                  "update=tiled,tile=weave8", "update=tiled,tile=flat",
                                   "update=tiled,tile=flat,flat_w2=16"])
 def test_update_large_magnitudes_slow_path(codec, oracle, plan, spec):
     """Values far outside the fast path (|x| >= 1, digits != 0, >= 2^31) force
@@ -354,88 +353,9 @@ def test_update_large_magnitudes_slow_path(codec, oracle, plan, spec):
     assert codec.update(ups, d) == oracle.update_fused(ups, d, hm) == oracle.update_faithful(ups, d)
 
 
-@pytest.mark.parametrize("mix", ["auto", "off"])
-def test_update_two_width_tiles(codec, oracle, plan, mix):
-    """k_update_tiled's two-width grid (whole rounds of 64-group tiles, the rest in
-    16-group tiles; tile_mix=off the one-width grid): 16,668 groups = one round of
-    256 wide tiles + 284 groups, the last narrow tile ragged; large magnitudes force
-    the in-stage fallbacks and the general-chain recompute in both tile widths."""
-    plan(f"update=tiled,tile=classic,tile_mix={mix}")
-    lay = synthetic(50_003)
-    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
-    rng = np.random.default_rng(11)
-    M = 6
-    ups = []
-    for c in range(M):
-        v = oracle.synth_upload(5, c, list(lay.w_sizes), list(lay.b_sizes))
-        big = (rng.random(len(v)) < 0.05) & (hm == 0)  # header slots keep the layout
-        v[big] = (np.exp(rng.uniform(0, 21, big.sum())) * rng.choice([-1, 1], big.sum())).astype(np.float32)
-        v[-5:-1] = [9.99e8, -9.99e8, 2.1e9, 0.999999]
-        ups.append(oracle.encode_floats(v))
-    d = [1.0, 7.5, 0.25, 10.0, 1 / 3, 1.0]
-    want = "k_update_tiled<64, false, %s, true>" % ("16" if mix == "auto" else "0")
-    assert F.update_kernel(len(ups[0])) == want
-    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
-
-
-@pytest.mark.parametrize("n,kernel", [(90_001, "k_update_weave<8>"), (160_003, "k_update_flat")])
-def test_update_default_small_windows(codec, oracle, plan, n, kernel):
-    """The default plan's update alone on windows the woven 8-wave tiles take (24 k groups
-    up to three 64-group tiles per CU) and just past them (the flat tiles), with large
-    magnitudes in a few slots (in-stage fallbacks, the general-chain recompute) and a
-    ragged last group."""
-    plan("")
-    lay = synthetic(n)
-    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
-    rng = np.random.default_rng(n)
-    M = 5
-    ups = []
-    for c in range(M):
-        v = oracle.synth_upload(21, c, list(lay.w_sizes), list(lay.b_sizes))
-        big = (rng.random(len(v)) < 0.01) & (hm == 0)
-        v[big] = (np.exp(rng.uniform(0, 21, big.sum())) * rng.choice([-1, 1], big.sum())).astype(np.float32)
-        ups.append(oracle.encode_floats(v))
-    d = [1.0, 0.5, 1 / 3, 2.0, 0.1]
-    assert F.update_kernel(len(ups[0])) == kernel
-    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
-
-
-@pytest.mark.parametrize("w2", ["auto", "16", "21", "32", "64"])
-def test_update_flat_tiles(codec, oracle, plan, w2):
-    """k_update_flat's one-round grid: whole rounds of 64-group tiles, then tiles of
-    w2 groups (21: a pass of 24 whole clients leaves 8 lanes idle; 16,668 groups = one
-    round of 256 wide tiles + 284 groups, the last
-    narrow tile ragged; cifar10: six rounds + 6,319 groups); large magnitudes force the
-    in-stage fallbacks and the general-chain recompute; dampening factors that are not
-    binary32 values take the per-lane f64 product in the narrow tiles."""
-    plan(f"update=tiled,tile=flat,flat_w2={w2}")
-    lay = synthetic(50_003)
-    hm = oracle.header_mask(list(lay.w_sizes), list(lay.b_sizes))
-    rng = np.random.default_rng(13)
-    M = 7
-    ups = []
-    for c in range(M):
-        v = oracle.synth_upload(9, c, list(lay.w_sizes), list(lay.b_sizes))
-        big = (rng.random(len(v)) < 0.05) & (hm == 0)  # header slots keep the layout
-        v[big] = (np.exp(rng.uniform(0, 21, big.sum())) * rng.choice([-1, 1], big.sum())).astype(np.float32)
-        v[-5:-1] = [9.99e8, -9.99e8, 2.1e9, 0.999999]
-        ups.append(oracle.encode_floats(v))
-    d = [1.0, 7.5, 0.25, 10.0, 1 / 3, 1.0, 0.1]
-    assert F.update_kernel(len(ups[0])) == "k_update_flat"
-    g = F.update_plan_grid(len(ups[0]))
-    if w2 != "auto":
-        assert g["n_a"] == int(w2)
-    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
-    ups = uploads_for(oracle, CIFAR10, 5, seed=3)
-    d = policy("inverse", 5)
-    hm = oracle.header_mask(list(CIFAR10.w_sizes), list(CIFAR10.b_sizes))
-    assert codec.update(ups, d) == oracle.update_fused(ups, d, hm)
-
-
-@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile=classic,tile_mix=off", "update=stream",
-                                  "update=stream,grid=plain", "update=stream,grid=lanes",
-                                  "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4",
-                                  "update=tiled,tile=weave6", "update=tiled,tile=weave8", "update=tiled,tile=flat",
+@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=stream", "update=stream,grid=plain",
+                                  "update=stream,grid=lanes", "update=tiled,tile=classic", "update=tiled,tile=weave6",
+                                  "update=tiled,tile=weave8", "update=tiled,tile=flat",
                                   "update=tiled,tile=flat,flat_w2=16"])
 def test_update_modes(codec, oracle, plan, spec):
     """Every aggregation kernel (pipelined and two-phase tiles for small
@@ -450,10 +370,9 @@ def test_update_modes(codec, oracle, plan, spec):
         assert codec.update(ups, d) == oracle.update_fused(ups, d, hm), (lay.name, M)
 
 
-@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=tiled,tile=classic,tile_mix=off", "update=stream",
-                                  "update=stream,grid=plain", "update=stream,grid=lanes",
-                                  "update=tiled,tile=classic", "update=tiled,tile=weave3", "update=tiled,tile=weave4",
-                                  "update=tiled,tile=weave6", "update=tiled,tile=weave8", "update=tiled,tile=flat",
+@pytest.mark.parametrize("spec", ["update=pipe", "update=tiled", "update=stream", "update=stream,grid=plain",
+                                  "update=stream,grid=lanes", "update=tiled,tile=classic", "update=tiled,tile=weave6",
+                                  "update=tiled,tile=weave8", "update=tiled,tile=flat",
                                   "update=tiled,tile=flat,flat_w2=16"])
 @pytest.mark.parametrize("extra", [200, 201])
 def test_update_keep_slots_past_the_walk(codec, oracle, plan, spec, extra):

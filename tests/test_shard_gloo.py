@@ -1,4 +1,5 @@
-"""N>1 path on CPU: element-range sharding + all_gather over gloo, world_size 2 and 3.
+"""N>1 path on CPU: element-range sharding + all_gather over gloo, world_size 2, 3 and 8
+(the node size bench.py's scaling run uses).
 
 fleet_amd.shard.ShardedUpdater is the product's multi-GPU driver; here its two
 per-rank compute hooks (layout, local_update) are replaced by the oracle so the
@@ -97,7 +98,7 @@ def _rank_main(rank, world, port, cases, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_update_gloo_matches_single_process(world, tmp_path):
     import torch.multiprocessing as mp
     cases = [("mnist", 4), ("1000", 3), ("1001", 1), ("4", 2)]
@@ -194,7 +195,7 @@ def test_client_sharded_needs_explicit_approx():
         cs.update([b"AAAA"], [1.0])
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_client_sharded_approx_gloo(world, tmp_path):
     """The approximate client-sharded mode: header slots exact, payload within a
     bound of the exact chain (|diff| <= 2e-6 max|exact| on the synthetic mix), the
