@@ -27,7 +27,8 @@
 // the dictionary order; NaN/inf match nothing (fabsf(NaN) < tol is false),
 // each creates an entry and prints index -1 (the reference's pass 2).
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
 #include <cstdint>
@@ -38,6 +39,22 @@
 #include "decimal6.h"
 
 namespace fleet {
+
+// Device-wide sums and the key sort on rocPRIM, AMD's own primitives library (its
+// wave-level scans and LDS radix passes are tuned for CDNA; no CUB-compatible layer).
+// Each call with tmp == nullptr only sizes the temporary storage, as in rocPRIM.
+template <class T>
+static hipError_t inclusive_sum(void* tmp, size_t& bytes, const T* in, T* out, size_t n, hipStream_t s) {
+  return rocprim::inclusive_scan(tmp, bytes, in, out, n, rocprim::plus<T>(), s);
+}
+template <class T>
+static hipError_t exclusive_sum(void* tmp, size_t& bytes, const T* in, T* out, size_t n, hipStream_t s) {
+  return rocprim::exclusive_scan(tmp, bytes, in, out, T(0), n, rocprim::plus<T>(), s);
+}
+static hipError_t sort_pairs(void* tmp, size_t& bytes, const uint32_t* keys, uint32_t* keys_out, const int32_t* vals,
+                             int32_t* vals_out, size_t n, hipStream_t s) {
+  return rocprim::radix_sort_pairs(tmp, bytes, keys, keys_out, vals, vals_out, n, 0u, 32u, s);
+}
 namespace {
 
 constexpr float kTol = 0.00000001f;
@@ -384,16 +401,16 @@ hipError_t model_quantize_index(const float* d_w, const int32_t* h_dims, int n_m
   MC_TRY(is_creator.alloc(n));
   hipLaunchKernelGGL(k_dict_keys, dim3(nb(n)), dim3(256), 0, s, d_wq, n, key.p, idx.p);
   size_t tmp_bytes = 0, t2 = 0, t3 = 0;
-  MC_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, key.p, key2.p, idx.p, sidx.p, (int)n, 0, 32, s));
-  MC_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, t2, start.p, cid.p, (int)n, s));
-  MC_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t3, flag32.p, rank.p, (int)n, s));
+  MC_TRY(sort_pairs(nullptr, tmp_bytes, key.p, key2.p, idx.p, sidx.p, n, s));
+  MC_TRY(inclusive_sum(nullptr, t2, start.p, cid.p, n, s));
+  MC_TRY(exclusive_sum(nullptr, t3, flag32.p, rank.p, n, s));
   tmp_bytes = std::max(tmp_bytes, std::max(t2, t3));
   DevBuf<uint8_t> tmp;
   MC_TRY(tmp.alloc(tmp_bytes));
-  MC_TRY(hipcub::DeviceRadixSort::SortPairs(tmp.p, tmp_bytes, key.p, key2.p, idx.p, sidx.p, (int)n, 0, 32, s));
+  MC_TRY(sort_pairs(tmp.p, tmp_bytes, key.p, key2.p, idx.p, sidx.p, n, s));
   hipLaunchKernelGGL(k_dict_starts, dim3(nb(n)), dim3(256), 0, s, d_wq, sidx.p, n, start.p);
   size_t tb = tmp_bytes;
-  MC_TRY(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, start.p, cid.p, (int)n, s));
+  MC_TRY(inclusive_sum(tmp.p, tb, start.p, cid.p, n, s));
   int32_t n_clusters = 0;
   MC_TRY(hipMemcpyAsync(&n_clusters, cid.p + (n - 1), sizeof(int32_t), hipMemcpyDeviceToHost, s));
   MC_TRY(hipStreamSynchronize(s));
@@ -405,7 +422,7 @@ hipError_t model_quantize_index(const float* d_w, const int32_t* h_dims, int n_m
                      creator.p, is_creator.p, scratch.p);
   hipLaunchKernelGGL(k_dict_u8_to_i32, dim3(nb(n)), dim3(256), 0, s, is_creator.p, n, flag32.p);
   tb = tmp_bytes;
-  MC_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, flag32.p, rank.p, (int)n, s));
+  MC_TRY(exclusive_sum(tmp.p, tb, flag32.p, rank.p, n, s));
   int32_t last_rank = 0, last_flag = 0;
   MC_TRY(hipMemcpyAsync(&last_rank, rank.p + (n - 1), sizeof(int32_t), hipMemcpyDeviceToHost, s));
   MC_TRY(hipMemcpyAsync(&last_flag, flag32.p + (n - 1), sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -468,10 +485,10 @@ hipError_t model_index_text(const int32_t* d_index, const int32_t* h_dims, int n
   MC_TRY(hipMemcpyAsync(d_off.p, off.data(), sizeof(int64_t) * (n_mats + 1), hipMemcpyHostToDevice, s));
   hipLaunchKernelGGL(k_text_len, dim3(nb(n)), dim3(256), 0, s, d_index, n, d_off.p, n_mats, len.p);
   size_t tb = 0;
-  MC_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, len.p, pos.p, (int)n, s));
+  MC_TRY(exclusive_sum(nullptr, tb, len.p, pos.p, n, s));
   DevBuf<uint8_t> tmp;
   MC_TRY(tmp.alloc(tb));
-  MC_TRY(hipcub::DeviceScan::ExclusiveSum(tmp.p, tb, len.p, pos.p, (int)n, s));
+  MC_TRY(exclusive_sum(tmp.p, tb, len.p, pos.p, n, s));
   int64_t last_pos = 0, last_len = 0;
   MC_TRY(hipMemcpyAsync(&last_pos, pos.p + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, s));
   MC_TRY(hipMemcpyAsync(&last_len, len.p + (n - 1), sizeof(int64_t), hipMemcpyDeviceToHost, s));
@@ -519,10 +536,10 @@ hipError_t model_read_index(const uint8_t* d_text, int64_t len, int64_t n_w, con
   MC_TRY(hipMemsetAsync(bad.p, 0, sizeof(int), s));
   hipLaunchKernelGGL(k_read_starts, dim3(nb(len)), dim3(256), 0, s, d_text, len, st.p);
   size_t tb = 0;
-  MC_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb, st.p, tok.p, (int)len, s));
+  MC_TRY(inclusive_sum(nullptr, tb, st.p, tok.p, (size_t)len, s));
   DevBuf<uint8_t> tmp;
   MC_TRY(tmp.alloc(tb));
-  MC_TRY(hipcub::DeviceScan::InclusiveSum(tmp.p, tb, st.p, tok.p, (int)len, s));
+  MC_TRY(inclusive_sum(tmp.p, tb, st.p, tok.p, (size_t)len, s));
   hipLaunchKernelGGL(k_read_tokens, dim3(nb(len)), dim3(256), 0, s, d_text, len, st.p, tok.p, n_w, d_keys, d_vals,
                      n_keys, d_w, bad.p);
   MC_TRY(hipGetLastError());

@@ -135,3 +135,14 @@ def test_launch_grid_covers_every_group(spec):
                 assert g["kind"] == want, (spec, g)
     finally:
         F.set_plan("")
+
+
+def test_no_cuda_compat_layers_in_the_product():
+    """The product sources use AMD's own libraries directly: no hipCUB (the CUB-compatible
+    layer; the model codec's sort and scans are rocPRIM), no CUDA headers or dual paths."""
+    import glob
+    import os
+    for path in glob.glob(os.path.join(F.ROOT, "fleet_amd", "csrc", "*")):
+        src = open(path).read()
+        assert "hipcub" not in src, path
+        assert "cuda_runtime" not in src and "__CUDACC__" not in src and "__HIP_PLATFORM_AMD__" not in src, path
