@@ -142,13 +142,16 @@ __device__ __forceinline__ uint32_t b64_decode_group(uint4 w, const B64Tables* t
   const uint32_t words[4] = {w.x, w.y, w.z, w.w};
   uint32_t V[4];
   uint32_t bad = 0;
+  // read sign-extended like b64_decode_group_full (the two share their first loads):
+  // the invalid marker is -1, bit 31 of its sextet word
+  const int8_t* from = reinterpret_cast<const int8_t*>(t->from);
 #pragma unroll
   for (int qd = 0; qd < 4; ++qd) {
-    uint32_t s0 = t->from[words[qd] & 0xff];
-    uint32_t s1 = t->from[(words[qd] >> 8) & 0xff];
-    uint32_t s2 = t->from[(words[qd] >> 16) & 0xff];
-    uint32_t s3 = t->from[words[qd] >> 24];
-    bad |= ((s0 >> 7) | ((s1 >> 7) << 1) | ((s2 >> 7) << 2) | ((s3 >> 7) << 3)) << (4 * qd);
+    const uint32_t s0 = (uint32_t)(int32_t)from[words[qd] & 0xff];
+    const uint32_t s1 = (uint32_t)(int32_t)from[(words[qd] >> 8) & 0xff];
+    const uint32_t s2 = (uint32_t)(int32_t)from[(words[qd] >> 16) & 0xff];
+    const uint32_t s3 = (uint32_t)(int32_t)from[words[qd] >> 24];
+    bad |= ((s0 >> 31) | ((s1 >> 31) << 1) | ((s2 >> 31) << 2) | ((s3 >> 31) << 3)) << (4 * qd);
     V[qd] = ((s0 & 63) << 18) | ((s1 & 63) << 12) | ((s2 & 63) << 6) | (s3 & 63);
   }
   // bytes of quad q are V[q] big-endian; codes are little-endian int32
@@ -158,41 +161,57 @@ __device__ __forceinline__ uint32_t b64_decode_group(uint4 w, const B64Tables* t
   return bad;
 }
 
-// (a << k) | b as ONE v_lshl_or_b32: written out, the two-level shift-or of four sextets
-// is re-associated by the compiler into four instructions (two shifts, v_lshl_or,
-// v_or3); three v_lshl_or are the minimum
-template <int K>
-__device__ __forceinline__ uint32_t lshl_or(uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(K), "v"(b));
-  return r;
-}
-// the 24 bits of one quad's sextets s0..s3 (big-endian)
-__device__ __forceinline__ uint32_t quad24(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3) {
-  return lshl_or<12>(lshl_or<6>(s0, s1), lshl_or<6>(s2, s3));
+// The shift-or assembly of four 6-bit sextets into 24 bits, written out, is re-associated
+// by the compiler into four instructions per quad (two shifts, v_lshl_or, v_or3); three
+// v_lshl_or are the minimum, so they are written as asm.
+// A whole group's four quads (s[4q..4q+3] -> 24 bits, big-endian) in ONE asm block of
+// twelve v_lshl_or: every sextet is an input, so the compiler issues all sixteen table
+// reads before it (one asm per quad made it wait on each quad's reads in turn)
+__device__ __forceinline__ void group24(const uint32_t (&s)[16], uint32_t (&V)[4]) {
+  uint32_t a0, b0, a1, b1, a2, b2, a3, b3;
+  asm("v_lshl_or_b32 %4, %12, 6, %13\n\t"
+      "v_lshl_or_b32 %5, %14, 6, %15\n\t"
+      "v_lshl_or_b32 %6, %16, 6, %17\n\t"
+      "v_lshl_or_b32 %7, %18, 6, %19\n\t"
+      "v_lshl_or_b32 %8, %20, 6, %21\n\t"
+      "v_lshl_or_b32 %9, %22, 6, %23\n\t"
+      "v_lshl_or_b32 %10, %24, 6, %25\n\t"
+      "v_lshl_or_b32 %11, %26, 6, %27\n\t"
+      "v_lshl_or_b32 %0, %4, 12, %5\n\t"
+      "v_lshl_or_b32 %1, %6, 12, %7\n\t"
+      "v_lshl_or_b32 %2, %8, 12, %9\n\t"
+      "v_lshl_or_b32 %3, %10, 12, %11"
+      : "=v"(V[0]), "=v"(V[1]), "=v"(V[2]), "=v"(V[3]), "=&v"(a0), "=&v"(b0), "=&v"(a1), "=&v"(b1), "=&v"(a2),
+        "=&v"(b2), "=&v"(a3), "=&v"(b3)
+      : "v"(s[0]), "v"(s[1]), "v"(s[2]), "v"(s[3]), "v"(s[4]), "v"(s[5]), "v"(s[6]), "v"(s[7]), "v"(s[8]), "v"(s[9]),
+        "v"(s[10]), "v"(s[11]), "v"(s[12]), "v"(s[13]), "v"(s[14]), "v"(s[15]));
 }
 
 // Same decode for a full group (all 16 chars carry data): returns nonzero if any
 // char is outside the alphabet. Sextets compose by shift-or; no per-char mask:
 // valid entries are 0..63 and the invalid marker 0xff has bit 6 set, so the OR of
 // the group's sextets flags it (the codes are garbage then, and the caller fails).
+// The sextets are read sign-extended (ds_read_i8): the invalid marker 0xff becomes -1,
+// whose set high bits survive the shift-or assembly in bits 24-31 of the quad's word
+// wherever the char sits (s3 or s2 in t2 = s2 << 6 | s3 fill bits 6..31; s1 or s0 in
+// t1 fill bits 6..31 / 12..31, shifted by 12 into 18..31 / 24..31), so one OR of the
+// four words flags the group; valid quads stay below 2^24.
 __device__ __forceinline__ uint32_t b64_decode_group_full(uint4 w, const B64Tables* t, int32_t codes[3]) {
   const uint32_t words[4] = {w.x, w.y, w.z, w.w};
-  uint32_t V[4];
-  uint32_t anyf = 0;
+  const int8_t* from = reinterpret_cast<const int8_t*>(t->from);
+  uint32_t sx[16], V[4];
 #pragma unroll
   for (int qd = 0; qd < 4; ++qd) {
-    const uint32_t s0 = t->from[words[qd] & 0xff];
-    const uint32_t s1 = t->from[(words[qd] >> 8) & 0xff];
-    const uint32_t s2 = t->from[(words[qd] >> 16) & 0xff];
-    const uint32_t s3 = t->from[words[qd] >> 24];
-    anyf |= s0 | s1 | s2 | s3;
-    V[qd] = quad24(s0, s1, s2, s3);  // (an invalid char's garbage: the call fails on anyf)
+    sx[4 * qd] = (uint32_t)(int32_t)from[words[qd] & 0xff];
+    sx[4 * qd + 1] = (uint32_t)(int32_t)from[(words[qd] >> 8) & 0xff];
+    sx[4 * qd + 2] = (uint32_t)(int32_t)from[(words[qd] >> 16) & 0xff];
+    sx[4 * qd + 3] = (uint32_t)(int32_t)from[words[qd] >> 24];
   }
+  group24(sx, V);
   codes[0] = (int32_t)__builtin_amdgcn_perm(V[1], V[0], 0x06000102u);
   codes[1] = (int32_t)__builtin_amdgcn_perm(V[2], V[1], 0x05060001u);
   codes[2] = (int32_t)__builtin_amdgcn_perm(V[3], V[2], 0x04050600u);
-  return anyf & 0x40u;
+  return (V[0] | V[1] | V[2] | V[3]) >> 24;
 }
 
 // One code of a group from the two 4-char quads that hold its bytes: value e of
@@ -205,31 +224,32 @@ __device__ __forceinline__ uint32_t b64_pair_selector(int e) {
 __device__ __forceinline__ uint32_t b64_decode_pair_full(uint32_t w0, uint32_t w1, uint32_t sel, const B64Tables* t,
                                                          int32_t& code) {
   const uint32_t words[2] = {w0, w1};
-  uint32_t V[2], anyf = 0;
+  const int8_t* from = reinterpret_cast<const int8_t*>(t->from);  // sign-extended: see b64_decode_group_full
+  uint32_t V[2];
 #pragma unroll
   for (int qd = 0; qd < 2; ++qd) {
-    const uint32_t s0 = t->from[words[qd] & 0xff];
-    const uint32_t s1 = t->from[(words[qd] >> 8) & 0xff];
-    const uint32_t s2 = t->from[(words[qd] >> 16) & 0xff];
-    const uint32_t s3 = t->from[words[qd] >> 24];
-    anyf |= s0 | s1 | s2 | s3;
-    V[qd] = quad24(s0, s1, s2, s3);
+    const uint32_t s0 = (uint32_t)(int32_t)from[words[qd] & 0xff];
+    const uint32_t s1 = (uint32_t)(int32_t)from[(words[qd] >> 8) & 0xff];
+    const uint32_t s2 = (uint32_t)(int32_t)from[(words[qd] >> 16) & 0xff];
+    const uint32_t s3 = (uint32_t)(int32_t)from[words[qd] >> 24];
+    V[qd] = (((s0 << 6) | s1) << 12) | ((s2 << 6) | s3);
   }
   code = (int32_t)__builtin_amdgcn_perm(V[1], V[0], sel);
-  return anyf & 0x40u;
+  return (V[0] | V[1]) >> 24;
 }
 // per-char mask of chars outside the alphabet (bit i = char 4e + i)
 __device__ __forceinline__ uint32_t b64_decode_pair(uint32_t w0, uint32_t w1, uint32_t sel, const B64Tables* t,
                                                     int32_t& code) {
   const uint32_t words[2] = {w0, w1};
+  const int8_t* from = reinterpret_cast<const int8_t*>(t->from);
   uint32_t V[2], bad = 0;
 #pragma unroll
   for (int qd = 0; qd < 2; ++qd) {
-    const uint32_t s0 = t->from[words[qd] & 0xff];
-    const uint32_t s1 = t->from[(words[qd] >> 8) & 0xff];
-    const uint32_t s2 = t->from[(words[qd] >> 16) & 0xff];
-    const uint32_t s3 = t->from[words[qd] >> 24];
-    bad |= ((s0 >> 7) | ((s1 >> 7) << 1) | ((s2 >> 7) << 2) | ((s3 >> 7) << 3)) << (4 * qd);
+    const uint32_t s0 = (uint32_t)(int32_t)from[words[qd] & 0xff];  // sign-extended, as above
+    const uint32_t s1 = (uint32_t)(int32_t)from[(words[qd] >> 8) & 0xff];
+    const uint32_t s2 = (uint32_t)(int32_t)from[(words[qd] >> 16) & 0xff];
+    const uint32_t s3 = (uint32_t)(int32_t)from[words[qd] >> 24];
+    bad |= ((s0 >> 31) | ((s1 >> 31) << 1) | ((s2 >> 31) << 2) | ((s3 >> 31) << 3)) << (4 * qd);
     V[qd] = ((s0 & 63) << 18) | ((s1 & 63) << 12) | ((s2 & 63) << 6) | (s3 & 63);
   }
   code = (int32_t)__builtin_amdgcn_perm(V[1], V[0], sel);
@@ -245,15 +265,33 @@ __device__ __forceinline__ uint4 b64_encode_group(const int32_t codes[3], const 
   V[1] = __builtin_amdgcn_perm(c1, c0, 0x0c030405u);  // b3<<16 | b4<<8 | b5
   V[2] = __builtin_amdgcn_perm(c2, c1, 0x0c020304u);  // b6<<16 | b7<<8 | b8
   V[3] = __builtin_amdgcn_perm(0u, c2, 0x0c010203u);  // b9<<16 | b10<<8 | b11
-  uint32_t out[4];
+  uint32_t ch[16];
 #pragma unroll
   for (int qd = 0; qd < 4; ++qd) {
-    uint32_t a = t->to[(V[qd] >> 18) & 63];
-    uint32_t b = t->to[(V[qd] >> 12) & 63];
-    uint32_t c = t->to[(V[qd] >> 6) & 63];
-    uint32_t d = t->to[V[qd] & 63];
-    out[qd] = lshl_or<16>(lshl_or<8>(d, c), lshl_or<8>(b, a));  // three instructions (the OR form takes four)
+    ch[4 * qd] = t->to[(V[qd] >> 18) & 63];
+    ch[4 * qd + 1] = t->to[(V[qd] >> 12) & 63];
+    ch[4 * qd + 2] = t->to[(V[qd] >> 6) & 63];
+    ch[4 * qd + 3] = t->to[V[qd] & 63];
   }
+  // chars a, b, c, d of a quad -> a | b << 8 | c << 16 | d << 24: three v_lshl_or per
+  // word (the OR form takes four), the group's twelve in one asm block (see group24)
+  uint32_t out[4], p0, q0, p1, q1, p2, q2, p3, q3;
+  asm("v_lshl_or_b32 %4, %13, 8, %12\n\t"
+      "v_lshl_or_b32 %5, %15, 8, %14\n\t"
+      "v_lshl_or_b32 %6, %17, 8, %16\n\t"
+      "v_lshl_or_b32 %7, %19, 8, %18\n\t"
+      "v_lshl_or_b32 %8, %21, 8, %20\n\t"
+      "v_lshl_or_b32 %9, %23, 8, %22\n\t"
+      "v_lshl_or_b32 %10, %25, 8, %24\n\t"
+      "v_lshl_or_b32 %11, %27, 8, %26\n\t"
+      "v_lshl_or_b32 %0, %5, 16, %4\n\t"
+      "v_lshl_or_b32 %1, %7, 16, %6\n\t"
+      "v_lshl_or_b32 %2, %9, 16, %8\n\t"
+      "v_lshl_or_b32 %3, %11, 16, %10"
+      : "=v"(out[0]), "=v"(out[1]), "=v"(out[2]), "=v"(out[3]), "=&v"(p0), "=&v"(q0), "=&v"(p1), "=&v"(q1),
+        "=&v"(p2), "=&v"(q2), "=&v"(p3), "=&v"(q3)
+      : "v"(ch[0]), "v"(ch[1]), "v"(ch[2]), "v"(ch[3]), "v"(ch[4]), "v"(ch[5]), "v"(ch[6]), "v"(ch[7]), "v"(ch[8]),
+        "v"(ch[9]), "v"(ch[10]), "v"(ch[11]), "v"(ch[12]), "v"(ch[13]), "v"(ch[14]), "v"(ch[15]));
   return make_uint4(out[0], out[1], out[2], out[3]);
 }
 

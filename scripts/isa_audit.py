@@ -105,3 +105,20 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def opcodes(path, kern, blocks):
+    """Opcode histogram (VALU only) over the named basic blocks of a kernel."""
+    lines = open(path).read().split("\n")
+    start = next(i for i, l in enumerate(lines) if l.startswith("_Z") and kern in l.split(":")[0])
+    end = next(i for i in range(start, len(lines)) if lines[i].startswith(".Lfunc_end"))
+    cur, hist = None, Counter()
+    for i in range(start + 1, end):
+        m = re.match(r"^(\.LBB\w+):", lines[i]) or re.match(r"^; (%bb\.\d+):", lines[i])
+        if m:
+            cur = m.group(1)
+            continue
+        s = lines[i].split(";")[0].strip()
+        if cur in blocks and s.startswith("v_"):
+            hist[s.split()[0]] += 1
+    return hist
