@@ -642,8 +642,11 @@ __device__ __forceinline__ void encode_prio(int p) {
 }
 
 
-// Buffer resource word 3 for raw byte-addressed dword loads on gfx9-family parts (gfx950).
+// Buffer resource word 3 for raw byte-addressed dword loads on gfx9-family parts (gfx950),
+// and the cache-policy operand of a non-temporal buffer store (the `nt` bit, as
+// __builtin_nontemporal_store gives global stores: store_stream16).
 constexpr int kBufferDword3 = 0x00020000;
+constexpr int kBufferNT = 2;
 
 // One lane's share of the fused update (the stream path): the values [e0, e0 + S)
 // of group g, S = 3 (the whole group) or S = 1 (one value; three lanes of a wave
@@ -1780,6 +1783,41 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
     if constexpr (D16) store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab, dt));
     else store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab));
   };
+  if (vpitch >= (size_t)(3 * groups)) {  // block-uniform: rows padded to whole groups (bench.py's buffers)
+    // Every lane loads its 12 bytes (a buffer load from the row's uniform address, SALU-
+    // advanced), so the loads need no per-lane form: the rows in flight rotate through
+    // the same registers, with no copies between rows (the branchy load made the compiler
+    // copy each row twice). The last group's slots past n are masked to +0.0, the value
+    // the unpadded load gives them.
+    typedef uint32_t u3v __attribute__((ext_vector_type(3)));
+    const uint32_t m1 = r > 1 ? ~0u : 0u, m2 = r > 2 ? ~0u : 0u;
+    const uint32_t off = (uint32_t)(12 * g);  // a row < 2 GiB (the launchers check)
+    auto ld = [&](int rr) -> u3v {
+      const __amdgpu_buffer_rsrc_t row = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(values + (size_t)rr * vpitch), (short)0, 0x7fffffff, kBufferDword3);
+      return __builtin_amdgcn_raw_buffer_load_b96(row, off, 0, 0);
+    };
+    const uint32_t ooff = (uint32_t)(16 * g);
+    auto emit_u = [&](int rr, const u3v& w) {
+      const float x[3] = {u2f(w.x), u2f(w.y & m1), u2f(w.z & m2)};
+      const uint4 t = D16 ? encode_group(x, r, tab, dt) : encode_group(x, r, tab);
+      typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+      const __amdgpu_buffer_rsrc_t orow = __builtin_amdgcn_make_buffer_rsrc(out + (size_t)rr * pitch, (short)0,
+                                                                             0x7fffffff, kBufferDword3);
+      __builtin_amdgcn_raw_buffer_store_b128(u4v{t.x, t.y, t.z, t.w}, orow, ooff, 0, kBufferNT);
+    };
+    // a row's registers are reloaded right after it is encoded (the other row in flight
+    // meanwhile), so no register is copied between rows; the loads are unconditional
+    // (the last row again at the end), so the loop carries no per-lane PHI either
+    u3v a = ld(row0), b = ld(min(row0 + 1, row1 - 1));
+    for (int row = row0; row < row1; row += 2) {
+      emit_u(row, a);
+      a = ld(min(row + 2, row1 - 1));
+      if (row + 1 < row1) emit_u(row + 1, b);  // block-uniform
+      b = ld(min(row + 3, row1 - 1));
+    }
+    return;
+  }
   if constexpr (ROT) {
     f3 buf[2];
 #pragma unroll
@@ -3187,6 +3225,7 @@ static int encode_rows_per_block(int64_t gx, int rows) {
 // uses the byte table.
 hipError_t launch_encode_f32(const float* values, int64_t n, size_t vpitch, int rows, uint8_t* out, size_t pitch,
                              hipStream_t s) {
+  if (!row_fits(n)) return hipErrorInvalidValue;
   int64_t groups = (n + 2) / 3;
   if (groups == 0 || rows == 0) return hipSuccess;
   const int64_t gx = blocks_for(groups, 256);
