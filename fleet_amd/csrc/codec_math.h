@@ -652,7 +652,12 @@ struct alignas(16) XlEntry {
   float h[4];     // /10 chain group multipliers
   float hx;       // extra /10 step: RN(0.1) or 1
   float pad;
+  // 112-byte stride: seven 16-byte LDS chunks, odd, so the serial consumer's entry reads
+  // (one entry per lane, six 16-byte reads) fall on 16 distinct bank offsets before two
+  // entries collide (the 96-byte stride repeated every 8 entries)
+  float pad2[4];
 };
+static_assert(sizeof(XlEntry) == 112, "XlEntry stride");
 FLEET_HDC XlEntry xl_entry(uint32_t idx) {
   XlEntry x{};
   const uint32_t sign = idx / kXlSpan, be = 126u + idx % kXlSpan;

@@ -1783,14 +1783,20 @@ __device__ __forceinline__ void encode_rows(const float* __restrict__ values, in
     if constexpr (D16) store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab, dt));
     else store_stream16(out + (size_t)rr * pitch + 16 * g, encode_group(x, r, tab));
   };
-  if (vpitch >= (size_t)(3 * groups)) {  // block-uniform: rows padded to whole groups (bench.py's buffers)
+  // the fused steps' encode blocks (D16) on rows padded to whole groups (bench.py's buffers):
+  // there the encode's VALU work shares the SIMDs with the aggregation's, and the form
+  // below has the fewest instructions; the standalone encode (HBM-bound) keeps two rows in
+  // flight ahead of the one it encodes (the form below, one row ahead, measured 3 % slower
+  // there: synth1m_256 443 -> 459 us, r06 call a5)
+  if (D16 && vpitch >= (size_t)(3 * groups)) {  // block-uniform
     // Every lane loads its 12 bytes (a buffer load from the row's uniform address, SALU-
     // advanced), so the loads need no per-lane form: the rows in flight rotate through
     // the same registers, with no copies between rows (the branchy load made the compiler
     // copy each row twice). The last group's slots past n are masked to +0.0, the value
     // the unpadded load gives them.
     typedef uint32_t u3v __attribute__((ext_vector_type(3)));
-    const uint32_t m1 = r > 1 ? ~0u : 0u, m2 = r > 2 ? ~0u : 0u;
+    uint32_t m1 = r > 1 ? ~0u : 0u, m2 = r > 2 ? ~0u : 0u;
+    asm("" : "+v"(m1), "+v"(m2));  // opaque masks: one v_and per slot, not a v_cndmask_e64 each
     const uint32_t off = (uint32_t)(12 * g);  // a row < 2 GiB (the launchers check)
     auto ld = [&](int rr) -> u3v {
       const __amdgpu_buffer_rsrc_t row = __builtin_amdgcn_make_buffer_rsrc(
@@ -1944,7 +1950,9 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   constexpr int CPP = ((WP ? 1 : NPW) * 64 * IPT) / TG;      // clients per pass
   constexpr int RING = (6144 / E) / CPP > 0 ? (6144 / E) / CPP : 1;  // passes in LDS (~24 KiB)
   FLEET_TSTAMP(0);
-  __shared__ TileShared<TG, NW> sh;
+  // the producers on the byte-table digit counts (D16: the stream kernel's stages; the
+  // tiles of a MNIST-size launch, 1.9 per CU, leave the LDS for its 9 KB)
+  __shared__ TileShared<TG, NW, true> sh;
   __shared__ XlTable xl;  // the consumer's one-lookup Q
   __shared__ float ptile[RING * CPP * E];
   __shared__ float finals[E];
@@ -1962,11 +1970,12 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   }
   if ((int)blockIdx.x >= nU) {  // block-uniform: a job riding in the launch
     b64_tables_init<64 * NW>(&sh.tab);
+    d16_table_init<64 * NW>(&sh.dt);
     __syncthreads();
     const int64_t e = (int64_t)blockIdx.x - nU;
-    // the next batch's client encode (fleet_update_encode_device)
-    encode_rows<false, 64 * NW>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
-                                (int)(e / ej.gx), &sh.tab, nullptr);
+    // the next batch's client encode (fleet_update_encode_device), on the byte table too
+    encode_rows<true, 64 * NW>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                               (int)(e / ej.gx), &sh.tab, &sh.dt);
     return;
   }
   const int64_t g0 = g_begin + (int64_t)blockIdx.x * TG;
