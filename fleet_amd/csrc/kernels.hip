@@ -1178,7 +1178,7 @@ template <int TG, int NW, bool D16>
 __device__ __forceinline__ void tile_epilogue(TileShared<TG, NW, D16>& sh, const float* __restrict__ vals,
                                               double inv_avg, int64_t n_up, int64_t walk_end, int64_t g0, int ng,
                                               uint8_t* __restrict__ merged, float* __restrict__ merged_f32,
-                                              int* __restrict__ err, int32_t* outc = nullptr) {
+                                              int* __restrict__ err, int32_t* outc = nullptr) {  // outc: E ints of LDS, D16 only
   const int tid = threadIdx.x;
   int32_t* oc;
   if constexpr (D16) oc = outc;
@@ -1949,6 +1949,7 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   constexpr int NPW = NW - 1;                                // producer waves
   constexpr int CPP = ((WP ? 1 : NPW) * 64 * IPT) / TG;      // clients per pass
   constexpr int RING = (6144 / E) / CPP > 0 ? (6144 / E) / CPP : 1;  // passes in LDS (~24 KiB)
+  static_assert(RING * CPP >= 1, "the ring holds the epilogue's E codes");
   FLEET_TSTAMP(0);
   // the producers on the byte-table digit counts (D16: the stream kernel's stages; the
   // tiles of a MNIST-size launch, 1.9 per CU, leave the LDS for its 9 KB)
@@ -2104,7 +2105,9 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   FLEET_TSTAMP(4);
   if (badacc) atomicOr(err, FLEET_ERRBIT_BASE64);
   __syncthreads();
-  tile_epilogue(sh, finals, inv_avg, n_up, hdr_block[2], g0, ng, merged, merged_f32, err);
+  // (the ring is free after the barrier: the merged codes are assembled there)
+  tile_epilogue(sh, finals, inv_avg, n_up, hdr_block[2], g0, ng, merged, merged_f32, err,
+                reinterpret_cast<int32_t*>(ptile));
   FLEET_TSTAMP(5);
 }
 

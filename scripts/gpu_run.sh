@@ -7,6 +7,7 @@
 #   tests            full pytest -m gpu
 #   smoke            __graft_entry__.smoke()
 #   bench            the default bench line (bench_default.json)
+#   benchn:N         bench.py --gpus N with every rank on device 0 over gloo (the N-rank path rehearsed)
 #   strong[:W]       per-rank pipelined windows of W (default synth1m_256) at N = 1, 2, 4, 8
 #                    on one GPU (scripts/strong_probe.py), fused / update-only
 #   windows:W        W at N = 1 only: the fused step, the update alone, the encode alone
@@ -44,6 +45,13 @@ for step in "$@"; do
     bench)
       timeout -k 10 900 python3 bench.py > "$O/bench_default.json" 2> "$O/bench_default.err" || { tail -20 "$O/bench_default.err"; exit 1; }
       cut -c1-400 "$O/bench_default.json" ;;
+    benchn)
+      # the N-rank bench path rehearsed on one GPU: N ranks on device 0, gloo collectives
+      # (a readiness check, its times measure nothing)
+      FLEET_BENCH_SAME_DEVICE=1 FLEET_BENCH_BACKEND=gloo timeout -k 10 1200 python3 bench.py --gpus "$arg" --steps 8 \
+        --warmup 2 > "$O/bench_n${arg}_same_device.json" 2> "$O/bench_n${arg}_same_device.err" \
+        || { tail -20 "$O/bench_n${arg}_same_device.err"; exit 1; }
+      cut -c1-300 "$O/bench_n${arg}_same_device.json" ;;
     strong)
       W=${arg:-synth1m_256}
       for mode in fused upd; do
