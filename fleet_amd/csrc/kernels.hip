@@ -469,13 +469,35 @@ __device__ __forceinline__ double pair_sum_f64(double a, double b) {
   }
 }
 
+// Four sums at once (Kardam's squared norms of two clients): a and b fold into the two
+// wave halves and c and d likewise (pair_sum_f64<64>'s first step), one permlane16 swap
+// folds the two results into one register by 16-lane rows -- a, c, b, d in rows 0..3 --
+// and one group_sum_f64<16> finishes: the sums in lanes 15 (a), 31 (c), 47 (b) and 63
+// (d); 21 instructions against 36 for two pair_sum_f64<64>. Every lane of the wave active.
+__device__ __forceinline__ double quad_sum_f64(double a, double b, double c, double d) {
+  auto fold32 = [](double u, double v) {
+    const uint64_t ub = __builtin_bit_cast(uint64_t, u), vb = __builtin_bit_cast(uint64_t, v);
+    const auto lo = __builtin_amdgcn_permlane32_swap((uint32_t)ub, (uint32_t)vb, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((uint32_t)(ub >> 32), (uint32_t)(vb >> 32), false, false);
+    return __builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]) +
+           __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]);
+  };
+  const double x = fold32(a, b), y = fold32(c, d);
+  const uint64_t xb = __builtin_bit_cast(uint64_t, x), yb = __builtin_bit_cast(uint64_t, y);
+  const auto lo = __builtin_amdgcn_permlane16_swap((uint32_t)xb, (uint32_t)yb, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((uint32_t)(xb >> 32), (uint32_t)(yb >> 32), false, false);
+  return group_sum_f64<16>(__builtin_bit_cast(double, ((uint64_t)hi[0] << 32) | lo[0]) +
+                           __builtin_bit_cast(double, ((uint64_t)hi[1] << 32) | lo[1]));
+}
+
 // Kardam's bookkeeping of one client step in a stream lane (KD = true; SURVEY.md f2,
 // CppNNUpdater.java:463-481, Kardam.java:48-106): G = Q(f32(f64(p) * lr)) -- the
 // picked gradient scalarMultiply(getLrate()) --, its squared norm and that of
 // Q(G - prev) (getNorm: float products summed in double), G stored in upload
 // coordinates for the next round's difference. `flat` bit i = value slot pos0 + i
 // is in the flat gradient (neither a header slot nor past the walk). The wave's
-// two sums go to its partial slot `part` (lanes 31 and 63; k_kardam_reduce sums the waves).
+// two per-lane sums are returned (sg, sd); the stream loop reduces them over the wave two
+// clients at a time (quad_sum_f64) into the wave's partial slots (k_kardam_reduce sums the waves).
 // The worker's previous G at the lane's slots (0 off the flat gradient): loaded a client
 // ahead by the stream loop, so the HBM latency of the prev rows overlaps the current
 // client's chain instead of stalling it. Returns has_prev[c] (uniform).
@@ -509,8 +531,8 @@ __device__ __forceinline__ bool kardam_prev_load(const KardamOut& kd, int c, uin
 template <int S, bool FULL = false>
 __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uint32_t flat, bool live, int64_t pos0,
                                                  int64_t n_up, const KardamOut& kd, const D16Table& dtab,
-                                                 const B64Tables& tab, double* __restrict__ part, bool hasp,
-                                                 const float (&pv)[S]) {
+                                                 const B64Tables& tab, bool hasp, const float (&pv)[S], double& sg,
+                                                 double& sd) {
   typedef float f3u __attribute__((ext_vector_type(3), aligned(4)));
   if constexpr (FULL) {
     flat = (1u << S) - 1u;
@@ -521,7 +543,8 @@ __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uin
   for (int i = 0; i < S; ++i) rg[i] = p[i];
   dampen_stage<S>(rg, kd.lr);  // lr is uniform
   q_stage_d16x<S>(G, rg, &dtab, tab.var);
-  double sg = 0.0, sd = 0.0;
+  sg = 0.0;
+  sd = 0.0;
 #pragma unroll
   for (int i = 0; i < S; ++i)
     if ((flat >> i) & 1u) sg += (double)(G[i] * G[i]);
@@ -552,9 +575,26 @@ __device__ __forceinline__ void kardam_lane_step(const float (&p)[S], int c, uin
       if (FULL || (live && pos0 < n_up)) go[0] = gv[0];
     }
   }
-  // every lane of the wave is here: the two sums in lanes 31 and 63
-  const double s = pair_sum_f64<64>(sg, sd);
-  if ((threadIdx.x & 31) == 31) part[(threadIdx.x >> 5) & 1] = s;
+}
+
+// The wave's norm partials of clients c - 1 and c (held sums sg0, sd0 and this client's
+// sg, sd) into their slots, or of client c alone when it is the last and even; nothing
+// for an even client with a successor (its sums are held). Every lane of the wave here;
+// c uniform.
+__device__ __forceinline__ void kardam_wave_partials(int c, int M, double& sg0, double& sd0, double sg, double sd,
+                                                     double* __restrict__ part, size_t stride) {
+  if (c & 1) {
+    const double s = quad_sum_f64(sg0, sd0, sg, sd);
+    const int lane = threadIdx.x & 63;
+    if ((lane & 15) == 15)  // rows 0..3: (c - 1, g), (c, g), (c - 1, d), (c, d)
+      part[(size_t)(c - 1 + ((lane >> 4) & 1)) * stride + (lane >> 5)] = s;
+  } else if (c + 1 == M) {
+    const double s = pair_sum_f64<64>(sg, sd);
+    if ((threadIdx.x & 31) == 31) part[(size_t)c * stride + ((threadIdx.x >> 5) & 1)] = s;
+  } else {
+    sg0 = sg;
+    sd0 = sd;
+  }
 }
 
 // Client-side encode: rows of fp32 -> rows of Base64 (Base64::encode(vector<float>)).
@@ -697,6 +737,7 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
   using Row = typename std::conditional<S == 3, uint4, uint2>::type;
   float kd_pv[S];       // KD: this client's prev values (loaded a client ahead)
   bool kd_hasp = false;
+  double kd_sg0 = 0.0, kd_sd0 = 0.0;  // KD: the lane's norm sums of the held (even) client
   auto client = [&](int c, const Row& cur) {
     if constexpr (S == 3) {
       if (need == 0xffffu) bad |= b64_decode_group_full(cur, &tab, codes);
@@ -721,12 +762,12 @@ __device__ __forceinline__ void update_lane(const B64Tables& tab, const D16Table
       q_stage_d16x<S>(y, y0, &dtab, tab.var);
       dampen_stage<S>(y, dampen[c]);
       q_stage_d16x<S>(p, y, &dtab, tab.var);
+      double sg, sd;
       if (kd_full)
-        kardam_lane_step<S, true>(p, c, flatbits, live, 3 * g + e0, n_up, kd, dtab, tab,
-                                  kd_part + (size_t)c * kd_stride, kd_hasp, kd_pv);
+        kardam_lane_step<S, true>(p, c, flatbits, live, 3 * g + e0, n_up, kd, dtab, tab, kd_hasp, kd_pv, sg, sd);
       else
-        kardam_lane_step<S>(p, c, flatbits, live, 3 * g + e0, n_up, kd, dtab, tab, kd_part + (size_t)c * kd_stride,
-                            kd_hasp, kd_pv);
+        kardam_lane_step<S>(p, c, flatbits, live, 3 * g + e0, n_up, kd, dtab, tab, kd_hasp, kd_pv, sg, sd);
+      kardam_wave_partials(c, M, kd_sg0, kd_sd0, sg, sd, kd_part, kd_stride);
     } else {
       q_stage_d16<S>(y, y0, &dtab, tab.var, dmax);
       dampen_stage<S>(y, dampen[c]);
@@ -1935,6 +1976,19 @@ __device__ __forceinline__ void kardam_reduce_block(const KardamReduceJob& kr, i
 // reading a pass, and publishes "passes consumed" so producers never overwrite
 // a ring slot still being read. Every wait has a partner that always makes
 // progress, so the grid drains.
+// p floats in the ring: 12 KiB = four passes of 16 clients at TG = 16, enough for the
+// producers to stay ahead (r04: the consumer waits 0.3 us in all), and it keeps the block
+// at 34.7 KB of LDS, four per CU, so the step's encode blocks get a slot beside the
+// 1.9 tiles per CU of a MNIST-size launch (24 KiB of ring: 46.7 KB, three per CU)
+#ifndef FLEET_PIPE_RING
+#define FLEET_PIPE_RING 3072
+#endif
+#ifndef FLEET_KD_RING
+#define FLEET_KD_RING 3072
+#endif
+#ifndef FLEET_PIPE_D16
+#define FLEET_PIPE_D16 1
+#endif
 template <int TG, int IPT, int NW, int WP = 0, bool KD = false>
 __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restrict__ uploads, size_t pitch, int M,
                                                      const double* __restrict__ dampen, double inv_avg,
@@ -1948,12 +2002,13 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   static_assert(E <= 64, "one consumer wave");
   constexpr int NPW = NW - 1;                                // producer waves
   constexpr int CPP = ((WP ? 1 : NPW) * 64 * IPT) / TG;      // clients per pass
-  constexpr int RING = (6144 / E) / CPP > 0 ? (6144 / E) / CPP : 1;  // passes in LDS (~24 KiB)
+  constexpr int RP = KD ? FLEET_KD_RING : FLEET_PIPE_RING;
+  constexpr int RING = (RP / E) / CPP > 0 ? (RP / E) / CPP : 1;  // passes in LDS
   static_assert(RING * CPP >= 1, "the ring holds the epilogue's E codes");
   FLEET_TSTAMP(0);
   // the producers on the byte-table digit counts (D16: the stream kernel's stages; the
   // tiles of a MNIST-size launch, 1.9 per CU, leave the LDS for its 9 KB)
-  __shared__ TileShared<TG, NW, true> sh;
+  __shared__ TileShared<TG, NW, (bool)FLEET_PIPE_D16> sh;
   __shared__ XlTable xl;  // the consumer's one-lookup Q
   __shared__ float ptile[RING * CPP * E];
   __shared__ float finals[E];
@@ -1971,12 +2026,19 @@ __global__ void __launch_bounds__(64 * NW) k_update_pipe(const uint8_t* __restri
   }
   if ((int)blockIdx.x >= nU) {  // block-uniform: a job riding in the launch
     b64_tables_init<64 * NW>(&sh.tab);
+#if FLEET_PIPE_D16
     d16_table_init<64 * NW>(&sh.dt);
+#endif
     __syncthreads();
     const int64_t e = (int64_t)blockIdx.x - nU;
     // the next batch's client encode (fleet_update_encode_device), on the byte table too
+#if FLEET_PIPE_D16
     encode_rows<true, 64 * NW>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
                                (int)(e / ej.gx), &sh.tab, &sh.dt);
+#else
+    encode_rows<false, 64 * NW>(ej.values, ej.n, ej.vpitch, ej.out, ej.pitch, ej.groups, ej.rows, ej.rpb, e % ej.gx,
+                                (int)(e / ej.gx), &sh.tab, nullptr);
+#endif
     return;
   }
   const int64_t g0 = g_begin + (int64_t)blockIdx.x * TG;
@@ -3156,9 +3218,12 @@ __global__ void __launch_bounds__(NT) k_kardam_reduce(const double* __restrict__
   }
 }
 
-// waves per block of the Kardam pipelined form (one consumer, the rest producers)
+// waves per block of the Kardam pipelined form (one consumer, the rest producers): the
+// side outputs double the producers' work, and 8 producer waves keep the consumer fed
+// where 4 do not (mnist64 under rocprof, r06 call a10: 27.3 us with 4 producer waves,
+// 24.4 with 8, 28.3 with 10, 43.2 with 12; the plain update 16.1 us)
 #ifndef FLEET_KD_NW
-#define FLEET_KD_NW 5
+#define FLEET_KD_NW 9
 #endif
 constexpr int kKdPipeNW = FLEET_KD_NW;
 

@@ -1,7 +1,7 @@
 # Kardam's side outputs per library build (LIBS = "label=path.so[,VAR=VALUE...] ...") and workload
 # (WORKLOADS): scripts/kardam_ab.py under rocprofv3 --kernel-trace --stats, the
 # per-kernel averages of the plain update, the update with side outputs and the reduce
-set -u
+set -u -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 O=${OUT:-gpurun_out/klibs}; mkdir -p $O
 for W in ${WORKLOADS:-mnist64 cifar10_256 synth1m_256}; do

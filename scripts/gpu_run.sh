@@ -7,6 +7,9 @@
 #   tests            full pytest -m gpu
 #   smoke            __graft_entry__.smoke()
 #   bench            the default bench line (bench_default.json)
+#   sqlds:W:N:MODE   LDS counters (bank conflicts, unaligned stalls) of strong_probe W at N, MODE
+#   bin:PATH         a prebuilt dev binary
+#   klibs:W1,W2      Kardam vs plain per library build in LIBS (scripts/gpu_kardam_libs.sh)
 #   benchn:N         bench.py --gpus N with every rank on device 0 over gloo (the N-rank path rehearsed)
 #   strong[:W]       per-rank pipelined windows of W (default synth1m_256) at N = 1, 2, 4, 8
 #                    on one GPU (scripts/strong_probe.py), fused / update-only
@@ -102,6 +105,15 @@ for r in csv.DictReader(open('$O/kardam_$w/run_kernel_stats.csv')):
       EC=$(python3 -c "import sys; sys.path.insert(0,'.'); import bench; from fleet_amd.layouts import LAYOUTS; l,m,_=bench.WORKLOADS['$W']; print(m*LAYOUTS[l].n_up/$N)")
       echo "-- $W N=$N $MODE ${FLEET_EXPERIMENTS:-default}" | tee -a "$O/sq.txt"
       python3 scripts/pmc_kernels.py "$D" "$EC" | grep -E "k_update|k_encode" | tee -a "$O/sq.txt" ;;
+    sqlds)
+      # LDS pass: bank conflicts / unaligned stalls / LDS-array cycles per kernel
+      IFS=: read -r W N MODE <<< "$arg"
+      D="$O/sqlds_${W}_n${N}_${MODE}${SQTAG:-}"
+      timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE \
+        SQ_LDS_UNALIGNED_STALL SQ_LDS_ADDR_CONFLICT SQ_WAVES SQ_INSTS_VALU SQ_BUSY_CU_CYCLES --output-format csv -d "$D" \
+        -o run -- python3 scripts/strong_probe.py "$W" "$N" "$MODE" > "$D.log" 2>&1 || { tail -20 "$D.log"; exit 1; }
+      echo "-- lds $W N=$N $MODE ${SQTAG:-} ${FLEET_EXPERIMENTS:-default}" | tee -a "$O/sqlds.txt"
+      python3 scripts/pmc_kernels.py "$D" | grep -E "k_update|k_encode" | tee -a "$O/sqlds.txt" ;;
     sqk)
       W=$arg
       D="$O/sqk_${W}${SQTAG:-}"
@@ -129,6 +141,14 @@ for r in csv.DictReader(open('$O/kardam_$w/run_kernel_stats.csv')):
       timeout -k 10 600 python3 "${PA[@]}" 2>&1 | grep -v amdgpu.ids >> "$O/$(basename "${PA[0]}").log" \
         || { tail -30 "$O/$(basename "${PA[0]}").log"; exit 1; }
       tail -12 "$O/$(basename "${PA[0]}").log" ;;
+    bin)
+      # a prebuilt dev binary (e.g. ab6/ubench_valu2): its output to bin_<name>.log
+      timeout -k 10 300 "$arg" > "$O/bin_$(basename "$arg").log" 2>&1 || { tail -30 "$O/bin_$(basename "$arg").log"; exit 1; }
+      tail -40 "$O/bin_$(basename "$arg").log" ;;
+    klibs)
+      # Kardam per library build (LIBS) on the workloads in arg (comma-separated)
+      OUT="$O/klibs" WORKLOADS="${arg//,/ }" bash scripts/gpu_kardam_libs.sh > "$O/klibs.txt" 2>&1 || { tail -20 "$O/klibs.txt"; exit 1; }
+      cat "$O/klibs.txt" ;;
     py)
       timeout -k 10 600 python3 "$arg" > "$O/$(basename "$arg").log" 2>&1 || { tail -30 "$O/$(basename "$arg").log"; exit 1; }
       tail -40 "$O/$(basename "$arg").log" ;;

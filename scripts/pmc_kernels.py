@@ -55,6 +55,11 @@ def main():
             for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS"):
                 if c in o:
                     line.append("%s %.2f" % (c[3:].lower(), o[c] / wc))
+        if o.get("SQ_LDS_IDX_ACTIVE"):
+            for c in ("SQ_LDS_BANK_CONFLICT", "SQ_LDS_UNALIGNED_STALL", "SQ_LDS_ADDR_CONFLICT"):
+                if c in o:
+                    line.append("%s %.3f" % (c[7:].lower(), o[c] / o["SQ_LDS_IDX_ACTIVE"]))
+            line.append("lds_active %.0f" % o["SQ_LDS_IDX_ACTIVE"])
         if "SQ_WAVES" in o:
             line.append("waves %.0f" % o["SQ_WAVES"])
         print("  ".join(line), flush=True)

@@ -9,7 +9,7 @@ set -u
 script=$1; tmo=$2; log=$3
 cd /root/repo
 rm -rf .snap && mkdir .snap
-tar --exclude ./.git --exclude ./.snap --exclude ./gpurun_out --exclude './ab/*.objs' --exclude '__pycache__' --exclude '*.pyc' \
+tar --exclude ./.git --exclude ./.snap --exclude ./gpurun_out --exclude ./ab --exclude './ab6/*.objs' --exclude '__pycache__' --exclude '*.pyc' \
   -cf - . | tar -xf - -C .snap
 trap 'rm -rf /root/repo/.snap' EXIT
 cmd="export OUTROOT=\$GRAFT_REPO_ROOT/gpurun_out; cd .snap && export GRAFT_REPO_ROOT=\$PWD && bash $script"

@@ -1,4 +1,4 @@
-// scripts/ubench_tiled.hip -- phase timing of k_update_tiled (dev tool).
+// scripts/ubench_tiled.hip -- phase timing of the pipelined tiles k_update_pipe (dev tool).
 // Builds kernels.hip with FLEET_TIMING and prints per-block phase durations.
 #define FLEET_TIMING 1
 #define FLEET_DEV_ALL_KERNELS 1
@@ -13,12 +13,9 @@ using namespace fleet;
 template <int TG, bool PIPE, int IPT = 1, int NW = 4, int WP = 0>
 static void launch(unsigned blocks, const uint8_t* text, size_t pitch, int M, const double* damp, int64_t n_up,
                    int64_t groups, const int32_t* hdr, uint8_t* merged, float* mf, int* err) {
-  if constexpr (PIPE)
-    hipLaunchKernelGGL((k_update_pipe<TG, IPT, NW, WP>), dim3(blocks), dim3(64 * NW), 0, 0, text, pitch, M, damp, 1.0 / M, n_up,
-                       (int64_t)0, groups, hdr, merged, mf, err, INT32_MAX, EncodeJob{});
-  else
-    hipLaunchKernelGGL(k_update_tiled<TG>, dim3(blocks), dim3(256), 0, 0, text, pitch, M, damp, 1.0 / M, n_up,
-                       (int64_t)0, groups, hdr, merged, mf, err);
+  static_assert(PIPE, "the classic tiles have no standalone kernel since r06");
+  hipLaunchKernelGGL((k_update_pipe<TG, IPT, NW, WP>), dim3(blocks), dim3(64 * NW), 0, 0, text, pitch, M, damp, 1.0 / M,
+                     n_up, (int64_t)0, groups, hdr, merged, mf, err, INT32_MAX, EncodeJob{});
 }
 
 static std::vector<int32_t> g_hpos;
