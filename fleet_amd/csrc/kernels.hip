@@ -3001,20 +3001,24 @@ static FlatGrid flat_grid(int64_t groups, const PlanOverrides& o, bool fused) {
 }
 
 // The aggregation's launch plan for a bucket (or window) of `groups` 3-value groups.
-//   pipe   -- k_update_pipe<16, 1, 5, 0>: 16-group tiles, 4 producer waves + one
-//             consumer wave (MNIST-size buckets: the serial chain is the critical path);
-//   tiled  -- k_update_tiled<64, ..., TG2 = 16 | 0, D16>: two-phase 64-group tiles on the
-//             byte-table digit counts, two widths when a partial round remains (CIFAR);
-//   stream -- k_update_mixed<256>: a lane walks its group down all M rows (from ~2 waves
-//             per SIMD up), whole rounds group-per-lane and the rest a value per lane.
-// Measured rules: the stream grid from 131,072 groups (2 waves per SIMD),
-// 64-group tiles from 32 k groups (below 4 per CU they still beat 32-group tiles, whose
-// phase 2 has half the serial lanes per tile), the pipelined tiles below.
+//   stream -- k_update_mixed<256> (fused: k_update_encode<256>): a lane walks its group
+//             down all M rows, whole rounds group-per-lane and the rest a value per lane;
+//   tiled  -- the one-width 64-group tiles of k_update_tiled_encode<64> (the fused step);
+//   flat   -- k_update_flat: two-phase tiles of a runtime width, one balanced round;
+//   woven  -- k_update_weave<8> / k_update_weave_encode<8 | 6>: both phases in one barrier
+//             interval (small windows, latency-bound);
+//   pipe   -- k_update_pipe<16, 1, 5, 0>: 16-group tiles, 4 producer waves + one consumer
+//             wave (MNIST-size buckets: the serial chain is the critical path).
+// Default ranges (DESIGN.md §4, 256 CUs): the update alone -- stream from 131,072 groups,
+// flat above 49,152 (three 64-group tiles per CU), woven 8-wave from 24 k, pipe below;
+// the fused step -- stream from 131,072, tiled from 65,536, flat from 40 k, woven 6-wave
+// from 32 k, woven 8-wave from 14 k, pipe below; Kardam's side outputs -- stream from
+// 131,072, flat from 32 k, pipe below.
 struct UpdatePlan {
   int kind;       // 0 stream, 1 tiled, 2 pipe, 3 woven tiles (k_update_weave<nw>), 4 flat tiles
   int nA;         // stream: blocks of group-per-lane waves (the rest a value per lane)
   int64_t blocks; // stream / tiled / pipe grid
-  int nw;         // woven tiles: waves per block (3 or 4)
+  int nw;         // woven tiles: waves per block (6 or 8)
   FlatGrid fg;    // flat tiles
 };
 static UpdatePlan plan_update(int64_t groups, const PlanOverrides& o, bool fused = false) {

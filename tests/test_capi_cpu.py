@@ -88,6 +88,37 @@ GRID_SIZES = [1, 2, 16, 17, 83, 84, 85, 255, 256, 257, 6_667, 7_654, 16_668, 32_
               104_623, 110_413, 131_072, 174_763, 349_526, 1_398_102]
 
 
+# The default launch plan per size (DESIGN.md §4 "Launch choice", kernels.hip plan_update),
+# planned for 256 CUs (the host has no device: device_simds' fallback). (groups, update
+# alone, fused step) at the ends of every range.
+DEFAULT_PLAN = [
+    (1_000, "k_update_pipe<16, 1, 5, 0, false>", "k_update_pipe<16, 1, 5, 0, false> (with the encode's blocks)"),
+    (14 * 1024 - 1, "k_update_pipe<16, 1, 5, 0, false>", "k_update_pipe<16, 1, 5, 0, false> (with the encode's blocks)"),
+    (14 * 1024, "k_update_pipe<16, 1, 5, 0, false>", "k_update_weave_encode<8>"),
+    (24 * 1024 - 1, "k_update_pipe<16, 1, 5, 0, false>", "k_update_weave_encode<8>"),
+    (24 * 1024, "k_update_weave<8>", "k_update_weave_encode<8>"),
+    (32 * 1024, "k_update_weave<8>", "k_update_weave_encode<6>"),
+    (40 * 1024 - 1, "k_update_weave<8>", "k_update_weave_encode<6>"),
+    (40 * 1024, "k_update_weave<8>", "k_update_flat"),
+    (3 * 64 * 256, "k_update_weave<8>", "k_update_flat"),
+    (3 * 64 * 256 + 1, "k_update_flat", "k_update_flat"),
+    (65_535, "k_update_flat", "k_update_flat"),
+    (65_536, "k_update_flat", "k_update_tiled_encode<64>"),
+    (131_071, "k_update_flat", "k_update_tiled_encode<64>"),
+    (131_072, "k_update_mixed<256, false>", "k_update_encode<256>"),
+    (349_526, "k_update_mixed<256, false>", "k_update_encode<256>"),
+]
+
+
+@pytest.mark.parametrize("groups,upd,fused", DEFAULT_PLAN)
+def test_default_plan_table(groups, upd, fused):
+    """Every remaining kernel form is the default at some size, in the ranges DESIGN.md
+    §4 lists."""
+    F.set_plan("")
+    assert F.update_kernel(16 * groups) == upd
+    assert F.update_encode_kernel(16 * groups) == fused
+
+
 @pytest.mark.parametrize("spec", ["", "update=stream", "update=stream,grid=plain", "update=stream,grid=lanes",
                                   "update=tiled", "update=tiled,tile=classic", "update=pipe",
                                   "update=tiled,tile=weave6", "update=tiled,tile=weave8", "update=tiled,tile=flat",
