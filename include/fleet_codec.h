@@ -503,9 +503,10 @@ int fleet_sampler_last_indices(fleet_sampler* s, int32_t* out, size_t cap, size_
 /* Name of the aggregation kernel fleet_update / fleet_update_device launch for
  * an upload of `len` Base64 bytes (or a group window of that many bytes), exactly
  * as rocprofv3 names it (every template argument spelled out): "k_update_mixed<256,
- * false>", "k_update_tiled<64, false, TG2, true>", "k_update_flat" or
- * "k_update_pipe<16, 1, 5, 0, false>"; and what fleet_update_encode_device launches
- * ("k_update_encode<256, false>", "k_update_tiled_encode<64>", "k_update_flat", ...;
+ * false>", "k_update_flat", "k_update_weave<8>", "k_update_tiled_encode<64>" (tile=classic)
+ * or "k_update_pipe<16, 1, 5, 0, false>"; and what fleet_update_encode_device launches
+ * ("k_update_encode<256>", "k_update_tiled_encode<64>", "k_update_flat",
+ * "k_update_weave_encode<8>", ...; DESIGN.md §4 lists the default per size;
  * profiling aid; thread-local storage, valid until the thread's next call). */
 const char* fleet_update_kernel(size_t len);
 const char* fleet_update_encode_kernel(size_t len);
