@@ -119,3 +119,20 @@ def test_fused_step_fuzz(codec, oracle, plan, case):
     assert merged_b.cpu().numpy()[:L].tobytes() == exp
     for c in sorted({0, M - 1, int(rng.integers(0, M))}):
         assert next_b[c].cpu().numpy()[:L].tobytes() == oracle.encode_floats(nxt[c, :n])
+
+
+KD_PLANS = ["", "update=stream", "update=stream,grid=lanes", "update=tiled", "update=tiled,flat_w2=16", "update=pipe"]
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_kardam_fuzz(codec, oracle, plan, case):
+    """Kardam's side outputs (fleet_update_kardam_device) on random bucket sizes, client
+    counts and plans, three rounds each (no prev, prev on every other client, prev
+    replaced in place): merged bytes, G rows and norms as test_gpu_kardam_fused checks."""
+    from test_gpu_kardam_fused import check_side_outputs
+    rng = np.random.default_rng(5150 + case)
+    n = int(np.exp(rng.uniform(np.log(8), np.log(200_000))))
+    while oracle.decode_floats(oracle.encode_floats(np.array([n - 3], np.float32)))[0] != n - 3:
+        n += 1
+    plan(KD_PLANS[case % len(KD_PLANS)])
+    check_side_outputs(codec, oracle, synthetic(n), int(rng.integers(1, 9)))
