@@ -136,3 +136,45 @@ def test_kardam_fuzz(codec, oracle, plan, case):
         n += 1
     plan(KD_PLANS[case % len(KD_PLANS)])
     check_side_outputs(codec, oracle, synthetic(n), int(rng.integers(1, 9)))
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_model_codec_fuzz(codec, oracle, case):
+    """The mode-1 model codec (quantisation, first-occurrence dictionary by rocPRIM radix
+    sort and scans, the weights section of getParams and network::read of it) on random
+    matrix shapes -- single values, thin and wide matrices, sizes either side of the sort's
+    single-block limit -- and value mixes (trained-like, few levels, constant matrices,
+    +-0, NaN / inf) against the oracle's sequential restatement (network.h:594-706)."""
+    rng = np.random.default_rng(9100 + case)
+    nm = int(rng.integers(1, 7))
+    dims = []
+    for _ in range(nm):
+        shape = rng.integers(0, 4)
+        if shape == 0:
+            dims.append((1, 1, 1))
+        elif shape == 1:
+            dims.append((int(rng.integers(1, 6)), int(rng.integers(1, 6)), int(rng.integers(1, 400))))
+        else:
+            dims.append((int(rng.integers(1, 40)), int(rng.integers(1, 40)), int(rng.integers(1, 12))))
+    n = sum(c * r * ch for c, r, ch in dims)
+    mix = case % 4
+    if mix == 0:
+        w = rng.normal(0, 0.05, n) * np.exp(rng.normal(0, 1, n))
+    elif mix == 1:
+        w = rng.integers(-4, 5, n) * 0.125 + rng.choice([0.0, 1e-9], n)
+    elif mix == 2:
+        w = np.full(n, float(rng.normal()))
+    else:
+        w = rng.normal(0, 1, n)
+        k = max(1, n // 50)
+        w[rng.integers(0, n, k)] = rng.choice([np.nan, np.inf, -np.inf, 0.0, -0.0], k)
+    w = w.astype(np.float32)
+    wq, dic, idx = codec.model_quantize_index(w, dims)
+    owq = oracle.quantize(w, dims)
+    assert np.array_equal(wq.view(np.uint32), owq.view(np.uint32)), (case, dims)
+    od, oi = oracle.dictionary(owq)
+    assert np.array_equal(dic.view(np.uint32), od.view(np.uint32)) and np.array_equal(idx, oi), (case, dims)
+    sec = codec.model_weights_text(w, dims)
+    assert sec == oracle.weights_section(owq, dims), (case, dims)
+    wr = codec.model_read_weights(sec, dims)
+    assert np.array_equal(wr.view(np.uint32), oracle.read_weights_section(sec, dims).view(np.uint32)), (case, dims)
