@@ -290,3 +290,16 @@ def test_oracle_model_version_matches_reference(oracle):
     w = np.where(idx >= 0, vals[np.maximum(idx, 0)], np.float32(0)).astype(np.float32)
     assert np.array_equal(w.view(np.uint32), f["w_out"].view(np.uint32))
     assert np.array_equal(_g6_strtof(f["b"]).view(np.uint32), f["b_out"].view(np.uint32))
+
+
+def test_layout_headers_round_trip(oracle):
+    """Every workload layout's header values survive Base64::encode / decode exactly, so the
+    reference's flatGrad walk (network.h:1206-1223) reads the layout the bench synthesises.
+    (A single block of 4,194,301 values would not: it decodes to 4194300.75 and the walk
+    would take a payload slot for the bias count; configs[4] uses two blocks instead.)"""
+    import numpy as np
+    from fleet_amd.layouts import LAYOUTS
+    for name, lay in LAYOUTS.items():
+        hv = np.asarray(lay.header_values(), np.float32)
+        rt = oracle.decode_floats(oracle.encode_floats(hv))
+        assert np.array_equal(rt.view(np.uint32), hv.view(np.uint32)), name
